@@ -1,0 +1,160 @@
+"""Device context: the Python face of libcpx on one GPU.
+
+PyTorch-ROCm is used here only as plumbing — device allocations, the HIP stream (torch's
+current stream is handed to libcpx so every kernel is ordered with torch work) and host<->device
+copies.  All per-FOV arithmetic runs in the hand-written HIP kernels of libcpx.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+
+import torch
+
+from . import _lib
+from ._lib import check
+
+_STATS_BYTES = 64
+_QC_BYTES = 24
+_LSTAT_BYTES = 64
+_OBJ_BYTES = 56
+_HDR_BYTES = 16
+
+OBJ_DTYPE = None  # numpy structured dtype, built lazily
+
+
+def _np_dtypes():
+    import numpy as np
+    global OBJ_DTYPE
+    if OBJ_DTYPE is None:
+        OBJ_DTYPE = {
+            "stats": np.dtype([("max_q", "f8"), ("min_q", "f8"), ("sum_q", "f8"), ("pct_max", "f8"),
+                               ("count_max", "i8"), ("n", "i8"), ("has_nan", "i4"), ("has_inf", "i4"),
+                               ("_pad", "i8")]),
+            "qc": np.dtype([("slope", "f8"), ("pct_max", "f8"), ("n_valid", "i4"), ("n_rings", "i4")]),
+            "object": np.dtype([("label", "i4"), ("area", "i4"), ("bbox", "i4", (4,)),
+                                ("centroid_r", "f8"), ("centroid_c", "f8"), ("yc", "i4"), ("xc", "i4"),
+                                ("kept", "i4"), ("cell_idx", "i4")]),
+            "hdr": np.dtype([("n_objects", "i4"), ("n_kept", "i4"), ("max_label", "i4"),
+                             ("overflow", "i4")]),
+        }
+        assert OBJ_DTYPE["stats"].itemsize == _STATS_BYTES
+        assert OBJ_DTYPE["qc"].itemsize == _QC_BYTES
+        assert OBJ_DTYPE["object"].itemsize == _OBJ_BYTES
+        assert OBJ_DTYPE["hdr"].itemsize == _HDR_BYTES
+    return OBJ_DTYPE
+
+
+def _ptr(t: torch.Tensor | None):
+    if t is None:
+        return None
+    assert t.is_cuda and t.is_contiguous(), "libcpx needs contiguous device tensors"
+    return ct.c_void_p(t.data_ptr())
+
+
+def _illum_dtype(illum: torch.Tensor | None) -> int:
+    if illum is None:
+        return _lib.CPX_DTYPE_NONE
+    if illum.dtype == torch.float32:
+        return _lib.CPX_DTYPE_F32
+    if illum.dtype == torch.float64:
+        return _lib.CPX_DTYPE_F64
+    raise TypeError(f"illumination function dtype {illum.dtype} unsupported (float32/float64)")
+
+
+class Device:
+    """One libcpx context bound to one GPU and to torch's current stream on it."""
+
+    def __init__(self, device: int = 0):
+        if not torch.cuda.is_available():
+            raise _lib.CpxNativeMissing("no HIP device visible: the product path has no CPU fallback")
+        self.lib = _lib.load()
+        self.index = device
+        self.torch_device = torch.device("cuda", device)
+        torch.cuda.set_device(self.torch_device)
+        h = ct.c_void_p()
+        check(self.lib.cpx_init(device, ct.byref(h)), "cpx_init")
+        self.h = h
+        self._bind_stream()
+
+    def _bind_stream(self):
+        s = torch.cuda.current_stream(self.torch_device).cuda_stream
+        check(self.lib.cpx_set_stream(self.h, ct.c_void_p(s)), "cpx_set_stream")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.cpx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        check(self.lib.cpx_sync(self.h), "cpx_sync")
+
+    def reserve(self, max_planes: int, H: int, W: int, max_fovs: int = 0, max_label: int = 0):
+        check(self.lib.cpx_reserve(self.h, max_planes, H, W, max_fovs, max_label), "cpx_reserve")
+
+    # ---- raw buffers -----------------------------------------------------------------------
+    def empty_bytes(self, nbytes: int) -> torch.Tensor:
+        return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=self.torch_device)
+
+    # ---- a1 + a4 ---------------------------------------------------------------------------
+    def illum_correct(self, raw: torch.Tensor, illum: torch.Tensor | None, C: int,
+                      corr: torch.Tensor | None, stats: torch.Tensor):
+        """raw: uint16 [n_planes, H, W] (int16 view ok); illum: [C,H,W] f32/f64 or None."""
+        n, H, W = raw.shape[-3], raw.shape[-2], raw.shape[-1]
+        self._bind_stream()
+        check(self.lib.cpx_illum_correct(self.h, _ptr(raw), _ptr(illum), _illum_dtype(illum), C, n, H, W,
+                                         _ptr(corr), _ptr(stats)), "cpx_illum_correct")
+
+    # ---- a2 + a3 ---------------------------------------------------------------------------
+    def qc_rps(self, raw: torch.Tensor, illum: torch.Tensor | None, C: int, stats: torch.Tensor,
+               qc: torch.Tensor, powersum: torch.Tensor | None = None):
+        n, H, W = raw.shape[-3], raw.shape[-2], raw.shape[-1]
+        self._bind_stream()
+        check(self.lib.cpx_qc_rps(self.h, _ptr(raw), _ptr(illum), _illum_dtype(illum), C, n, H, W,
+                                  _ptr(stats), _ptr(powersum), _ptr(qc)), "cpx_qc_rps")
+
+    # ---- a5 ------------------------------------------------------------------------------
+    def zmax(self, src: torch.Tensor, out: torch.Tensor):
+        """src: uint16 [G, Z, ...] ; out: uint16 [G, ...]."""
+        G, Z = src.shape[0], src.shape[1]
+        N = src[0, 0].numel()
+        self._bind_stream()
+        check(self.lib.cpx_zmax_u16(self.h, _ptr(src), G, Z, N, _ptr(out)), "cpx_zmax_u16")
+
+    # ---- a7 ------------------------------------------------------------------------------
+    def objects(self, labels: torch.Tensor, max_label: int, box: int, lstats: torch.Tensor,
+                objects: torch.Tensor, hdr: torch.Tensor):
+        B, H, W = labels.shape
+        self._bind_stream()
+        check(self.lib.cpx_objects(self.h, _ptr(labels), B, H, W, max_label, box, _ptr(lstats),
+                                   _ptr(objects), _ptr(hdr)), "cpx_objects")
+
+    def crops(self, labels, corr, C, max_label, objects, hdr, box, max_crops, crops, crops8=None):
+        B, H, W = labels.shape
+        self._bind_stream()
+        check(self.lib.cpx_crops(self.h, _ptr(labels), _ptr(corr), B, C, H, W, max_label, _ptr(objects),
+                                 _ptr(hdr), box, max_crops, _ptr(crops), _ptr(crops8)), "cpx_crops")
+
+    # ---- a8 ------------------------------------------------------------------------------
+    def features(self, labels, corr, C, max_label, objects, hdr, feats):
+        B, H, W = labels.shape
+        self._bind_stream()
+        check(self.lib.cpx_features(self.h, _ptr(labels), _ptr(corr), B, C, H, W, max_label,
+                                    _ptr(objects), _ptr(hdr), _ptr(feats)), "cpx_features")
+
+
+def n_features(C: int) -> int:
+    return _lib.N_SHAPE + C * _lib.FEATURES_PER_CHANNEL
+
+
+def as_numpy(t: torch.Tensor, kind: str):
+    """View a raw byte tensor (device or host) as a numpy structured array of `kind`."""
+    import numpy as np
+    dt = _np_dtypes()[kind]
+    b = t.detach().cpu().numpy().view(np.uint8)
+    return b[: (b.size // dt.itemsize) * dt.itemsize].view(dt)

@@ -1,0 +1,111 @@
+// Context management and error plumbing for libcpx (the C ABI declared in include/cpx.h).
+#include "cpx_internal.h"
+#include <stdarg.h>
+#include <stdio.h>
+#include <new>
+
+static thread_local char g_err[1024] = {0};
+
+void cpx_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int cpx_hip_fail(hipError_t e, const char* what) {
+  cpx_set_error("HIP error %d (%s) in %s", (int)e, hipGetErrorString(e), what);
+  return e == hipErrorOutOfMemory ? CPX_ERR_OOM : CPX_ERR_HIP;
+}
+
+void* cpx_ws(cpx_ctx* ctx, int slot, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (ctx->ws_bytes[slot] >= bytes) return ctx->ws[slot];
+  if (ctx->ws[slot]) {
+    // the old buffer may still be in use by enqueued work
+    hipStreamSynchronize(ctx->stream);
+    hipFree(ctx->ws[slot]);
+    ctx->ws[slot] = nullptr;
+    ctx->ws_bytes[slot] = 0;
+  }
+  size_t want = bytes + bytes / 4;  // headroom so small growth does not re-allocate
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, want);
+  if (e != hipSuccess) {
+    cpx_hip_fail(e, "workspace hipMalloc");
+    return nullptr;
+  }
+  ctx->ws[slot] = p;
+  ctx->ws_bytes[slot] = want;
+  return p;
+}
+
+extern "C" {
+
+int cpx_abi_version(void) { return CPX_ABI_VERSION; }
+
+const char* cpx_last_error(void) { return g_err; }
+
+int cpx_init(int device, cpx_ctx** out) {
+  CPX_REQUIRE(out != nullptr, CPX_ERR_ARG, "cpx_init: out is NULL");
+  g_err[0] = 0;
+  int n = 0;
+  CPX_CHECK_HIP(hipGetDeviceCount(&n));
+  CPX_REQUIRE(device >= 0 && device < n, CPX_ERR_ARG, "cpx_init: device %d of %d", device, n);
+  CPX_CHECK_HIP(hipSetDevice(device));
+  cpx_ctx* c = new (std::nothrow) cpx_ctx();
+  CPX_REQUIRE(c != nullptr, CPX_ERR_OOM, "cpx_init: host allocation failed");
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return cpx_hip_fail(e, "hipStreamCreate");
+  }
+  c->stream = c->own_stream;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+  *out = c;
+  return CPX_OK;
+}
+
+void cpx_destroy(cpx_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  for (int i = 0; i < 8; ++i)
+    if (ctx->ws[i]) hipFree(ctx->ws[i]);
+  if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+}
+
+int cpx_set_stream(cpx_ctx* ctx, void* hip_stream) {
+  CPX_REQUIRE(ctx != nullptr, CPX_ERR_ARG, "cpx_set_stream: ctx is NULL");
+  // NULL selects the legacy default stream (torch's default stream handle is 0)
+  ctx->stream = (hipStream_t)hip_stream;
+  return CPX_OK;
+}
+
+int cpx_sync(cpx_ctx* ctx) {
+  CPX_REQUIRE(ctx != nullptr, CPX_ERR_ARG, "cpx_sync: ctx is NULL");
+  CPX_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  return CPX_OK;
+}
+
+}  // extern "C"
+
+extern "C" int cpx_reserve(cpx_ctx* ctx, int max_planes, int H, int W, int max_fovs,
+                           int max_label) {
+  CPX_REQUIRE(ctx != nullptr, CPX_ERR_ARG, "cpx_reserve: ctx is NULL");
+  CPX_REQUIRE(max_planes > 0 && H > 0 && W > 0 && max_fovs >= 0 && max_label >= 0, CPX_ERR_ARG,
+              "cpx_reserve: bad sizes");
+  // keep in sync with k_illum.hip (64 blocks/plane x 48-B partials) and k_qc.hip
+  if (!cpx_ws(ctx, WS_PARTIALS, (size_t)48 * 64 * max_planes)) return CPX_ERR_OOM;
+  const int K = std::max(std::min(H, W) / 8, 1);
+  const int nr = std::max(K - 2, 1);
+  if (!cpx_ws(ctx, WS_QC_ROWS, (size_t)16 * max_planes * H * K)) return CPX_ERR_OOM;
+  size_t ring = (size_t)8 * max_planes * K * nr;
+  ring = ((ring + 255) / 256) * 256 + (size_t)8 * max_planes + 256;
+  if (!cpx_ws(ctx, WS_QC_RINGS, ring)) return CPX_ERR_OOM;
+  if (!cpx_ws(ctx, WS_QC_MISC, (size_t)16 * (H + W) + 256)) return CPX_ERR_OOM;
+  return CPX_OK;
+}

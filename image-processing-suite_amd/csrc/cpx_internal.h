@@ -1,0 +1,84 @@
+// Internal helpers shared by the libcpx HIP translation units (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include <string>
+#include <algorithm>
+#include "../../include/cpx.h"
+
+struct cpx_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  // generic growable device workspaces (never shrunk; see cpx_reserve)
+  void* ws[8] = {nullptr};
+  size_t ws_bytes[8] = {0};
+  int n_cu = 256;
+  // QC FFT twiddle tables currently uploaded (WS_QC_MISC)
+  int qc_H = 0, qc_W = 0;
+  void* qc_tw = nullptr;
+};
+
+// workspace slots
+enum {
+  WS_PARTIALS = 0,   // illum per-block partials
+  WS_QC_ROWS = 1,    // row-pass spectrum [plane][H][R+1] complex f64
+  WS_QC_RINGS = 2,   // per-column ring partials
+  WS_QC_MISC = 3,    // FFT twiddles / plans
+  WS_MISC = 4,
+  WS_FEAT = 5,
+};
+
+void cpx_set_error(const char* fmt, ...);
+int cpx_hip_fail(hipError_t e, const char* what);
+// Ensure workspace slot has >= bytes; returns nullptr on failure (error already set).
+void* cpx_ws(cpx_ctx* ctx, int slot, size_t bytes);
+
+#define CPX_CHECK_HIP(expr)                                  \
+  do {                                                       \
+    hipError_t _e = (expr);                                  \
+    if (_e != hipSuccess) return cpx_hip_fail(_e, #expr);    \
+  } while (0)
+
+#define CPX_CHECK_LAUNCH(what)                                       \
+  do {                                                               \
+    hipError_t _e = hipGetLastError();                               \
+    if (_e != hipSuccess) return cpx_hip_fail(_e, what);             \
+  } while (0)
+
+#define CPX_REQUIRE(cond, code, ...)      \
+  do {                                    \
+    if (!(cond)) {                        \
+      cpx_set_error(__VA_ARGS__);         \
+      return (code);                      \
+    }                                     \
+  } while (0)
+
+static inline int cpx_div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// Wave-64 reductions (gfx950 wavefront = 64 lanes).
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    T o = __shfl_xor(v, off, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    T o = __shfl_xor(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}

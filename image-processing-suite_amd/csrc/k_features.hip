@@ -1,0 +1,382 @@
+// a8: per-object AreaShape / Intensity / Texture features (the CellProfiler measurement step that
+// Feature_extraction_opt.py:164-167 delegates to a docker image; definitions pinned to
+// scikit-image 0.18.3):
+//   AreaShape: regionprops area, perimeter (Benkrid-Crookes weights, 4-neighbour border),
+//              centroid, bbox, extent, equivalent diameter, inertia-tensor axes / eccentricity /
+//              orientation.
+//   Intensity (per channel, object pixels of the fp32 corrected plane): integrated, mean, std,
+//              min, max.
+//   Texture   (per channel, per angle 0/45/90/135 deg, distance 3): greycomatrix/greycoprops
+//              (contrast, dissimilarity, homogeneity, ASM, energy, correlation, 256 levels,
+//              symmetric=False) of the masked bbox crop quantised by scale_to_8bit
+//              (Cellpose_GPU_s3fs.py:34-43).
+// MI355X design: one workgroup per (object, channel) streams the object's bbox (L2-resident);
+// every GLCM property except ASM is linear in the co-occurrence counts, so it is accumulated
+// from exact integer pair sums; ASM = sum c_ij^2 / T^2 is accumulated without ever scanning the
+// 256x256 matrix: each LDS atomic increment returns the previous count c and contributes 2c+1.
+// Background pairs (0,0) dominate masked crops and are counted by ballot, not atomics.  All
+// sums are integers or fixed-order fp64, so results are bit-reproducible.
+#include "cpx_internal.h"
+#include <math.h>
+
+namespace {
+
+constexpr int kShapeThreads = 256;
+constexpr int kTexThreads = 512;
+constexpr int kTabWords = 32768;  // 128 KiB of LDS: 65536 x u16 counters, or 32768 x u32
+
+typedef __int128 i128;
+
+template <typename T, int NT>
+__device__ T block_sum(T v, T* scratch) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  T t = 0;
+  for (int w = 0; w < NT / 64; ++w) t += scratch[w];
+  return t;
+}
+template <typename T, int NT>
+__device__ T block_min(T v, T* scratch) {
+  v = wave_min(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  T t = scratch[0];
+  for (int w = 1; w < NT / 64; ++w) t = scratch[w] < t ? scratch[w] : t;
+  return t;
+}
+template <typename T, int NT>
+__device__ T block_max(T v, T* scratch) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  T t = scratch[0];
+  for (int w = 1; w < NT / 64; ++w) t = scratch[w] > t ? scratch[w] : t;
+  return t;
+}
+
+__device__ __forceinline__ bool in_obj(const int* lab, int H, int W, int r, int c, int L) {
+  return r >= 0 && r < H && c >= 0 && c < W && lab[(long long)r * W + c] == L;
+}
+__device__ __forceinline__ bool is_border(const int* lab, int H, int W, int r, int c, int L) {
+  return in_obj(lab, H, W, r, c, L) &&
+         !(in_obj(lab, H, W, r - 1, c, L) && in_obj(lab, H, W, r + 1, c, L) &&
+           in_obj(lab, H, W, r, c - 1, L) && in_obj(lab, H, W, r, c + 1, L));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Shape: one block per (object, fov).
+__global__ __launch_bounds__(kShapeThreads) void k_shape(const int* __restrict__ labels, int H,
+                                                         int W, int max_label, int F,
+                                                         const cpx_object* __restrict__ objects,
+                                                         const cpx_fov_objects* __restrict__ hdr,
+                                                         double* __restrict__ feats) {
+  const int k = blockIdx.x, fov = blockIdx.y;
+  if (k >= hdr[fov].n_objects) return;
+  const cpx_object o = objects[(long long)fov * max_label + k];
+  const int* lab = labels + (long long)fov * H * W;
+  const int L = o.label;
+  const int r0 = o.bbox[0], c0 = o.bbox[1], r1 = o.bbox[2], c1 = o.bbox[3];
+  const int bw = c1 - c0;
+  const long long nb = (long long)(r1 - r0) * bw;
+  long long n = 0, sr = 0, sc = 0, srr = 0, scc = 0, src = 0;
+  int n1 = 0, n2 = 0, n3 = 0;
+  for (long long p = threadIdx.x; p < nb; p += kShapeThreads) {
+    const int rr = (int)(p / bw), cc = (int)(p % bw);
+    const int r = r0 + rr, c = c0 + cc;
+    if (lab[(long long)r * W + c] != L) continue;
+    n += 1;
+    sr += rr;
+    sc += cc;
+    srr += (long long)rr * rr;
+    scc += (long long)cc * cc;
+    src += (long long)rr * cc;
+    if (!is_border(lab, H, W, r, c, L)) continue;
+    // skimage perimeter: code = 1 + 2 * (# 4-neighbour border px) + 10 * (# diagonal border px)
+    int code = 1;
+    code += 2 * (is_border(lab, H, W, r - 1, c, L) + is_border(lab, H, W, r + 1, c, L) +
+                 is_border(lab, H, W, r, c - 1, L) + is_border(lab, H, W, r, c + 1, L));
+    code += 10 * (is_border(lab, H, W, r - 1, c - 1, L) + is_border(lab, H, W, r - 1, c + 1, L) +
+                  is_border(lab, H, W, r + 1, c - 1, L) + is_border(lab, H, W, r + 1, c + 1, L));
+    if (code == 5 || code == 7 || code == 15 || code == 17 || code == 25 || code == 27) n1 += 1;
+    else if (code == 21 || code == 33) n2 += 1;
+    else if (code == 13 || code == 23) n3 += 1;
+  }
+  __shared__ long long s64[kShapeThreads / 64];
+  __shared__ int s32[kShapeThreads / 64];
+  n = block_sum<long long, kShapeThreads>(n, s64);
+  sr = block_sum<long long, kShapeThreads>(sr, s64);
+  sc = block_sum<long long, kShapeThreads>(sc, s64);
+  srr = block_sum<long long, kShapeThreads>(srr, s64);
+  scc = block_sum<long long, kShapeThreads>(scc, s64);
+  src = block_sum<long long, kShapeThreads>(src, s64);
+  n1 = block_sum<int, kShapeThreads>(n1, s32);
+  n2 = block_sum<int, kShapeThreads>(n2, s32);
+  n3 = block_sum<int, kShapeThreads>(n3, s32);
+  if (threadIdx.x != 0) return;
+  double* f = feats + ((long long)fov * max_label + k) * F;
+  const double SQ2 = 1.4142135623730951;
+  const double area = (double)n;
+  f[CPX_SHAPE_AREA] = area;
+  f[CPX_SHAPE_PERIMETER] = (double)n1 + (double)n2 * SQ2 + (double)n3 * ((1.0 + SQ2) / 2.0);
+  f[CPX_SHAPE_CENTER_Y] = o.centroid_r;
+  f[CPX_SHAPE_CENTER_X] = o.centroid_c;
+  const double bba = (double)nb;
+  f[CPX_SHAPE_BBOX_AREA] = bba;
+  f[CPX_SHAPE_EXTENT] = area / bba;
+  f[CPX_SHAPE_EQUIV_DIAMETER] = sqrt(4.0 * area / 3.14159265358979323846);
+  // exact central moments: n*mu20 = n*srr - sr^2 etc. (int128), T = [[mu02,-mu11],[-mu11,mu20]]/mu0
+  const i128 N = n;
+  const i128 m20n = N * srr - (i128)sr * sr;  // rows
+  const i128 m02n = N * scc - (i128)sc * sc;  // cols
+  const i128 m11n = N * src - (i128)sr * sc;
+  const double n2d = area * area;
+  const double a = (double)m02n / n2d;   // T[0,0] = mu02/mu0
+  const double b = -(double)m11n / n2d;  // T[0,1] = -mu11/mu0
+  const double c = (double)m20n / n2d;   // T[1,1] = mu20/mu0
+  // eigenvalues: l1 = larger via stable formula, l2 = det / l1 with exact det
+  const double hm = 0.5 * (a + c);
+  const double hd = 0.5 * (a - c);
+  const double rt = sqrt(hd * hd + b * b);
+  double l1 = hm + rt;
+  const i128 detn4 = m02n * m20n - m11n * m11n;  // det * n^4 (exact, >= 0)
+  double l2 = (l1 > 0.0) ? ((double)detn4 / (n2d * n2d)) / l1 : 0.0;
+  if (l1 < 0.0) l1 = 0.0;
+  if (l2 < 0.0) l2 = 0.0;
+  if (l2 > l1) l2 = l1;
+  f[CPX_SHAPE_MAJOR_AXIS] = 4.0 * sqrt(l1);
+  f[CPX_SHAPE_MINOR_AXIS] = 4.0 * sqrt(l2);
+  f[CPX_SHAPE_ECCENTRICITY] = (l1 == 0.0) ? 0.0 : sqrt(1.0 - l2 / l1);
+  double orient;
+  if (a - c == 0.0) orient = (b < 0.0) ? -3.14159265358979323846 / 4.0 : 3.14159265358979323846 / 4.0;
+  else orient = 0.5 * atan2(-2.0 * b, c - a);
+  f[CPX_SHAPE_ORIENTATION] = orient;
+  f[CPX_SHAPE_BBOX_MIN_Y] = r0;
+  f[CPX_SHAPE_BBOX_MIN_X] = c0;
+  f[CPX_SHAPE_BBOX_MAX_Y] = r1;
+  f[CPX_SHAPE_BBOX_MAX_X] = c1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Intensity + texture: one block per (object, channel, fov) with a 128 KiB LDS pair table.
+struct TexCtx {
+  const int* lab;
+  const float* img;
+  int W, L;
+  float mn, rng;
+  bool flat;
+};
+
+__device__ __forceinline__ int quant8(const TexCtx& t, int r, int c) {
+  const long long i = (long long)r * t.W + c;
+  const float v = t.img[i] * (t.lab[i] == t.L ? 1.0f : 0.0f);
+  if (t.flat) return 0;
+  float x = v - t.mn;  // scale_to_8bit, same fp32 operation order as numpy
+  x = 255.0f * x;
+  x = x / t.rng;
+  return (int)(unsigned char)(int)x;
+}
+
+template <bool PACKED>
+__device__ void glcm_angle(const TexCtx& t, int r0, int c0, int r1, int c1, int dr, int dc,
+                           unsigned int* tab, unsigned int* dh, long long* s64, double* out) {
+  // zero the table and the |i-j| histogram
+  for (int w = threadIdx.x; w < kTabWords; w += kTexThreads) tab[w] = 0u;
+  for (int w = threadIdx.x; w < 256; w += kTexThreads) dh[w] = 0u;
+  __syncthreads();
+  const int ra = r0, rb = r1 - dr;                       // dr >= 0
+  const int ca = dc >= 0 ? c0 : c0 - dc, cb = dc >= 0 ? c1 - dc : c1;
+  const int w = cb - ca;
+  const long long npairs = (rb > ra && w > 0) ? (long long)(rb - ra) * w : 0;
+  long long zero = 0, si = 0, sj = 0, sii = 0, sjj = 0, sij = 0, ssq = 0;
+  const int passes = PACKED ? 1 : 2;
+  for (int pass = 0; pass < passes; ++pass) {
+    if (pass == 1) {
+      __syncthreads();
+      for (int x = threadIdx.x; x < kTabWords; x += kTexThreads) tab[x] = 0u;
+      __syncthreads();
+    }
+    for (long long p = threadIdx.x; p < npairs; p += kTexThreads) {
+      const int r = ra + (int)(p / w), c = ca + (int)(p % w);
+      const int i = quant8(t, r, c), j = quant8(t, r + dr, c + dc);
+      const int key = (i << 8) | j;
+      if (pass == 0) {
+        si += i;
+        sj += j;
+        sii += i * i;
+        sjj += j * j;
+        sij += i * j;
+        if (key != 0) atomicAdd(&dh[abs(i - j)], 1u);
+      }
+      if (key == 0) {
+        if (pass == 0) zero += 1;
+        continue;
+      }
+      if (PACKED) {
+        const unsigned int sh = (key & 1) * 16;
+        const unsigned int old = atomicAdd(&tab[key >> 1], 1u << sh);
+        const long long c_old = (old >> sh) & 0xffffu;
+        ssq += 2 * c_old + 1;
+      } else {
+        if ((key >> 15) != pass) continue;
+        const unsigned int old = atomicAdd(&tab[key & 0x7fff], 1u);
+        ssq += 2 * (long long)old + 1;
+      }
+    }
+  }
+  zero = block_sum<long long, kTexThreads>(zero, s64);
+  si = block_sum<long long, kTexThreads>(si, s64);
+  sj = block_sum<long long, kTexThreads>(sj, s64);
+  sii = block_sum<long long, kTexThreads>(sii, s64);
+  sjj = block_sum<long long, kTexThreads>(sjj, s64);
+  sij = block_sum<long long, kTexThreads>(sij, s64);
+  ssq = block_sum<long long, kTexThreads>(ssq, s64);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const long long T = npairs;
+    double con = 0.0, dis = 0.0, hom = 0.0, asmv = 0.0, ene = 0.0, cor = 1.0;
+    if (T > 0) {
+      const double Td = (double)T;
+      long long cnum = 0, dnum = 0;
+      const long long d0 = (long long)dh[0] + zero;  // d = 0 includes the ballot-counted (0,0)
+      double hsum = 0.0;
+      for (int d = 0; d < 256; ++d) {
+        const long long cnt = (d == 0) ? d0 : (long long)dh[d];
+        cnum += cnt * d * d;
+        dnum += cnt * d;
+        hsum += (double)cnt * (1.0 / (1.0 + (double)(d * d)));
+      }
+      con = (double)cnum / Td;
+      dis = (double)dnum / Td;
+      hom = hsum / Td;
+      const long long ssq_all = ssq + zero * zero;
+      asmv = (double)ssq_all / (Td * Td);
+      ene = sqrt(asmv);
+      const i128 vi = (i128)T * sii - (i128)si * si;
+      const i128 vj = (i128)T * sjj - (i128)sj * sj;
+      const i128 cv = (i128)T * sij - (i128)si * sj;
+      const double std_i = sqrt((double)vi) / Td, std_j = sqrt((double)vj) / Td;
+      if (std_i < 1e-15 || std_j < 1e-15) cor = 1.0;
+      else cor = ((double)cv / (Td * Td)) / (std_i * std_j);
+    }
+    out[CPX_TEX_CONTRAST] = con;
+    out[CPX_TEX_DISSIMILARITY] = dis;
+    out[CPX_TEX_HOMOGENEITY] = hom;
+    out[CPX_TEX_ASM] = asmv;
+    out[CPX_TEX_ENERGY] = ene;
+    out[CPX_TEX_CORRELATION] = cor;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kTexThreads) void k_intensity_texture(
+    const int* __restrict__ labels, const float* __restrict__ corr, int C, int H, int W,
+    int max_label, int F, const cpx_object* __restrict__ objects,
+    const cpx_fov_objects* __restrict__ hdr, double* __restrict__ feats) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned int* tab = reinterpret_cast<unsigned int*>(smem);
+  unsigned int* dh = tab + kTabWords;
+  __shared__ long long s64[kTexThreads / 64];
+  __shared__ double sd[kTexThreads / 64];
+  __shared__ float sf[kTexThreads / 64];
+  const int fov = blockIdx.y;
+  const int n_items = hdr[fov].n_objects * C;
+  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+  const int k = item / C, ch = item % C;
+  const cpx_object o = objects[(long long)fov * max_label + k];
+  const long long N = (long long)H * W;
+  TexCtx t;
+  t.lab = labels + (long long)fov * N;
+  t.img = corr + ((long long)fov * C + ch) * N;
+  t.W = W;
+  t.L = o.label;
+  const int r0 = o.bbox[0], c0 = o.bbox[1], r1 = o.bbox[2], c1 = o.bbox[3];
+  const int bw = c1 - c0;
+  const long long nb = (long long)(r1 - r0) * bw;
+  // pass 1: object intensity stats + masked-crop min/max (scale_to_8bit range)
+  double s = 0.0, ss = 0.0;
+  float omin = INFINITY, omax = -INFINITY, mmin = INFINITY, mmax = -INFINITY;
+  long long n = 0;
+  for (long long p = threadIdx.x; p < nb; p += kTexThreads) {
+    const int r = r0 + (int)(p / bw), c = c0 + (int)(p % bw);
+    const long long i = (long long)r * W + c;
+    const float v = t.img[i];
+    const bool in = t.lab[i] == t.L;
+    const float m = v * (in ? 1.0f : 0.0f);
+    mmin = fminf(mmin, m);
+    mmax = fmaxf(mmax, m);
+    if (in) {
+      n += 1;
+      s += (double)v;
+      ss += (double)v * (double)v;
+      omin = fminf(omin, v);
+      omax = fmaxf(omax, v);
+    }
+  }
+  n = block_sum<long long, kTexThreads>(n, s64);
+  s = block_sum<double, kTexThreads>(s, sd);
+  ss = block_sum<double, kTexThreads>(ss, sd);
+  omin = block_min<float, kTexThreads>(omin, sf);
+  omax = block_max<float, kTexThreads>(omax, sf);
+  mmin = block_min<float, kTexThreads>(mmin, sf);
+  mmax = block_max<float, kTexThreads>(mmax, sf);
+  double* f = feats + ((long long)fov * max_label + k) * F + CPX_N_SHAPE +
+              (long long)ch * CPX_FEATURES_PER_CHANNEL;
+  if (threadIdx.x == 0) {
+    const double mean = n ? s / (double)n : 0.0;
+    double var = n ? (ss - s * mean) / (double)n : 0.0;
+    if (var < 0.0) var = 0.0;
+    f[CPX_INT_INTEGRATED] = s;
+    f[CPX_INT_MEAN] = mean;
+    f[CPX_INT_STD] = sqrt(var);
+    f[CPX_INT_MIN] = (double)omin;
+    f[CPX_INT_MAX] = (double)omax;
+  }
+  t.mn = mmin;
+  t.rng = mmax - mmin;
+  t.flat = !(mmax != mmin);
+  // texture: offsets (dr, dc) = (round(sin a * 3), round(cos a * 3)) for a = 0, 45, 90, 135 deg
+  const int DR[4] = {0, 2, 3, 2}, DC[4] = {3, 2, 0, -2};
+  const bool packed = nb <= 65535;
+  for (int a = 0; a < CPX_N_ANGLES; ++a) {
+    double* out = f + CPX_N_INT + a * CPX_N_TEX_PROPS;
+    if (packed) glcm_angle<true>(t, r0, c0, r1, c1, DR[a], DC[a], tab, dh, s64, out);
+    else glcm_angle<false>(t, r0, c0, r1, c1, DR[a], DC[a], tab, dh, s64, out);
+  }
+  __syncthreads();
+  }  // item loop
+}
+
+}  // namespace
+
+extern "C" int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B,
+                            int C, int H, int W, int max_label, const cpx_object* objects_dev,
+                            const cpx_fov_objects* hdr_dev, double* feats_dev) {
+  CPX_REQUIRE(ctx && labels_dev && corr_dev && objects_dev && hdr_dev && feats_dev, CPX_ERR_ARG,
+              "cpx_features: null argument");
+  CPX_REQUIRE(B > 0 && B <= 65535 && C > 0 && C <= 65535 && H > 0 && W > 0 && max_label > 0,
+              CPX_ERR_ARG, "cpx_features: bad sizes");
+  const int F = CPX_N_SHAPE + C * CPX_FEATURES_PER_CHANNEL;
+  hipLaunchKernelGGL(k_shape, dim3(max_label, B), dim3(kShapeThreads), 0, ctx->stream,
+                     (const int*)labels_dev, H, W, max_label, F, objects_dev, hdr_dev, feats_dev);
+  CPX_CHECK_LAUNCH("k_shape");
+  static bool attr = false;
+  const size_t lds = sizeof(unsigned int) * (kTabWords + 256);
+  if (!attr) {
+    CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_intensity_texture,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  const int per_fov = std::max(1, std::min(max_label * C, (ctx->n_cu * 2 + B - 1) / B));
+  hipLaunchKernelGGL(k_intensity_texture, dim3(per_fov, B), dim3(kTexThreads), lds,
+                     ctx->stream, (const int*)labels_dev, corr_dev, C, H, W, max_label, F,
+                     objects_dev, hdr_dev, feats_dev);
+  CPX_CHECK_LAUNCH("k_intensity_texture");
+  return CPX_OK;
+}

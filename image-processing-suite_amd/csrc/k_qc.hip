@@ -1,0 +1,475 @@
+// a2 + a3: ImageQuality_PowerLogLogSlope — radial power spectrum slope.
+//
+// Reference (Illumination_QC_mult.py:31-70, rps; :104-116, linregress):
+//   radii2 = i^2 + j^2 folded with flipud/fliplr  ->  fi = min(i, H-1-i), fj = min(j, W-1-j)
+//   img /= median(|img - mean|) (if ptp > 0);  power = |fft2(img - mean)|^2
+//   radii = floor(sqrt(fi^2 + fj^2)) + 1 ; labels = 2 .. floor(min(H,W)/8) - 1
+//   powersum[R] = ndimage.sum(power, radii, R);  slope = linregress(log R, log powersum)[valid]
+// MI355X restatement:
+//   * the median normalisation multiplies every power by the same constant, so the log-log slope
+//     and the (power > 0) validity test are invariant to it — it is skipped (edge cases handled:
+//     ptp == 0, non-finite pixels, median == 0 -> slope 0.0 as in the reference);
+//   * only rings <= R_max = floor(min/8)-1 are binned, so only column frequencies 0..R_max of each
+//     row transform are kept (real-input pair trick: two rows per complex FFT), then a full
+//     column FFT over those R_max+1 columns; positions with j > W/2 are read from the conjugate
+//     symmetric partner X[(H-i)%H, W-j];
+//   * fp64 mixed-radix Stockham FFTs in LDS (radices 2,3,4,5,7,8,11,13), fp64 quotient
+//     recomputed from raw/illum (bit-identical to the reference's fp64 input);
+//   * ring sums are fixed-order (one lane per ring per column, then a fixed-order column sum),
+//     the slope is computed on device exactly as scipy.stats.linregress (np.cov, bias=1).
+#include "cpx_internal.h"
+#include <math.h>
+#include <vector>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxN = 4096;
+constexpr int kMaxStages = 12;
+
+struct Plan {
+  int n;
+  int nst;
+  int radix[kMaxStages];
+};
+
+struct cplx {
+  double x, y;
+};
+__device__ __forceinline__ cplx cadd(cplx a, cplx b) { return {a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ cplx csub(cplx a, cplx b) { return {a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ cplx cmul(cplx a, cplx b) {
+  return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+}
+__device__ __forceinline__ cplx mul_negi(cplx a) { return {a.y, -a.x}; }  // a * (-i)
+
+// In-place R-point forward DFT (exp(-2 pi i / R) convention) of v[0..R-1].
+// tw = W_N table, step = N / R so that W_R^m = tw[m * step].
+template <int R>
+__device__ __forceinline__ void dft(cplx* v, const cplx* __restrict__ tw, int step) {
+  if (R == 2) {
+    cplx a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+  } else if (R == 4) {
+    cplx t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+    cplx t2 = cadd(v[1], v[3]), t3 = mul_negi(csub(v[1], v[3]));
+    v[0] = cadd(t0, t2);
+    v[2] = csub(t0, t2);
+    v[1] = cadd(t1, t3);
+    v[3] = csub(t1, t3);
+  } else if (R == 8) {
+    cplx e[4] = {v[0], v[2], v[4], v[6]};
+    cplx o[4] = {v[1], v[3], v[5], v[7]};
+    dft<4>(e, tw, 0);
+    dft<4>(o, tw, 0);
+    const double s = 0.70710678118654752440;  // 1/sqrt(2)
+    cplx w1 = {s, -s}, w3 = {-s, -s};
+    cplx o1 = cmul(o[1], w1), o2 = mul_negi(o[2]), o3 = cmul(o[3], w3);
+    v[0] = cadd(e[0], o[0]);
+    v[4] = csub(e[0], o[0]);
+    v[1] = cadd(e[1], o1);
+    v[5] = csub(e[1], o1);
+    v[2] = cadd(e[2], o2);
+    v[6] = csub(e[2], o2);
+    v[3] = cadd(e[3], o3);
+    v[7] = csub(e[3], o3);
+  } else {
+    cplx out[R];
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      cplx acc = v[0];
+#pragma unroll
+      for (int r = 1; r < R; ++r) acc = cadd(acc, cmul(v[r], tw[((r * m) % R) * step]));
+      out[m] = acc;
+    }
+#pragma unroll
+    for (int m = 0; m < R; ++m) v[m] = out[m];
+  }
+}
+
+template <int R>
+__device__ __forceinline__ void stockham_stage(const cplx* __restrict__ in, cplx* __restrict__ out,
+                                               const cplx* __restrict__ tw, int N, int Ns) {
+  const int nb = N / R;
+  const int tstep = N / (Ns * R);
+  for (int j = threadIdx.x; j < nb; j += blockDim.x) {
+    const int k = j % Ns;
+    cplx v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = in[j + r * nb];
+    if (Ns > 1) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[k * r * tstep]);
+    }
+    dft<R>(v, tw, N / R);
+    const int d = (j / Ns) * Ns * R + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) out[d + r * Ns] = v[r];
+  }
+}
+
+// Runs the planned FFT on a (in LDS), ping-ponging with b; returns the buffer holding the result.
+__device__ cplx* fft_lds(cplx* a, cplx* b, const cplx* __restrict__ tw, const Plan& p) {
+  int Ns = 1;
+  for (int s = 0; s < p.nst; ++s) {
+    const int R = p.radix[s];
+    switch (R) {
+      case 2: stockham_stage<2>(a, b, tw, p.n, Ns); break;
+      case 3: stockham_stage<3>(a, b, tw, p.n, Ns); break;
+      case 4: stockham_stage<4>(a, b, tw, p.n, Ns); break;
+      case 5: stockham_stage<5>(a, b, tw, p.n, Ns); break;
+      case 7: stockham_stage<7>(a, b, tw, p.n, Ns); break;
+      case 8: stockham_stage<8>(a, b, tw, p.n, Ns); break;
+      case 11: stockham_stage<11>(a, b, tw, p.n, Ns); break;
+      case 13: stockham_stage<13>(a, b, tw, p.n, Ns); break;
+      default: break;
+    }
+    Ns *= R;
+    __syncthreads();
+    cplx* t = a;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+struct QcAux {
+  unsigned long long eq_count;  // # pixels with q == mean (median(|q-mean|) == 0 test)
+};
+
+template <int ILLUM>
+__device__ __forceinline__ double qval(const unsigned short* rp, const void* il, long long i) {
+  double r = (double)rp[i];
+  if (ILLUM == 1) return r / (double)static_cast<const float*>(il)[i];
+  if (ILLUM == 2) return r / static_cast<const double*>(il)[i];
+  return r;
+}
+
+// Row pass: one block per (row pair, plane).  rowspec[plane][row][k], k < KC, complex f64.
+template <int ILLUM>
+__global__ __launch_bounds__(kThreads) void k_qc_rows(
+    const unsigned short* __restrict__ raw, const void* __restrict__ illum, int C, int H, int W,
+    const cpx_plane_stats* __restrict__ stats, const cplx* __restrict__ twW, Plan pw, int KC,
+    cplx* __restrict__ rowspec, QcAux* __restrict__ aux) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  cplx* a = reinterpret_cast<cplx*>(smem);
+  cplx* b = a + W;
+  const int plane = blockIdx.y;
+  const int ch = plane % C;
+  const int r0 = 2 * blockIdx.x, r1 = r0 + 1;
+  const long long N = (long long)H * W;
+  const unsigned short* rp = raw + (long long)plane * N;
+  const void* il = nullptr;
+  if (ILLUM == 1) il = static_cast<const float*>(illum) + (long long)ch * N;
+  if (ILLUM == 2) il = static_cast<const double*>(illum) + (long long)ch * N;
+  const cpx_plane_stats st = stats[plane];
+  const double mean = st.sum_q / (double)st.n;
+  unsigned long long eq = 0;
+  for (int c = threadIdx.x; c < W; c += kThreads) {
+    double qa = qval<ILLUM>(rp, il, (long long)r0 * W + c);
+    double qb = r1 < H ? qval<ILLUM>(rp, il, (long long)r1 * W + c) : mean;
+    eq += (qa == mean) + (r1 < H && qb == mean);
+    a[c] = cplx{qa - mean, qb - mean};
+  }
+  // count of exact-mean pixels (integer, order independent)
+  eq = wave_sum(eq);
+  if ((threadIdx.x & 63) == 0 && eq) atomicAdd(&aux[plane].eq_count, eq);
+  __syncthreads();
+  cplx* z = fft_lds(a, b, twW, pw);
+  // Unpack the two real transforms for k < KC:
+  //   Xa[k] = (Z[k] + conj(Z[-k])) / 2 ;  Xb[k] = (Z[k] - conj(Z[-k])) / (2i)
+  cplx* outa = rowspec + ((long long)plane * H + r0) * KC;
+  for (int k = threadIdx.x; k < KC; k += kThreads) {
+    cplx zk = z[k];
+    cplx zn = z[k == 0 ? 0 : W - k];
+    cplx xa = {0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)};
+    // (zk - conj(zn)) / (2i) = -i/2 * (zk - conj(zn))
+    cplx dlt = {zk.x - zn.x, zk.y + zn.y};
+    cplx xb = {0.5 * dlt.y, -0.5 * dlt.x};
+    outa[k] = xa;
+    if (r1 < H) outa[KC + k] = xb;
+  }
+}
+
+__device__ __forceinline__ int isqrt_ll(long long v) {
+  if (v <= 0) return 0;
+  long long s = (long long)sqrt((double)v);
+  while (s * s > v) --s;
+  while ((s + 1) * (s + 1) <= v) ++s;
+  return (int)s;
+}
+
+// smallest f >= 0 with f*f >= v
+__device__ __forceinline__ int ceil_sqrt_ll(long long v) {
+  if (v <= 0) return 0;
+  int s = isqrt_ll(v);
+  return ((long long)s * s == v) ? s : s + 1;
+}
+
+// Sum of p[row(i)] over rows i whose folded index fi gives radius R for the given fj.
+// row(i) = i (direct) or (H - i) % H (mirrored partner).
+__device__ __forceinline__ double ring_rows(const double* __restrict__ p, int H, int R, int fj,
+                                            bool mirrored) {
+  const long long fj2 = (long long)fj * fj;
+  const long long lo2 = (long long)(R - 1) * (R - 1) - fj2;
+  const long long hi2 = (long long)R * R - fj2;  // fi^2 < hi2
+  if (hi2 <= 0) return 0.0;
+  int lo = ceil_sqrt_ll(lo2);
+  int hi = isqrt_ll(hi2 - 1);
+  const int fmax = (H - 1) / 2;
+  if (hi > fmax) hi = fmax;
+  double s = 0.0;
+  for (int fi = lo; fi <= hi; ++fi) {
+    const int i0 = fi, i1 = H - 1 - fi;
+    const int s0 = mirrored ? (H - i0) % H : i0;
+    s += p[s0];
+    if (i1 != i0) {
+      const int s1 = mirrored ? (H - i1) % H : i1;
+      s += p[s1];
+    }
+  }
+  return s;
+}
+
+// Column pass: one block per (column j < KC, plane).  Writes ringpart[plane][j][ring].
+__global__ __launch_bounds__(kThreads) void k_qc_cols(const cplx* __restrict__ rowspec, int H,
+                                                      int W, int KC, const cplx* __restrict__ twH,
+                                                      Plan ph, int n_rings,
+                                                      double* __restrict__ ringpart) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  cplx* a = reinterpret_cast<cplx*>(smem);
+  cplx* b = a + H;
+  const int j = blockIdx.x;
+  const int plane = blockIdx.y;
+  const cplx* src = rowspec + (long long)plane * H * KC + j;
+  for (int r = threadIdx.x; r < H; r += kThreads) a[r] = src[(long long)r * KC];
+  __syncthreads();
+  cplx* x = fft_lds(a, b, twH, ph);
+  // power in place (as doubles in the other buffer)
+  double* pw = reinterpret_cast<double*>(x == a ? b : a);
+  for (int r = threadIdx.x; r < H; r += kThreads) {
+    cplx v = x[r];
+    pw[r] = v.x * v.x + v.y * v.y;
+  }
+  __syncthreads();
+  double* out = ringpart + ((long long)plane * KC + j) * n_rings;
+  for (int t = threadIdx.x; t < n_rings; t += kThreads) {
+    const int R = t + 2;
+    double s = 0.0;
+    // direct positions (i, j): fj = min(j, W-1-j)
+    s += ring_rows(pw, H, R, min(j, W - 1 - j), false);
+    // mirrored positions (i, W-j), j >= 1: power = |X[(H-i)%H, j]|^2, fj = min(W-j, j-1)
+    if (j >= 1) s += ring_rows(pw, H, R, min(W - j, j - 1), true);
+    out[t] = s;
+  }
+}
+
+// Final: per plane, fixed-order column sum per ring, then linregress on (log R, log P).
+__global__ __launch_bounds__(kThreads) void k_qc_slope(const double* __restrict__ ringpart, int KC,
+                                                       int n_rings,
+                                                       const cpx_plane_stats* __restrict__ stats,
+                                                       const QcAux* __restrict__ aux,
+                                                       double* __restrict__ powersum,
+                                                       cpx_qc_result* __restrict__ qc) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* ps = reinterpret_cast<double*>(smem);  // [n_rings]
+  __shared__ double red[4][kThreads / 64];
+  __shared__ int redi[kThreads / 64];
+  const int plane = blockIdx.x;
+  const cpx_plane_stats st = stats[plane];
+  // reference edge cases -> no valid rings (slope 0.0):
+  //   NaN/inf pixels: mean is NaN/inf so img - mean is all-NaN;  ptp == 0: constant image;
+  //   median(|img - mean|) == 0 (> half the pixels equal the mean): img / 0 -> NaN/inf.
+  const bool nonfinite = st.has_nan || st.has_inf;
+  const bool mad_zero = aux[plane].eq_count >= (unsigned long long)(st.n / 2 + 1);
+  const bool dead = nonfinite || !(st.max_q > st.min_q) || mad_zero;
+  const bool nan_out = nonfinite || (mad_zero && st.max_q > st.min_q);
+  const double* src = ringpart + (long long)plane * KC * n_rings;
+  for (int t = threadIdx.x; t < n_rings; t += kThreads) {
+    double s = 0.0;
+    for (int j = 0; j < KC; ++j) s += src[(long long)j * n_rings + t];
+    if (dead) s = nan_out ? NAN : 0.0;
+    ps[t] = s;
+    if (powersum) powersum[(long long)plane * n_rings + t] = s;
+  }
+  __syncthreads();
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // pass 1: count valid, sum x, sum y
+  double sx = 0.0, sy = 0.0;
+  int nv = 0;
+  for (int t = threadIdx.x; t < n_rings; t += kThreads) {
+    if (ps[t] > 0.0) {
+      nv += 1;
+      sx += log((double)(t + 2));
+      sy += log(ps[t]);
+    }
+  }
+  sx = wave_sum(sx);
+  sy = wave_sum(sy);
+  nv = wave_sum(nv);
+  if (lane == 0) {
+    red[0][wid] = sx;
+    red[1][wid] = sy;
+    redi[wid] = nv;
+  }
+  __syncthreads();
+  double SX = 0.0, SY = 0.0;
+  int NV = 0;
+  for (int w = 0; w < kThreads / 64; ++w) {
+    SX += red[0][w];
+    SY += red[1][w];
+    NV += redi[w];
+  }
+  __syncthreads();
+  const double xm = NV ? SX / NV : 0.0, ym = NV ? SY / NV : 0.0;
+  double sxx = 0.0, sxy = 0.0;
+  for (int t = threadIdx.x; t < n_rings; t += kThreads) {
+    if (ps[t] > 0.0) {
+      const double dx = log((double)(t + 2)) - xm, dy = log(ps[t]) - ym;
+      sxx += dx * dx;
+      sxy += dx * dy;
+    }
+  }
+  sxx = wave_sum(sxx);
+  sxy = wave_sum(sxy);
+  if (lane == 0) {
+    red[2][wid] = sxx;
+    red[3][wid] = sxy;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double SXX = 0.0, SXY = 0.0;
+    for (int w = 0; w < kThreads / 64; ++w) {
+      SXX += red[2][w];
+      SXY += red[3][w];
+    }
+    cpx_qc_result r;
+    r.n_valid = NV;
+    r.n_rings = n_rings;
+    // np.cov(bias=1): ssxm = SXX/n, ssxym = SXY/n ; slope = ssxym / ssxm
+    r.slope = (NV > 2) ? (SXY / NV) / (SXX / NV) : 0.0;
+    // min(H,W) < 24: rps returns the list fallback [2],[0],[0] and `powersum > 0` raises
+    // TypeError inside calculate_qc_metrics -> NaN (Illumination_QC_mult.py:70, :115-116)
+    if (n_rings == 0) r.slope = NAN;
+    r.pct_max = st.pct_max;
+    qc[plane] = r;
+  }
+}
+
+bool make_plan(int n, Plan& p) {
+  if (n < 1 || n > kMaxN) return false;
+  p.n = n;
+  p.nst = 0;
+  int m = n;
+  const int order[] = {8, 4, 2, 13, 11, 7, 5, 3};
+  for (int r : order) {
+    while (m % r == 0) {
+      if (r == 2 && (m % 4 == 0)) break;  // prefer radix 4/8
+      if (p.nst >= kMaxStages) return false;
+      p.radix[p.nst++] = r;
+      m /= r;
+    }
+  }
+  // leftover powers of two handled above; any other factor is unsupported
+  while (m % 2 == 0 && p.nst < kMaxStages) {
+    p.radix[p.nst++] = 2;
+    m /= 2;
+  }
+  return m == 1;
+}
+
+void fill_twiddles(int n, std::vector<double>& t) {
+  t.resize(2 * (size_t)n);
+  for (int k = 0; k < n; ++k) {
+    long double ang = -2.0L * 3.14159265358979323846264338327950288L * (long double)k / n;
+    t[2 * k] = (double)cosl(ang);
+    t[2 * k + 1] = (double)sinl(ang);
+  }
+}
+
+}  // namespace
+
+extern "C" int cpx_qc_rps(cpx_ctx* ctx, const uint16_t* raw_dev, const void* illum_dev,
+                          int illum_dtype, int C, int n_planes, int H, int W,
+                          const cpx_plane_stats* stats_dev, double* powersum_dev,
+                          cpx_qc_result* qc_dev) {
+  CPX_REQUIRE(ctx && raw_dev && stats_dev && qc_dev, CPX_ERR_ARG, "cpx_qc_rps: null argument");
+  CPX_REQUIRE(C > 0 && n_planes > 0 && n_planes <= 65535 && H > 0 && W > 0, CPX_ERR_ARG,
+              "cpx_qc_rps: bad sizes");
+  CPX_REQUIRE(illum_dtype == CPX_DTYPE_NONE || illum_dev != nullptr, CPX_ERR_ARG,
+              "cpx_qc_rps: illum dtype %d without data", illum_dtype);
+  const int K = std::min(H, W) / 8;  // floor(min(H,W)/8.0)
+  const int n_rings = std::max(0, K - 2);
+  if (n_rings == 0) {
+    // labels empty -> rps returns [2],[0],[0] -> 1 valid ring < 3 -> slope 0.0
+    // Still need pct_max: a tiny kernel-free path via the generic slope kernel with no rings.
+  }
+  Plan pw, ph;
+  CPX_REQUIRE(make_plan(W, pw) && make_plan(H, ph), CPX_ERR_SHAPE,
+              "cpx_qc_rps: FFT size %dx%d unsupported (radices 2,3,5,7,11,13, <= %d)", H, W, kMaxN);
+  const int KC = std::max(K, 1);  // columns 0..K-1 (= R_max + 1)
+  // workspaces
+  const size_t tw_bytes = sizeof(double) * 2 * ((size_t)H + W);
+  void* misc = cpx_ws(ctx, WS_QC_MISC, tw_bytes + 256);
+  if (!misc) return CPX_ERR_OOM;
+  double* twH = (double*)misc;
+  double* twW = twH + 2 * (size_t)H;
+  if (ctx->qc_H != H || ctx->qc_W != W || ctx->qc_tw != misc) {
+    std::vector<double> th, tw;
+    fill_twiddles(H, th);
+    fill_twiddles(W, tw);
+    CPX_CHECK_HIP(hipMemcpyAsync(twH, th.data(), th.size() * sizeof(double), hipMemcpyHostToDevice,
+                                 ctx->stream));
+    CPX_CHECK_HIP(hipMemcpyAsync(twW, tw.data(), tw.size() * sizeof(double), hipMemcpyHostToDevice,
+                                 ctx->stream));
+    CPX_CHECK_HIP(hipStreamSynchronize(ctx->stream));  // host vectors go out of scope
+    ctx->qc_H = H;
+    ctx->qc_W = W;
+    ctx->qc_tw = misc;
+  }
+  const size_t rows_bytes = sizeof(cplx) * (size_t)n_planes * H * KC;
+  const size_t ring_bytes = sizeof(double) * (size_t)n_planes * KC * std::max(n_rings, 1);
+  const size_t aux_bytes = sizeof(QcAux) * (size_t)n_planes;
+  cplx* rowspec = (cplx*)cpx_ws(ctx, WS_QC_ROWS, rows_bytes);
+  if (!rowspec) return CPX_ERR_OOM;
+  unsigned char* rb = (unsigned char*)cpx_ws(ctx, WS_QC_RINGS, ring_bytes + aux_bytes + 256);
+  if (!rb) return CPX_ERR_OOM;
+  double* ringpart = (double*)rb;
+  QcAux* aux = (QcAux*)(rb + ((ring_bytes + 255) / 256) * 256);
+  CPX_CHECK_HIP(hipMemsetAsync(aux, 0, aux_bytes, ctx->stream));
+  if (n_rings > 0) {
+    static bool attrs = false;
+    if (!attrs) {
+      const int lds_max = 160 * 1024;
+      hipFuncSetAttribute((const void*)k_qc_rows<0>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+      hipFuncSetAttribute((const void*)k_qc_rows<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+      hipFuncSetAttribute((const void*)k_qc_rows<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+      hipFuncSetAttribute((const void*)k_qc_cols, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+      attrs = true;
+    }
+    const size_t sh_rows = 2 * sizeof(cplx) * (size_t)W;
+    dim3 grow((H + 1) / 2, n_planes);
+    const void* il = illum_dtype == CPX_DTYPE_NONE ? nullptr : illum_dev;
+    if (illum_dtype == CPX_DTYPE_F32)
+      hipLaunchKernelGGL(k_qc_rows<1>, grow, dim3(kThreads), sh_rows, ctx->stream, raw_dev, il, C,
+                         H, W, stats_dev, (const cplx*)twW, pw, KC, rowspec, aux);
+    else if (illum_dtype == CPX_DTYPE_F64)
+      hipLaunchKernelGGL(k_qc_rows<2>, grow, dim3(kThreads), sh_rows, ctx->stream, raw_dev, il, C,
+                         H, W, stats_dev, (const cplx*)twW, pw, KC, rowspec, aux);
+    else
+      hipLaunchKernelGGL(k_qc_rows<0>, grow, dim3(kThreads), sh_rows, ctx->stream, raw_dev, il, C,
+                         H, W, stats_dev, (const cplx*)twW, pw, KC, rowspec, aux);
+    CPX_CHECK_LAUNCH("k_qc_rows");
+    const size_t sh_cols = 2 * sizeof(cplx) * (size_t)H;
+    hipLaunchKernelGGL(k_qc_cols, dim3(KC, n_planes), dim3(kThreads), sh_cols, ctx->stream,
+                       (const cplx*)rowspec, H, W, KC, (const cplx*)twH, ph, n_rings, ringpart);
+    CPX_CHECK_LAUNCH("k_qc_cols");
+  }
+  hipLaunchKernelGGL(k_qc_slope, dim3(n_planes), dim3(kThreads),
+                     sizeof(double) * (size_t)std::max(n_rings, 1), ctx->stream,
+                     (const double*)ringpart, KC, n_rings, stats_dev, (const QcAux*)aux,
+                     powersum_dev, qc_dev);
+  CPX_CHECK_LAUNCH("k_qc_slope");
+  return CPX_OK;
+}

@@ -1,0 +1,211 @@
+/*
+ * cpx.h — C ABI of the MI355X-native per-field-of-view (FOV) cell-painting hot path.
+ *
+ * This is the drop-in boundary: a plain C ABI (pointers, sizes, int error codes; no torch or
+ * HIP types in any signature) over the hand-written gfx950 HIP kernels in libcpx.so.  The
+ * reference (Saguaro-Biosciences/image-processing-suite) has no FFI of its own — its per-FOV
+ * workers are Python functions — so each entry point below names the reference function whose
+ * per-FOV arithmetic it replaces (file:line in the reference checkout).  The Python host package
+ * (`image-processing-suite_amd/cpx`) mirrors those Python signatures on top of this ABI; see
+ * INTEGRATION.md for the ctypes binding a maintainer of the reference would add.
+ *
+ * Conventions
+ *   - Every compute entry point only ENQUEUES work on the context's HIP stream (cpx_set_stream)
+ *     and returns; device pointers ("dev") must stay valid until cpx_sync() or a later sync on
+ *     that stream.  Host pointers ("host") are read/written synchronously.
+ *   - Return value 0 = CPX_OK; otherwise a CPX_ERR_* code and a message from cpx_last_error()
+ *     (thread-local).  Nothing aborts the process.
+ *   - Images are planar: a plane is H*W contiguous pixels, row-major.  A batch of FOVs is
+ *     [fov][channel][H][W].  Label images are int32 [fov][H][W], 0 = background.
+ *   - One context per GPU per host process (single-threaded use).
+ */
+#ifndef CPX_H
+#define CPX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CPX_ABI_VERSION 1
+
+#define CPX_OK 0
+#define CPX_ERR_ARG 1     /* bad argument (null pointer, bad size)                    */
+#define CPX_ERR_HIP 2     /* HIP runtime error                                        */
+#define CPX_ERR_SHAPE 3   /* unsupported shape (e.g. FFT length with a prime > 13)    */
+#define CPX_ERR_OOM 4     /* device allocation failed                                 */
+#define CPX_ERR_STATE 5   /* context misuse                                           */
+
+#define CPX_DTYPE_NONE 0  /* no flat-field: raw planes are used uncorrected           */
+#define CPX_DTYPE_F32 1
+#define CPX_DTYPE_F64 2
+
+typedef struct cpx_ctx cpx_ctx;
+
+/* Per-plane statistics of the flat-field-corrected plane, all computed on the fp64 quotient
+ * raw/illum exactly as Illumination_QC_mult.py:145-150 does (uint16 -> float64 / illum).   */
+typedef struct cpx_plane_stats {
+  double max_q;       /* np.max of the quotient (NaN if any NaN)                          */
+  double min_q;       /* np.min of the quotient                                           */
+  double sum_q;       /* fp64 sum (fixed-order), used for the FFT mean removal            */
+  double pct_max;     /* ImageQuality_PercentMaximal = 100*count_max/n (:73-95)           */
+  int64_t count_max;  /* # pixels equal to max_q                                          */
+  int64_t n;          /* pixel count                                                      */
+  int32_t has_nan;    /* any NaN                                                          */
+  int32_t has_inf;    /* any +-inf                                                        */
+  int64_t _pad;
+} cpx_plane_stats;    /* 64 bytes */
+
+/* Per-plane QC result (Illumination_QC_mult.py:98-125). */
+typedef struct cpx_qc_result {
+  double slope;       /* ImageQuality_PowerLogLogSlope (0.0 when <= 2 valid rings)        */
+  double pct_max;     /* ImageQuality_PercentMaximal                                      */
+  int32_t n_valid;    /* rings with powersum > 0                                          */
+  int32_t n_rings;    /* len(labels) = max(0, floor(min(H,W)/8) - 2)                      */
+} cpx_qc_result;      /* 24 bytes */
+
+/* Raw per-label accumulators (device), index = label value, 0..max_label.  Exact integers. */
+typedef struct cpx_label_stats {
+  int64_t area, sum_r, sum_c, sum_rr, sum_cc, sum_rc;
+  int32_t rmin, rmax, cmin, cmax; /* inclusive; rmin = INT32_MAX when the label is absent    */
+} cpx_label_stats;    /* 64 bytes */
+
+/* One object in ascending-label order (skimage regionprops order; Cellpose_GPU_s3fs.py:149-170). */
+typedef struct cpx_object {
+  int32_t label;      /* label value                                                      */
+  int32_t area;       /* pixel count                                                      */
+  int32_t bbox[4];    /* min_row, min_col, max_row (excl), max_col (excl) = regionprops.bbox */
+  double centroid_r;  /* regionprops.centroid (float64 mean of pixel coords)              */
+  double centroid_c;
+  int32_t yc, xc;     /* map(int, centroid): truncation (:160)                            */
+  int32_t kept;       /* 1 if the box x box crop lies inside the image (:162)             */
+  int32_t cell_idx;   /* 0-based rank among kept objects (Cell_ID suffix, :391-393), else -1 */
+} cpx_object;         /* 56 bytes */
+
+/* Per-FOV object-table header (device). */
+typedef struct cpx_fov_objects {
+  int32_t n_objects;  /* present labels                                                   */
+  int32_t n_kept;     /* objects whose crop box is inside the image                       */
+  int32_t max_label;  /* largest label value seen                                         */
+  int32_t overflow;   /* 1 if a label exceeded the table capacity (objects dropped)       */
+} cpx_fov_objects;
+
+/* ---- feature table layout (per object, float64) ---------------------------------------- */
+/* Shape block (AreaShape_*, skimage 0.18.3 regionprops definitions). */
+#define CPX_SHAPE_AREA 0
+#define CPX_SHAPE_PERIMETER 1
+#define CPX_SHAPE_CENTER_Y 2
+#define CPX_SHAPE_CENTER_X 3
+#define CPX_SHAPE_BBOX_AREA 4
+#define CPX_SHAPE_EXTENT 5
+#define CPX_SHAPE_EQUIV_DIAMETER 6
+#define CPX_SHAPE_MAJOR_AXIS 7
+#define CPX_SHAPE_MINOR_AXIS 8
+#define CPX_SHAPE_ECCENTRICITY 9
+#define CPX_SHAPE_ORIENTATION 10
+#define CPX_SHAPE_BBOX_MIN_Y 11
+#define CPX_SHAPE_BBOX_MIN_X 12
+#define CPX_SHAPE_BBOX_MAX_Y 13
+#define CPX_SHAPE_BBOX_MAX_X 14
+#define CPX_N_SHAPE 15
+/* Intensity block, per channel (Intensity_*_<ch>). */
+#define CPX_INT_INTEGRATED 0
+#define CPX_INT_MEAN 1
+#define CPX_INT_STD 2
+#define CPX_INT_MIN 3
+#define CPX_INT_MAX 4
+#define CPX_N_INT 5
+/* Texture block, per channel, per angle a in {0, 45, 90, 135} deg, distance 3, 256 levels
+ * (skimage greycomatrix/greycoprops on the masked 8-bit bbox crop); index = a*6 + prop.   */
+#define CPX_TEX_CONTRAST 0
+#define CPX_TEX_DISSIMILARITY 1
+#define CPX_TEX_HOMOGENEITY 2
+#define CPX_TEX_ASM 3
+#define CPX_TEX_ENERGY 4
+#define CPX_TEX_CORRELATION 5
+#define CPX_N_TEX_PROPS 6
+#define CPX_N_ANGLES 4
+#define CPX_N_TEX (CPX_N_TEX_PROPS * CPX_N_ANGLES)
+#define CPX_TEX_DISTANCE 3
+/* Row layout: [shape(15)] + C * [intensity(5) + texture(24)]. */
+#define CPX_FEATURES_PER_CHANNEL (CPX_N_INT + CPX_N_TEX)
+
+/* ---- context ------------------------------------------------------------------------ */
+int cpx_abi_version(void);
+/* Select HIP device `device`, create the context (workspace grows on demand). */
+int cpx_init(int device, cpx_ctx** out);
+void cpx_destroy(cpx_ctx* ctx);
+/* Message of the last error on this thread ("" if none). */
+const char* cpx_last_error(void);
+/* Enqueue all further work on `hip_stream` (a hipStream_t; NULL = the legacy default stream).
+ * Until the first call the context uses a private non-blocking stream.  The Python host passes
+ * torch's current stream so allocations and kernels stay ordered.                          */
+int cpx_set_stream(cpx_ctx* ctx, void* hip_stream);
+int cpx_sync(cpx_ctx* ctx);
+/* Pre-size internal workspaces (so a later hipGraph capture performs no allocation). */
+int cpx_reserve(cpx_ctx* ctx, int max_planes, int H, int W, int max_fovs, int max_label);
+
+/* ---- a1 + a4: flat-field correction fused with PercentMaximal --------------------------- *
+ * Replaces Illumination_QC_mult.py:145-153 (read, astype(float), img/illum) + :73-95
+ * (calculate_saturation_cp_exact) and Cellpose_GPU_s3fs.py:72 (tifffile.imread(p)/illum[n]).
+ * raw_dev   : uint16 [n_planes][H][W]; plane p is channel (p % C).
+ * illum_dev : [C][H][W] of illum_dtype (CPX_DTYPE_F32/F64), or NULL with CPX_DTYPE_NONE.
+ * corr_dev  : float32 [n_planes][H][W] out, the producer-path value raw/illum rounded to fp32
+ *             (bit-exact to numpy's uint16/float32 division); may be NULL.
+ * stats_dev : cpx_plane_stats [n_planes] out (fp64 quotient statistics, the QC-path values). */
+int cpx_illum_correct(cpx_ctx* ctx, const uint16_t* raw_dev, const void* illum_dev,
+                      int illum_dtype, int C, int n_planes, int H, int W, float* corr_dev,
+                      cpx_plane_stats* stats_dev);
+
+/* ---- a2 + a3: radial power spectrum slope (rps + linregress) ------------------------- *
+ * Replaces Illumination_QC_mult.py:31-70 (rps) and :104-116 (linregress of log powersum).
+ * Recomputes the fp64 quotient from raw/illum (same inputs as cpx_illum_correct, whose stats
+ * must already be enqueued), runs a pruned fp64 2-D DFT (only rings 2..floor(min(H,W)/8)-1 are
+ * needed) and bins power by the reference's folded radii.  H and W must factor into
+ * {2,3,4,5,7,8,11,13} and be <= 4096.
+ * powersum_dev : float64 [n_planes][n_rings] out (may be NULL); qc_dev: cpx_qc_result [n_planes]. */
+int cpx_qc_rps(cpx_ctx* ctx, const uint16_t* raw_dev, const void* illum_dev, int illum_dtype,
+               int C, int n_planes, int H, int W, const cpx_plane_stats* stats_dev,
+               double* powersum_dev, cpx_qc_result* qc_dev);
+
+/* ---- a5: z max-projection ---------------------------------------------------------------- *
+ * Replaces MaxProjection.py:45 (np.maximum.reduce over the Z planes of one channel group).
+ * src_dev: uint16 [G][Z][N] ; out_dev: uint16 [G][N].                                        */
+int cpx_zmax_u16(cpx_ctx* ctx, const uint16_t* src_dev, int G, int Z, int64_t N,
+                 uint16_t* out_dev);
+
+/* ---- a7: object table (regionprops order, int centroids, edge filter, kept index) ------- *
+ * Replaces Cellpose_GPU_s3fs.py:149-163 (regionprops(masks), map(int, centroid), box test).
+ * labels_dev : int32 [B][H][W].  max_label: capacity per FOV (labels above it are flagged in
+ * overflow and ignored).  stats_dev: cpx_label_stats [B][max_label+1] (workspace, out).
+ * objects_dev: cpx_object [B][max_label] out (first n_objects rows valid per FOV).
+ * hdr_dev    : cpx_fov_objects [B] out.                                                    */
+int cpx_objects(cpx_ctx* ctx, const int32_t* labels_dev, int B, int H, int W, int max_label,
+                int box, cpx_label_stats* stats_dev, cpx_object* objects_dev,
+                cpx_fov_objects* hdr_dev);
+
+/* ---- a7 crops + a9 scale_to_8bit ------------------------------------------------------------ *
+ * Replaces Cellpose_GPU_s3fs.py:164-170 (img[y1:y2,x1:x2,:] * (mask==label)) and :34-43 /
+ * :178-181 (scale_to_8bit per crop-channel).  For every kept object of every FOV, writes
+ * crops_dev [B][max_crops][box][box][C] float32 (HWC, as the reference's crop) and, if non-NULL,
+ * crops8_dev [B][max_crops][C][box][box] uint8.  Slot = cell_idx; cell_idx >= max_crops is
+ * skipped.  corr_dev is planar [B][C][H][W].                                                    */
+int cpx_crops(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B, int C,
+              int H, int W, int max_label, const cpx_object* objects_dev,
+              const cpx_fov_objects* hdr_dev, int box, int max_crops, float* crops_dev,
+              uint8_t* crops8_dev);
+
+/* ---- a8: per-object features (AreaShape / Intensity / Texture) --------------------------- *
+ * Replaces the CellProfiler measurement step launched by Feature_extraction_opt.py:164-167
+ * (pipeline not in the reference; definitions pinned to skimage 0.18.3).
+ * feats_dev: float64 [B][max_label][CPX_N_SHAPE + C*CPX_FEATURES_PER_CHANNEL]; row k is the
+ * k-th object of the FOV's table (rows >= n_objects untouched).                               */
+int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B, int C,
+                 int H, int W, int max_label, const cpx_object* objects_dev,
+                 const cpx_fov_objects* hdr_dev, double* feats_dev);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CPX_H */
