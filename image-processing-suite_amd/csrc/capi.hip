@@ -72,7 +72,7 @@ void cpx_destroy(cpx_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < kWsSlots; ++i)
     if (ctx->ws[i]) hipFree(ctx->ws[i]);
   if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
   delete ctx;

@@ -7,17 +7,22 @@
 #include <algorithm>
 #include "../../include/cpx.h"
 
+constexpr int kWsSlots = 16;
+
 struct cpx_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   // generic growable device workspaces (never shrunk; see cpx_reserve)
-  void* ws[8] = {nullptr};
-  size_t ws_bytes[8] = {0};
+  void* ws[kWsSlots] = {nullptr};
+  size_t ws_bytes[kWsSlots] = {0};
   int n_cu = 256;
   // QC FFT twiddle tables currently uploaded (WS_QC_MISC)
   int qc_H = 0, qc_W = 0;
   void* qc_tw = nullptr;
+  // segmentation coefficient tables currently uploaded (WS_SEG_TAB)
+  int seg_key[6] = {0, 0, 0, 0, 0, 0};
+  void* seg_tab = nullptr;
 };
 
 // workspace slots
@@ -28,6 +33,11 @@ enum {
   WS_QC_MISC = 3,    // FFT twiddles / plans
   WS_MISC = 4,
   WS_FEAT = 5,
+  WS_SEG_PCT = 6,    // percentile histograms + state
+  WS_SEG_TAB = 7,    // resize / nearest coefficient tables
+  WS_SEG_DYN = 8,    // dPs, p, h, M, M0, seeds, counts
+  WS_SEG_OBJ = 9,    // label stats / objects for flow error + fill holes
+  WS_SEG_FILL = 10,  // fill-hole owner map
 };
 
 void cpx_set_error(const char* fmt, ...);

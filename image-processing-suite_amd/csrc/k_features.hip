@@ -164,7 +164,14 @@ __global__ __launch_bounds__(kShapeThreads) void k_shape(const int* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
-// Intensity + texture: one block per (object, channel, fov) with a 128 KiB LDS pair table.
+// Intensity + texture: one block per (object, channel) work item with a 128 KiB LDS pair table.
+// The object's masked bbox is quantised once (scale_to_8bit) into an LDS crop when it fits
+// (kCropBytes); the four GLCM angles then run entirely out of LDS.  Larger bboxes quantise on
+// the fly from global memory (L2-resident) with the same arithmetic.
+constexpr int kCropBytes = 28 * 1024;
+constexpr int kNRed = 15;  // values reduced per angle
+constexpr int kRedWords = kNRed * (kTexThreads / 64) + kNRed + 8 + 4 + 4;  // int64 words of scratch
+
 struct TexCtx {
   const int* lab;
   const float* img;
@@ -173,94 +180,84 @@ struct TexCtx {
   bool flat;
 };
 
-__device__ __forceinline__ int quant8(const TexCtx& t, int r, int c) {
-  const long long i = (long long)r * t.W + c;
-  const float v = t.img[i] * (t.lab[i] == t.L ? 1.0f : 0.0f);
+__device__ __forceinline__ int quant_val(const TexCtx& t, float v, bool in) {
+  const float m = v * (in ? 1.0f : 0.0f);
   if (t.flat) return 0;
-  float x = v - t.mn;  // scale_to_8bit, same fp32 operation order as numpy
+  float x = m - t.mn;  // scale_to_8bit, same fp32 operation order as numpy
   x = 255.0f * x;
   x = x / t.rng;
   return (int)(unsigned char)(int)x;
 }
 
-template <bool PACKED>
-__device__ void glcm_angle(const TexCtx& t, int r0, int c0, int r1, int c1, int dr, int dc,
-                           unsigned int* tab, unsigned int* dh, long long* s64, double* out) {
-  // zero the table and the |i-j| histogram
-  for (int w = threadIdx.x; w < kTabWords; w += kTexThreads) tab[w] = 0u;
-  for (int w = threadIdx.x; w < 256; w += kTexThreads) dh[w] = 0u;
-  __syncthreads();
-  const int ra = r0, rb = r1 - dr;                       // dr >= 0
-  const int ca = dc >= 0 ? c0 : c0 - dc, cb = dc >= 0 ? c1 - dc : c1;
-  const int w = cb - ca;
-  const long long npairs = (rb > ra && w > 0) ? (long long)(rb - ra) * w : 0;
-  long long zero = 0, si = 0, sj = 0, sii = 0, sjj = 0, sij = 0, ssq = 0;
-  const int passes = PACKED ? 1 : 2;
-  for (int pass = 0; pass < passes; ++pass) {
-    if (pass == 1) {
-      __syncthreads();
-      for (int x = threadIdx.x; x < kTabWords; x += kTexThreads) tab[x] = 0u;
-      __syncthreads();
-    }
-    for (long long p = threadIdx.x; p < npairs; p += kTexThreads) {
-      const int r = ra + (int)(p / w), c = ca + (int)(p % w);
-      const int i = quant8(t, r, c), j = quant8(t, r + dr, c + dc);
-      const int key = (i << 8) | j;
-      if (pass == 0) {
-        si += i;
-        sj += j;
-        sii += i * i;
-        sjj += j * j;
-        sij += i * j;
-        if (key != 0) atomicAdd(&dh[abs(i - j)], 1u);
-      }
-      if (key == 0) {
-        if (pass == 0) zero += 1;
-        continue;
-      }
-      if (PACKED) {
-        const unsigned int sh = (key & 1) * 16;
-        const unsigned int old = atomicAdd(&tab[key >> 1], 1u << sh);
-        const long long c_old = (old >> sh) & 0xffffu;
-        ssq += 2 * c_old + 1;
-      } else {
-        if ((key >> 15) != pass) continue;
-        const unsigned int old = atomicAdd(&tab[key & 0x7fff], 1u);
-        ssq += 2 * (long long)old + 1;
-      }
-    }
+__device__ __forceinline__ int quant8(const TexCtx& t, int r, int c) {
+  const long long i = (long long)r * t.W + c;
+  return quant_val(t, t.img[i], t.lab[i] == t.L);
+}
+
+// wave-then-block reduction of kNRed int64 values; result valid in thread 0
+__device__ __forceinline__ void block_reduce_n(long long* v, long long* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kNRed; ++k) v[k] = wave_sum(v[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < kNRed; ++k) red[k * (kTexThreads / 64) + wid] = v[k];
   }
-  zero = block_sum<long long, kTexThreads>(zero, s64);
-  si = block_sum<long long, kTexThreads>(si, s64);
-  sj = block_sum<long long, kTexThreads>(sj, s64);
-  sii = block_sum<long long, kTexThreads>(sii, s64);
-  sjj = block_sum<long long, kTexThreads>(sjj, s64);
-  sij = block_sum<long long, kTexThreads>(sij, s64);
-  ssq = block_sum<long long, kTexThreads>(ssq, s64);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const long long T = npairs;
+#pragma unroll
+    for (int k = 0; k < kNRed; ++k) {
+      long long s = 0;
+      for (int w = 0; w < kTexThreads / 64; ++w) s += red[k * (kTexThreads / 64) + w];
+      v[k] = s;
+    }
+  }
+}
+
+// Turns the reduced sums (thread 0's v[]) into the six greycoprops; the 256-bin |i-j| sums are
+// spread over the first 256 threads (fixed reduction tree -> deterministic).
+__device__ void glcm_props(long long* v, const unsigned int* dh, long long T, double* out,
+                           long long* bcast, double* redd) {
+  if (threadIdx.x == 0)
+    for (int k = 0; k < kNRed; ++k) bcast[k] = v[k];
+  __syncthreads();
+  double hterm = 0.0;
+  long long cterm = 0, dterm = 0;
+  const int d = threadIdx.x;
+  if (d < 256) {
+    long long cnt = (d < 8) ? bcast[7 + d] : (long long)dh[d];
+    if (d == 0) cnt += bcast[0];
+    cterm = cnt * d * d;
+    dterm = cnt * d;
+    hterm = (double)cnt * (1.0 / (1.0 + (double)(d * d)));
+  }
+  hterm = wave_sum(hterm);
+  cterm = wave_sum(cterm);
+  dterm = wave_sum(dterm);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0 && wid < 4) {
+    redd[wid] = hterm;
+    bcast[kNRed + wid] = cterm;
+    bcast[kNRed + 4 + wid] = dterm;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
     double con = 0.0, dis = 0.0, hom = 0.0, asmv = 0.0, ene = 0.0, cor = 1.0;
     if (T > 0) {
       const double Td = (double)T;
-      long long cnum = 0, dnum = 0;
-      const long long d0 = (long long)dh[0] + zero;  // d = 0 includes the ballot-counted (0,0)
-      double hsum = 0.0;
-      for (int d = 0; d < 256; ++d) {
-        const long long cnt = (d == 0) ? d0 : (long long)dh[d];
-        cnum += cnt * d * d;
-        dnum += cnt * d;
-        hsum += (double)cnt * (1.0 / (1.0 + (double)(d * d)));
-      }
+      const double hsum = (redd[0] + redd[1]) + (redd[2] + redd[3]);
+      const long long cnum = bcast[kNRed] + bcast[kNRed + 1] + bcast[kNRed + 2] + bcast[kNRed + 3];
+      const long long dnum = bcast[kNRed + 4] + bcast[kNRed + 5] + bcast[kNRed + 6] + bcast[kNRed + 7];
       con = (double)cnum / Td;
       dis = (double)dnum / Td;
       hom = hsum / Td;
-      const long long ssq_all = ssq + zero * zero;
+      const long long ssq_all = v[6] + v[0] * v[0];
       asmv = (double)ssq_all / (Td * Td);
       ene = sqrt(asmv);
-      const i128 vi = (i128)T * sii - (i128)si * si;
-      const i128 vj = (i128)T * sjj - (i128)sj * sj;
-      const i128 cv = (i128)T * sij - (i128)si * sj;
+      const i128 vi = (i128)T * v[3] - (i128)v[1] * v[1];
+      const i128 vj = (i128)T * v[4] - (i128)v[2] * v[2];
+      const i128 cv = (i128)T * v[5] - (i128)v[1] * v[2];
       const double std_i = sqrt((double)vi) / Td, std_j = sqrt((double)vj) / Td;
       if (std_i < 1e-15 || std_j < 1e-15) cor = 1.0;
       else cor = ((double)cv / (Td * Td)) / (std_i * std_j);
@@ -272,6 +269,91 @@ __device__ void glcm_angle(const TexCtx& t, int r0, int c0, int r1, int c1, int 
     out[CPX_TEX_ENERGY] = ene;
     out[CPX_TEX_CORRELATION] = cor;
   }
+}
+
+// One angle.  STAGED: i/j come from the LDS crop (packed table, replay-zero afterwards).
+// Otherwise from global; PACKED selects the u16x2 table (bbox <= 65535 px) vs two u32 passes.
+template <bool STAGED, bool PACKED>
+__device__ void glcm_angle(const TexCtx& t, const unsigned char* crop, int r0, int c0, int r1,
+                           int c1, int dr, int dc, unsigned int* tab, unsigned int* dh,
+                           long long* red, double* out) {
+  const int bw = c1 - c0;
+  const int ra = r0, rb = r1 - dr;  // dr >= 0
+  const int ca = dc >= 0 ? c0 : c0 - dc, cb = dc >= 0 ? c1 - dc : c1;
+  const int w = cb - ca;
+  const int npairs = (rb > ra && w > 0) ? (rb - ra) * w : 0;
+  long long v[kNRed];
+#pragma unroll
+  for (int k = 0; k < kNRed; ++k) v[k] = 0;
+  unsigned long long dlo = 0, dhi = 0;  // 16-bit counters for |i-j| = 0..3 / 4..7
+  const int passes = PACKED ? 1 : 2;
+  for (int pass = 0; pass < passes; ++pass) {
+    if (pass == 1) {
+      __syncthreads();
+      for (int x = threadIdx.x; x < kTabWords; x += kTexThreads) tab[x] = 0u;
+      __syncthreads();
+    }
+    for (int p = threadIdx.x; p < npairs; p += kTexThreads) {
+      const int rr = p / w, cc = p - rr * w;
+      int i, j;
+      if (STAGED) {
+        const int o = (ra - r0 + rr) * bw + (ca - c0 + cc);
+        i = crop[o];
+        j = crop[o + dr * bw + dc];
+      } else {
+        i = quant8(t, ra + rr, ca + cc);
+        j = quant8(t, ra + rr + dr, ca + cc + dc);
+      }
+      const int key = (i << 8) | j;
+      if (pass == 0) {
+        v[1] += i;
+        v[2] += j;
+        v[3] += i * i;
+        v[4] += j * j;
+        v[5] += i * j;
+        if (key == 0) {
+          v[0] += 1;
+        } else {
+          const int d = abs(i - j);
+          if (d < 4) dlo += 1ull << (16 * d);
+          else if (d < 8) dhi += 1ull << (16 * (d - 4));
+          else atomicAdd(&dh[d], 1u);
+        }
+      }
+      if (key == 0) continue;
+      if (PACKED) {
+        const unsigned int sh = (key & 1) * 16;
+        const unsigned int old = atomicAdd(&tab[key >> 1], 1u << sh);
+        v[6] += 2 * (long long)((old >> sh) & 0xffffu) + 1;
+      } else {
+        if ((key >> 15) != pass) continue;
+        const unsigned int old = atomicAdd(&tab[key & 0x7fff], 1u);
+        v[6] += 2 * (long long)old + 1;
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    v[7 + d] = (long long)((dlo >> (16 * d)) & 0xffffull);
+    v[11 + d] = (long long)((dhi >> (16 * d)) & 0xffffull);
+  }
+  __syncthreads();  // all table / dh atomics done
+  block_reduce_n(v, red);
+  glcm_props(v, dh, npairs, out, red + kNRed * (kTexThreads / 64),
+             reinterpret_cast<double*>(red + kNRed * (kTexThreads / 64) + kNRed + 8));
+  __syncthreads();
+  // restore the all-zero table / histogram for the next angle
+  if (STAGED) {
+    for (int p = threadIdx.x; p < npairs; p += kTexThreads) {
+      const int rr = p / w, cc = p - rr * w;
+      const int o = (ra - r0 + rr) * bw + (ca - c0 + cc);
+      const int key = ((int)crop[o] << 8) | (int)crop[o + dr * bw + dc];
+      tab[key >> 1] = 0u;
+    }
+  } else {
+    for (int x = threadIdx.x; x < kTabWords; x += kTexThreads) tab[x] = 0u;
+  }
+  for (int x = threadIdx.x; x < 256; x += kTexThreads) dh[x] = 0u;
   __syncthreads();
 }
 
@@ -282,74 +364,114 @@ __global__ __launch_bounds__(kTexThreads) void k_intensity_texture(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned int* tab = reinterpret_cast<unsigned int*>(smem);
   unsigned int* dh = tab + kTabWords;
-  __shared__ long long s64[kTexThreads / 64];
-  __shared__ double sd[kTexThreads / 64];
-  __shared__ float sf[kTexThreads / 64];
+  long long* red = reinterpret_cast<long long*>(dh + 256);          // kNRed * 8 waves
+  unsigned char* crop = reinterpret_cast<unsigned char*>(red + kRedWords);
+  double* redd = reinterpret_cast<double*>(red);
+  float* redf = reinterpret_cast<float*>(red);
   const int fov = blockIdx.y;
   const int n_items = hdr[fov].n_objects * C;
-  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
-  const int k = item / C, ch = item % C;
-  const cpx_object o = objects[(long long)fov * max_label + k];
-  const long long N = (long long)H * W;
-  TexCtx t;
-  t.lab = labels + (long long)fov * N;
-  t.img = corr + ((long long)fov * C + ch) * N;
-  t.W = W;
-  t.L = o.label;
-  const int r0 = o.bbox[0], c0 = o.bbox[1], r1 = o.bbox[2], c1 = o.bbox[3];
-  const int bw = c1 - c0;
-  const long long nb = (long long)(r1 - r0) * bw;
-  // pass 1: object intensity stats + masked-crop min/max (scale_to_8bit range)
-  double s = 0.0, ss = 0.0;
-  float omin = INFINITY, omax = -INFINITY, mmin = INFINITY, mmax = -INFINITY;
-  long long n = 0;
-  for (long long p = threadIdx.x; p < nb; p += kTexThreads) {
-    const int r = r0 + (int)(p / bw), c = c0 + (int)(p % bw);
-    const long long i = (long long)r * W + c;
-    const float v = t.img[i];
-    const bool in = t.lab[i] == t.L;
-    const float m = v * (in ? 1.0f : 0.0f);
-    mmin = fminf(mmin, m);
-    mmax = fmaxf(mmax, m);
-    if (in) {
-      n += 1;
-      s += (double)v;
-      ss += (double)v * (double)v;
-      omin = fminf(omin, v);
-      omax = fmaxf(omax, v);
-    }
-  }
-  n = block_sum<long long, kTexThreads>(n, s64);
-  s = block_sum<double, kTexThreads>(s, sd);
-  ss = block_sum<double, kTexThreads>(ss, sd);
-  omin = block_min<float, kTexThreads>(omin, sf);
-  omax = block_max<float, kTexThreads>(omax, sf);
-  mmin = block_min<float, kTexThreads>(mmin, sf);
-  mmax = block_max<float, kTexThreads>(mmax, sf);
-  double* f = feats + ((long long)fov * max_label + k) * F + CPX_N_SHAPE +
-              (long long)ch * CPX_FEATURES_PER_CHANNEL;
-  if (threadIdx.x == 0) {
-    const double mean = n ? s / (double)n : 0.0;
-    double var = n ? (ss - s * mean) / (double)n : 0.0;
-    if (var < 0.0) var = 0.0;
-    f[CPX_INT_INTEGRATED] = s;
-    f[CPX_INT_MEAN] = mean;
-    f[CPX_INT_STD] = sqrt(var);
-    f[CPX_INT_MIN] = (double)omin;
-    f[CPX_INT_MAX] = (double)omax;
-  }
-  t.mn = mmin;
-  t.rng = mmax - mmin;
-  t.flat = !(mmax != mmin);
-  // texture: offsets (dr, dc) = (round(sin a * 3), round(cos a * 3)) for a = 0, 45, 90, 135 deg
-  const int DR[4] = {0, 2, 3, 2}, DC[4] = {3, 2, 0, -2};
-  const bool packed = nb <= 65535;
-  for (int a = 0; a < CPX_N_ANGLES; ++a) {
-    double* out = f + CPX_N_INT + a * CPX_N_TEX_PROPS;
-    if (packed) glcm_angle<true>(t, r0, c0, r1, c1, DR[a], DC[a], tab, dh, s64, out);
-    else glcm_angle<false>(t, r0, c0, r1, c1, DR[a], DC[a], tab, dh, s64, out);
-  }
+  if ((int)blockIdx.x >= n_items) return;
+  for (int x = threadIdx.x; x < kTabWords; x += kTexThreads) tab[x] = 0u;
+  for (int x = threadIdx.x; x < 256; x += kTexThreads) dh[x] = 0u;
   __syncthreads();
+  const long long N = (long long)H * W;
+  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+    const int k = item / C, ch = item % C;
+    const cpx_object o = objects[(long long)fov * max_label + k];
+    TexCtx t;
+    t.lab = labels + (long long)fov * N;
+    t.img = corr + ((long long)fov * C + ch) * N;
+    t.W = W;
+    t.L = o.label;
+    const int r0 = o.bbox[0], c0 = o.bbox[1], r1 = o.bbox[2], c1 = o.bbox[3];
+    const int bw = c1 - c0;
+    const int nb = (r1 - r0) * bw;
+    // pass 1: object intensity stats + masked-crop min/max (scale_to_8bit range)
+    double s = 0.0, ss = 0.0;
+    float omin = INFINITY, omax = -INFINITY, mmin = INFINITY, mmax = -INFINITY;
+    long long n = 0;
+    for (int p0 = threadIdx.x; p0 < nb; p0 += 4 * kTexThreads) {
+      float vv[4];
+      bool ii[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // issue all loads first (memory-level parallelism)
+        const int p = p0 + u * kTexThreads;
+        const int rr = p / bw, cc = p - rr * bw;
+        const long long gi = (long long)(r0 + rr) * W + (c0 + cc);
+        const bool ok = p < nb;
+        vv[u] = ok ? t.img[gi] : 0.0f;
+        ii[u] = ok && t.lab[gi] == t.L;
+        if (!ok) vv[u] = NAN;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (p0 + u * kTexThreads >= nb) continue;
+        const float v = vv[u];
+        const float m = v * (ii[u] ? 1.0f : 0.0f);
+        mmin = fminf(mmin, m);
+        mmax = fmaxf(mmax, m);
+        if (ii[u]) {
+          n += 1;
+          s += (double)v;
+          ss += (double)v * (double)v;
+          omin = fminf(omin, v);
+          omax = fmaxf(omax, v);
+        }
+      }
+    }
+    n = block_sum<long long, kTexThreads>(n, red);
+    s = block_sum<double, kTexThreads>(s, redd);
+    ss = block_sum<double, kTexThreads>(ss, redd);
+    omin = block_min<float, kTexThreads>(omin, redf);
+    omax = block_max<float, kTexThreads>(omax, redf);
+    mmin = block_min<float, kTexThreads>(mmin, redf);
+    mmax = block_max<float, kTexThreads>(mmax, redf);
+    __syncthreads();
+    double* f = feats + ((long long)fov * max_label + k) * F + CPX_N_SHAPE +
+                (long long)ch * CPX_FEATURES_PER_CHANNEL;
+    if (threadIdx.x == 0) {
+      const double mean = n ? s / (double)n : 0.0;
+      double var = n ? (ss - s * mean) / (double)n : 0.0;
+      if (var < 0.0) var = 0.0;
+      f[CPX_INT_INTEGRATED] = s;
+      f[CPX_INT_MEAN] = mean;
+      f[CPX_INT_STD] = sqrt(var);
+      f[CPX_INT_MIN] = (double)omin;
+      f[CPX_INT_MAX] = (double)omax;
+    }
+    t.mn = mmin;
+    t.rng = mmax - mmin;
+    t.flat = !(mmax != mmin);
+    const bool staged = nb <= kCropBytes;
+    if (staged) {
+      for (int p0 = threadIdx.x; p0 < nb; p0 += 4 * kTexThreads) {
+        float vv[4];
+        bool ii[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int p = p0 + u * kTexThreads;
+          const int rr = p / bw, cc = p - rr * bw;
+          const long long gi = (long long)(r0 + rr) * W + (c0 + cc);
+          const bool ok = p < nb;
+          vv[u] = ok ? t.img[gi] : 0.0f;
+          ii[u] = ok && t.lab[gi] == t.L;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int p = p0 + u * kTexThreads;
+          if (p < nb) crop[p] = (unsigned char)quant_val(t, vv[u], ii[u]);
+        }
+      }
+      __syncthreads();
+    }
+    // offsets (dr, dc) = (round(sin a * 3), round(cos a * 3)) for a = 0, 45, 90, 135 deg
+    const int DR[4] = {0, 2, 3, 2}, DC[4] = {3, 2, 0, -2};
+    for (int a = 0; a < CPX_N_ANGLES; ++a) {
+      double* out = f + CPX_N_INT + a * CPX_N_TEX_PROPS;
+      if (staged) glcm_angle<true, true>(t, crop, r0, c0, r1, c1, DR[a], DC[a], tab, dh, red, out);
+      else if (nb <= 65535) glcm_angle<false, true>(t, crop, r0, c0, r1, c1, DR[a], DC[a], tab, dh, red, out);
+      else glcm_angle<false, false>(t, crop, r0, c0, r1, c1, DR[a], DC[a], tab, dh, red, out);
+    }
   }  // item loop
 }
 
@@ -367,13 +489,14 @@ extern "C" int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float
                      (const int*)labels_dev, H, W, max_label, F, objects_dev, hdr_dev, feats_dev);
   CPX_CHECK_LAUNCH("k_shape");
   static bool attr = false;
-  const size_t lds = sizeof(unsigned int) * (kTabWords + 256);
+  const size_t lds = sizeof(unsigned int) * (kTabWords + 256) +
+                     sizeof(long long) * kRedWords + kCropBytes;
   if (!attr) {
     CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_intensity_texture,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  const int per_fov = std::max(1, std::min(max_label * C, (ctx->n_cu * 2 + B - 1) / B));
+  const int per_fov = std::max(1, std::min(max_label * C, (ctx->n_cu + B - 1) / B));
   hipLaunchKernelGGL(k_intensity_texture, dim3(per_fov, B), dim3(kTexThreads), lds,
                      ctx->stream, (const int*)labels_dev, corr_dev, C, H, W, max_label, F,
                      objects_dev, hdr_dev, feats_dev);

@@ -44,9 +44,9 @@ __device__ __forceinline__ cplx cmul(cplx a, cplx b) {
 __device__ __forceinline__ cplx mul_negi(cplx a) { return {a.y, -a.x}; }  // a * (-i)
 
 // In-place R-point forward DFT (exp(-2 pi i / R) convention) of v[0..R-1].
-// tw = W_N table, step = N / R so that W_R^m = tw[m * step].
+// root[m] = W_R^m (held in registers; only the odd radices use it).
 template <int R>
-__device__ __forceinline__ void dft(cplx* v, const cplx* __restrict__ tw, int step) {
+__device__ __forceinline__ void dft(cplx* v, const cplx* root) {
   if (R == 2) {
     cplx a = v[0], b = v[1];
     v[0] = cadd(a, b);
@@ -61,8 +61,8 @@ __device__ __forceinline__ void dft(cplx* v, const cplx* __restrict__ tw, int st
   } else if (R == 8) {
     cplx e[4] = {v[0], v[2], v[4], v[6]};
     cplx o[4] = {v[1], v[3], v[5], v[7]};
-    dft<4>(e, tw, 0);
-    dft<4>(o, tw, 0);
+    dft<4>(e, root);
+    dft<4>(o, root);
     const double s = 0.70710678118654752440;  // 1/sqrt(2)
     cplx w1 = {s, -s}, w3 = {-s, -s};
     cplx o1 = cmul(o[1], w1), o2 = mul_negi(o[2]), o3 = cmul(o[3], w3);
@@ -80,7 +80,7 @@ __device__ __forceinline__ void dft(cplx* v, const cplx* __restrict__ tw, int st
     for (int m = 0; m < R; ++m) {
       cplx acc = v[0];
 #pragma unroll
-      for (int r = 1; r < R; ++r) acc = cadd(acc, cmul(v[r], tw[((r * m) % R) * step]));
+      for (int r = 1; r < R; ++r) acc = cadd(acc, cmul(v[r], root[(r * m) % R]));
       out[m] = acc;
     }
 #pragma unroll
@@ -93,6 +93,9 @@ __device__ __forceinline__ void stockham_stage(const cplx* __restrict__ in, cplx
                                                const cplx* __restrict__ tw, int N, int Ns) {
   const int nb = N / R;
   const int tstep = N / (Ns * R);
+  cplx root[R];
+#pragma unroll
+  for (int m = 0; m < R; ++m) root[m] = (R == 2 || R == 4 || R == 8) ? cplx{0.0, 0.0} : tw[m * nb];
   for (int j = threadIdx.x; j < nb; j += blockDim.x) {
     const int k = j % Ns;
     cplx v[R];
@@ -102,7 +105,7 @@ __device__ __forceinline__ void stockham_stage(const cplx* __restrict__ in, cplx
 #pragma unroll
       for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[k * r * tstep]);
     }
-    dft<R>(v, tw, N / R);
+    dft<R>(v, root);
     const int d = (j / Ns) * Ns * R + k;
 #pragma unroll
     for (int r = 0; r < R; ++r) out[d + r * Ns] = v[r];

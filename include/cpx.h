@@ -205,6 +205,53 @@ int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev,
                  int H, int W, int max_label, const cpx_object* objects_dev,
                  const cpx_fov_objects* hdr_dev, double* feats_dev);
 
+/* ---- a6: segmentation (Cellpose <= v3 evaluation, restated) -- *
+ * Replaces the work inside cell_model.eval(image_4ch, diameter=100) (Cellpose_GPU_s3fs.py:143)
+ * except the CPnet U-Net forward itself, which runs in PyTorch-ROCm between cpx_seg_tiles and
+ * cpx_seg_average.                                                                           */
+#define CPX_SEG_MAX_TILES_AXIS 16
+typedef struct cpx_seg_geom {
+  int32_t Ly, Lx;     /* network-resolution image (int(H * diam_mean / diameter))             */
+  int32_t py0, px0;   /* zero padding before the image (transforms.pad_image_ND)              */
+  int32_t Lyp, Lxp;   /* padded size                                                         */
+  int32_t by, bx;     /* tile size (224)                                                     */
+  int32_t ny, nx;     /* tiles per axis (transforms.make_tiles, overlap 0.1)                  */
+  int32_t ys[CPX_SEG_MAX_TILES_AXIS], xs[CPX_SEG_MAX_TILES_AXIS]; /* tile origins             */
+} cpx_seg_geom;
+
+typedef struct cpx_seg_stats {
+  int32_t n_moving;   /* pixels that follow the flow (|dY/5| > 1e-3 inside cellprob > 0)       */
+  int32_t n_seeds;    /* histogram maxima (h > 10)                                            */
+  int32_t n_masks;    /* labels after get_masks (big masks removed, renumbered)               */
+  int32_t n_bad_flow; /* masks removed by the flow-error test                                 */
+  int32_t n_final;    /* labels after fill_holes_and_remove_small_masks                       */
+  int32_t overflow;   /* capacity exceeded (seeds or labels truncated)                        */
+  int32_t _pad[2];
+} cpx_seg_stats;      /* 32 bytes */
+
+#define CPX_TILE_F32_NCHW 0  /* tiles/net output as float32 [n][c][by][bx]                   */
+#define CPX_TILE_BF16_NHWC 1 /* tiles/net output as bfloat16 [n][by][bx][c] (channels_last)  */
+
+/* normalize99 statistics: pct_dev float64 [B][nchan][2] = (p1, p99) of channels 0..nchan-1 of
+ * each FOV (exact order statistics of the fp32 corrected planes, linear interpolation).       */
+int cpx_seg_percentiles(cpx_ctx* ctx, const float* corr_dev, int B, int C, int H, int W,
+                        int nchan, double* pct_dev);
+/* Normalise, bilinearly resize to (Ly, Lx), zero-pad and cut the network tiles:
+ * tiles_dev: [B * ny * nx] tiles of nchan channels in `layout`.                               */
+int cpx_seg_tiles(cpx_ctx* ctx, const float* corr_dev, int B, int C, int H, int W, int nchan,
+                  const double* pct_dev, const cpx_seg_geom* geom, int layout, void* tiles_dev);
+/* Taper-weighted average of the network outputs (transforms.average_tiles), pad cropped:
+ * taper_dev float32 [by][bx] (transforms._taper_mask, computed by the host with numpy);
+ * yf_dev float32 [B][nout][Ly][Lx] (dy, dx, cellprob).                                       */
+int cpx_seg_average(cpx_ctx* ctx, const void* net_dev, int layout, int B, int nout,
+                    const cpx_seg_geom* geom, const float* taper_dev, float* yf_dev);
+/* compute_masks at network resolution (follow_flows, get_masks, flow-error filter), nearest
+ * resize to (H, W), fill_holes_and_remove_small_masks.  labels_dev int32 [B][H][W];
+ * stats_dev cpx_seg_stats [B].  max_objects bounds labels per FOV.                           */
+int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx_seg_geom* geom, int H,
+                  int W, int niter, double flow_threshold, int min_size, int max_objects,
+                  int32_t* labels_dev, cpx_seg_stats* stats_dev);
+
 #ifdef __cplusplus
 }
 #endif

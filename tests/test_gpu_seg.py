@@ -1,0 +1,160 @@
+"""GPU: segmentation kernels vs the Cellpose restatement oracle (oracle/seg_oracle.py).
+
+Parity vs real Cellpose is unpinned (third-party, absent, unversioned, weights unavailable);
+these tests pin libcpx to the restatement: percentiles, tiles, tile averaging and masks are
+bit-exact on identical inputs; the CPnet forward (PyTorch-ROCm) is checked against the same
+network on the CPU in fp32.
+"""
+import ctypes as ct
+
+import numpy as np
+import pytest
+import torch
+
+import seg_oracle as so
+import synth_golden as sg
+from cpx._lib import check
+from cpx.cpnet import build_cpnet
+from cpx.device import _ptr
+from cpx.segment import SEG_STATS_DTYPE, Segmenter, make_geom, taper_mask
+
+pytestmark = pytest.mark.gpu
+
+
+def _planes(B, C, H, W, seed=0):
+    out = np.zeros((B, C, H, W), np.float32)
+    for b in range(B):
+        for c in range(C):
+            out[b, c] = sg.plane(seed + 10 * b + c, H, W, n_blobs=25).astype(np.float32) / sg.illum(seed + 99 + c, H, W)
+    return out
+
+
+def _geom_ptr(g):
+    return ct.c_void_p(ct.addressof(g))
+
+
+def test_percentiles_exact(dev):
+    B, C, H, W = 2, 3, 301, 257
+    planes = _planes(B, C, H, W)
+    planes[1, 1, :5, :7] = -3.5  # negative values and ties
+    corr = torch.from_numpy(planes).to(dev.torch_device)
+    pct = torch.empty((B, 2, 2), dtype=torch.float64, device=dev.torch_device)
+    check(dev.lib.cpx_seg_percentiles(dev.h, _ptr(corr), B, C, H, W, 2, _ptr(pct)), "pct")
+    got = pct.cpu().numpy()
+    for b in range(B):
+        for c in range(2):
+            assert got[b, c, 0] == so.percentile(planes[b, c], 1.0)
+            assert got[b, c, 1] == so.percentile(planes[b, c], 99.0)
+
+
+def test_tiles_and_average_bit_exact(dev):
+    B, C, H, W = 2, 3, 700, 760
+    g = make_geom(H, W)  # nuclei, diameter 100 -> 119 x 129, padded 144 x 160 -> 1x1 tiles?
+    planes = _planes(B, C, H, W, seed=5)
+    corr = torch.from_numpy(planes).to(dev.torch_device)
+    pct = torch.empty((B, 2, 2), dtype=torch.float64, device=dev.torch_device)
+    check(dev.lib.cpx_seg_percentiles(dev.h, _ptr(corr), B, C, H, W, 2, _ptr(pct)), "pct")
+    nt = g.ny * g.nx
+    tiles = torch.empty((B * nt, 2, g.by, g.bx), dtype=torch.float32, device=dev.torch_device)
+    check(dev.lib.cpx_seg_tiles(dev.h, _ptr(corr), B, C, H, W, 2, _ptr(pct), _geom_ptr(g), 0, _ptr(tiles)), "tiles")
+    got = tiles.cpu().numpy().reshape(B, nt, 2, g.by, g.bx)
+    for b in range(B):
+        ref, tg = so.make_net_input(planes[b], g.Ly, g.Lx)
+        assert tg.tiles == [(int(g.ys[i // g.nx]), int(g.xs[i % g.nx])) for i in range(nt)]
+        np.testing.assert_array_equal(got[b], ref)
+    # averaging with arbitrary network outputs
+    rng = np.random.default_rng(3)
+    net = rng.standard_normal((B * nt, 3, g.by, g.bx)).astype(np.float32)
+    nt_t = torch.from_numpy(net).to(dev.torch_device)
+    taper = torch.from_numpy(taper_mask(g.by, g.bx)).to(dev.torch_device)
+    yf = torch.empty((B, 3, g.Ly, g.Lx), dtype=torch.float32, device=dev.torch_device)
+    check(dev.lib.cpx_seg_average(dev.h, _ptr(nt_t), 0, B, 3, _geom_ptr(g), _ptr(taper), _ptr(yf)), "avg")
+    got = yf.cpu().numpy()
+    for b in range(B):
+        np.testing.assert_array_equal(got[b], so.average_tiles(net[b * nt:(b + 1) * nt], so.TileGeom(g.Ly, g.Lx)))
+
+
+def test_multi_tile_geometry_2080():
+    g = make_geom(2080, 2080)
+    t = so.TileGeom(g.Ly, g.Lx)
+    assert (g.Ly, g.Lyp, g.ny, g.nx) == (353, 384, 3, 3)
+    assert t.tiles == [(int(g.ys[i // 3]), int(g.xs[i % 3])) for i in range(9)]
+
+
+def _synthetic_yf(Ly, Lx, seed, noise=0.05):
+    lab = sg.labels(seed, Ly, Lx, n=18, rmin=3, rmax=10, skip_every=0)
+    mu = so.masks_to_flows(lab)
+    rng = np.random.default_rng(seed)
+    yf = np.zeros((3, Ly, Lx), np.float32)
+    yf[0] = 5.0 * mu[0] + noise * rng.standard_normal((Ly, Lx))
+    yf[1] = 5.0 * mu[1] + noise * rng.standard_normal((Ly, Lx))
+    yf[2] = np.where(lab > 0, 3.0, -3.0) + 0.5 * rng.standard_normal((Ly, Lx))
+    return yf, lab
+
+
+def _gpu_masks(dev, yf, g, H, W, flow_threshold=0.4, min_size=15):
+    B = yf.shape[0]
+    yft = torch.from_numpy(np.ascontiguousarray(yf)).to(dev.torch_device)
+    labels = torch.empty((B, H, W), dtype=torch.int32, device=dev.torch_device)
+    stats = torch.zeros(32 * B, dtype=torch.uint8, device=dev.torch_device)
+    check(dev.lib.cpx_seg_masks(dev.h, _ptr(yft), B, _geom_ptr(g), H, W, 200, float(flow_threshold),
+                                min_size, 1024, _ptr(labels), _ptr(stats)), "masks")
+    dev.sync()
+    return labels.cpu().numpy(), stats.cpu().numpy().view(SEG_STATS_DTYPE)
+
+
+def test_masks_bit_exact_vs_oracle(dev):
+    H, W = 700, 760
+    g = make_geom(H, W)
+    yfs = []
+    for s in (1, 2, 3):
+        yf, _ = _synthetic_yf(g.Ly, g.Lx, s)
+        yfs.append(yf)
+    yfs.append(np.full((3, g.Ly, g.Lx), -1.0, np.float32))  # no cells at all
+    yf = np.stack(yfs)
+    got, st = _gpu_masks(dev, yf, g, H, W)
+    for b in range(yf.shape[0]):
+        ref = so.compute_masks(yf[b], H, W)
+        np.testing.assert_array_equal(got[b], ref, err_msg=f"fov {b}")
+        assert st[b]["n_final"] == ref.max()
+    assert st[0]["n_final"] >= 8  # the synthetic objects were recovered
+    assert st[3]["n_final"] == 0 and st[3]["n_moving"] == 0
+
+
+def test_masks_without_flow_filter_and_min_size(dev):
+    H, W = 700, 760
+    g = make_geom(H, W)
+    yf, _ = _synthetic_yf(g.Ly, g.Lx, 7, noise=0.3)
+    got, _ = _gpu_masks(dev, yf[None], g, H, W, flow_threshold=0.0, min_size=400)
+    ref = so.compute_masks(yf, H, W, flow_threshold=0.0, min_size=400)
+    np.testing.assert_array_equal(got[0], ref)
+
+
+def test_cpnet_forward_gpu_vs_cpu_fp32(dev):
+    net_cpu = build_cpnet(seed=1)
+    net_gpu = build_cpnet(seed=1).to(dev.torch_device)
+    x = torch.randn(2, 2, 224, 224, generator=torch.Generator().manual_seed(0))
+    with torch.no_grad():
+        ref = net_cpu(x)
+        out = net_gpu(x.to(dev.torch_device)).cpu()
+        scale = ref.abs().max().item()
+        assert (out - ref).abs().max().item() <= 1e-3 * scale
+        bf = net_gpu.to(memory_format=torch.channels_last, dtype=torch.bfloat16)
+        ob = bf(x.to(dev.torch_device, torch.bfloat16).contiguous(memory_format=torch.channels_last)).float().cpu()
+    c = np.corrcoef(ob.numpy().ravel(), ref.numpy().ravel())[0, 1]
+    assert c > 0.99
+
+
+def test_segmenter_end_to_end(dev):
+    B, C, H, W = 2, 3, 700, 760
+    planes = _planes(B, C, H, W, seed=11)
+    corr = torch.from_numpy(planes).to(dev.torch_device)
+    seg = Segmenter(dev, H, W, B, use_graph=True)
+    lab = seg.segment(corr)
+    lab2 = seg.segment(corr)  # graph replay is deterministic
+    dev.sync()
+    a, b = lab.cpu().numpy(), lab2.cpu().numpy()
+    np.testing.assert_array_equal(a, b)
+    st = seg.seg_stats()
+    for i in range(B):
+        assert a[i].min() >= 0 and a[i].max() == st[i]["n_final"]
