@@ -1,0 +1,207 @@
+"""Headline benchmark: fields-of-view/sec of the 2080x2080x5ch illum -> seg -> feat pipeline.
+
+Workload (BASELINE.json configs[1]): one 384-well plate, 1 FOV/well, 2080x2080x5ch synthetic,
+processed in steps of --batch FOVs that are resident in HBM when the timed region starts.  One
+step = flat-field + QC (PercentMaximal, PowerLogLogSlope) -> Cellpose-restated segmentation
+(CPnet bf16 + HIP post-processing) -> Cells/Cytoplasm -> object tables -> shape/intensity/texture
+features for Nuclei, Cells, Cytoplasm -> results copied to the host.  Multi-GPU: one process per
+GPU, FOVs (wells) sharded by rank, no data-path collective (scaling "weak").
+
+  python bench.py [--gpus N --steps K --warmup W --batch B]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "image-processing-suite_amd"))
+
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=24)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=16, help="FOVs per step per GPU")
+    ap.add_argument("--pool", type=int, default=2, help="distinct synthetic batches cycled per GPU")
+    ap.add_argument("--size", type=int, default=2080)
+    ap.add_argument("--channels", type=int, default=5)
+    ap.add_argument("--weights", default=None, help="CPnet state_dict (default: seeded random init)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--stage-steps", type=int, default=3, help="instrumented steps after timing")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from cpx.cpnet import count_flops
+    from cpx.device import Device
+    from cpx.pipeline import FovPipeline, PipelineConfig
+    from cpx.synth import synth_fovs, synth_illum
+
+    H = W = a.size
+    C, B = a.channels, a.batch
+    dev = Device(local)
+    td = dev.torch_device
+    weights = a.weights
+    if weights is None:
+        cand = os.path.join(REPO, "image-processing-suite_amd", "cpx", "weights", "cpnet_nuclei_synth.pt")
+        weights = cand if os.path.exists(cand) else None
+    cfg = PipelineConfig(H=H, W=W, C=C, batch=B, weights=weights)
+    illum = synth_illum(C, H, W, seed=1)
+    pipe = FovPipeline(dev, cfg, illum)
+    pool = [synth_fovs(B, C, H, W, td, seed=7919 * rank + 101 * i) for i in range(a.pool)]
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    n_obj = []
+    for i in range(a.warmup):
+        pipe.run(pool[i % a.pool])
+        pipe.fetch()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        pipe.run(pool[i % a.pool])
+        res = pipe.fetch()
+        n_obj.append([int(res.hdr[s]["n_objects"].sum()) for s in ("Nuclei", "Cells", "Cytoplasm")])
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=td)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    total_fovs = world * a.steps * B
+    value = total_fovs / dt
+
+    # ---- instrumented steps (outside the timed region): per-stage device time by HIP events on
+    # the stream every stage is launched on (torch's current stream; libcpx is bound to it)
+    stages = ["illum_qc", "segment", "objects_features"]
+    acc = {s: 0.0 for s in stages}
+    sub = {"illum": 0.0, "qc_rps": 0.0, "seg_prep": 0.0, "cpnet": 0.0, "seg_post": 0.0}
+    for i in range(a.stage_steps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(9)]
+        ev[0].record()
+        dev.illum_correct(pool[i % a.pool], pipe.illum, C, pipe.corr, pipe.stats)
+        ev[1].record()
+        dev.qc_rps(pool[i % a.pool], pipe.illum, C, pipe.stats, pipe.qc)
+        ev[2].record()
+        pipe.seg.prepare(pipe.corr)
+        ev[3].record()
+        pipe.seg._run_net()
+        ev[4].record()
+        pipe.seg.postprocess(pipe.labels["Nuclei"])
+        ev[5].record()
+        pipe.stage_objects()
+        ev[6].record()
+        torch.cuda.synchronize()
+        sub["illum"] += ev[0].elapsed_time(ev[1])
+        sub["qc_rps"] += ev[1].elapsed_time(ev[2])
+        sub["seg_prep"] += ev[2].elapsed_time(ev[3])
+        sub["cpnet"] += ev[3].elapsed_time(ev[4])
+        sub["seg_post"] += ev[4].elapsed_time(ev[5])
+        acc["illum_qc"] += ev[0].elapsed_time(ev[2])
+        acc["segment"] += ev[2].elapsed_time(ev[5])
+        acc["objects_features"] += ev[5].elapsed_time(ev[6])
+    per_step_ms = {k: v / a.stage_steps for k, v in acc.items()}
+    sub_ms = {k: v / a.stage_steps for k, v in sub.items()}
+    N = H * W
+    n_tiles = pipe.seg.geom.n_tiles
+    # algorithmic bytes / flops per launch (one batch of B FOVs)
+    illum_bytes = B * C * N * (2 + 4 + 4)                # raw u16 + illum f32 in, fp32 plane out
+    feat_bytes = 3 * B * N * (4 * C + 4)                 # per object set: fp32 planes + int32 labels
+    cpnet_flops = B * n_tiles * count_flops(pipe.seg.geom.by)
+    kernels = {
+        "illum": dict(bound="hbm", work=illum_bytes, ms=sub_ms["illum"]),
+        "cpnet": dict(bound="mfma", work=cpnet_flops, ms=sub_ms["cpnet"]),
+        "objects_features": dict(bound="hbm", work=feat_bytes, ms=per_step_ms["objects_features"]),
+    }
+
+    def roof(k):
+        d = kernels[k]
+        if d["bound"] == "hbm":
+            ach = d["work"] / (d["ms"] * 1e-3) / 1e9
+            return {"kernel": k, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "algorithmic_bytes_per_launch": d["work"], "avg_launch_ms": round(d["ms"], 4)}
+        ach = d["work"] / (d["ms"] * 1e-3) / 1e12
+        return {"kernel": k, "bound": "mfma", "achieved": round(ach, 1), "peak": BF16_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                "algorithmic_flops_per_launch": d["work"], "avg_launch_ms": round(d["ms"], 4)}
+
+    dominant = max(kernels, key=lambda k: kernels[k]["ms"])
+    line = {
+        "metric": "fields-of-view/sec, 2080x2080x5ch illum+seg+feat pipe",
+        "value": round(value, 2),
+        "unit": "FOV/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(dt / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32 planes / fp64 QC+features / bf16 CPnet",
+        "data": "synthetic (HBM-resident uint16 plates, Poisson background, Gaussian nuclei + halos)",
+        "config": {"workload": "configs[1]: 384-well plate, 1 FOV/well, 2080x2080x5ch, illum->seg->feat",
+                   "fovs_per_step": B * world, "batch_per_gpu": B, "H": H, "W": W, "C": C,
+                   "cellpose_model": cfg.model, "diameter": cfg.diameter,
+                   "cpnet_weights": os.path.basename(weights) if weights else "seeded-random-init",
+                   "tiles_per_fov": n_tiles, "parallelism": f"fov-sharded x{world}"},
+        "objects_per_fov": ([round(x / (B * world) * world, 1) for x in np.mean(np.array(n_obj), axis=0)]
+                            if n_obj else None),
+        "stage_ms_per_step": {k: round(v, 3) for k, v in {**per_step_ms, **sub_ms}.items()},
+        "roofline": roof(dominant),
+        "roofline_all": {k: roof(k) for k in kernels},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(pool[0], illum, C, H, W, cfg)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(pool_batch, illum, C, H, W, cfg):
+    """The oracle (CPU restatement) on ONE FOV of the same workload, single thread."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import cpu_pipeline
+    from cpx.cpnet import build_cpnet
+    torch.set_num_threads(1)
+    raw = pool_batch[:C].cpu().numpy().view(np.uint16)
+    net = build_cpnet(seed=cfg.seed, model=cfg.model, state_dict_path=cfg.weights)
+    tm = {}
+    cpu_pipeline.run_fov(raw, illum, net, cfg.cell_expand, cfg.model, cfg.diameter, timings=tm)
+    return {"value": round(1.0 / tm["total"], 5), "unit": "FOV/s", "cores": 1, "kind": "port",
+            "sample": f"1 FOV of the same synthetic plate ({H}x{W}x{C}), oracle/cpu_pipeline.py, "
+                      f"torch/numpy single-threaded; stage seconds: " +
+                      ", ".join(f"{k}={v:.2f}" for k, v in tm.items())}
+
+
+if __name__ == "__main__":
+    main()

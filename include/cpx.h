@@ -205,6 +205,14 @@ int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev,
                  int H, int W, int max_label, const cpx_object* objects_dev,
                  const cpx_fov_objects* hdr_dev, double* feats_dev);
 
+/* ---- secondary objects for the Cells / Cytoplasm tables (Pycyto_pertime.py:46-49) -------- *
+ * cells = skimage.segmentation.expand_labels(nuclei, distance) (0.18.3: nearest label pixel by
+ * scipy's exact Euclidean feature transform, kept where the distance <= `distance`);
+ * cyto = cells where nuclei == 0 (Cytoplasm shares the Cells/Nuclei ObjectNumber).  Either
+ * output may be NULL.  All int32 [B][H][W].                                                  */
+int cpx_expand_labels(cpx_ctx* ctx, const int32_t* nuclei_dev, int B, int H, int W, int distance,
+                      int32_t* cells_dev, int32_t* cyto_dev);
+
 /* ---- a6: segmentation (Cellpose <= v3 evaluation, restated) -- *
  * Replaces the work inside cell_model.eval(image_4ch, diameter=100) (Cellpose_GPU_s3fs.py:143)
  * except the CPnet U-Net forward itself, which runs in PyTorch-ROCm between cpx_seg_tiles and

@@ -329,6 +329,22 @@ def texture_input(plane32: np.ndarray, masks: np.ndarray, sl, label: int) -> np.
     return scale_to_8bit(crop)
 
 
+def expand_labels(label_image: np.ndarray, distance: int) -> np.ndarray:
+    """skimage 0.18.3 segmentation.expand_labels (scipy exact EDT feature transform)."""
+    distances, nearest = ndi.distance_transform_edt(label_image == 0, return_indices=True)
+    out = np.zeros_like(label_image)
+    dil = distances <= distance
+    out[dil] = label_image[tuple(idx[dil] for idx in nearest)]
+    return out
+
+
+def secondary_objects(nuclei: np.ndarray, distance: int):
+    """Cells = expand_labels(nuclei, distance); Cytoplasm = Cells where Nuclei == 0."""
+    cells = expand_labels(nuclei, distance)
+    cyto = np.where(nuclei == 0, cells, 0).astype(cells.dtype)
+    return cells, cyto
+
+
 def features(masks: np.ndarray, planes32: np.ndarray) -> np.ndarray:
     """Per-object feature matrix [n_objects, 15 + C*29] in ascending label order.
     planes32: [C, H, W] float32 corrected planes."""

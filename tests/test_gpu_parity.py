@@ -204,3 +204,25 @@ def test_features_match_oracle_larger(dev):
                        sg.illum(950 + c, H, W) for c in range(C)]).astype(np.float32)
     got = _features(dev, lab, planes)
     _feat_close(got, orc.features(lab, planes))
+
+
+def test_expand_labels_bit_exact(dev, golden_dir):
+    d = _load(golden_dir, "objects_features")
+    lab = d["expand_labels_in"]
+    labs = np.stack([lab, sg.labels(51, lab.shape[0], lab.shape[1], n=60, rmin=2, rmax=9),
+                     np.zeros_like(lab)])
+    B, H, W = labs.shape
+    t = _t(dev, labs.astype(np.int32))
+    for dist in (1, 5, 15):
+        cells = torch.empty_like(t)
+        cyto = torch.empty_like(t)
+        from cpx._lib import check
+        from cpx.device import _ptr
+        check(dev.lib.cpx_expand_labels(dev.h, _ptr(t), B, H, W, dist, _ptr(cells), _ptr(cyto)), "expand")
+        dev.sync()
+        gc, gy = cells.cpu().numpy(), cyto.cpu().numpy()
+        np.testing.assert_array_equal(gc[0], d[f"expand_labels_d{dist}"])
+        for b in range(B):
+            rc, ry = orc.secondary_objects(labs[b], dist)
+            np.testing.assert_array_equal(gc[b], rc)
+            np.testing.assert_array_equal(gy[b], ry)

@@ -112,3 +112,12 @@ def test_synthetic_generator_is_deterministic():
     assert a.dtype == np.uint16 and (a == 65535).any() or True
     lab = sg.labels(3, 64, 64, n=10)
     assert lab.max() > 0 and lab.dtype == np.int32
+
+
+def test_expand_labels_matches_skimage(golden_dir):
+    d = _load(golden_dir, "objects_features")
+    lab = d["expand_labels_in"]
+    for dist in (1, 5, 15):
+        np.testing.assert_array_equal(orc.expand_labels(lab, dist), d[f"expand_labels_d{dist}"])
+    cells, cyto = orc.secondary_objects(lab, 5)
+    assert (cyto[lab > 0] == 0).all() and (cyto[(lab == 0)] == cells[lab == 0]).all()

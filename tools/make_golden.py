@@ -224,6 +224,14 @@ def gen_objects_features():
                         ["contrast", "dissimilarity", "homogeneity", "ASM", "energy", "correlation"]]
         frows.append(row)
     arrays["feat_expected"] = np.array(frows, dtype=np.float64)
+    # (c) secondary objects: skimage expand_labels on touching / gapped nuclei (ties included)
+    from skimage.segmentation import expand_labels
+    lab3 = sg.labels(23, 257, 301, n=30, rmin=3, rmax=20)
+    lab3[100:104, 50:54] = 77  # two small squares at even distance -> equidistant pixels
+    lab3[100:104, 64:68] = 78
+    arrays["expand_labels_in"] = lab3
+    for dist in (1, 5, 15):
+        arrays[f"expand_labels_d{dist}"] = expand_labels(lab3, dist)
     meta["features"] = dict(H=H, W=W, C=C, n_objects=len(frows))
     np.savez_compressed(os.path.join(OUT, "objects_features.npz"), **arrays)
     with open(os.path.join(OUT, "objects_features.json"), "w") as f:
