@@ -92,3 +92,18 @@ __device__ __forceinline__ T wave_max(T v) {
   }
   return v;
 }
+
+// Objects handled by the LDS fast paths in k_texture.hip; the rest go to the k_features.hip
+// fallback kernels (the two predicates must agree between the translation units).
+constexpr int kFastCropPx = 24576;
+constexpr int kFastMaskWords = 1024;
+constexpr int kFastShapeWords = 12288;
+__host__ __device__ inline bool cpx_tex_fits(int bh, int bw) {
+  return bh * bw <= kFastCropPx && bh * ((bw + 31) >> 5) <= kFastMaskWords;
+}
+__host__ __device__ inline bool cpx_shape_fits(int bh, int bw) {
+  return (bh + 4) * ((bw + 4 + 31) >> 5) <= kFastShapeWords;
+}
+int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B, int C,
+                      int H, int W, int max_label, int F, const cpx_object* objects_dev,
+                      const cpx_fov_objects* hdr_dev, double* feats_dev, long long** crop_off_out);

@@ -80,6 +80,7 @@ __global__ __launch_bounds__(kShapeThreads) void k_shape(const int* __restrict__
   const int k = blockIdx.x, fov = blockIdx.y;
   if (k >= hdr[fov].n_objects) return;
   const cpx_object o = objects[(long long)fov * max_label + k];
+  if (cpx_shape_fits(o.bbox[2] - o.bbox[0], o.bbox[3] - o.bbox[1])) return;  // fast path did it
   const int* lab = labels + (long long)fov * H * W;
   const int L = o.label;
   const int r0 = o.bbox[0], c0 = o.bbox[1], r1 = o.bbox[2], c1 = o.bbox[3];
@@ -360,7 +361,8 @@ __device__ void glcm_angle(const TexCtx& t, const unsigned char* crop, int r0, i
 __global__ __launch_bounds__(kTexThreads) void k_intensity_texture(
     const int* __restrict__ labels, const float* __restrict__ corr, int C, int H, int W,
     int max_label, int F, const cpx_object* __restrict__ objects,
-    const cpx_fov_objects* __restrict__ hdr, double* __restrict__ feats) {
+    const cpx_fov_objects* __restrict__ hdr, double* __restrict__ feats,
+    const long long* __restrict__ crop_off) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned int* tab = reinterpret_cast<unsigned int*>(smem);
   unsigned int* dh = tab + kTabWords;
@@ -378,6 +380,7 @@ __global__ __launch_bounds__(kTexThreads) void k_intensity_texture(
   for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
     const int k = item / C, ch = item % C;
     const cpx_object o = objects[(long long)fov * max_label + k];
+    if (crop_off[(long long)fov * max_label + k] >= 0) continue;  // fast path did it
     TexCtx t;
     t.lab = labels + (long long)fov * N;
     t.img = corr + ((long long)fov * C + ch) * N;
@@ -485,6 +488,11 @@ extern "C" int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float
   CPX_REQUIRE(B > 0 && B <= 65535 && C > 0 && C <= 65535 && H > 0 && W > 0 && max_label > 0,
               CPX_ERR_ARG, "cpx_features: bad sizes");
   const int F = CPX_N_SHAPE + C * CPX_FEATURES_PER_CHANNEL;
+  long long* crop_off = nullptr;
+  const int rc = cpx_features_fast(ctx, labels_dev, corr_dev, B, C, H, W, max_label, F, objects_dev,
+                                   hdr_dev, feats_dev, &crop_off);
+  if (rc) return rc;
+  // fallback kernels for objects too large for the LDS fast paths (skip the others)
   hipLaunchKernelGGL(k_shape, dim3(max_label, B), dim3(kShapeThreads), 0, ctx->stream,
                      (const int*)labels_dev, H, W, max_label, F, objects_dev, hdr_dev, feats_dev);
   CPX_CHECK_LAUNCH("k_shape");
@@ -499,7 +507,7 @@ extern "C" int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float
   const int per_fov = std::max(1, std::min(max_label * C, (ctx->n_cu + B - 1) / B));
   hipLaunchKernelGGL(k_intensity_texture, dim3(per_fov, B), dim3(kTexThreads), lds,
                      ctx->stream, (const int*)labels_dev, corr_dev, C, H, W, max_label, F,
-                     objects_dev, hdr_dev, feats_dev);
+                     objects_dev, hdr_dev, feats_dev, (const long long*)crop_off);
   CPX_CHECK_LAUNCH("k_intensity_texture");
   return CPX_OK;
 }

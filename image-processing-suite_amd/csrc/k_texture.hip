@@ -1,0 +1,679 @@
+// a8 fast path: AreaShape + Intensity + Texture for objects whose bbox fits in LDS (the common
+// case; larger objects fall back to k_shape / k_intensity_texture in k_features.hip with the same
+// arithmetic).  Same definitions and bit-identical results as the fallback; see k_features.hip.
+//
+// Design:
+//  * texture in two phases: phase A (high occupancy, one block per object-channel) makes one
+//    coalesced pass over the bbox (2-D thread layout, 4 rows of loads in flight per thread)
+//    for the intensity statistics and the scale_to_8bit range, then writes the 8-bit masked
+//    crop to a global scratch slot (offsets from a per-FOV scan); phase B (one 1024-thread
+//    block per CU with a 128 KiB LDS pair table) copies the crop to LDS and runs the four GLCM
+//    angles from LDS: exact u32 pair sums in registers, |i-j| < 8 counted in packed
+//    registers, ASM from the returned counts of a 64K-entry packed u16 LDS table, background
+//    (0,0) pairs by branch; DPP wave sums, greycoprops on one wave while the others clear the
+//    table with 16-byte stores.
+//  * AreaShape: bbox + 2-pixel margin bitmask in LDS; the 4-neighbour border and the
+//    Benkrid-Crookes perimeter code are evaluated bit-parallel, moments are exact int64 sums.
+#include "cpx_internal.h"
+#include <math.h>
+
+namespace {
+
+typedef __int128 i128;
+
+// Development-only phase timer of k_tex_glcm (build with -DCPX_GLCM_PROF; tools/tex_bench.py).
+#ifdef CPX_GLCM_PROF
+__device__ unsigned long long g_glcm_prof[8];
+#define GLCM_MARK(k, pt)                                    \
+  do {                                                      \
+    if (threadIdx.x == 0) {                                 \
+      const long long t_ = clock64();                       \
+      atomicAdd(&g_glcm_prof[k], (unsigned long long)(t_ - *(pt))); \
+      *(pt) = t_;                                           \
+    }                                                       \
+  } while (0)
+#else
+#define GLCM_MARK(k, pt) \
+  do {                   \
+  } while (0)
+#endif
+
+constexpr int kTT = 1024;            // GLCM block: 32 rows x 32 columns (16 waves)
+constexpr int kRows = kTT / 32;
+constexpr int kTabW = 32768;         // packed u16 pair counters (128 KiB)
+constexpr int kCrop = kFastCropPx;   // u8 crop capacity (pixels)
+constexpr int kMaskW = kFastMaskWords;  // membership bitmask words (bh * ceil(bw/32))
+constexpr int kNW = kTT / 64;
+constexpr int kNG = 11;              // u32 partial sums per thread and angle (see glcm_angle)
+constexpr int kRedW = 192;           // LDS words for the cross-wave reduction (>= kNG * kNW)
+
+__device__ __forceinline__ int quantize(float v, bool in, float mn, float rng, bool flat) {
+  const float m = v * (in ? 1.0f : 0.0f);
+  if (flat) return 0;
+  float x = m - mn;  // scale_to_8bit: 255.0 * (x - min) / (max - min), fp32, truncation
+  x = 255.0f * x;
+  x = x / rng;
+  return (int)(unsigned char)(int)x;
+}
+
+__device__ __forceinline__ bool mask_bit(const unsigned int* m, int wpr, int r, int c) {
+  return (m[r * wpr + (c >> 5)] >> (c & 31)) & 1u;
+}
+
+// Wave-wide sum of a u32 on the VALU/DPP path (no LDS traffic); the result is wave-uniform.
+// row_shr 1,2,4,8 = inclusive scan within each row of 16 lanes; row_bcast:15 / row_bcast:31
+// carry the row totals upward, so lane 63 holds the wave total.
+__device__ __forceinline__ unsigned int wave_sum_u32(unsigned int v) {
+  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+  return (unsigned int)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// One GLCM angle (skimage graycomatrix offset (dr, dc), symmetric=False, normed) over an 8-bit
+// crop in LDS (or the global scratch slot), followed by greycoprops.  Every sum is an exact
+// integer: with at most 65535 pairs per object all block totals fit in u32 (sum i^2 <=
+// 65535 * 255^2 < 2^32, sum c^2 <= 65535^2 < 2^32), so a thread keeps
+//   (sum i << 32 | sum j), (sum i^2 << 32 | sum j^2), sum ij, ASM, background pairs,
+//   |i-j| counts for d < 8 in packed 16-bit fields, d >= 8 in an LDS histogram,
+// and the ASM (= sum over keys of count^2) comes from the returned old counts of a packed u16
+// 64K-entry LDS table: adding 1 to count c adds 2c + 1.  Pairs (0, 0) (background) bypass
+// the table and enter ASM as bg^2.
+template <bool LDS_CROP>
+__device__ void glcm_angle(const unsigned char* __restrict__ crop, unsigned int* tab,
+                           unsigned int* dh, unsigned int* red, int bh, int bw, int dr, int dc,
+                           double* out, long long* pt) {
+  const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int rend = bh - dr;  // dr >= 0
+  const int cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
+  const long long T = (rend > 0 && cend > cbeg) ? (long long)rend * (cend - cbeg) : 0;
+  unsigned long long s1 = 0, s2 = 0, dlo = 0, dhi = 0;
+  unsigned int sx = 0, asum = 0, bg = 0;
+  for (int r = ty; r < rend; r += kRows) {
+    const unsigned char* row = crop + r * bw;
+    const unsigned char* row2 = crop + (r + dr) * bw + dc;
+    for (int c0 = cbeg + tx; c0 < cend; c0 += 128) {
+      int key[4];
+      unsigned int old[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = c0 + 32 * u;
+        key[u] = 0;
+        if (c < cend) {
+          const unsigned int i = row[c], j = row2[c];
+          s1 += ((unsigned long long)i << 32) | j;
+          s2 += ((unsigned long long)(i * i) << 32) | (j * j);
+          sx += i * j;
+          if ((i | j) == 0) {
+            ++bg;
+          } else {
+            const int d = abs((int)i - (int)j);
+            if (d < 4) dlo += 1ull << (16 * d);
+            else if (d < 8) dhi += 1ull << (16 * (d - 4));
+            else atomicAdd(&dh[d], 1u);
+            key[u] = (int)((i << 8) | j);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        old[u] = key[u] != 0 ? atomicAdd(&tab[key[u] >> 1], 1u << ((key[u] & 1) * 16)) : 0u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (key[u] != 0) asum += 2u * ((old[u] >> ((key[u] & 1) * 16)) & 0xffffu) + 1u;
+    }
+  }
+  __syncthreads();
+  GLCM_MARK(2, pt);
+  {
+    const unsigned int w[kNG] = {(unsigned int)(s1 >> 32), (unsigned int)s1,
+                                 (unsigned int)(s2 >> 32), (unsigned int)s2,
+                                 sx, asum, bg,
+                                 (unsigned int)dlo, (unsigned int)(dlo >> 32),
+                                 (unsigned int)dhi, (unsigned int)(dhi >> 32)};
+#pragma unroll
+    for (int k = 0; k < kNG; ++k) {
+      const unsigned int t = wave_sum_u32(w[k]);
+      if (lane == 0) red[k * kNW + wid] = t;
+    }
+  }
+  __syncthreads();
+  GLCM_MARK(3, pt);
+  if (wid == 0) {  // greycoprops on one wave; the others clear the pair table meanwhile
+    unsigned int t = 0;
+    if (lane < kNG)
+#pragma unroll
+      for (int x = 0; x < kNW; ++x) t += red[lane * kNW + x];
+    const unsigned int si = __builtin_amdgcn_readlane(t, 0), sj = __builtin_amdgcn_readlane(t, 1);
+    const unsigned int sii = __builtin_amdgcn_readlane(t, 2), sjj = __builtin_amdgcn_readlane(t, 3);
+    const unsigned int sij = __builtin_amdgcn_readlane(t, 4), as = __builtin_amdgcn_readlane(t, 5);
+    const unsigned int nbg = __builtin_amdgcn_readlane(t, 6);
+    const unsigned int p01 = __builtin_amdgcn_readlane(t, 7), p23 = __builtin_amdgcn_readlane(t, 8);
+    const unsigned int p45 = __builtin_amdgcn_readlane(t, 9), p67 = __builtin_amdgcn_readlane(t, 10);
+    unsigned int ct = 0, dt = 0;
+    double h = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int d = lane * 4 + q;
+      unsigned int cnt;
+      if (d < 8) {
+        const unsigned int pw = d < 2 ? p01 : d < 4 ? p23 : d < 6 ? p45 : p67;
+        cnt = (pw >> (16 * (d & 1))) & 0xffffu;
+        if (d == 0) cnt += nbg;
+      } else {
+        cnt = dh[d];
+        dh[d] = 0u;  // restore for the next angle (this wave is the only reader)
+      }
+      ct += cnt * (unsigned int)(d * d);
+      dt += cnt * (unsigned int)d;
+      h += (double)cnt * (1.0 / (1.0 + (double)(d * d)));
+    }
+    ct = wave_sum_u32(ct);
+    dt = wave_sum_u32(dt);
+    h = wave_sum(h);
+    if (lane == 0) {
+      double con = 0.0, dis = 0.0, hom = 0.0, asmv = 0.0, ene = 0.0, cor = 1.0;
+      if (T > 0) {
+        const double Td = (double)T;
+        con = (double)ct / Td;
+        dis = (double)dt / Td;
+        hom = h / Td;
+        asmv = (double)((unsigned long long)as + (unsigned long long)nbg * nbg) / (Td * Td);
+        ene = sqrt(asmv);
+        const long long vi = T * (long long)sii - (long long)si * si;
+        const long long vj = T * (long long)sjj - (long long)sj * sj;
+        const long long cv = T * (long long)sij - (long long)si * sj;
+        const double sdi = sqrt((double)vi) / Td, sdj = sqrt((double)vj) / Td;
+        cor = (sdi < 1e-15 || sdj < 1e-15) ? 1.0 : ((double)cv / (Td * Td)) / (sdi * sdj);
+      }
+      out[CPX_TEX_CONTRAST] = con;
+      out[CPX_TEX_DISSIMILARITY] = dis;
+      out[CPX_TEX_HOMOGENEITY] = hom;
+      out[CPX_TEX_ASM] = asmv;
+      out[CPX_TEX_ENERGY] = ene;
+      out[CPX_TEX_CORRELATION] = cor;
+    }
+  } else {
+    // clearing the whole table with 16-byte stores (~1K LDS cycles) beats replaying the pairs
+    const uint4 z = {0u, 0u, 0u, 0u};
+    for (int x = threadIdx.x - 64; x < kTabW / 4; x += kTT - 64) reinterpret_cast<uint4*>(tab)[x] = z;
+  }
+  __syncthreads();
+  GLCM_MARK(4, pt);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Phase A (high occupancy, one block per (object, channel) item): intensity features and the
+// scale_to_8bit range from one coalesced pass over the bbox, then the 8-bit masked crop is
+// written to a global scratch slot (L2-resident until phase B reads it).
+constexpr int kAT = 256;  // 8 rows x 32 columns
+
+__global__ __launch_bounds__(kAT) void k_tex_stage(const int* __restrict__ labels,
+                                                  const float* __restrict__ corr, int C, int H,
+                                                  int W, int max_label, int F,
+                                                  const cpx_object* __restrict__ objects,
+                                                  const cpx_fov_objects* __restrict__ hdr,
+                                                  const long long* __restrict__ crop_off,
+                                                  unsigned char* __restrict__ scratch,
+                                                  long long scratch_per_fov,
+                                                  double* __restrict__ feats) {
+  __shared__ double sd[2][kAT / 64];
+  __shared__ long long sn[kAT / 64];
+  __shared__ float sf[4][kAT / 64];
+  const int fov = blockIdx.y;
+  const int n_items = hdr[fov].n_objects * C;
+  const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31, lane = threadIdx.x & 63,
+            wid = threadIdx.x >> 6;
+  const long long N = (long long)H * W;
+  const int* lab = labels + (long long)fov * N;
+  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+    const int k = item / C, ch = item - k * C;
+    const long long off = crop_off[(long long)fov * max_label + k];
+    if (off < 0) continue;  // not staged: fallback kernel
+    const cpx_object o = objects[(long long)fov * max_label + k];
+    const int r0 = o.bbox[0], c0 = o.bbox[1];
+    const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
+    const int L = o.label;
+    const float* img = corr + ((long long)fov * C + ch) * N + (long long)r0 * W + c0;
+    const int* lb = lab + (long long)r0 * W + c0;
+    long long n = 0;
+    double sm = 0.0, ss = 0.0;
+    float omin = INFINITY, omax = -INFINITY, mmin = INFINITY, mmax = -INFINITY;
+    for (int rb = 0; rb < bh; rb += 32) {  // 4 rows in flight per thread
+      float vv[4];
+      int ll[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = rb + ty + 8 * u;
+        vv[u] = 0.0f;
+        ll[u] = -1;
+        (void)r;
+      }
+      for (int c = tx; c < bw; c += 32) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = rb + ty + 8 * u;
+          if (r < bh) {
+            vv[u] = img[(long long)r * W + c];
+            ll[u] = lb[(long long)r * W + c];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = rb + ty + 8 * u;
+          if (r >= bh) continue;
+          const float v = vv[u];
+          const bool in = ll[u] == L;
+          const float m = v * (in ? 1.0f : 0.0f);
+          mmin = fminf(mmin, m);
+          mmax = fmaxf(mmax, m);
+          if (in) {
+            n += 1;
+            sm += (double)v;
+            ss += (double)v * (double)v;
+            omin = fminf(omin, v);
+            omax = fmaxf(omax, v);
+          }
+        }
+      }
+    }
+    n = wave_sum(n);
+    sm = wave_sum(sm);
+    ss = wave_sum(ss);
+    omin = wave_min(omin);
+    omax = wave_max(omax);
+    mmin = wave_min(mmin);
+    mmax = wave_max(mmax);
+    if (lane == 0) {
+      sn[wid] = n;
+      sd[0][wid] = sm;
+      sd[1][wid] = ss;
+      sf[0][wid] = omin;
+      sf[1][wid] = omax;
+      sf[2][wid] = mmin;
+      sf[3][wid] = mmax;
+    }
+    __syncthreads();
+    n = 0;
+    sm = ss = 0.0;
+    omin = mmin = INFINITY;
+    omax = mmax = -INFINITY;
+    for (int w = 0; w < kAT / 64; ++w) {
+      n += sn[w];
+      sm += sd[0][w];
+      ss += sd[1][w];
+      omin = fminf(omin, sf[0][w]);
+      omax = fmaxf(omax, sf[1][w]);
+      mmin = fminf(mmin, sf[2][w]);
+      mmax = fmaxf(mmax, sf[3][w]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double* f = feats + ((long long)fov * max_label + k) * F + CPX_N_SHAPE +
+                  (long long)ch * CPX_FEATURES_PER_CHANNEL;
+      const double mean = n ? sm / (double)n : 0.0;
+      double var = n ? (ss - sm * mean) / (double)n : 0.0;
+      if (var < 0.0) var = 0.0;
+      f[CPX_INT_INTEGRATED] = sm;
+      f[CPX_INT_MEAN] = mean;
+      f[CPX_INT_STD] = sqrt(var);
+      f[CPX_INT_MIN] = (double)omin;
+      f[CPX_INT_MAX] = (double)omax;
+    }
+    const float rng = mmax - mmin;
+    const bool flat = !(mmax != mmin);
+    unsigned char* dst = scratch + (long long)fov * scratch_per_fov + off +
+                         (long long)ch * (((long long)bh * bw + 15) / 16 * 16);
+    for (int r = ty; r < bh; r += 8)
+      for (int c = tx; c < bw; c += 32)
+        dst[r * bw + c] = (unsigned char)quantize(img[(long long)r * W + c],
+                                                  lb[(long long)r * W + c] == L, mmin, rng, flat);
+  }
+}
+
+struct GlcmItem {
+  int k, ch, bh, bw, nb;  // nb <= 0: nothing to do (past the end, no slot, or > 65535 px)
+  const unsigned char* src;
+};
+
+constexpr int kPre = (kCrop / 16 + kTT - 1) / kTT;  // uint4 prefetch registers per thread
+static_assert(kPre == 2, "glcm_prefetch holds two uint4 per thread");
+
+__device__ __forceinline__ GlcmItem glcm_item(int item, int n_items, int C, int fov,
+                                              int max_label, const cpx_object* objects,
+                                              const long long* crop_off,
+                                              const unsigned char* scratch,
+                                              long long scratch_per_fov) {
+  GlcmItem g{0, 0, 0, 0, 0, nullptr};
+  if (item >= n_items) return g;
+  g.k = item / C;
+  g.ch = item - g.k * C;
+  const long long off = crop_off[(long long)fov * max_label + g.k];
+  const cpx_object& o = objects[(long long)fov * max_label + g.k];
+  g.bh = o.bbox[2] - o.bbox[0];
+  g.bw = o.bbox[3] - o.bbox[1];
+  const int nb = g.bh * g.bw;
+  if (off < 0 || nb > 65535) return g;  // u32 / packed u16 sums: fallback kernel
+  g.nb = nb;
+  g.src = scratch + (long long)fov * scratch_per_fov + off + (long long)g.ch * ((nb + 15) / 16 * 16);
+  return g;
+}
+
+__device__ __forceinline__ void glcm_prefetch(const GlcmItem& g, uint4& p0, uint4& p1) {
+  if (g.nb <= 0 || g.nb > kCrop) return;
+  const int n16 = (g.nb + 15) / 16;
+  const uint4* s16 = reinterpret_cast<const uint4*>(g.src);
+  if ((int)threadIdx.x < n16) p0 = s16[threadIdx.x];
+  if ((int)threadIdx.x + kTT < n16) p1 = s16[threadIdx.x + kTT];
+}
+
+// Phase B (one 1024-thread block per CU, 128 KiB LDS pair table): GLCM of staged crops.
+__global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
+                                                 const cpx_object* __restrict__ objects,
+                                                 const cpx_fov_objects* __restrict__ hdr,
+                                                 const long long* __restrict__ crop_off,
+                                                 const unsigned char* __restrict__ scratch,
+                                                 long long scratch_per_fov,
+                                                 double* __restrict__ feats) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned int* tab = reinterpret_cast<unsigned int*>(smem);
+  unsigned int* dh = tab + kTabW;
+  unsigned int* red = dh + 256;
+  unsigned char* crop = reinterpret_cast<unsigned char*>(red + kRedW);
+  const int fov = blockIdx.y;
+  const int n_items = hdr[fov].n_objects * C;
+  if ((int)blockIdx.x >= n_items) return;
+  for (int x = threadIdx.x; x < kTabW; x += kTT) tab[x] = 0u;
+  for (int x = threadIdx.x; x < 256; x += kTT) dh[x] = 0u;
+  __syncthreads();
+  // software pipeline: the next item's metadata and LDS-sized crop are loaded into registers
+  // while the current item runs its four angles (the crop was written by k_tex_stage, possibly
+  // on another XCD, so the loads are HBM/MALL latency).
+  GlcmItem cur = glcm_item(blockIdx.x, n_items, C, fov, max_label, objects, crop_off, scratch,
+                           scratch_per_fov);
+  uint4 p0 = {0u, 0u, 0u, 0u}, p1 = {0u, 0u, 0u, 0u};
+  glcm_prefetch(cur, p0, p1);
+  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+    if (cur.nb > 0 && cur.nb <= kCrop) {
+      const int n16 = (cur.nb + 15) / 16;
+      if ((int)threadIdx.x < n16) reinterpret_cast<uint4*>(crop)[threadIdx.x] = p0;
+      if ((int)threadIdx.x + kTT < n16) reinterpret_cast<uint4*>(crop)[threadIdx.x + kTT] = p1;
+    }
+    __syncthreads();
+    const GlcmItem it = cur;
+    cur = glcm_item(item + gridDim.x, n_items, C, fov, max_label, objects, crop_off, scratch,
+                    scratch_per_fov);
+    glcm_prefetch(cur, p0, p1);
+    if (it.nb <= 0) continue;
+    double* f = feats + ((long long)fov * max_label + it.k) * F + CPX_N_SHAPE +
+                (long long)it.ch * CPX_FEATURES_PER_CHANNEL + CPX_N_INT;
+    long long pt = 0;
+#ifdef CPX_GLCM_PROF
+    if (threadIdx.x == 0) {
+      pt = clock64();
+      atomicAdd(&g_glcm_prof[5], 1ull);
+      atomicAdd(&g_glcm_prof[6], (unsigned long long)it.nb);
+      if (it.nb > kCrop) atomicAdd(&g_glcm_prof[7], 1ull);
+    }
+#endif
+    // skimage offsets (dr, dc) for angles 0, pi/4, pi/2, 3pi/4 at distance 3
+    for (int a = 0; a < CPX_N_ANGLES; ++a) {
+      const int dr = a == 0 ? 0 : a == 2 ? 3 : 2;
+      const int dc = a == 0 ? 3 : a == 1 ? 2 : a == 2 ? 0 : -2;
+      if (it.nb <= kCrop)
+        glcm_angle<true>(crop, tab, dh, red, it.bh, it.bw, dr, dc, f + a * CPX_N_TEX_PROPS, &pt);
+      else
+        glcm_angle<false>(it.src, tab, dh, red, it.bh, it.bw, dr, dc, f + a * CPX_N_TEX_PROPS, &pt);
+    }
+  }
+}
+
+// crop slots: per FOV exclusive scan of C * bbox area; objects beyond the scratch capacity or
+// with bbox > 65535 px get -1 (fallback kernel).
+__global__ __launch_bounds__(1024) void k_crop_offsets(int C, int max_label,
+                                                      const cpx_object* __restrict__ objects,
+                                                      const cpx_fov_objects* __restrict__ hdr,
+                                                      long long cap, long long* __restrict__ crop_off) {
+  const int fov = blockIdx.x;
+  const int n = hdr[fov].n_objects;
+  __shared__ long long wsum[16];
+  __shared__ long long base;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int k0 = 0; k0 < n; k0 += blockDim.x) {
+    const int k = k0 + threadIdx.x;
+    long long sz = 0;
+    if (k < n) {
+      const cpx_object o = objects[(long long)fov * max_label + k];
+      const long long nb = (long long)(o.bbox[2] - o.bbox[0]) * (o.bbox[3] - o.bbox[1]);
+      sz = nb <= 65535 ? ((nb + 15) / 16) * 16 * C : 0;
+    }
+    // inclusive wave scan
+    long long x = sz;
+    for (int d = 1; d < 64; d <<= 1) {
+      const long long y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    long long off = base;
+    for (int w = 0; w < wid; ++w) off += wsum[w];
+    off += x - sz;
+    if (k < n) crop_off[(long long)fov * max_label + k] = (sz > 0 && off + sz <= cap) ? off : -1;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      long long t = 0;
+      for (int w = 0; w < nw; ++w) t += wsum[w];
+      base += t;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// AreaShape fast path: bbox + 2-px margin membership bitmask in LDS
+constexpr int kST = 256;
+constexpr int kShapeW = kFastShapeWords;  // 48 KiB per bitmask (x2: membership + border)
+
+__device__ __forceinline__ unsigned int getw(const unsigned int* m, int wpr, int rows, int r, int cw) {
+  return (r < 0 || r >= rows || cw < 0 || cw >= wpr) ? 0u : m[r * wpr + cw];
+}
+
+__device__ __forceinline__ bool shape_fits(const cpx_object& o) {
+  return cpx_shape_fits(o.bbox[2] - o.bbox[0], o.bbox[3] - o.bbox[1]);
+}
+
+__global__ __launch_bounds__(kST) void k_shape_fast(const int* __restrict__ labels, int H, int W,
+                                                   int max_label, int F,
+                                                   const cpx_object* __restrict__ objects,
+                                                   const cpx_fov_objects* __restrict__ hdr,
+                                                   double* __restrict__ feats) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned int* M = reinterpret_cast<unsigned int*>(smem);
+  unsigned int* Bd = M + kShapeW;
+  __shared__ long long red[6][kST / 64];
+  __shared__ int redi[3][kST / 64];
+  const int fov = blockIdx.y;
+  const int nobj = hdr[fov].n_objects;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31;  // 8 x 32
+  const int* lab = labels + (long long)fov * H * W;
+  for (int k = blockIdx.x; k < nobj; k += gridDim.x) {
+    const cpx_object o = objects[(long long)fov * max_label + k];
+    if (!shape_fits(o)) continue;
+    const int L = o.label;
+    const int R0 = o.bbox[0] - 2, C0 = o.bbox[1] - 2;  // region origin (2-px margin)
+    const int rows = o.bbox[2] - o.bbox[0] + 4, cols = o.bbox[3] - o.bbox[1] + 4;
+    const int wpr = (cols + 31) >> 5;
+    __syncthreads();
+    for (int r = ty; r < rows; r += 8) {
+      for (int cw = 0; cw < wpr; ++cw) {
+        const int c = cw * 32 + tx;
+        const int gr = R0 + r, gc = C0 + c;
+        const bool in = c < cols && gr >= 0 && gr < H && gc >= 0 && gc < W &&
+                        lab[(long long)gr * W + gc] == L;
+        const unsigned long long b = __ballot(in);
+        if (lane == 0) M[r * wpr + cw] = (unsigned int)b;
+        if (lane == 32) M[r * wpr + cw] = (unsigned int)(b >> 32);
+      }
+    }
+    __syncthreads();
+    // border = in & !(up & down & left & right)
+    for (int w = threadIdx.x; w < rows * wpr; w += kST) {
+      const int r = w / wpr, cw = w - r * wpr;
+      const unsigned int x = M[w];
+      const unsigned int up = getw(M, wpr, rows, r - 1, cw), dn = getw(M, wpr, rows, r + 1, cw);
+      const unsigned int lf = (x << 1) | (getw(M, wpr, rows, r, cw - 1) >> 31);
+      const unsigned int rt = (x >> 1) | (getw(M, wpr, rows, r, cw + 1) << 31);
+      Bd[w] = x & ~(up & dn & lf & rt);
+    }
+    __syncthreads();
+    long long n = 0, sr = 0, sc = 0, srr = 0, scc = 0, src = 0;
+    int n1 = 0, n2 = 0, n3 = 0;
+    for (int w = threadIdx.x; w < rows * wpr; w += kST) {
+      const int r = w / wpr, cw = w - r * wpr;
+      unsigned int x = M[w];
+      const unsigned int bx = Bd[w];
+      while (x) {
+        const int b = __ffs(x) - 1;
+        x &= x - 1;
+        const int c = cw * 32 + b;
+        const long long rr = r - 2, cc = c - 2;  // bbox-local coordinates
+        n += 1;
+        sr += rr;
+        sc += cc;
+        srr += rr * rr;
+        scc += cc * cc;
+        src += rr * cc;
+        if (!((bx >> b) & 1u)) continue;
+        auto bit = [&](int rr2, int cc2) -> int {
+          return (int)((getw(Bd, wpr, rows, rr2, cc2 >> 5) >> (cc2 & 31)) & 1u);
+        };
+        const int code = 1 + 2 * (bit(r - 1, c) + bit(r + 1, c) + bit(r, c - 1) + bit(r, c + 1)) +
+                         10 * (bit(r - 1, c - 1) + bit(r - 1, c + 1) + bit(r + 1, c - 1) + bit(r + 1, c + 1));
+        if (code == 5 || code == 7 || code == 15 || code == 17 || code == 25 || code == 27) n1 += 1;
+        else if (code == 21 || code == 33) n2 += 1;
+        else if (code == 13 || code == 23) n3 += 1;
+      }
+    }
+    n = wave_sum(n); sr = wave_sum(sr); sc = wave_sum(sc);
+    srr = wave_sum(srr); scc = wave_sum(scc); src = wave_sum(src);
+    n1 = wave_sum(n1); n2 = wave_sum(n2); n3 = wave_sum(n3);
+    if (lane == 0) {
+      red[0][wid] = n; red[1][wid] = sr; red[2][wid] = sc;
+      red[3][wid] = srr; red[4][wid] = scc; red[5][wid] = src;
+      redi[0][wid] = n1; redi[1][wid] = n2; redi[2][wid] = n3;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      n = sr = sc = srr = scc = src = 0;
+      n1 = n2 = n3 = 0;
+      for (int w = 0; w < kST / 64; ++w) {
+        n += red[0][w]; sr += red[1][w]; sc += red[2][w];
+        srr += red[3][w]; scc += red[4][w]; src += red[5][w];
+        n1 += redi[0][w]; n2 += redi[1][w]; n3 += redi[2][w];
+      }
+      double* f = feats + ((long long)fov * max_label + k) * F;
+      const double SQ2 = 1.4142135623730951;
+      const double area = (double)n;
+      const int r0 = o.bbox[0], c0 = o.bbox[1], r1 = o.bbox[2], c1 = o.bbox[3];
+      const double bba = (double)(r1 - r0) * (double)(c1 - c0);
+      f[CPX_SHAPE_AREA] = area;
+      f[CPX_SHAPE_PERIMETER] = (double)n1 + (double)n2 * SQ2 + (double)n3 * ((1.0 + SQ2) / 2.0);
+      f[CPX_SHAPE_CENTER_Y] = o.centroid_r;
+      f[CPX_SHAPE_CENTER_X] = o.centroid_c;
+      f[CPX_SHAPE_BBOX_AREA] = bba;
+      f[CPX_SHAPE_EXTENT] = area / bba;
+      f[CPX_SHAPE_EQUIV_DIAMETER] = sqrt(4.0 * area / 3.14159265358979323846);
+      const i128 NN = n;
+      const i128 m20n = NN * srr - (i128)sr * sr;
+      const i128 m02n = NN * scc - (i128)sc * sc;
+      const i128 m11n = NN * src - (i128)sr * sc;
+      const double n2d = area * area;
+      const double a = (double)m02n / n2d, b = -(double)m11n / n2d, c = (double)m20n / n2d;
+      const double hm = 0.5 * (a + c), hd = 0.5 * (a - c);
+      const double rt = sqrt(hd * hd + b * b);
+      double l1 = hm + rt;
+      const i128 detn4 = m02n * m20n - m11n * m11n;
+      double l2 = (l1 > 0.0) ? ((double)detn4 / (n2d * n2d)) / l1 : 0.0;
+      if (l1 < 0.0) l1 = 0.0;
+      if (l2 < 0.0) l2 = 0.0;
+      if (l2 > l1) l2 = l1;
+      f[CPX_SHAPE_MAJOR_AXIS] = 4.0 * sqrt(l1);
+      f[CPX_SHAPE_MINOR_AXIS] = 4.0 * sqrt(l2);
+      f[CPX_SHAPE_ECCENTRICITY] = (l1 == 0.0) ? 0.0 : sqrt(1.0 - l2 / l1);
+      f[CPX_SHAPE_ORIENTATION] = (a - c == 0.0) ? ((b < 0.0) ? -3.14159265358979323846 / 4.0
+                                                              : 3.14159265358979323846 / 4.0)
+                                                : 0.5 * atan2(-2.0 * b, c - a);
+      f[CPX_SHAPE_BBOX_MIN_Y] = r0;
+      f[CPX_SHAPE_BBOX_MIN_X] = c0;
+      f[CPX_SHAPE_BBOX_MAX_Y] = r1;
+      f[CPX_SHAPE_BBOX_MAX_X] = c1;
+    }
+  }
+}
+
+}  // namespace
+
+
+// internal launchers used by cpx_features (k_features.hip)
+int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B, int C,
+                      int H, int W, int max_label, int F, const cpx_object* objects_dev,
+                      const cpx_fov_objects* hdr_dev, double* feats_dev, long long** crop_off_out) {
+  static bool attr = false;
+  const size_t lds_t = sizeof(unsigned int) * (kTabW + 256 + kRedW) + kCrop;
+  static_assert(sizeof(unsigned int) * (kTabW + 256 + kRedW) + kCrop <= 160 * 1024,
+                "GLCM LDS budget");
+  static_assert(kNG * kNW <= kRedW, "reduction scratch");
+  const size_t lds_s = sizeof(unsigned int) * 2 * kShapeW;
+  if (!attr) {
+    CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_tex_glcm,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_t));
+    CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_shape_fast,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_s));
+    attr = true;
+  }
+  // workspace: crop offsets [B][max_label] + scratch (2 bytes per pixel-channel per FOV)
+  const long long per_fov = ((2LL * H * W * C + 255) / 256) * 256;
+  const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + 255) / 256) * 256;
+  unsigned char* ws = (unsigned char*)cpx_ws(ctx, WS_MISC, off_bytes + (size_t)B * per_fov);
+  if (!ws) return CPX_ERR_OOM;
+  long long* crop_off = (long long*)ws;
+  unsigned char* scratch = ws + off_bytes;
+  *crop_off_out = crop_off;
+  hipLaunchKernelGGL(k_crop_offsets, dim3(B), dim3(1024), 0, ctx->stream, C, max_label,
+                     objects_dev, hdr_dev, per_fov, crop_off);
+  CPX_CHECK_LAUNCH("k_crop_offsets");
+  const int per_fov_s = std::max(1, std::min(max_label, (4 * ctx->n_cu + B - 1) / B));
+  hipLaunchKernelGGL(k_shape_fast, dim3(per_fov_s, B), dim3(kST), lds_s, ctx->stream,
+                     (const int*)labels_dev, H, W, max_label, F, objects_dev, hdr_dev, feats_dev);
+  CPX_CHECK_LAUNCH("k_shape_fast");
+  const int per_fov_a = std::max(1, std::min(max_label * C, (16 * ctx->n_cu + B - 1) / B));
+  hipLaunchKernelGGL(k_tex_stage, dim3(per_fov_a, B), dim3(kAT), 0, ctx->stream,
+                     (const int*)labels_dev, corr_dev, C, H, W, max_label, F, objects_dev, hdr_dev,
+                     (const long long*)crop_off, scratch, per_fov, feats_dev);
+  CPX_CHECK_LAUNCH("k_tex_stage");
+  const int per_fov_t = std::max(1, std::min(max_label * C, (ctx->n_cu + B - 1) / B));
+  hipLaunchKernelGGL(k_tex_glcm, dim3(per_fov_t, B), dim3(kTT), lds_t, ctx->stream, C, max_label,
+                     F, objects_dev, hdr_dev, (const long long*)crop_off,
+                     (const unsigned char*)scratch, per_fov, feats_dev);
+  CPX_CHECK_LAUNCH("k_tex_glcm");
+  return CPX_OK;
+}
+
+#ifdef CPX_GLCM_PROF
+extern "C" int cpx_debug_glcm_prof(unsigned long long* host8, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return CPX_ERR_HIP;
+  if (host8 && hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_glcm_prof), 64) != hipSuccess) return CPX_ERR_HIP;
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_glcm_prof), z, 64) != hipSuccess) return CPX_ERR_HIP;
+  }
+  return CPX_OK;
+}
+#endif
