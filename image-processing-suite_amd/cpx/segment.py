@@ -16,6 +16,7 @@ import torch
 from . import _lib
 from ._lib import check
 from .cpnet import build_cpnet
+from .cpnet_fused import FusedCPnet
 from .device import Device, _ptr
 
 DIAM_MEAN = {"nuclei": 17.0, "cyto": 30.0, "cyto2": 30.0, "cyto3": 30.0}
@@ -98,6 +99,7 @@ class Segmenter:
     def __init__(self, dev: Device, H: int, W: int, batch: int, model: str = CELLPOSE_MODEL,
                  diameter: float = DIAMETER, weights: str | None = None, seed: int = 0,
                  use_graph: bool = True, max_objects: int = 4096, net_dtype=torch.bfloat16,
+                 fused: bool = True,
                  niter: int = NITER, flow_threshold: float = FLOW_THRESHOLD, min_size: int = MIN_SIZE):
         self.dev = dev
         self.H, self.W, self.B = H, W, batch
@@ -108,8 +110,10 @@ class Segmenter:
         self.niter, self.flow_threshold, self.min_size = niter, flow_threshold, min_size
         self.net_dtype = net_dtype
         self.net = build_cpnet(seed=seed, model=model, state_dict_path=weights).to(td)
-        self.net = self.net.to(memory_format=torch.channels_last, dtype=net_dtype)
         self.layout = 1 if net_dtype == torch.bfloat16 else 0
+        # bf16: MIOpen convs + libcpx fused epilogues (cpnet_fused); fp32: the eager module
+        self.fnet = FusedCPnet(self.net, dev) if (fused and self.layout == 1) else None
+        self.net = self.net.to(memory_format=torch.channels_last, dtype=net_dtype)
         nt = batch * g.n_tiles
         if self.layout == 1:
             self.tiles = torch.empty((nt, g.by, g.bx, NET_CHANNELS), dtype=torch.bfloat16, device=td)
@@ -128,6 +132,8 @@ class Segmenter:
 
     # -- network -----------------------------------------------------------------------------
     def _forward(self):
+        if self.fnet is not None:
+            return self.fnet(self.tiles_nchw)
         with torch.no_grad():
             y = self.net(self.tiles_nchw)
         return y

@@ -23,8 +23,8 @@ void* cpx_ws(cpx_ctx* ctx, int slot, size_t bytes) {
   if (ctx->ws_bytes[slot] >= bytes) return ctx->ws[slot];
   if (ctx->ws[slot]) {
     // the old buffer may still be in use by enqueued work
-    hipStreamSynchronize(ctx->stream);
-    hipFree(ctx->ws[slot]);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ctx->ws[slot]);
     ctx->ws[slot] = nullptr;
     ctx->ws_bytes[slot] = 0;
   }
@@ -70,11 +70,11 @@ int cpx_init(int device, cpx_ctx** out) {
 
 void cpx_destroy(cpx_ctx* ctx) {
   if (!ctx) return;
-  hipSetDevice(ctx->device);
-  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (int i = 0; i < kWsSlots; ++i)
-    if (ctx->ws[i]) hipFree(ctx->ws[i]);
-  if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+    if (ctx->ws[i]) (void)hipFree(ctx->ws[i]);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }
 

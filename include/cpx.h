@@ -260,6 +260,25 @@ int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx_seg_geom* 
                   int W, int niter, double flow_threshold, int min_size, int max_objects,
                   int32_t* labels_dev, cpx_seg_stats* stats_dev);
 
+/* ---- a4 CPnet glue (bf16 NHWC activations around MIOpen convolutions) ----------------------
+ * Cellpose resnet_torch.CPnet forward (used at Cellpose_GPU_s3fs.py:108-110 through
+ * models.CellposeModel.eval): every batchconv is BatchNorm -> ReLU -> Conv2d, blocks add
+ * residuals and (up path) a per-image style bias before the BatchNorm.  cpx_cpnet_epilogue
+ * fuses everything between two convolutions into one pass over [N, Hh, Ww, Cn] bf16:
+ *   t = conv + bias[c] + res          (conv, bias, res optional; res_up: res is [N,Hh/2,Ww/2,Cn]
+ *                                      read nearest-upsampled)            -> y_out (optional)
+ *   z = relu?(scale[c] * (t + style[n*Cn+c]) + shift[c])  (style, scale/shift optional)
+ *                                                                        -> z_out (optional;
+ *                                      z_up: written 2x nearest-upsampled, [N,2Hh,2Ww,Cn])
+ * cpx_cpnet_pool: 2x2/2 max-pool of [N,2Hh,2Ww,Cn] -> x_out [N,Hh,Ww,Cn] and
+ *   z_out = relu?(scale[c] * x + shift[c]).  fp32 arithmetic, bf16 (RNE) stores.            */
+int cpx_cpnet_epilogue(cpx_ctx* ctx, const void* conv, const float* bias, const void* res,
+                       int res_up, const float* style, const float* scale, const float* shift,
+                       int relu, int N, int Hh, int Ww, int Cn, void* y_out, void* z_out,
+                       int z_up);
+int cpx_cpnet_pool(cpx_ctx* ctx, const void* in, const float* scale, const float* shift,
+                   int relu, int N, int Hh, int Ww, int Cn, void* x_out, void* z_out);
+
 #ifdef __cplusplus
 }
 #endif

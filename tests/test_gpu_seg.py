@@ -158,3 +158,102 @@ def test_segmenter_end_to_end(dev):
     st = seg.seg_stats()
     for i in range(B):
         assert a[i].min() >= 0 and a[i].max() == st[i]["n_final"]
+
+
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,res_up,z_up,style,relu", [(32, False, False, True, True),
+                                                     (64, True, False, True, True),
+                                                     (128, False, True, False, True),
+                                                     (3, True, True, True, False),
+                                                     (2, False, False, False, True)])
+def test_cpnet_epilogue_exact(dev, C, res_up, z_up, style, relu):
+    """cpx_cpnet_epilogue == the same fp32 op sequence in torch, rounded once to bf16."""
+    from cpx.cpnet_fused import FusedCPnet  # noqa: F401  (module under test uses the same lib)
+    from cpx.cpnet_fused import _p
+    td = dev.torch_device
+    g = torch.Generator().manual_seed(C)
+    N, H, W = 3, 16, 24
+    CL = torch.channels_last
+    conv = _bf(torch.randn(N, C, H, W, generator=g)).to(td).contiguous(memory_format=CL)
+    bias = torch.randn(C, generator=g).to(td)
+    rs = (N, C, H // 2, W // 2) if res_up else (N, C, H, W)
+    res = _bf(torch.randn(*rs, generator=g)).to(td).contiguous(memory_format=CL)
+    sty = torch.randn(N, C, generator=g).to(td) if style else None
+    scale = torch.randn(C, generator=g).to(td)
+    shift = torch.randn(C, generator=g).to(td)
+    yo = torch.empty_like(conv, memory_format=CL)
+    zs = (N, C, 2 * H, 2 * W) if z_up else (N, C, H, W)
+    zo = torch.empty(zs, dtype=torch.bfloat16, device=td, memory_format=CL)
+    check(dev.lib.cpx_cpnet_epilogue(dev.h, _p(conv), _p(bias), _p(res), int(res_up), _p(sty),
+                                     _p(scale), _p(shift), int(relu), N, H, W, C, _p(yo), _p(zo),
+                                     int(z_up)), "epilogue")
+    r = res.float()
+    if res_up:
+        r = r.repeat_interleave(2, 2).repeat_interleave(2, 3)
+    t = conv.float() + bias[None, :, None, None] + r
+    u = t + (sty[:, :, None, None] if style else 0.0)
+    z = scale[None, :, None, None] * u + shift[None, :, None, None]
+    if relu:
+        z = torch.clamp_min(z, 0.0)
+    zb = _bf(z)
+    if z_up:
+        zb = zb.repeat_interleave(2, 2).repeat_interleave(2, 3)
+    dev.sync()
+    assert torch.equal(yo.float().cpu(), _bf(t).float().cpu())
+    assert torch.equal(zo.float().cpu(), zb.float().cpu())
+
+
+@pytest.mark.gpu
+def test_cpnet_pool_exact(dev):
+    from cpx.cpnet_fused import _p
+    td = dev.torch_device
+    g = torch.Generator().manual_seed(5)
+    N, C, H, W = 2, 64, 28, 20
+    CL = torch.channels_last
+    x = _bf(torch.randn(N, C, H, W, generator=g)).to(td).contiguous(memory_format=CL)
+    scale = torch.randn(C, generator=g).to(td)
+    shift = torch.randn(C, generator=g).to(td)
+    xo = torch.empty((N, C, H // 2, W // 2), dtype=torch.bfloat16, device=td, memory_format=CL)
+    zo = torch.empty_like(xo, memory_format=CL)
+    check(dev.lib.cpx_cpnet_pool(dev.h, _p(x), _p(scale), _p(shift), 1, N, H // 2, W // 2, C,
+                                 _p(xo), _p(zo)), "pool")
+    ref = torch.nn.functional.max_pool2d(x.float(), 2, 2)
+    z = torch.clamp_min(scale[None, :, None, None] * ref + shift[None, :, None, None], 0.0)
+    dev.sync()
+    assert torch.equal(xo.float().cpu(), ref.cpu())
+    assert torch.equal(zo.float().cpu(), _bf(z).float().cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,trained", [((2, 224, 224), False), ((3, 144, 160), False),
+                                           ((2, 224, 224), True)])
+def test_fused_cpnet_matches_fp32_module(dev, shape, trained):
+    """Fused bf16 schedule vs the eager fp32 module (same weights): bf16-level agreement."""
+    import os
+    from cpx.cpnet_fused import FusedCPnet
+    wpath = os.path.join(os.path.dirname(__file__), "..", "image-processing-suite_amd", "cpx",
+                         "weights", "cpnet_nuclei_synth.pt")
+    if trained and not os.path.exists(wpath):
+        pytest.skip("no trained weights")
+    net = build_cpnet(seed=3, state_dict_path=wpath if trained else None).to(dev.torch_device)
+    fused = FusedCPnet(net, dev)
+    N, H, W = shape
+    g = torch.Generator().manual_seed(N * H)
+    x = torch.rand(N, 2, H, W, generator=g).to(dev.torch_device) * 3.0
+    with torch.no_grad():
+        ref = net(x).float()
+        out = fused(_bf(x).contiguous(memory_format=torch.channels_last)).float()
+        eager = net.to(memory_format=torch.channels_last, dtype=torch.bfloat16)(
+            _bf(x).contiguous(memory_format=torch.channels_last)).float()
+    dev.sync()
+    err_f = (out - ref).abs()
+    err_e = (eager - ref).abs()
+    c = np.corrcoef(out.cpu().numpy().ravel(), ref.cpu().numpy().ravel())[0, 1]
+    assert c > 0.999, c
+    # no worse than the eager bf16 module (which rounds after every op)
+    assert err_f.mean().item() <= 1.25 * err_e.mean().item(), (err_f.mean().item(), err_e.mean().item())
+    assert err_f.max().item() <= 2.0 * err_e.max().item(), (err_f.max().item(), err_e.max().item())
