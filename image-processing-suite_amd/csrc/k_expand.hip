@@ -12,8 +12,8 @@
 // the lexicographic minimum of (squared distance, column, row) — which only needs the columns
 // within `distance` of the pixel when the result is kept (distance <= D), so both passes are
 // bounded-window here:
-//   pass 1 (one thread per column, coalesced): signed offset to the nearest feature row in the
-//          column within D (int8; none = -128);
+//   pass 1 (one thread per column and 64-row tile, coalesced): signed offset to the nearest
+//          feature row in the column within D (int8; none = -128);
 //   pass 2 (one thread per pixel, row segment + halo staged in LDS): scan the 2D+1 columns in
 //          ascending order with a strict `<` (smaller column wins ties), threshold d^2 <= D^2.
 // Bit-identical to skimage/scipy (tests/test_gpu_parity.py, including equidistant ties).
@@ -24,26 +24,32 @@ namespace {
 constexpr int kT = 256;
 constexpr signed char kNone = -128;
 
-// pass 1: per column, nearest feature row within +-D (down sweep then up sweep)
+// pass 1: per column and tile of kColTile rows, nearest feature row within +-D (down sweep from
+// D rows above the tile, then up sweep from D rows below it)
+constexpr int kColTile = 64;
+
 __global__ __launch_bounds__(kT) void k_edt_cols(const int* __restrict__ labels, int H, int W,
                                                  int D, signed char* __restrict__ off) {
-  const int fov = blockIdx.y;
+  const int fov = blockIdx.z;
   const int col = blockIdx.x * kT + threadIdx.x;
   if (col >= W) return;
+  const int r0 = blockIdx.y * kColTile, r1 = min(H, r0 + kColTile);
   const long long base = (long long)fov * H * W + col;
   const int* lab = labels + base;
   signed char* o = off + base;
   // down sweep: distance to the last feature at or above (stored), capped at D+1
   int last = -0x40000000;
-  for (int r = 0; r < H; ++r) {
+  for (int r = max(0, r0 - D); r < r1; ++r) {
     if (lab[(long long)r * W] != 0) last = r;
+    if (r < r0) continue;
     const int du = r - last;
     o[(long long)r * W] = du <= D ? (signed char)(-du) : kNone;  // feature above (or here)
   }
   // up sweep: next feature at or below; keep the above one on ties (smaller row)
   int next = 0x40000000;
-  for (int r = H - 1; r >= 0; --r) {
+  for (int r = min(H, r1 + D) - 1; r >= r0; --r) {
     if (lab[(long long)r * W] != 0) next = r;
+    if (r >= r1) continue;
     const int dd = next - r;
     if (dd > D) continue;
     const signed char cur = o[(long long)r * W];
@@ -95,7 +101,8 @@ extern "C" int cpx_expand_labels(cpx_ctx* ctx, const int32_t* nuclei_dev, int B,
               CPX_ERR_ARG, "cpx_expand_labels: bad sizes (distance must be <= 127)");
   signed char* off = (signed char*)cpx_ws(ctx, WS_FEAT, (size_t)B * H * W + 256);
   if (!off) return CPX_ERR_OOM;
-  hipLaunchKernelGGL(k_edt_cols, dim3(cpx_div_up(W, kT), B), dim3(kT), 0, ctx->stream,
+  hipLaunchKernelGGL(k_edt_cols, dim3(cpx_div_up(W, kT), cpx_div_up(H, kColTile), B), dim3(kT),
+                     0, ctx->stream,
                      (const int*)nuclei_dev, H, W, distance, off);
   CPX_CHECK_LAUNCH("k_edt_cols");
   hipLaunchKernelGGL(k_edt_rows, dim3(cpx_div_up(W, kT), H, B), dim3(kT), kT + 2 * distance,

@@ -9,9 +9,10 @@
 //   :391-393 Cell_ID = f"{well}_{site}_cell{cell_idx}", cell_idx = rank among kept cells
 //   :34-43 scale_to_8bit: uint8(255.0 * (x.astype(f32) - min) / (max - min)), zeros if max == min
 // MI355X design: one streaming pass over the int32 label image accumulates exact int64 moments and
-// the bbox per label (runs along a row are aggregated in registers, one set of atomics per run —
-// integer atomics, so results are order independent and exact); a one-block-per-FOV finisher
-// compacts present labels in ascending order with a block scan.
+// the bbox per label (vertical runs aggregated in registers, merged per tile in an LDS hash table,
+// one set of global atomics per tile and label — integer atomics, so results are order
+// independent and exact); a one-block-per-FOV finisher compacts present labels in ascending
+// order with a block scan.
 #include "cpx_internal.h"
 #include <limits.h>
 #include <math.h>
@@ -19,7 +20,6 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kRun = 32;  // pixels per thread along a row
 
 __global__ void k_stats_init(cpx_label_stats* __restrict__ st, long long n,
                              cpx_fov_objects* __restrict__ hdr, int B) {
@@ -36,44 +36,91 @@ __global__ void k_stats_init(cpx_label_stats* __restrict__ st, long long n,
   if (i < B) hdr[i] = cpx_fov_objects{0, 0, 0, 0};
 }
 
-__device__ __forceinline__ void flush_run(cpx_label_stats* st, int label, int r, long long cnt,
-                                          long long sc, long long scc, int c0, int c1) {
-  cpx_label_stats* s = st + label;
+// Label statistics, one block per 32-row x 256-column tile of a FOV.  A thread walks one
+// column of the tile (loads coalesced across the wave), aggregates vertical runs of one label in
+// registers, and merges each run into a block-private LDS hash table keyed by label (exact
+// integer LDS atomics); the table is flushed with one set of global atomics per (tile, label).
+// Labels are compact, so a tile holds a handful of them: global atomics drop from one set per
+// run to one per tile and label.  A full table (pathological label images) spills runs
+// straight to global memory, so results never depend on the table size.
+constexpr int kTileR = 32;
+constexpr int kHash = 256;
+
+struct LdsStat {
+  int key;
+  unsigned int area, sum_r;
+  int rmin, rmax, cmin, cmax;
+  unsigned int sum_c;
+  unsigned long long sum_rr, sum_cc, sum_rc;
+};
+
+__device__ __forceinline__ void lds_flush_run(LdsStat* tab, cpx_label_stats* st, int label, int c,
+                                              int r0, int r1) {
+  // vertical run rows r0..r1 (inclusive) in column c
+  const long long cnt = r1 - r0 + 1;
+  const long long sr = (long long)(r0 + r1) * cnt / 2;
+  const long long srr = ((long long)r1 * (r1 + 1) * (2LL * r1 + 1) -
+                         (long long)(r0 - 1) * r0 * (2LL * r0 - 1)) / 6;
+  unsigned int h = ((unsigned int)label * 2654435761u) >> 24;
+  for (int probe = 0; probe < kHash; ++probe, h = (h + 1) & (kHash - 1)) {
+    const int k = atomicCAS(&tab[h].key, 0, label);
+    if (k == 0 || k == label) {
+      LdsStat* e = tab + h;
+      atomicAdd(&e->area, (unsigned int)cnt);
+      atomicAdd(&e->sum_r, (unsigned int)sr);
+      atomicAdd(&e->sum_c, (unsigned int)(cnt * c));
+      atomicAdd(&e->sum_rr, (unsigned long long)srr);
+      atomicAdd(&e->sum_cc, (unsigned long long)(cnt * c * c));
+      atomicAdd(&e->sum_rc, (unsigned long long)(sr * c));
+      atomicMin(&e->rmin, r0);
+      atomicMax(&e->rmax, r1);
+      atomicMin(&e->cmin, c);
+      atomicMax(&e->cmax, c);
+      return;
+    }
+  }
+  cpx_label_stats* s = st + label;  // table full: straight to global
   atomicAdd((unsigned long long*)&s->area, (unsigned long long)cnt);
-  atomicAdd((unsigned long long*)&s->sum_r, (unsigned long long)(cnt * r));
-  atomicAdd((unsigned long long*)&s->sum_c, (unsigned long long)sc);
-  atomicAdd((unsigned long long*)&s->sum_rr, (unsigned long long)(cnt * (long long)r * r));
-  atomicAdd((unsigned long long*)&s->sum_cc, (unsigned long long)scc);
-  atomicAdd((unsigned long long*)&s->sum_rc, (unsigned long long)(sc * r));
-  atomicMin(&s->rmin, r);
-  atomicMax(&s->rmax, r);
-  atomicMin(&s->cmin, c0);
-  atomicMax(&s->cmax, c1);
+  atomicAdd((unsigned long long*)&s->sum_r, (unsigned long long)sr);
+  atomicAdd((unsigned long long*)&s->sum_c, (unsigned long long)(cnt * c));
+  atomicAdd((unsigned long long*)&s->sum_rr, (unsigned long long)srr);
+  atomicAdd((unsigned long long*)&s->sum_cc, (unsigned long long)(cnt * c * c));
+  atomicAdd((unsigned long long*)&s->sum_rc, (unsigned long long)(sr * c));
+  atomicMin(&s->rmin, r0);
+  atomicMax(&s->rmax, r1);
+  atomicMin(&s->cmin, c);
+  atomicMax(&s->cmax, c);
 }
 
-// grid: (ceil(W/kRun/kThreads) * H rows..., B)
+// grid: (ceil(W / kThreads), ceil(H / kTileR), B)
 __global__ __launch_bounds__(kThreads) void k_label_stats(const int* __restrict__ labels, int H,
                                                           int W, int max_label,
                                                           cpx_label_stats* __restrict__ stats,
                                                           cpx_fov_objects* __restrict__ hdr) {
-  const int fov = blockIdx.y;
-  const int segs_per_row = (W + kRun - 1) / kRun;
-  const long long seg = (long long)blockIdx.x * kThreads + threadIdx.x;
-  if (seg >= (long long)segs_per_row * H) return;
-  const int r = (int)(seg / segs_per_row);
-  const int c0 = (int)(seg % segs_per_row) * kRun;
-  const int c1 = min(W, c0 + kRun);
-  const int* row = labels + ((long long)fov * H + r) * W;
+  __shared__ LdsStat tab[kHash];
+  const int fov = blockIdx.z;
+  {
+    LdsStat e;
+    e.key = 0;
+    e.area = e.sum_r = e.sum_c = 0;
+    e.rmin = INT_MAX;
+    e.rmax = -1;
+    e.cmin = INT_MAX;
+    e.cmax = -1;
+    e.sum_rr = e.sum_cc = e.sum_rc = 0;
+    for (int i = threadIdx.x; i < kHash; i += kThreads) tab[i] = e;
+  }
+  __syncthreads();
+  const int c = blockIdx.x * kThreads + threadIdx.x;
+  const int r0 = blockIdx.y * kTileR, r1 = min(H, r0 + kTileR);
   cpx_label_stats* st = stats + (long long)fov * (max_label + 1);
-  int cur = 0, cmin = 0, cmax = 0, seen_max = 0;
-  long long cnt = 0, sc = 0, scc = 0;
+  int seen_max = 0;
   bool overflow = false;
-  for (int c = c0; c < c1; ++c) {
-    int l = row[c];
-    if (l != cur) {
-      if (cur > 0) flush_run(st, cur, r, cnt, sc, scc, cmin, cmax);
-      cur = 0;
-      cnt = sc = scc = 0;
+  if (c < W) {
+    const int* col = labels + (long long)fov * H * W + c;
+    int cur = 0, start = 0;
+    for (int r = r0; r < r1; ++r) {
+      int l = col[(long long)r * W];
       if (l > 0) {
         seen_max = max(seen_max, l);
         if (l > max_label) {
@@ -81,17 +128,30 @@ __global__ __launch_bounds__(kThreads) void k_label_stats(const int* __restrict_
           l = 0;
         }
       }
-      cur = l;
-      cmin = c;
+      if (l != cur) {
+        if (cur > 0) lds_flush_run(tab, st, cur, c, start, r - 1);
+        cur = l;
+        start = r;
+      }
     }
-    if (cur > 0) {
-      cnt += 1;
-      sc += c;
-      scc += (long long)c * c;
-      cmax = c;
-    }
+    if (cur > 0) lds_flush_run(tab, st, cur, c, start, r1 - 1);
   }
-  if (cur > 0) flush_run(st, cur, r, cnt, sc, scc, cmin, cmax);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHash; i += kThreads) {
+    const LdsStat e = tab[i];
+    if (e.key == 0) continue;
+    cpx_label_stats* s = st + e.key;
+    atomicAdd((unsigned long long*)&s->area, (unsigned long long)e.area);
+    atomicAdd((unsigned long long*)&s->sum_r, (unsigned long long)e.sum_r);
+    atomicAdd((unsigned long long*)&s->sum_c, (unsigned long long)e.sum_c);
+    atomicAdd((unsigned long long*)&s->sum_rr, e.sum_rr);
+    atomicAdd((unsigned long long*)&s->sum_cc, e.sum_cc);
+    atomicAdd((unsigned long long*)&s->sum_rc, e.sum_rc);
+    atomicMin(&s->rmin, e.rmin);
+    atomicMax(&s->rmax, e.rmax);
+    atomicMin(&s->cmin, e.cmin);
+    atomicMax(&s->cmax, e.cmax);
+  }
   // max label / overflow (wave-aggregated)
   seen_max = wave_max(seen_max);
   int ov = wave_max((int)overflow);
@@ -275,9 +335,9 @@ extern "C" int cpx_objects(cpx_ctx* ctx, const int32_t* labels_dev, int B, int H
   hipLaunchKernelGGL(k_stats_init, dim3(cpx_div_up(std::max<long long>(nst, B), kThreads)),
                      dim3(kThreads), 0, ctx->stream, stats_dev, nst, hdr_dev, B);
   CPX_CHECK_LAUNCH("k_stats_init");
-  const long long segs = (long long)((W + kRun - 1) / kRun) * H;
-  hipLaunchKernelGGL(k_label_stats, dim3(cpx_div_up(segs, kThreads), B), dim3(kThreads), 0,
-                     ctx->stream, (const int*)labels_dev, H, W, max_label, stats_dev, hdr_dev);
+  hipLaunchKernelGGL(k_label_stats, dim3(cpx_div_up(W, kThreads), cpx_div_up(H, kTileR), B),
+                     dim3(kThreads), 0, ctx->stream, (const int*)labels_dev, H, W, max_label,
+                     stats_dev, hdr_dev);
   CPX_CHECK_LAUNCH("k_label_stats");
   hipLaunchKernelGGL(k_objects_finalize, dim3(B), dim3(1024), 0, ctx->stream,
                      (const cpx_label_stats*)stats_dev, H, W, max_label, box, objects_dev, hdr_dev);
