@@ -93,6 +93,8 @@ SIGNATURES = {
     "cpx_seg_masks": (_I, [_P, _P, _I, _P, _I, _I, _I, ct.c_double, _I, _I, _P, _P]),
     "cpx_cpnet_epilogue": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I]),
     "cpx_cpnet_pool": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "cpx_cpnet_conv_cfg": (_I, [_I, _I, _P, _P]),
+    "cpx_cpnet_conv3x3": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P, _I, _P, _P, _I]),
 }
 
 _lib = None

@@ -12,7 +12,10 @@ Further rewrites, all exact in real arithmetic:
     BatchNorm+ReLU is applied before upsampling, written straight to the upsampled tensor;
   * the down path's 2x2 max-pool is fused with the next block's BatchNorm+ReLU
     (cpx_cpnet_pool).
-Eager PyTorch runs ~9 full-tensor passes per convolution; this runs ~2.
+Every 3x3 convolution with 32..256 channels runs as ONE native launch (cpx_cpnet_conv3x3,
+k_conv.hip: MFMA implicit GEMM with the epilogue applied to the fp32 accumulators); the
+2-channel input convolution and the 1x1 convolutions stay on MIOpen.  Eager PyTorch runs ~9
+full-tensor passes per convolution; this runs one.
 """
 from __future__ import annotations
 
@@ -49,6 +52,19 @@ def _bias(conv, dev):
     return conv.bias.detach().float().to(dev).contiguous()
 
 
+def _pack3x3(lib, w, dev):
+    """[cout][cin][3][3] -> the cpx_cpnet_conv3x3 layout [cout/bn][cin/ck][ky][kx][bn][ck] bf16,
+    or None when the native kernel has no instance for (cin, cout)."""
+    cout, cin = w.shape[0], w.shape[1]
+    bn, ck = ct.c_int(), ct.c_int()
+    if lib is None or lib.cpx_cpnet_conv_cfg(cin, cout, ct.byref(bn), ct.byref(ck)) != 0:
+        return None
+    bn, ck = bn.value, ck.value
+    t = w.detach().float().cpu().reshape(cout // bn, bn, cin // ck, ck, 3, 3)
+    t = t.permute(0, 2, 4, 5, 1, 3).contiguous()
+    return t.to(dev, torch.bfloat16).contiguous()
+
+
 def _fold_proj(seq, dev):
     """BatchNorm (no ReLU) -> 1x1 conv  ==  1x1 conv with w * scale[in], b + w @ shift."""
     bn, conv = seq[0], seq[-1]
@@ -61,18 +77,20 @@ def _fold_proj(seq, dev):
 
 
 class FusedCPnet:
-    def __init__(self, net: CPnet, dev):
+    def __init__(self, net: CPnet, dev, native_conv: bool = True):
         self.dev = dev
         self.lib = dev.lib
         td = dev.torch_device
         net = net.float().eval()
+        lib = self.lib if native_conv else None
         self.down = []
         for blk in net.down:
             wp, bp = _fold_proj(blk.proj, td)
             d = dict(wp=wp,
                      bn=[_bn_affine(blk.conv[t][0], td) for t in range(4)],
                      w=[_conv_w(blk.conv[t][-1], td) for t in range(4)],
-                     b=[_bias(blk.conv[t][-1], td) for t in range(4)])
+                     b=[_bias(blk.conv[t][-1], td) for t in range(4)],
+                     pk=[_pack3x3(lib, blk.conv[t][-1].weight, td) for t in range(4)])
             d["b1p"] = (d["b"][1] + bp).contiguous()
             self.down.append(d)
         self.up = []
@@ -83,6 +101,7 @@ class FusedCPnet:
                      bn=[_bn_affine(c[0], td) for c in convs],
                      w=[_conv_w(c[-1], td) for c in convs],
                      b=[_bias(c[-1], td) for c in convs],
+                     pk=[_pack3x3(lib, c[-1].weight, td) for c in convs],
                      full=[(m.full.weight.detach().float().to(td), m.full.bias.detach().float().to(td))
                            for m in (blk.conv1, blk.conv2, blk.conv3)])
             u["b1p"] = (u["b"][1] + bp).contiguous()
@@ -105,6 +124,28 @@ class FusedCPnet:
         check(self.lib.cpx_cpnet_epilogue(self.dev.h, _p(conv), _p(bias), _p(res), int(res_up),
                                           _p(style), _p(scale), _p(shift), int(relu), N, H, W, C,
                                           _p(yo), _p(zo), int(z_up)), "cpx_cpnet_epilogue")
+        return yo, zo
+
+    def _conv(self, x, blk, i, bias, res=None, res_up=False, style=None, bn=None, relu=True,
+              y=False, z=True, z_up=False):
+        """3x3 conv i of block blk + fused epilogue: one native MFMA launch when packed weights
+        exist, else MIOpen + cpx_cpnet_epilogue."""
+        pk = blk["pk"][i]
+        if pk is None:
+            return self._epi(F.conv2d(x, blk["w"][i], padding=1), bias, res=res, res_up=res_up,
+                             style=style, bn=bn, relu=relu, y=y, z=z, z_up=z_up)
+        N, Cin, H, W = x.shape
+        Cout = blk["w"][i].shape[0]
+        assert x.is_contiguous(memory_format=CL)
+        yo = torch.empty((N, Cout, H, W), dtype=x.dtype, device=x.device, memory_format=CL) if y else None
+        zo = None
+        if z:
+            zs = (N, Cout, 2 * H, 2 * W) if z_up else (N, Cout, H, W)
+            zo = torch.empty(zs, dtype=x.dtype, device=x.device, memory_format=CL)
+        scale, shift = bn if bn is not None else (None, None)
+        check(self.lib.cpx_cpnet_conv3x3(self.dev.h, _p(x), N, H, W, Cin, Cout, _p(pk), _p(bias),
+                                         _p(res), int(res_up), _p(style), _p(scale), _p(shift),
+                                         int(relu), _p(yo), _p(zo), int(z_up)), "cpx_cpnet_conv3x3")
         return yo, zo
 
     def _pool(self, x, bn):
@@ -131,17 +172,13 @@ class FusedCPnet:
             else:
                 xin, z0 = self._pool(xd[-1], d["bn"][0])
             p = F.conv2d(xin, d["wp"])
-            h = F.conv2d(z0, d["w"][0], padding=1)
-            _, z = self._epi(h, d["b"][0], bn=d["bn"][1])
-            h = F.conv2d(z, d["w"][1], padding=1)
-            x1, z = self._epi(h, d["b1p"], res=p, bn=d["bn"][2], y=True)
-            h = F.conv2d(z, d["w"][2], padding=1)
-            _, z = self._epi(h, d["b"][2], bn=d["bn"][3])
-            h = F.conv2d(z, d["w"][3], padding=1)
+            _, z = self._conv(z0, d, 0, d["b"][0], bn=d["bn"][1])
+            x1, z = self._conv(z, d, 1, d["b1p"], res=p, bn=d["bn"][2], y=True)
+            _, z = self._conv(z, d, 2, d["b"][2], bn=d["bn"][3])
             if n < len(self.down) - 1:
-                xo, _ = self._epi(h, d["b"][3], res=x1, y=True, z=False)
+                xo, _ = self._conv(z, d, 3, d["b"][3], res=x1, y=True, z=False)
             else:  # deepest level also feeds the first up block's BatchNorm+ReLU
-                xo, zu = self._epi(h, d["b"][3], res=x1, bn=self.up[-1]["bn"][0], y=True)
+                xo, zu = self._conv(z, d, 3, d["b"][3], res=x1, bn=self.up[-1]["bn"][0], y=True)
             xd.append(xo)
         style = xd[-1].float().mean(dim=(2, 3))
         style = style / torch.sum(style ** 2, dim=1, keepdim=True) ** 0.5
@@ -151,17 +188,13 @@ class FusedCPnet:
             u = self.up[n]
             s = [(style @ w.t() + b).contiguous() for (w, b) in u["full"]]
             p = F.conv2d(x_small, u["wp"])
-            h = F.conv2d(z0, u["w"][0], padding=1)
-            _, z = self._epi(h, u["b"][0], res=xd[n], style=s[0], bn=u["bn"][1])
-            h = F.conv2d(z, u["w"][1], padding=1)
-            x1, z = self._epi(h, u["b1p"], res=p, res_up=(n < len(self.up) - 1), style=s[1],
-                              bn=u["bn"][2], y=True)
-            h = F.conv2d(z, u["w"][2], padding=1)
-            _, z = self._epi(h, u["b"][2], style=s[2], bn=u["bn"][3])
-            h = F.conv2d(z, u["w"][3], padding=1)
+            _, z = self._conv(z0, u, 0, u["b"][0], res=xd[n], style=s[0], bn=u["bn"][1])
+            x1, z = self._conv(z, u, 1, u["b1p"], res=p, res_up=(n < len(self.up) - 1), style=s[1],
+                               bn=u["bn"][2], y=True)
+            _, z = self._conv(z, u, 2, u["b"][2], style=s[2], bn=u["bn"][3])
             if n > 0:
-                x_small, z0 = self._epi(h, u["b"][3], res=x1, bn=self.up[n - 1]["bn"][0], y=True,
-                                        z_up=True)
+                x_small, z0 = self._conv(z, u, 3, u["b"][3], res=x1, bn=self.up[n - 1]["bn"][0],
+                                         y=True, z_up=True)
             else:
-                _, out_in = self._epi(h, u["b"][3], res=x1, bn=self.bn_out)
+                _, out_in = self._conv(z, u, 3, u["b"][3], res=x1, bn=self.bn_out)
         return F.conv2d(out_in, self.w_out, self.b_out)

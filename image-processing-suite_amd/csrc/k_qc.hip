@@ -445,10 +445,10 @@ extern "C" int cpx_qc_rps(cpx_ctx* ctx, const uint16_t* raw_dev, const void* ill
     static bool attrs = false;
     if (!attrs) {
       const int lds_max = 160 * 1024;
-      hipFuncSetAttribute((const void*)k_qc_rows<0>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
-      hipFuncSetAttribute((const void*)k_qc_rows<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
-      hipFuncSetAttribute((const void*)k_qc_rows<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
-      hipFuncSetAttribute((const void*)k_qc_cols, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
+      CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_qc_rows<0>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
+      CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_qc_rows<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
+      CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_qc_rows<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
+      CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_qc_cols, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
       attrs = true;
     }
     const size_t sh_rows = 2 * sizeof(cplx) * (size_t)W;

@@ -44,8 +44,9 @@ constexpr int kTabW = 32768;         // packed u16 pair counters (128 KiB)
 constexpr int kCrop = kFastCropPx;   // u8 crop capacity (pixels)
 constexpr int kMaskW = kFastMaskWords;  // membership bitmask words (bh * ceil(bw/32))
 constexpr int kNW = kTT / 64;
-constexpr int kNG = 11;              // u32 partial sums per thread and angle (see glcm_angle)
-constexpr int kRedW = 192;           // LDS words for the cross-wave reduction (>= kNG * kNW)
+constexpr int kNG = 9;               // u32 partial sums per thread and angle (see glcm_angle)
+constexpr int kRedW = 192;           // LDS words for the cross-wave reduction (u32 + f64 parts)
+constexpr int kList = 3696;          // distinct-key list capacity (u16 keys)
 
 __device__ __forceinline__ int quantize(float v, bool in, float mn, float rng, bool flat) {
   const float m = v * (in ? 1.0f : 0.0f);
@@ -74,119 +75,168 @@ __device__ __forceinline__ unsigned int wave_sum_u32(unsigned int v) {
 }
 
 // One GLCM angle (skimage graycomatrix offset (dr, dc), symmetric=False, normed) over an 8-bit
-// crop in LDS (or the global scratch slot), followed by greycoprops.  Every sum is an exact
-// integer: with at most 65535 pairs per object all block totals fit in u32 (sum i^2 <=
-// 65535 * 255^2 < 2^32, sum c^2 <= 65535^2 < 2^32), so a thread keeps
-//   (sum i << 32 | sum j), (sum i^2 << 32 | sum j^2), sum ij, ASM, background pairs,
-//   |i-j| counts for d < 8 in packed 16-bit fields, d >= 8 in an LDS histogram,
-// and the ASM (= sum over keys of count^2) comes from the returned old counts of a packed u16
-// 64K-entry LDS table: adding 1 to count c adds 2c + 1.  Pairs (0, 0) (background) bypass
-// the table and enter ASM as bg^2.
+// crop in LDS (or the global scratch slot), followed by greycoprops.
+//  1. count: every pixel pair adds 1 to its packed-u16 counter in a 64K-key LDS table
+//     (background pairs (0, 0) are only counted in a register); a pair that finds its counter
+//     at 0 appends the key to a distinct-key list (wave-aggregated slot reservation);
+//  2. per distinct key (i, j) with count c: c*i, c*j, c*i^2, c*j^2, c*i*j, c^2 (ASM),
+//     c*d, c*d^2 (d = |i-j|) in exact u32 (with at most 65535 pairs per object every total
+//     fits: sum c*i^2 <= 65535 * 255^2 < 2^32, sum c^2 <= 65535^2 < 2^32) and
+//     c * (1 / (1 + d^2)) in fp64; the listed counters are then cleared.  A crop with more
+//     distinct keys than the list holds scans (and clears) the whole table instead;
+//  3. DPP wave sums, one cross-wave pass, greycoprops on one lane.
+__device__ __forceinline__ void glcm_key(unsigned int c, unsigned int i, unsigned int j,
+                                         unsigned int* acc, double& h) {
+  const unsigned int ci = c * i, cj = c * j;
+  acc[0] += ci;
+  acc[1] += cj;
+  acc[2] += ci * i;
+  acc[3] += cj * j;
+  acc[4] += ci * j;
+  acc[5] += c * c;
+  const unsigned int d = i > j ? i - j : j - i;
+  acc[6] += c * d * d;
+  acc[7] += c * d;
+  h += (double)c * (1.0 / (1.0 + (double)(d * d)));
+}
+
+// Add a run of cnt pairs of one key; the lane that finds the counter at 0 appends the key to
+// the distinct-key list (slots reserved once per wave among the flushing lanes).
+__device__ __forceinline__ void glcm_flush(unsigned int* tab, unsigned short* list, int* nlist,
+                                           unsigned int key, unsigned int cnt, int lane) {
+  const unsigned int sh = (key & 1u) << 4;
+  const unsigned int old = atomicAdd(&tab[key >> 1], cnt << sh);
+  const bool fresh = ((old >> sh) & 0xffffu) == 0u;
+  const unsigned long long m = __ballot(fresh);
+  if (m) {
+    const int leader = __builtin_ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(nlist, __popcll(m));
+    base = __shfl(base, leader);
+    const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+    if (fresh && pos < kList) list[pos] = (unsigned short)key;
+  }
+}
+
 template <bool LDS_CROP>
 __device__ void glcm_angle(const unsigned char* __restrict__ crop, unsigned int* tab,
-                           unsigned int* dh, unsigned int* red, int bh, int bw, int dr, int dc,
-                           double* out, long long* pt) {
+                           unsigned short* list, int* nlist, unsigned int* red, int bh, int bw,
+                           int dr, int dc, double* out, long long* pt) {
   const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int rend = bh - dr;  // dr >= 0
   const int cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
   const long long T = (rend > 0 && cend > cbeg) ? (long long)rend * (cend - cbeg) : 0;
-  unsigned long long s1 = 0, s2 = 0, dlo = 0, dhi = 0;
-  unsigned int sx = 0, asum = 0, bg = 0;
-  for (int r = ty; r < rend; r += kRows) {
-    const unsigned char* row = crop + r * bw;
-    const unsigned char* row2 = crop + (r + dr) * bw + dc;
-    for (int c0 = cbeg + tx; c0 < cend; c0 += 128) {
-      int key[4];
-      unsigned int old[4];
+  // Thread = one contiguous run of the angle's T pairs (row-major); the 64 lanes of a wave
+  // take runs T/64 apart (segment lane*16 + wave), so one wave-instruction touches unrelated
+  // keys, and a lane adds a whole run of equal keys at once: LDS atomics to one address are
+  // serialised (~2 cycles per lane), and smooth crops repeat keys along a row.
+  unsigned int bg = 0;
+  {
+    const int Wc = cend - cbeg;
+    const int seg = (int)((T + kTT - 1) / kTT);
+    int p = (lane * kNW + wid) * seg;
+    const int pend = (int)min((long long)p + seg, T);
+    unsigned int cur = 0, cnt = 0;
+    if (p < pend) {
+      const int r = p / Wc, c = p - r * Wc;
+      const unsigned char* a = crop + r * bw + cbeg + c;
+      const unsigned char* b = a + dr * bw + dc;
+      int left = Wc - c;  // pairs left in this row
+      for (; p < pend; p += 4) {
+        // four keys loaded ahead (the 8 byte loads issue together), then consumed in order
+        unsigned int key[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int c = c0 + 32 * u;
-        key[u] = 0;
-        if (c < cend) {
-          const unsigned int i = row[c], j = row2[c];
-          s1 += ((unsigned long long)i << 32) | j;
-          s2 += ((unsigned long long)(i * i) << 32) | (j * j);
-          sx += i * j;
-          if ((i | j) == 0) {
-            ++bg;
-          } else {
-            const int d = abs((int)i - (int)j);
-            if (d < 4) dlo += 1ull << (16 * d);
-            else if (d < 8) dhi += 1ull << (16 * (d - 4));
-            else atomicAdd(&dh[d], 1u);
-            key[u] = (int)((i << 8) | j);
+        for (int u = 0; u < 4; ++u) {
+          key[u] = ((unsigned int)*a << 8) | (unsigned int)*b;
+          const bool wrap = --left == 0;
+          a += wrap ? (bw - Wc + 1) : 1;
+          b += wrap ? (bw - Wc + 1) : 1;
+          left = wrap ? Wc : left;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (p + u >= pend) break;
+          if (key[u] != cur) {
+            if (cur) glcm_flush(tab, list, nlist, cur, cnt, lane);
+            else bg += cnt;
+            cur = key[u];
+            cnt = 0;
           }
+          ++cnt;
         }
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        old[u] = key[u] != 0 ? atomicAdd(&tab[key[u] >> 1], 1u << ((key[u] & 1) * 16)) : 0u;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (key[u] != 0) asum += 2u * ((old[u] >> ((key[u] & 1) * 16)) & 0xffffu) + 1u;
     }
+    if (cur) glcm_flush(tab, list, nlist, cur, cnt, lane);
+    else bg += cnt;
   }
   __syncthreads();
   GLCM_MARK(2, pt);
+  const int n = *nlist;
+  unsigned int acc[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  double h = 0.0;
+  if (n <= kList) {
+    for (int x = threadIdx.x; x < n; x += kTT) {
+      const unsigned int key = list[x];
+      const unsigned int c = (tab[key >> 1] >> ((key & 1u) << 4)) & 0xffffu;
+      glcm_key(c, key >> 8, key & 255u, acc, h);
+    }
+  } else {  // dense fallback: scan and clear the whole table
+    uint4* t4 = reinterpret_cast<uint4*>(tab);
+    for (int x = threadIdx.x; x < kTabW / 4; x += kTT) {
+      const uint4 v = t4[x];
+      if ((v.x | v.y | v.z | v.w) == 0u) continue;
+      t4[x] = uint4{0u, 0u, 0u, 0u};
+      const unsigned int i = (unsigned int)x >> 5;  // the 8 keys 8x .. 8x+7 share i
+      const unsigned int w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const unsigned int c = (w4[e] >> (16 * hh)) & 0xffffu;
+          if (c) glcm_key(c, i, ((unsigned int)(8 * x) & 255u) + 2u * e + hh, acc, h);
+        }
+      }
+    }
+  }
   {
-    const unsigned int w[kNG] = {(unsigned int)(s1 >> 32), (unsigned int)s1,
-                                 (unsigned int)(s2 >> 32), (unsigned int)s2,
-                                 sx, asum, bg,
-                                 (unsigned int)dlo, (unsigned int)(dlo >> 32),
-                                 (unsigned int)dhi, (unsigned int)(dhi >> 32)};
+    const unsigned int w[kNG] = {acc[0], acc[1], acc[2], acc[3], acc[4], acc[5], acc[6], acc[7], bg};
 #pragma unroll
     for (int k = 0; k < kNG; ++k) {
       const unsigned int t = wave_sum_u32(w[k]);
       if (lane == 0) red[k * kNW + wid] = t;
     }
+    h = wave_sum(h);
+    if (lane == 0) reinterpret_cast<double*>(red + kNG * kNW)[wid] = h;
   }
   __syncthreads();
   GLCM_MARK(3, pt);
-  if (wid == 0) {  // greycoprops on one wave; the others clear the pair table meanwhile
+  if (n <= kList)  // clear the listed counters (all reads are done)
+    for (int x = threadIdx.x; x < n; x += kTT) tab[list[x] >> 1] = 0u;
+  if (wid == 0) {  // greycoprops on one wave
     unsigned int t = 0;
     if (lane < kNG)
 #pragma unroll
       for (int x = 0; x < kNW; ++x) t += red[lane * kNW + x];
-    const unsigned int si = __builtin_amdgcn_readlane(t, 0), sj = __builtin_amdgcn_readlane(t, 1);
-    const unsigned int sii = __builtin_amdgcn_readlane(t, 2), sjj = __builtin_amdgcn_readlane(t, 3);
-    const unsigned int sij = __builtin_amdgcn_readlane(t, 4), as = __builtin_amdgcn_readlane(t, 5);
-    const unsigned int nbg = __builtin_amdgcn_readlane(t, 6);
-    const unsigned int p01 = __builtin_amdgcn_readlane(t, 7), p23 = __builtin_amdgcn_readlane(t, 8);
-    const unsigned int p45 = __builtin_amdgcn_readlane(t, 9), p67 = __builtin_amdgcn_readlane(t, 10);
-    unsigned int ct = 0, dt = 0;
-    double h = 0.0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int d = lane * 4 + q;
-      unsigned int cnt;
-      if (d < 8) {
-        const unsigned int pw = d < 2 ? p01 : d < 4 ? p23 : d < 6 ? p45 : p67;
-        cnt = (pw >> (16 * (d & 1))) & 0xffffu;
-        if (d == 0) cnt += nbg;
-      } else {
-        cnt = dh[d];
-        dh[d] = 0u;  // restore for the next angle (this wave is the only reader)
-      }
-      ct += cnt * (unsigned int)(d * d);
-      dt += cnt * (unsigned int)d;
-      h += (double)cnt * (1.0 / (1.0 + (double)(d * d)));
-    }
-    ct = wave_sum_u32(ct);
-    dt = wave_sum_u32(dt);
-    h = wave_sum(h);
+    double hw = lane < kNW ? reinterpret_cast<const double*>(red + kNG * kNW)[lane] : 0.0;
+    hw = wave_sum(hw);
+    const unsigned int tsi = __builtin_amdgcn_readlane(t, 0), tsj = __builtin_amdgcn_readlane(t, 1);
+    const unsigned int tsii = __builtin_amdgcn_readlane(t, 2), tsjj = __builtin_amdgcn_readlane(t, 3);
+    const unsigned int tsij = __builtin_amdgcn_readlane(t, 4), tas = __builtin_amdgcn_readlane(t, 5);
+    const unsigned int tct = __builtin_amdgcn_readlane(t, 6), tdt = __builtin_amdgcn_readlane(t, 7);
+    const unsigned int nbg = __builtin_amdgcn_readlane(t, 8);
     if (lane == 0) {
       double con = 0.0, dis = 0.0, hom = 0.0, asmv = 0.0, ene = 0.0, cor = 1.0;
       if (T > 0) {
         const double Td = (double)T;
-        con = (double)ct / Td;
-        dis = (double)dt / Td;
-        hom = h / Td;
-        asmv = (double)((unsigned long long)as + (unsigned long long)nbg * nbg) / (Td * Td);
+        con = (double)tct / Td;
+        dis = (double)tdt / Td;
+        hom = (hw + (double)nbg) / Td;  // background pairs: d = 0, weight 1
+        asmv = (double)((unsigned long long)tas + (unsigned long long)nbg * nbg) / (Td * Td);
         ene = sqrt(asmv);
-        const long long vi = T * (long long)sii - (long long)si * si;
-        const long long vj = T * (long long)sjj - (long long)sj * sj;
-        const long long cv = T * (long long)sij - (long long)si * sj;
+        const long long vi = T * (long long)tsii - (long long)tsi * tsi;
+        const long long vj = T * (long long)tsjj - (long long)tsj * tsj;
+        const long long cv = T * (long long)tsij - (long long)tsi * tsj;
         const double sdi = sqrt((double)vi) / Td, sdj = sqrt((double)vj) / Td;
         cor = (sdi < 1e-15 || sdj < 1e-15) ? 1.0 : ((double)cv / (Td * Td)) / (sdi * sdj);
       }
@@ -197,10 +247,7 @@ __device__ void glcm_angle(const unsigned char* __restrict__ crop, unsigned int*
       out[CPX_TEX_ENERGY] = ene;
       out[CPX_TEX_CORRELATION] = cor;
     }
-  } else {
-    // clearing the whole table with 16-byte stores (~1K LDS cycles) beats replaying the pairs
-    const uint4 z = {0u, 0u, 0u, 0u};
-    for (int x = threadIdx.x - 64; x < kTabW / 4; x += kTT - 64) reinterpret_cast<uint4*>(tab)[x] = z;
+    if (lane == 0) *nlist = 0;
   }
   __syncthreads();
   GLCM_MARK(4, pt);
@@ -381,14 +428,15 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
                                                  double* __restrict__ feats) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned int* tab = reinterpret_cast<unsigned int*>(smem);
-  unsigned int* dh = tab + kTabW;
-  unsigned int* red = dh + 256;
-  unsigned char* crop = reinterpret_cast<unsigned char*>(red + kRedW);
+  unsigned int* red = tab + kTabW;
+  int* nlist = reinterpret_cast<int*>(red + kRedW);
+  unsigned char* crop = reinterpret_cast<unsigned char*>(nlist + 4);
+  unsigned short* list = reinterpret_cast<unsigned short*>(crop + kCrop);
   const int fov = blockIdx.y;
   const int n_items = hdr[fov].n_objects * C;
   if ((int)blockIdx.x >= n_items) return;
   for (int x = threadIdx.x; x < kTabW; x += kTT) tab[x] = 0u;
-  for (int x = threadIdx.x; x < 256; x += kTT) dh[x] = 0u;
+  if (threadIdx.x == 0) *nlist = 0;
   __syncthreads();
   // software pipeline: the next item's metadata and LDS-sized crop are loaded into registers
   // while the current item runs its four angles (the crop was written by k_tex_stage, possibly
@@ -425,9 +473,11 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
       const int dr = a == 0 ? 0 : a == 2 ? 3 : 2;
       const int dc = a == 0 ? 3 : a == 1 ? 2 : a == 2 ? 0 : -2;
       if (it.nb <= kCrop)
-        glcm_angle<true>(crop, tab, dh, red, it.bh, it.bw, dr, dc, f + a * CPX_N_TEX_PROPS, &pt);
+        glcm_angle<true>(crop, tab, list, nlist, red, it.bh, it.bw, dr, dc,
+                         f + a * CPX_N_TEX_PROPS, &pt);
       else
-        glcm_angle<false>(it.src, tab, dh, red, it.bh, it.bw, dr, dc, f + a * CPX_N_TEX_PROPS, &pt);
+        glcm_angle<false>(it.src, tab, list, nlist, red, it.bh, it.bw, dr, dc,
+                          f + a * CPX_N_TEX_PROPS, &pt);
     }
   }
 }
@@ -626,10 +676,10 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
                       int H, int W, int max_label, int F, const cpx_object* objects_dev,
                       const cpx_fov_objects* hdr_dev, double* feats_dev, long long** crop_off_out) {
   static bool attr = false;
-  const size_t lds_t = sizeof(unsigned int) * (kTabW + 256 + kRedW) + kCrop;
-  static_assert(sizeof(unsigned int) * (kTabW + 256 + kRedW) + kCrop <= 160 * 1024,
+  const size_t lds_t = sizeof(unsigned int) * (kTabW + kRedW + 4) + kCrop + 2 * kList;
+  static_assert(sizeof(unsigned int) * (kTabW + kRedW + 4) + kCrop + 2 * kList <= 160 * 1024,
                 "GLCM LDS budget");
-  static_assert(kNG * kNW <= kRedW, "reduction scratch");
+  static_assert(kNG * kNW + 2 * kNW <= kRedW, "reduction scratch");
   const size_t lds_s = sizeof(unsigned int) * 2 * kShapeW;
   if (!attr) {
     CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_tex_glcm,
@@ -641,7 +691,7 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   // workspace: crop offsets [B][max_label] + scratch (2 bytes per pixel-channel per FOV)
   const long long per_fov = ((2LL * H * W * C + 255) / 256) * 256;
   const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + 255) / 256) * 256;
-  unsigned char* ws = (unsigned char*)cpx_ws(ctx, WS_MISC, off_bytes + (size_t)B * per_fov);
+  unsigned char* ws = (unsigned char*)cpx_ws(ctx, WS_MISC, off_bytes + (size_t)B * per_fov + 256);  // +256: GLCM key read-ahead
   if (!ws) return CPX_ERR_OOM;
   long long* crop_off = (long long*)ws;
   unsigned char* scratch = ws + off_bytes;

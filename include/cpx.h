@@ -278,6 +278,15 @@ int cpx_cpnet_epilogue(cpx_ctx* ctx, const void* conv, const float* bias, const 
                        int z_up);
 int cpx_cpnet_pool(cpx_ctx* ctx, const void* in, const float* scale, const float* shift,
                    int relu, int N, int Hh, int Ww, int Cn, void* x_out, void* z_out);
+/* 3x3 / pad 1 convolution of in [N,H,W,cin] bf16 (MFMA implicit GEMM) with the epilogue of
+ * cpx_cpnet_epilogue fused (the raw convolution is never stored).  cin, cout in {32, 64, 128,
+ * 256} (pairs used by CPnet).  wpk = weights packed by cpx_cpnet_conv_cfg's (bn, ck):
+ * [cout/bn][cin/ck][ky][kx][bn][ck] bf16.                                                    */
+int cpx_cpnet_conv_cfg(int cin, int cout, int* bn, int* ck);
+int cpx_cpnet_conv3x3(cpx_ctx* ctx, const void* in, int N, int H, int W, int cin, int cout,
+                      const void* wpk, const float* bias, const void* res, int res_up,
+                      const float* style, const float* scale, const float* shift, int relu,
+                      void* y_out, void* z_out, int z_up);
 
 #ifdef __cplusplus
 }

@@ -257,3 +257,54 @@ def test_fused_cpnet_matches_fp32_module(dev, shape, trained):
     # no worse than the eager bf16 module (which rounds after every op)
     assert err_f.mean().item() <= 1.25 * err_e.mean().item(), (err_f.mean().item(), err_e.mean().item())
     assert err_f.max().item() <= 2.0 * err_e.max().item(), (err_f.max().item(), err_e.max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,H,W,res_up,z_up", [(32, 32, 40, 56, False, False),
+                                                      (64, 32, 32, 48, True, True),
+                                                      (32, 64, 24, 40, False, False),
+                                                      (64, 64, 20, 36, True, False),
+                                                      (128, 64, 16, 16, False, True),
+                                                      (64, 128, 14, 28, False, False),
+                                                      (128, 128, 12, 20, True, False),
+                                                      (256, 128, 8, 16, False, True),
+                                                      (128, 256, 10, 14, False, False),
+                                                      (256, 256, 28, 28, True, False)])
+def test_cpnet_conv3x3_native(dev, cin, cout, H, W, res_up, z_up):
+    """MFMA conv + fused epilogue vs torch fp32 conv2d of the same bf16 operands."""
+    from cpx.cpnet_fused import _p, _pack3x3
+    td = dev.torch_device
+    CL = torch.channels_last
+    g = torch.Generator().manual_seed(cin + cout + H)
+    N = 3
+    x = _bf(torch.randn(N, cin, H, W, generator=g)).to(td).contiguous(memory_format=CL)
+    w = _bf(torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (9 * cin)) ** 0.5)
+    pk = _pack3x3(dev.lib, w, td)
+    assert pk is not None
+    bias = torch.randn(cout, generator=g).to(td)
+    rs = (N, cout, H // 2, W // 2) if res_up else (N, cout, H, W)
+    res = _bf(torch.randn(*rs, generator=g)).to(td).contiguous(memory_format=CL)
+    sty = torch.randn(N, cout, generator=g).to(td)
+    scale = torch.randn(cout, generator=g).to(td)
+    shift = torch.randn(cout, generator=g).to(td)
+    yo = torch.empty((N, cout, H, W), dtype=torch.bfloat16, device=td, memory_format=CL)
+    zs = (N, cout, 2 * H, 2 * W) if z_up else (N, cout, H, W)
+    zo = torch.empty(zs, dtype=torch.bfloat16, device=td, memory_format=CL)
+    check(dev.lib.cpx_cpnet_conv3x3(dev.h, _p(x), N, H, W, cin, cout, _p(pk), _p(bias), _p(res),
+                                    int(res_up), _p(sty), _p(scale), _p(shift), 1, _p(yo), _p(zo),
+                                    int(z_up)), "conv3x3")
+    ref = torch.nn.functional.conv2d(x.float(), w.float().to(td), padding=1)
+    r = res.float()
+    if res_up:
+        r = r.repeat_interleave(2, 2).repeat_interleave(2, 3)
+    t = ref + bias[None, :, None, None] + r
+    z = torch.clamp_min(scale[None, :, None, None] * (t + sty[:, :, None, None])
+                        + shift[None, :, None, None], 0.0)
+    if z_up:
+        z = z.repeat_interleave(2, 2).repeat_interleave(2, 3)
+    dev.sync()
+    ty = yo.float()
+    # fp32 accumulation in a different order + one bf16 rounding
+    assert ((ty - t).abs() <= 1e-2 * t.abs() + 1e-2).all(), (ty - t).abs().max().item()
+    tz = zo.float()
+    assert ((tz - z).abs() <= 1e-2 * z.abs() + 3e-2).all(), (tz - z).abs().max().item()
