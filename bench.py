@@ -53,6 +53,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    from cpx import shard
     from cpx.cpnet import count_flops
     from cpx.device import Device
     from cpx.pipeline import FovPipeline, PipelineConfig
@@ -69,7 +70,11 @@ def main():
     cfg = PipelineConfig(H=H, W=W, C=C, batch=B, weights=weights)
     illum = synth_illum(C, H, W, seed=1)
     pipe = FovPipeline(dev, cfg, illum)
-    pool = [synth_fovs(B, C, H, W, td, seed=7919 * rank + 101 * i) for i in range(a.pool)]
+    # this rank's wells (well w -> rank w % world); the synthetic batches are seeded
+    # by the rank's own FOV keys, so ranks never share inputs and exchange nothing
+    mine = shard.shard(shard.plate_fovs(n_wells=384), rank, world)
+    pool = [synth_fovs(B, C, H, W, td, seed=shard.fov_seed(mine[(i * B) % len(mine)]))
+            for i in range(a.pool)]
     torch.cuda.synchronize()
 
     def barrier():
@@ -89,12 +94,8 @@ def main():
         n_obj.append([int(res.hdr[s]["n_objects"].sum()) for s in ("Nuclei", "Cells", "Cytoplasm")])
     torch.cuda.synchronize()
     barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=td)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    total_fovs = world * a.steps * B
+    dt = shard.max_over_ranks(time.perf_counter() - t0, device=td)
+    total_fovs = shard.sum_over_ranks(a.steps * B, device=td)
     value = total_fovs / dt
 
     # ---- instrumented steps (outside the timed region): per-stage device time by HIP events on

@@ -15,7 +15,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CPX_LIB", os.path.join(_HERE, "libcpx.so"))
 
 CPX_OK = 0
-CPX_DTYPE_NONE, CPX_DTYPE_F32, CPX_DTYPE_F64 = 0, 1, 2
+CPX_DTYPE_NONE, CPX_DTYPE_F32, CPX_DTYPE_F64, CPX_DTYPE_IMAGE_F64 = 0, 1, 2, 3
+CPX_QC_OK, CPX_QC_FLAT, CPX_QC_NAN = 0, 1, 2
 
 # feature layout constants (mirror include/cpx.h)
 N_SHAPE = 15
@@ -94,6 +95,15 @@ SIGNATURES = {
     "cpx_cpnet_epilogue": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I]),
     "cpx_cpnet_pool": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "cpx_cpnet_conv_cfg": (_I, [_I, _I, _P, _P]),
+    "cpx_set_illum": (_I, [_P, _I, _P, _I, _I, _I]),
+    "cpx_fov_submit": (_I, [_P, ct.c_int64, _P, _I, _I, _I, _I]),
+    "cpx_fov_qc": (_I, [_P, _P, _P, _P]),
+    "cpx_fov_planes": (_I, [_P, _P, _P]),
+    "cpx_fov_read_plane": (_I, [_P, _I, _P]),
+    "cpx_fov_segment_post": (_I, [_P, _P, _I, _P, _P, _I, ct.c_double, _I, _I, _P, _P]),
+    "cpx_fov_object_table": (_I, [_P, _P, _I, _I, _P, _P]),
+    "cpx_fov_features": (_I, [_P, _P, _I, _P, _P]),
+    "cpx_fov_wait": (_I, [_P]),
     "cpx_cpnet_conv3x3": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P, _I, _P, _P, _I]),
 }
 

@@ -40,9 +40,11 @@ def _read_ifd(buf: bytes, off: int, bo: str) -> dict:
 
 
 def imread(src) -> np.ndarray:
-    """Decode the first page of a TIFF (path or bytes) to a numpy array."""
+    """Decode the first page of a TIFF (path, bytes or binary file object) to a numpy array."""
     if isinstance(src, (bytes, bytearray, memoryview)):
         buf = bytes(src)
+    elif hasattr(src, "read"):
+        buf = src.read()
     else:
         with open(src, "rb") as f:
             buf = f.read()
@@ -99,7 +101,7 @@ def imwrite_bytes(arr: np.ndarray) -> bytes:
             extra += b"\0"
         return o
 
-    o_desc = put(desc)
+    o_desc = put(desc + b"\0" * 16)  # tifffile reserves 16 spare bytes after the shape JSON
     o_xres = put(struct.pack("<II", 1, 1))
     o_yres = put(struct.pack("<II", 1, 1))
     o_soft = put(soft)

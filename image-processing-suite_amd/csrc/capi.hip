@@ -72,6 +72,7 @@ void cpx_destroy(cpx_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  cpx_fov_free(ctx);
   for (int i = 0; i < kWsSlots; ++i)
     if (ctx->ws[i]) (void)hipFree(ctx->ws[i]);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);

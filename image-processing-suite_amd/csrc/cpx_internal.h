@@ -9,6 +9,8 @@
 
 constexpr int kWsSlots = 16;
 
+struct cpx_fov_state;  // per-FOV session state (capi_fov.hip)
+
 struct cpx_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -23,7 +25,10 @@ struct cpx_ctx {
   // segmentation coefficient tables currently uploaded (WS_SEG_TAB)
   int seg_key[6] = {0, 0, 0, 0, 0, 0};
   void* seg_tab = nullptr;
+  cpx_fov_state* fov = nullptr;
 };
+
+void cpx_fov_free(cpx_ctx* ctx);
 
 // workspace slots
 enum {

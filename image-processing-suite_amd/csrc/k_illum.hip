@@ -81,7 +81,7 @@ __device__ __forceinline__ void wave_merge(Acc& a) {
   }
 }
 
-// Quotient for one pixel.  ILLUM: 0 none, 1 f32, 2 f64.
+// Quotient for one pixel.  ILLUM: 0 none, 1 f32, 2 f64, 3 = `illum` is the float64 image itself.
 template <int ILLUM>
 __device__ __forceinline__ void quot(unsigned short r, const void* illum, long long idx, double& q,
                                      float& f) {
@@ -93,6 +93,9 @@ __device__ __forceinline__ void quot(unsigned short r, const void* illum, long l
     double il = static_cast<const double*>(illum)[idx];
     q = (double)r / il;
     f = (float)q;                   // producer path would be f64; stored as fp32
+  } else if (ILLUM == 3) {
+    q = static_cast<const double*>(illum)[idx];
+    f = (float)q;
   } else {
     q = (double)r;
     f = (float)r;
@@ -208,7 +211,7 @@ extern "C" int cpx_illum_correct(cpx_ctx* ctx, const uint16_t* raw_dev, const vo
               "cpx_illum_correct: bad sizes C=%d n_planes=%d H=%d W=%d", C, n_planes, H, W);
   CPX_REQUIRE(illum_dtype == CPX_DTYPE_NONE || illum_dev != nullptr, CPX_ERR_ARG,
               "cpx_illum_correct: illum dtype %d without data", illum_dtype);
-  CPX_REQUIRE(illum_dtype >= 0 && illum_dtype <= 2, CPX_ERR_ARG, "bad illum dtype %d", illum_dtype);
+  CPX_REQUIRE(illum_dtype >= 0 && illum_dtype <= 3, CPX_ERR_ARG, "bad illum dtype %d", illum_dtype);
   CPX_REQUIRE(n_planes <= 65535, CPX_ERR_ARG, "cpx_illum_correct: too many planes");
   const long long N = (long long)H * W;
   const int nb = kBlocksPerPlane;
@@ -224,10 +227,12 @@ extern "C" int cpx_illum_correct(cpx_ctx* ctx, const uint16_t* raw_dev, const vo
   if (vec) {
     if (illum_dtype == CPX_DTYPE_F32) LAUNCH(1, true);
     else if (illum_dtype == CPX_DTYPE_F64) LAUNCH(2, true);
+    else if (illum_dtype == CPX_DTYPE_IMAGE_F64) LAUNCH(3, true);
     else LAUNCH(0, true);
   } else {
     if (illum_dtype == CPX_DTYPE_F32) LAUNCH(1, false);
     else if (illum_dtype == CPX_DTYPE_F64) LAUNCH(2, false);
+    else if (illum_dtype == CPX_DTYPE_IMAGE_F64) LAUNCH(3, false);
     else LAUNCH(0, false);
   }
 #undef LAUNCH

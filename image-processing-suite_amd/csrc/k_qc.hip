@@ -146,6 +146,7 @@ __device__ __forceinline__ double qval(const unsigned short* rp, const void* il,
   double r = (double)rp[i];
   if (ILLUM == 1) return r / (double)static_cast<const float*>(il)[i];
   if (ILLUM == 2) return r / static_cast<const double*>(il)[i];
+  if (ILLUM == 3) return static_cast<const double*>(il)[i];
   return r;
 }
 
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(kThreads) void k_qc_rows(
   const unsigned short* rp = raw + (long long)plane * N;
   const void* il = nullptr;
   if (ILLUM == 1) il = static_cast<const float*>(illum) + (long long)ch * N;
-  if (ILLUM == 2) il = static_cast<const double*>(illum) + (long long)ch * N;
+  if (ILLUM == 2 || ILLUM == 3) il = static_cast<const double*>(illum) + (long long)ch * N;
   const cpx_plane_stats st = stats[plane];
   const double mean = st.sum_q / (double)st.n;
   unsigned long long eq = 0;
@@ -448,6 +449,7 @@ extern "C" int cpx_qc_rps(cpx_ctx* ctx, const uint16_t* raw_dev, const void* ill
       CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_qc_rows<0>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
       CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_qc_rows<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
       CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_qc_rows<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
+      CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_qc_rows<3>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
       CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_qc_cols, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
       attrs = true;
     }
@@ -459,6 +461,9 @@ extern "C" int cpx_qc_rps(cpx_ctx* ctx, const uint16_t* raw_dev, const void* ill
                          H, W, stats_dev, (const cplx*)twW, pw, KC, rowspec, aux);
     else if (illum_dtype == CPX_DTYPE_F64)
       hipLaunchKernelGGL(k_qc_rows<2>, grow, dim3(kThreads), sh_rows, ctx->stream, raw_dev, il, C,
+                         H, W, stats_dev, (const cplx*)twW, pw, KC, rowspec, aux);
+    else if (illum_dtype == CPX_DTYPE_IMAGE_F64)
+      hipLaunchKernelGGL(k_qc_rows<3>, grow, dim3(kThreads), sh_rows, ctx->stream, raw_dev, il, C,
                          H, W, stats_dev, (const cplx*)twW, pw, KC, rowspec, aux);
     else
       hipLaunchKernelGGL(k_qc_rows<0>, grow, dim3(kThreads), sh_rows, ctx->stream, raw_dev, il, C,

@@ -44,9 +44,9 @@ constexpr int kTabW = 32768;         // packed u16 pair counters (128 KiB)
 constexpr int kCrop = kFastCropPx;   // u8 crop capacity (pixels)
 constexpr int kMaskW = kFastMaskWords;  // membership bitmask words (bh * ceil(bw/32))
 constexpr int kNW = kTT / 64;
-constexpr int kNG = 9;               // u32 partial sums per thread and angle (see glcm_angle)
+constexpr int kNG = 7;               // u32 partial sums per thread and angle (see glcm_angle)
 constexpr int kRedW = 192;           // LDS words for the cross-wave reduction (u32 + f64 parts)
-constexpr int kList = 3696;          // distinct-key list capacity (u16 keys)
+constexpr int kList = 3184;          // distinct-key list capacity (u16 keys)
 
 __device__ __forceinline__ int quantize(float v, bool in, float mn, float rng, bool flat) {
   const float m = v * (in ? 1.0f : 0.0f);
@@ -79,14 +79,16 @@ __device__ __forceinline__ unsigned int wave_sum_u32(unsigned int v) {
 //  1. count: every pixel pair adds 1 to its packed-u16 counter in a 64K-key LDS table
 //     (background pairs (0, 0) are only counted in a register); a pair that finds its counter
 //     at 0 appends the key to a distinct-key list (wave-aggregated slot reservation);
-//  2. per distinct key (i, j) with count c: c*i, c*j, c*i^2, c*j^2, c*i*j, c^2 (ASM),
-//     c*d, c*d^2 (d = |i-j|) in exact u32 (with at most 65535 pairs per object every total
-//     fits: sum c*i^2 <= 65535 * 255^2 < 2^32, sum c^2 <= 65535^2 < 2^32) and
-//     c * (1 / (1 + d^2)) in fp64; the listed counters are then cleared.  A crop with more
-//     distinct keys than the list holds scans (and clears) the whole table instead;
-//  3. DPP wave sums, one cross-wave pass, greycoprops on one lane.
+//  2. per distinct key (i, j) with count c: c*i, c*j, c*i^2, c*j^2, c*i*j, c^2 (ASM) in exact
+//     u32 (with at most 65535 pairs per object every total fits: sum c*i^2 <= 65535 * 255^2
+//     < 2^32, sum c^2 <= 65535^2 < 2^32), and c into an integer |i-j| histogram; the listed
+//     counters are then cleared.  A crop with more distinct keys than the list holds scans (and
+//     clears) the whole table instead;
+//  3. DPP wave sums, one cross-wave pass; one wave turns the |i-j| histogram into contrast,
+//     dissimilarity and homogeneity in a fixed order (results never depend on the order in
+//     which keys were first seen), greycoprops on one lane.
 __device__ __forceinline__ void glcm_key(unsigned int c, unsigned int i, unsigned int j,
-                                         unsigned int* acc, double& h) {
+                                         unsigned int* acc, unsigned int* dh) {
   const unsigned int ci = c * i, cj = c * j;
   acc[0] += ci;
   acc[1] += cj;
@@ -94,10 +96,7 @@ __device__ __forceinline__ void glcm_key(unsigned int c, unsigned int i, unsigne
   acc[3] += cj * j;
   acc[4] += ci * j;
   acc[5] += c * c;
-  const unsigned int d = i > j ? i - j : j - i;
-  acc[6] += c * d * d;
-  acc[7] += c * d;
-  h += (double)c * (1.0 / (1.0 + (double)(d * d)));
+  atomicAdd(&dh[i > j ? i - j : j - i], c);
 }
 
 // Add a run of cnt pairs of one key; the lane that finds the counter at 0 appends the key to
@@ -120,9 +119,8 @@ __device__ __forceinline__ void glcm_flush(unsigned int* tab, unsigned short* li
 
 template <bool LDS_CROP>
 __device__ void glcm_angle(const unsigned char* __restrict__ crop, unsigned int* tab,
-                           unsigned short* list, int* nlist, unsigned int* red, int bh, int bw,
-                           int dr, int dc, double* out, long long* pt) {
-  const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31;
+                           unsigned short* list, int* nlist, unsigned int* dh, unsigned int* red,
+                           int bh, int bw, int dr, int dc, double* out, long long* pt) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int rend = bh - dr;  // dr >= 0
   const int cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
@@ -173,13 +171,12 @@ __device__ void glcm_angle(const unsigned char* __restrict__ crop, unsigned int*
   __syncthreads();
   GLCM_MARK(2, pt);
   const int n = *nlist;
-  unsigned int acc[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-  double h = 0.0;
+  unsigned int acc[6] = {0u, 0u, 0u, 0u, 0u, 0u};
   if (n <= kList) {
     for (int x = threadIdx.x; x < n; x += kTT) {
       const unsigned int key = list[x];
       const unsigned int c = (tab[key >> 1] >> ((key & 1u) << 4)) & 0xffffu;
-      glcm_key(c, key >> 8, key & 255u, acc, h);
+      glcm_key(c, key >> 8, key & 255u, acc, dh);
     }
   } else {  // dense fallback: scan and clear the whole table
     uint4* t4 = reinterpret_cast<uint4*>(tab);
@@ -194,44 +191,54 @@ __device__ void glcm_angle(const unsigned char* __restrict__ crop, unsigned int*
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           const unsigned int c = (w4[e] >> (16 * hh)) & 0xffffu;
-          if (c) glcm_key(c, i, ((unsigned int)(8 * x) & 255u) + 2u * e + hh, acc, h);
+          if (c) glcm_key(c, i, ((unsigned int)(8 * x) & 255u) + 2u * e + hh, acc, dh);
         }
       }
     }
   }
   {
-    const unsigned int w[kNG] = {acc[0], acc[1], acc[2], acc[3], acc[4], acc[5], acc[6], acc[7], bg};
+    const unsigned int w[kNG] = {acc[0], acc[1], acc[2], acc[3], acc[4], acc[5], bg};
 #pragma unroll
     for (int k = 0; k < kNG; ++k) {
       const unsigned int t = wave_sum_u32(w[k]);
       if (lane == 0) red[k * kNW + wid] = t;
     }
-    h = wave_sum(h);
-    if (lane == 0) reinterpret_cast<double*>(red + kNG * kNW)[wid] = h;
   }
   __syncthreads();
   GLCM_MARK(3, pt);
   if (n <= kList)  // clear the listed counters (all reads are done)
     for (int x = threadIdx.x; x < n; x += kTT) tab[list[x] >> 1] = 0u;
-  if (wid == 0) {  // greycoprops on one wave
+  if (wid == 0) {  // |i-j| terms and greycoprops on one wave
     unsigned int t = 0;
     if (lane < kNG)
 #pragma unroll
       for (int x = 0; x < kNW; ++x) t += red[lane * kNW + x];
-    double hw = lane < kNW ? reinterpret_cast<const double*>(red + kNG * kNW)[lane] : 0.0;
-    hw = wave_sum(hw);
     const unsigned int tsi = __builtin_amdgcn_readlane(t, 0), tsj = __builtin_amdgcn_readlane(t, 1);
     const unsigned int tsii = __builtin_amdgcn_readlane(t, 2), tsjj = __builtin_amdgcn_readlane(t, 3);
     const unsigned int tsij = __builtin_amdgcn_readlane(t, 4), tas = __builtin_amdgcn_readlane(t, 5);
-    const unsigned int tct = __builtin_amdgcn_readlane(t, 6), tdt = __builtin_amdgcn_readlane(t, 7);
-    const unsigned int nbg = __builtin_amdgcn_readlane(t, 8);
+    const unsigned int nbg = __builtin_amdgcn_readlane(t, 6);
+    unsigned int ct = 0, dt = 0;
+    double h = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int d = lane * 4 + q;
+      unsigned int cnt = dh[d];
+      dh[d] = 0u;  // restore for the next angle (this wave is the only reader)
+      if (d == 0) cnt += nbg;  // background pairs: d = 0
+      ct += cnt * (unsigned int)(d * d);
+      dt += cnt * (unsigned int)d;
+      h += (double)cnt * (1.0 / (1.0 + (double)(d * d)));
+    }
+    ct = wave_sum_u32(ct);
+    dt = wave_sum_u32(dt);
+    h = wave_sum(h);
     if (lane == 0) {
       double con = 0.0, dis = 0.0, hom = 0.0, asmv = 0.0, ene = 0.0, cor = 1.0;
       if (T > 0) {
         const double Td = (double)T;
-        con = (double)tct / Td;
-        dis = (double)tdt / Td;
-        hom = (hw + (double)nbg) / Td;  // background pairs: d = 0, weight 1
+        con = (double)ct / Td;
+        dis = (double)dt / Td;
+        hom = h / Td;
         asmv = (double)((unsigned long long)tas + (unsigned long long)nbg * nbg) / (Td * Td);
         ene = sqrt(asmv);
         const long long vi = T * (long long)tsii - (long long)tsi * tsi;
@@ -430,12 +437,14 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
   unsigned int* tab = reinterpret_cast<unsigned int*>(smem);
   unsigned int* red = tab + kTabW;
   int* nlist = reinterpret_cast<int*>(red + kRedW);
-  unsigned char* crop = reinterpret_cast<unsigned char*>(nlist + 4);
+  unsigned int* dh = reinterpret_cast<unsigned int*>(nlist + 4);  // |i-j| histogram [256]
+  unsigned char* crop = reinterpret_cast<unsigned char*>(dh + 256);
   unsigned short* list = reinterpret_cast<unsigned short*>(crop + kCrop);
   const int fov = blockIdx.y;
   const int n_items = hdr[fov].n_objects * C;
   if ((int)blockIdx.x >= n_items) return;
   for (int x = threadIdx.x; x < kTabW; x += kTT) tab[x] = 0u;
+  for (int x = threadIdx.x; x < 256; x += kTT) dh[x] = 0u;
   if (threadIdx.x == 0) *nlist = 0;
   __syncthreads();
   // software pipeline: the next item's metadata and LDS-sized crop are loaded into registers
@@ -473,10 +482,10 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
       const int dr = a == 0 ? 0 : a == 2 ? 3 : 2;
       const int dc = a == 0 ? 3 : a == 1 ? 2 : a == 2 ? 0 : -2;
       if (it.nb <= kCrop)
-        glcm_angle<true>(crop, tab, list, nlist, red, it.bh, it.bw, dr, dc,
+        glcm_angle<true>(crop, tab, list, nlist, dh, red, it.bh, it.bw, dr, dc,
                          f + a * CPX_N_TEX_PROPS, &pt);
       else
-        glcm_angle<false>(it.src, tab, list, nlist, red, it.bh, it.bw, dr, dc,
+        glcm_angle<false>(it.src, tab, list, nlist, dh, red, it.bh, it.bw, dr, dc,
                           f + a * CPX_N_TEX_PROPS, &pt);
     }
   }
@@ -676,8 +685,8 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
                       int H, int W, int max_label, int F, const cpx_object* objects_dev,
                       const cpx_fov_objects* hdr_dev, double* feats_dev, long long** crop_off_out) {
   static bool attr = false;
-  const size_t lds_t = sizeof(unsigned int) * (kTabW + kRedW + 4) + kCrop + 2 * kList;
-  static_assert(sizeof(unsigned int) * (kTabW + kRedW + 4) + kCrop + 2 * kList <= 160 * 1024,
+  const size_t lds_t = sizeof(unsigned int) * (kTabW + kRedW + 4 + 256) + kCrop + 2 * kList;
+  static_assert(sizeof(unsigned int) * (kTabW + kRedW + 4 + 256) + kCrop + 2 * kList <= 160 * 1024,
                 "GLCM LDS budget");
   static_assert(kNG * kNW + 2 * kNW <= kRedW, "reduction scratch");
   const size_t lds_s = sizeof(unsigned int) * 2 * kShapeW;

@@ -40,6 +40,8 @@ extern "C" {
 #define CPX_DTYPE_NONE 0  /* no flat-field: raw planes are used uncorrected           */
 #define CPX_DTYPE_F32 1
 #define CPX_DTYPE_F64 2
+#define CPX_DTYPE_IMAGE_F64 3 /* the "illum" buffer is the float64 plane itself (raw ignored): QC of
+                                 an image corrected on the host, calculate_qc_metrics(image, ch) */
 
 typedef struct cpx_ctx cpx_ctx;
 
@@ -287,6 +289,54 @@ int cpx_cpnet_conv3x3(cpx_ctx* ctx, const void* in, int N, int H, int W, int cin
                       const void* wpk, const float* bias, const void* res, int res_up,
                       const float* style, const float* scale, const float* shift, int relu,
                       void* y_out, void* z_out, int z_up);
+
+/* ==== per-FOV drop-in boundary ============================================
+ * Host planes in, host tables out, one context per GPU and one FOV at a time — the shape of the
+ * reference's per-site workers, for callers that are not PyTorch programs.  Everything is
+ * enqueued on the context's stream; cpx_fov_qc / _object_table / _features / _read_plane return
+ * results (they synchronise), cpx_fov_wait drains the stream.                                */
+#define CPX_QC_OK 0    /* slope from linregress                                               */
+#define CPX_QC_FLAT 1  /* <= 2 rings with power > 0: slope reported as 0.0 (:109-114)         */
+#define CPX_QC_NAN 2   /* the reference's exception path: slope NaN (:115-116)                */
+
+/* Illumination cache entry for channel `ch` (Illumination_QC_mult.py:180-199 illum_cache /
+ * Cellpose_GPU_s3fs.py:56-60): host [H][W] of dtype CPX_DTYPE_F32 / _F64, copied to the device.
+ * host == NULL: no file for this channel, raw planes are used (:195-197).  An illum whose shape
+ * differs from a FOV's planes is skipped for that FOV (:148-153).                            */
+int cpx_set_illum(cpx_ctx* ctx, int ch, const void* host, int dtype, int H, int W);
+/* Submit one FOV: planes[z*C + c] are host uint16 [H][W] (the plane-major chunk order of
+ * MaxProjection.py:81-86; Z = 1 for a plain site).  H2D, z max-projection (Z > 1,
+ * MaxProjection.py:45), flat-field division + PercentMaximal statistics per channel
+ * (Illumination_QC_mult.py:145-153 / Cellpose_GPU_s3fs.py:72).  The host planes must stay
+ * valid until the next synchronising call.                                                  */
+int cpx_fov_submit(cpx_ctx* ctx, int64_t site_id, const uint16_t* const* planes, int C, int Z,
+                   int H, int W);
+/* a2-a4 for the submitted FOV (calculate_qc_metrics, Illumination_QC_mult.py:98-125):
+ * slope_out / pctmax_out / status: [C] (any may be NULL).                                    */
+int cpx_fov_qc(cpx_ctx* ctx, double* slope_out, double* pctmax_out, int* status);
+/* Device views of the submitted FOV: corrected float32 [C][H][W] and the (z-max'd) uint16
+ * planes [C][H][W] (valid until the next cpx_fov_submit).                                     */
+int cpx_fov_planes(cpx_ctx* ctx, const float** corr_dev, const uint16_t** plane_dev);
+/* Copy channel `ch` of the (z-max'd) uint16 planes to host [H][W] (MaxProjection output).   */
+int cpx_fov_read_plane(cpx_ctx* ctx, int ch, uint16_t* host);
+/* a6 post-processing of one FOV from the CPnet output tiles (net_dev in `layout`, geom as for
+ * cpx_seg_average): tile average, flow dynamics, masks, resize, fill holes
+ * (Cellpose_GPU_s3fs.py:108,143-147, models.CellposeModel.eval).  labels_dev int32 [H][W].  */
+int cpx_fov_segment_post(cpx_ctx* ctx, const void* net_dev, int layout, const cpx_seg_geom* geom,
+                         const float* taper_dev, int niter, double flow_threshold, int min_size,
+                         int max_objects, int32_t* labels_dev, cpx_seg_stats* stats_dev);
+/* a7 object table of a label image (int32 [H][W], device) for the submitted FOV's shape:
+ * regionprops order, int centroids, `box` edge filter, kept index (Cellpose_GPU_s3fs.py:
+ * 149-163).  host_out: cpx_object [max_objects] (may be NULL, then only *n_out is set).
+ * A label above max_objects is an error (CPX_ERR_SHAPE) — size max_objects >= max label.   */
+int cpx_fov_object_table(cpx_ctx* ctx, const int32_t* labels_dev, int box, int max_objects,
+                    cpx_object* host_out, int* n_out);
+/* a8 feature rows of every object of labels_dev over the submitted FOV's corrected planes:
+ * host_out float64 [n][CPX_N_SHAPE + C*CPX_FEATURES_PER_CHANNEL] (row k = k-th object in
+ * ascending label order; the CellProfiler step of Feature_extraction_opt.py:164-167).       */
+int cpx_fov_features(cpx_ctx* ctx, const int32_t* labels_dev, int max_objects, double* host_out,
+                     int* n_out);
+int cpx_fov_wait(cpx_ctx* ctx);
 
 #ifdef __cplusplus
 }

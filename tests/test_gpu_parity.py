@@ -226,3 +226,13 @@ def test_expand_labels_bit_exact(dev, golden_dir):
             rc, ry = orc.secondary_objects(labs[b], dist)
             np.testing.assert_array_equal(gc[b], rc)
             np.testing.assert_array_equal(gy[b], ry)
+
+
+def test_features_bit_reproducible(dev):
+    """Two runs of cpx_features give identical bits (no order-dependent float sums)."""
+    H, W, C = 400, 420, 2
+    lab = sg.labels(77, H, W, n=30, rmin=5, rmax=60, skip_every=0)
+    planes = np.stack([sg.plane(780 + c, H, W, n_blobs=20).astype(np.float32) for c in range(C)])
+    a = _features(dev, lab, planes)
+    b = _features(dev, lab, planes)
+    np.testing.assert_array_equal(a, b)
