@@ -141,16 +141,21 @@ def main():
         "objects_features": dict(bound="hbm", work=feat_bytes, ms=per_step_ms["objects_features"]),
     }
 
+    pmc, pmc_src = pmc_traffic(B)
+
     def roof(k):
         d = kernels[k]
+        traffic = pmc.get(k)
         if d["bound"] == "hbm":
             ach = d["work"] / (d["ms"] * 1e-3) / 1e9
             return {"kernel": k, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "traffic_source": pmc_src if traffic else None,
                     "algorithmic_bytes_per_launch": d["work"], "avg_launch_ms": round(d["ms"], 4)}
         ach = d["work"] / (d["ms"] * 1e-3) / 1e12
         return {"kernel": k, "bound": "mfma", "achieved": round(ach, 1), "peak": BF16_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": traffic,
+                "traffic_source": pmc_src if traffic else None,
                 "algorithmic_flops_per_launch": d["work"], "avg_launch_ms": round(d["ms"], 4)}
 
     dominant = max(kernels, key=lambda k: kernels[k]["ms"])
@@ -184,6 +189,25 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(batch):
+    """HBM bytes per launch (one pipeline step of `batch` FOVs) per stage, from the newest
+    profiles/r*_pmc_traffic.json (tools/pmc_traffic.py: separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes over this bench, FETCH_SIZE doubled per the gfx950 correction).  Counters
+    cannot be read inside a timed run, so the committed measurement of the same workload is
+    used; {} if none is present."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return {}, None
+    d = json.load(open(files[-1]))
+    scale = batch / float(d.get("fovs_per_step", batch))
+    fam = d["per_family_bytes_per_step"]
+    out = {k: int(v["total"] * scale) for k, v in fam.items()}
+    if "cpnet" in fam:
+        out.setdefault("cpnet", int(fam["cpnet"]["total"] * scale))
+    return out, os.path.relpath(files[-1], REPO)
 
 
 def cpu_baseline(pool_batch, illum, C, H, W, cfg):
