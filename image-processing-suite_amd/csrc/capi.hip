@@ -15,6 +15,8 @@ void cpx_set_error(const char* fmt, ...) {
 
 int cpx_hip_fail(hipError_t e, const char* what) {
   cpx_set_error("HIP error %d (%s) in %s", (int)e, hipGetErrorString(e), what);
+  // consume the runtime's sticky last-error so the next launch check does not report it again
+  (void)hipGetLastError();
   return e == hipErrorOutOfMemory ? CPX_ERR_OOM : CPX_ERR_HIP;
 }
 

@@ -18,11 +18,12 @@ struct cpx_fov_state {
   int64_t site_id = -1;
   bool have = false;
   uint16_t* raw = nullptr;    // [C][Z][H][W] staging
-  uint16_t* plane = nullptr;  // [C][H][W] (z-max'd when Z > 1; aliases raw when Z == 1)
+  uint16_t* zplane = nullptr;  // [C][H][W] z max-projection (owned, allocated for Z > 1)
+  uint16_t* plane = nullptr;   // view of the current planes: zplane (Z > 1) or raw (Z == 1)
   float* corr = nullptr;      // [C][H][W]
   cpx_plane_stats* stats = nullptr;
   cpx_qc_result* qc = nullptr;
-  size_t raw_cap = 0, plane_cap = 0, corr_cap = 0;
+  size_t raw_cap = 0, zplane_cap = 0, corr_cap = 0;
   int chan_cap = 0;
   // object tables
   int max_label = 0;
@@ -40,7 +41,7 @@ void cpx_fov_free(cpx_ctx* ctx) {
   if (!f) return;
   for (void* p : f->illum)
     if (p) (void)hipFree(p);
-  void* bufs[] = {f->raw, f->plane == f->raw ? nullptr : f->plane, f->corr, f->stats, f->qc,
+  void* bufs[] = {f->raw, f->zplane, f->corr, f->stats, f->qc,
                   f->lstats, f->objects, f->hdr, f->feats, f->yf};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -146,15 +147,10 @@ int cpx_fov_submit(cpx_ctx* ctx, int64_t site_id, const uint16_t* const* planes,
   int rc;
   if ((rc = grow(ctx, (void**)&f->raw, &f->raw_cap, (size_t)C * Z * N * 2, "fov raw")) != CPX_OK) return rc;
   if (Z > 1) {
-    if (f->plane == f->raw) f->plane = nullptr, f->plane_cap = 0;
-    if ((rc = grow(ctx, (void**)&f->plane, &f->plane_cap, (size_t)C * N * 2, "fov plane")) != CPX_OK) return rc;
+    if ((rc = grow(ctx, (void**)&f->zplane, &f->zplane_cap, (size_t)C * N * 2, "fov plane")) != CPX_OK) return rc;
+    f->plane = f->zplane;
   } else {
-    if (f->plane && f->plane != f->raw) {
-      CPX_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-      CPX_CHECK_HIP(hipFree(f->plane));
-    }
-    f->plane = f->raw;
-    f->plane_cap = 0;
+    f->plane = f->raw;  // non-owning view: a single Z plane needs no projection buffer
   }
   if ((rc = grow(ctx, (void**)&f->corr, &f->corr_cap, (size_t)C * N * 4, "fov corr")) != CPX_OK) return rc;
   if (f->chan_cap < C) {

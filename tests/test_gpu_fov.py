@@ -30,8 +30,8 @@ def test_qc_cli_matches_reference_csv(sess, golden_dir, tmp_path):
     qc.main(["--load-data", os.path.join(d, "load_data.csv"), "--data-path", os.path.join(d, "images"),
              "--illum-path", os.path.join(d, "illum"), "--channels", "DNA", "AGP", "Mito",
              "--output", str(out), "--threads", "3"])
-    got = pd.read_csv(out)
-    exp = pd.read_csv(os.path.join(d, "expected_qc.csv"))
+    got = pd.read_csv(out, float_precision="round_trip")
+    exp = pd.read_csv(os.path.join(d, "expected_qc.csv"), float_precision="round_trip")
     assert list(got.columns) == list(exp.columns)
     assert len(got) == len(exp)
     for c in exp.columns:
