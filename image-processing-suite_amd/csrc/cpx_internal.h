@@ -102,7 +102,7 @@ __device__ __forceinline__ T wave_max(T v) {
 // fallback kernels (the two predicates must agree between the translation units).
 constexpr int kFastCropPx = 24576;
 constexpr int kFastMaskWords = 1024;
-constexpr int kFastShapeWords = 12288;
+constexpr int kFastShapeWords = 2048;  // 16 KiB of LDS for both masks: 8 blocks per CU
 __host__ __device__ inline bool cpx_tex_fits(int bh, int bw) {
   return bh * bw <= kFastCropPx && bh * ((bw + 31) >> 5) <= kFastMaskWords;
 }

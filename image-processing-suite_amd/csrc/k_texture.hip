@@ -537,7 +537,7 @@ __global__ __launch_bounds__(1024) void k_crop_offsets(int C, int max_label,
 // ---------------------------------------------------------------------------------------------
 // AreaShape fast path: bbox + 2-px margin membership bitmask in LDS
 constexpr int kST = 256;
-constexpr int kShapeW = kFastShapeWords;  // 48 KiB per bitmask (x2: membership + border)
+constexpr int kShapeW = kFastShapeWords;  // 8 KiB per bitmask (x2: membership + border)
 
 __device__ __forceinline__ unsigned int getw(const unsigned int* m, int wpr, int rows, int r, int cw) {
   return (r < 0 || r >= rows || cw < 0 || cw >= wpr) ? 0u : m[r * wpr + cw];
@@ -570,15 +570,28 @@ __global__ __launch_bounds__(kST) void k_shape_fast(const int* __restrict__ labe
     const int rows = o.bbox[2] - o.bbox[0] + 4, cols = o.bbox[3] - o.bbox[1] + 4;
     const int wpr = (cols + 31) >> 5;
     __syncthreads();
-    for (int r = ty; r < rows; r += 8) {
-      for (int cw = 0; cw < wpr; ++cw) {
+    // membership bitmask: each 32-lane half-wave builds one 32-bit word (r, cw); four words per
+    // half-wave are loaded before the first ballot so the label loads overlap
+    const int nw = rows * wpr;
+    for (int w0 = 0; w0 < nw; w0 += 4 * (kST / 32)) {
+      int lv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int w = w0 + u * (kST / 32) + ty;
+        const int r = w / wpr, cw = w - r * wpr;
         const int c = cw * 32 + tx;
         const int gr = R0 + r, gc = C0 + c;
-        const bool in = c < cols && gr >= 0 && gr < H && gc >= 0 && gc < W &&
-                        lab[(long long)gr * W + gc] == L;
-        const unsigned long long b = __ballot(in);
-        if (lane == 0) M[r * wpr + cw] = (unsigned int)b;
-        if (lane == 32) M[r * wpr + cw] = (unsigned int)(b >> 32);
+        const bool ok = w < nw && c < cols && gr >= 0 && gr < H && gc >= 0 && gc < W;
+        lv[u] = ok ? lab[(long long)gr * W + gc] : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int w = w0 + u * (kST / 32) + ty;
+        const unsigned long long b = __ballot(lv[u] == L);
+        if (w < nw) {
+          if (lane == 0) M[w] = (unsigned int)b;
+          if (lane == 32) M[w] = (unsigned int)(b >> 32);
+        }
       }
     }
     __syncthreads();
@@ -708,7 +721,7 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   hipLaunchKernelGGL(k_crop_offsets, dim3(B), dim3(1024), 0, ctx->stream, C, max_label,
                      objects_dev, hdr_dev, per_fov, crop_off);
   CPX_CHECK_LAUNCH("k_crop_offsets");
-  const int per_fov_s = std::max(1, std::min(max_label, (4 * ctx->n_cu + B - 1) / B));
+  const int per_fov_s = std::max(1, std::min(max_label, (8 * ctx->n_cu + B - 1) / B));
   hipLaunchKernelGGL(k_shape_fast, dim3(per_fov_s, B), dim3(kST), lds_s, ctx->stream,
                      (const int*)labels_dev, H, W, max_label, F, objects_dev, hdr_dev, feats_dev);
   CPX_CHECK_LAUNCH("k_shape_fast");
