@@ -44,9 +44,7 @@ constexpr int kTabW = 32768;         // packed u16 pair counters (128 KiB)
 constexpr int kCrop = kFastCropPx;   // u8 crop capacity (pixels)
 constexpr int kMaskW = kFastMaskWords;  // membership bitmask words (bh * ceil(bw/32))
 constexpr int kNW = kTT / 64;
-constexpr int kNG = 7;               // u32 partial sums per thread and angle (see glcm_angle)
-constexpr int kRedW = 192;           // LDS words for the cross-wave reduction (u32 + f64 parts)
-constexpr int kList = 3184;          // distinct-key list capacity (u16 keys)
+constexpr int kList = 3680;          // distinct-key list capacity (u16 keys)
 
 __device__ __forceinline__ int quantize(float v, bool in, float mn, float rng, bool flat) {
   const float m = v * (in ? 1.0f : 0.0f);
@@ -74,29 +72,47 @@ __device__ __forceinline__ unsigned int wave_sum_u32(unsigned int v) {
   return (unsigned int)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-// One GLCM angle (skimage graycomatrix offset (dr, dc), symmetric=False, normed) over an 8-bit
-// crop in LDS (or the global scratch slot), followed by greycoprops.
-//  1. count: every pixel pair adds 1 to its packed-u16 counter in a 64K-key LDS table
-//     (background pairs (0, 0) are only counted in a register); a pair that finds its counter
-//     at 0 appends the key to a distinct-key list (wave-aggregated slot reservation);
-//  2. per distinct key (i, j) with count c: c*i, c*j, c*i^2, c*j^2, c*i*j, c^2 (ASM) in exact
-//     u32 (with at most 65535 pairs per object every total fits: sum c*i^2 <= 65535 * 255^2
-//     < 2^32, sum c^2 <= 65535^2 < 2^32), and c into an integer |i-j| histogram; the listed
-//     counters are then cleared.  A crop with more distinct keys than the list holds scans (and
-//     clears) the whole table instead;
-//  3. DPP wave sums, one cross-wave pass; one wave turns the |i-j| histogram into contrast,
-//     dissimilarity and homogeneity in a fixed order (results never depend on the order in
-//     which keys were first seen), greycoprops on one lane.
-__device__ __forceinline__ void glcm_key(unsigned int c, unsigned int i, unsigned int j,
-                                         unsigned int* acc, unsigned int* dh) {
+// GLCM of one (object, channel) item: skimage graycomatrix offsets (dr, dc) for angles
+// 0, pi/4, pi/2, 3pi/4 at distance 3, symmetric=False, normed, then greycoprops.
+//  1. count (per angle): every pixel pair adds 1 to its packed-u16 counter in a 64K-key LDS
+//     table (background pairs (0, 0) are only counted in a register); a pair that finds its
+//     counter at 0 appends the key to a distinct-key list (wave-aggregated slot reservation);
+//  2. walk (per angle): per distinct key (i, j) with count c, exact u32 sums of c*i, c*j, c*i^2,
+//     c*j^2, c*i*j, c^2 (ASM), c*d^2 and c*d (d = |i-j|), and a u64 fixed-point sum of
+//     c * round(2^48 / (1 + d^2)) for homogeneity (per-term relative error <= 1.2e-10); the
+//     counter half is cleared by an LDS atomic AND as it is read.  With at most 65535 pairs per
+//     item every total fits (sum c*d^2 <= 65535 * 255^2 < 2^32, sum c^2 <= 65535^2 < 2^32).  A
+//     crop with more distinct keys than the list holds scans (and clears) the whole table;
+//  3. finish (once per item, all four angles): DPP wave sums, one cross-wave pass through the
+//     (by then all-zero) table, greycoprops on four lanes.  All sums are integer, so the result
+//     never depends on the order in which pairs or keys were visited.
+struct HomTable {
+  unsigned long long m[256];
+  constexpr HomTable() : m() {
+    for (int d = 0; d < 256; ++d) m[d] = (unsigned long long)(281474976710656.0 / (1.0 + (double)(d * d)) + 0.5);
+  }
+};
+__constant__ HomTable kHom = HomTable();
+constexpr double kHomScale = 1.0 / 281474976710656.0;  // 2^-48
+
+struct GlcmAcc {
+  unsigned int si, sj, sii, sjj, sij, asq, con, dis, bg;
+  unsigned long long hom;
+};
+constexpr int kAccW = 11;  // 32-bit words per angle in the cross-wave reduction
+
+__device__ __forceinline__ void glcm_key(unsigned int c, unsigned int i, unsigned int j, GlcmAcc& A) {
   const unsigned int ci = c * i, cj = c * j;
-  acc[0] += ci;
-  acc[1] += cj;
-  acc[2] += ci * i;
-  acc[3] += cj * j;
-  acc[4] += ci * j;
-  acc[5] += c * c;
-  atomicAdd(&dh[i > j ? i - j : j - i], c);
+  const unsigned int d = i > j ? i - j : j - i;
+  A.si += ci;
+  A.sj += cj;
+  A.sii += ci * i;
+  A.sjj += cj * j;
+  A.sij += ci * j;
+  A.asq += c * c;
+  A.con += c * d * d;
+  A.dis += c * d;
+  A.hom += (unsigned long long)c * kHom.m[d];
 }
 
 // Add a run of cnt pairs of one key; the lane that finds the counter at 0 appends the key to
@@ -117,10 +133,11 @@ __device__ __forceinline__ void glcm_flush(unsigned int* tab, unsigned short* li
   }
 }
 
+// Phase 1 of one angle over an 8-bit crop in LDS (or the global scratch slot); returns this
+// thread's background-pair count.
 template <bool LDS_CROP>
-__device__ void glcm_angle(const unsigned char* __restrict__ crop, unsigned int* tab,
-                           unsigned short* list, int* nlist, unsigned int* dh, unsigned int* red,
-                           int bh, int bw, int dr, int dc, double* out, long long* pt) {
+__device__ unsigned int glcm_count(const unsigned char* __restrict__ crop, unsigned int* tab,
+                                   unsigned short* list, int* nlist, int bh, int bw, int dr, int dc) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int rend = bh - dr;  // dr >= 0
   const int cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
@@ -130,53 +147,57 @@ __device__ void glcm_angle(const unsigned char* __restrict__ crop, unsigned int*
   // keys, and a lane adds a whole run of equal keys at once: LDS atomics to one address are
   // serialised (~2 cycles per lane), and smooth crops repeat keys along a row.
   unsigned int bg = 0;
-  {
-    const int Wc = cend - cbeg;
-    const int seg = (int)((T + kTT - 1) / kTT);
-    int p = (lane * kNW + wid) * seg;
-    const int pend = (int)min((long long)p + seg, T);
-    unsigned int cur = 0, cnt = 0;
-    if (p < pend) {
-      const int r = p / Wc, c = p - r * Wc;
-      const unsigned char* a = crop + r * bw + cbeg + c;
-      const unsigned char* b = a + dr * bw + dc;
-      int left = Wc - c;  // pairs left in this row
-      for (; p < pend; p += 4) {
-        // four keys loaded ahead (the 8 byte loads issue together), then consumed in order
-        unsigned int key[4];
+  const int Wc = cend - cbeg;
+  const int seg = (int)((T + kTT - 1) / kTT);
+  int p = (lane * kNW + wid) * seg;
+  const int pend = (int)min((long long)p + seg, T);
+  unsigned int cur = 0, cnt = 0;
+  if (p < pend) {
+    const int r = p / Wc, c = p - r * Wc;
+    const unsigned char* a = crop + r * bw + cbeg + c;
+    const unsigned char* b = a + dr * bw + dc;
+    int left = Wc - c;  // pairs left in this row
+    for (; p < pend; p += 4) {
+      // four keys loaded ahead (the 8 byte loads issue together), then consumed in order
+      unsigned int key[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          key[u] = ((unsigned int)*a << 8) | (unsigned int)*b;
-          const bool wrap = --left == 0;
-          a += wrap ? (bw - Wc + 1) : 1;
-          b += wrap ? (bw - Wc + 1) : 1;
-          left = wrap ? Wc : left;
-        }
+      for (int u = 0; u < 4; ++u) {
+        key[u] = ((unsigned int)*a << 8) | (unsigned int)*b;
+        const bool wrap = --left == 0;
+        a += wrap ? (bw - Wc + 1) : 1;
+        b += wrap ? (bw - Wc + 1) : 1;
+        left = wrap ? Wc : left;
+      }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (p + u >= pend) break;
-          if (key[u] != cur) {
-            if (cur) glcm_flush(tab, list, nlist, cur, cnt, lane);
-            else bg += cnt;
-            cur = key[u];
-            cnt = 0;
-          }
-          ++cnt;
+      for (int u = 0; u < 4; ++u) {
+        if (p + u >= pend) break;
+        if (key[u] != cur) {
+          if (cur) glcm_flush(tab, list, nlist, cur, cnt, lane);
+          else bg += cnt;
+          cur = key[u];
+          cnt = 0;
         }
+        ++cnt;
       }
     }
-    if (cur) glcm_flush(tab, list, nlist, cur, cnt, lane);
-    else bg += cnt;
   }
-  __syncthreads();
-  GLCM_MARK(2, pt);
-  const int n = *nlist;
-  unsigned int acc[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+  if (cur) glcm_flush(tab, list, nlist, cur, cnt, lane);
+  else bg += cnt;
+  return bg;
+}
+
+// Phase 2 of one angle: the n listed keys (or the whole table if the list overflowed) into A,
+// leaving every counter at zero.
+__device__ void glcm_walk(unsigned int* tab, const unsigned short* list, int n, GlcmAcc& A) {
   if (n <= kList) {
     for (int x = threadIdx.x; x < n; x += kTT) {
       const unsigned int key = list[x];
-      const unsigned int c = (tab[key >> 1] >> ((key & 1u) << 4)) & 0xffffu;
-      glcm_key(c, key >> 8, key & 255u, acc, dh);
+      const unsigned int sh = (key & 1u) << 4;
+      const unsigned int c = (tab[key >> 1] >> sh) & 0xffffu;
+      // the partner key of the same word may be read by another thread: clear only this half
+      __hip_atomic_fetch_and(&tab[key >> 1], ~(0xffffu << sh), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      glcm_key(c, key >> 8, key & 255u, A);
     }
   } else {  // dense fallback: scan and clear the whole table
     uint4* t4 = reinterpret_cast<uint4*>(tab);
@@ -191,54 +212,59 @@ __device__ void glcm_angle(const unsigned char* __restrict__ crop, unsigned int*
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           const unsigned int c = (w4[e] >> (16 * hh)) & 0xffffu;
-          if (c) glcm_key(c, i, ((unsigned int)(8 * x) & 255u) + 2u * e + hh, acc, dh);
+          if (c) glcm_key(c, i, ((unsigned int)(8 * x) & 255u) + 2u * e + hh, A);
         }
       }
     }
   }
-  {
-    const unsigned int w[kNG] = {acc[0], acc[1], acc[2], acc[3], acc[4], acc[5], bg};
+}
+
+// Phase 3: reduce the four angles' sums over the block and write greycoprops.  `red` is
+// kNW * 4 * kAccW words of the all-zero table; wave 0 zeroes them again before returning.
+__device__ void glcm_finish(const GlcmAcc (&A)[4], unsigned int* red, int bh, int bw,
+                            double* __restrict__ out) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-    for (int k = 0; k < kNG; ++k) {
+  for (int a = 0; a < 4; ++a) {
+    const unsigned int w[9] = {A[a].si, A[a].sj, A[a].sii, A[a].sjj, A[a].sij,
+                               A[a].asq, A[a].con, A[a].dis, A[a].bg};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
       const unsigned int t = wave_sum_u32(w[k]);
-      if (lane == 0) red[k * kNW + wid] = t;
+      if (lane == 0) red[(wid * 4 + a) * kAccW + k] = t;
+    }
+    const unsigned long long hs = wave_sum(A[a].hom);
+    if (lane == 0) {
+      red[(wid * 4 + a) * kAccW + 9] = (unsigned int)hs;
+      red[(wid * 4 + a) * kAccW + 10] = (unsigned int)(hs >> 32);
     }
   }
   __syncthreads();
-  GLCM_MARK(3, pt);
-  if (n <= kList)  // clear the listed counters (all reads are done)
-    for (int x = threadIdx.x; x < n; x += kTT) tab[list[x] >> 1] = 0u;
-  if (wid == 0) {  // |i-j| terms and greycoprops on one wave
-    unsigned int t = 0;
-    if (lane < kNG)
+  if (wid == 0) {
+    if (lane < 4) {
+      const int a = lane;
+      const int dr = a == 0 ? 0 : a == 2 ? 3 : 2;
+      const int dc = a == 0 ? 3 : a == 1 ? 2 : a == 2 ? 0 : -2;
+      const int rend = bh - dr;
+      const int cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
+      const long long T = (rend > 0 && cend > cbeg) ? (long long)rend * (cend - cbeg) : 0;
+      unsigned int v[9] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+      unsigned long long hs = 0;
+      for (int x = 0; x < kNW; ++x) {
+        const unsigned int* r = red + (x * 4 + a) * kAccW;
 #pragma unroll
-      for (int x = 0; x < kNW; ++x) t += red[lane * kNW + x];
-    const unsigned int tsi = __builtin_amdgcn_readlane(t, 0), tsj = __builtin_amdgcn_readlane(t, 1);
-    const unsigned int tsii = __builtin_amdgcn_readlane(t, 2), tsjj = __builtin_amdgcn_readlane(t, 3);
-    const unsigned int tsij = __builtin_amdgcn_readlane(t, 4), tas = __builtin_amdgcn_readlane(t, 5);
-    const unsigned int nbg = __builtin_amdgcn_readlane(t, 6);
-    unsigned int ct = 0, dt = 0;
-    double h = 0.0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int d = lane * 4 + q;
-      unsigned int cnt = dh[d];
-      dh[d] = 0u;  // restore for the next angle (this wave is the only reader)
-      if (d == 0) cnt += nbg;  // background pairs: d = 0
-      ct += cnt * (unsigned int)(d * d);
-      dt += cnt * (unsigned int)d;
-      h += (double)cnt * (1.0 / (1.0 + (double)(d * d)));
-    }
-    ct = wave_sum_u32(ct);
-    dt = wave_sum_u32(dt);
-    h = wave_sum(h);
-    if (lane == 0) {
+        for (int k = 0; k < 9; ++k) v[k] += r[k];
+        hs += (unsigned long long)r[9] | ((unsigned long long)r[10] << 32);
+      }
+      const unsigned int tsi = v[0], tsj = v[1], tsii = v[2], tsjj = v[3], tsij = v[4];
+      const unsigned int tas = v[5], ct = v[6], dt = v[7], nbg = v[8];
+      hs += (unsigned long long)nbg * kHom.m[0];  // background pairs: d = 0
       double con = 0.0, dis = 0.0, hom = 0.0, asmv = 0.0, ene = 0.0, cor = 1.0;
       if (T > 0) {
         const double Td = (double)T;
         con = (double)ct / Td;
         dis = (double)dt / Td;
-        hom = h / Td;
+        hom = ((double)hs * kHomScale) / Td;
         asmv = (double)((unsigned long long)tas + (unsigned long long)nbg * nbg) / (Td * Td);
         ene = sqrt(asmv);
         const long long vi = T * (long long)tsii - (long long)tsi * tsi;
@@ -247,17 +273,17 @@ __device__ void glcm_angle(const unsigned char* __restrict__ crop, unsigned int*
         const double sdi = sqrt((double)vi) / Td, sdj = sqrt((double)vj) / Td;
         cor = (sdi < 1e-15 || sdj < 1e-15) ? 1.0 : ((double)cv / (Td * Td)) / (sdi * sdj);
       }
-      out[CPX_TEX_CONTRAST] = con;
-      out[CPX_TEX_DISSIMILARITY] = dis;
-      out[CPX_TEX_HOMOGENEITY] = hom;
-      out[CPX_TEX_ASM] = asmv;
-      out[CPX_TEX_ENERGY] = ene;
-      out[CPX_TEX_CORRELATION] = cor;
+      double* o = out + a * CPX_N_TEX_PROPS;
+      o[CPX_TEX_CONTRAST] = con;
+      o[CPX_TEX_DISSIMILARITY] = dis;
+      o[CPX_TEX_HOMOGENEITY] = hom;
+      o[CPX_TEX_ASM] = asmv;
+      o[CPX_TEX_ENERGY] = ene;
+      o[CPX_TEX_CORRELATION] = cor;
     }
-    if (lane == 0) *nlist = 0;
+    // re-zero the reduction words (the table must be all-zero for the next item)
+    for (int x = lane; x < kNW * 4 * kAccW; x += 64) red[x] = 0u;
   }
-  __syncthreads();
-  GLCM_MARK(4, pt);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -435,17 +461,14 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
                                                  double* __restrict__ feats) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned int* tab = reinterpret_cast<unsigned int*>(smem);
-  unsigned int* red = tab + kTabW;
-  int* nlist = reinterpret_cast<int*>(red + kRedW);
-  unsigned int* dh = reinterpret_cast<unsigned int*>(nlist + 4);  // |i-j| histogram [256]
-  unsigned char* crop = reinterpret_cast<unsigned char*>(dh + 256);
+  int* nlist = reinterpret_cast<int*>(tab + kTabW);  // two counters: angle a uses a & 1
+  unsigned char* crop = reinterpret_cast<unsigned char*>(nlist + 4);
   unsigned short* list = reinterpret_cast<unsigned short*>(crop + kCrop);
   const int fov = blockIdx.y;
   const int n_items = hdr[fov].n_objects * C;
   if ((int)blockIdx.x >= n_items) return;
   for (int x = threadIdx.x; x < kTabW; x += kTT) tab[x] = 0u;
-  for (int x = threadIdx.x; x < 256; x += kTT) dh[x] = 0u;
-  if (threadIdx.x == 0) *nlist = 0;
+  if (threadIdx.x < 4) nlist[threadIdx.x] = 0;
   __syncthreads();
   // software pipeline: the next item's metadata and LDS-sized crop are loaded into registers
   // while the current item runs its four angles (the crop was written by k_tex_stage, possibly
@@ -478,16 +501,26 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
     }
 #endif
     // skimage offsets (dr, dc) for angles 0, pi/4, pi/2, 3pi/4 at distance 3
+    GlcmAcc acc[4] = {};
+#pragma unroll
     for (int a = 0; a < CPX_N_ANGLES; ++a) {
       const int dr = a == 0 ? 0 : a == 2 ? 3 : 2;
       const int dc = a == 0 ? 3 : a == 1 ? 2 : a == 2 ? 0 : -2;
-      if (it.nb <= kCrop)
-        glcm_angle<true>(crop, tab, list, nlist, dh, red, it.bh, it.bw, dr, dc,
-                         f + a * CPX_N_TEX_PROPS, &pt);
-      else
-        glcm_angle<false>(it.src, tab, list, nlist, dh, red, it.bh, it.bw, dr, dc,
-                          f + a * CPX_N_TEX_PROPS, &pt);
+      int* nl = nlist + (a & 1);
+      acc[a].bg = it.nb <= kCrop
+                      ? glcm_count<true>(crop, tab, list, nl, it.bh, it.bw, dr, dc)
+                      : glcm_count<false>(it.src, tab, list, nl, it.bh, it.bw, dr, dc);
+      __syncthreads();
+      GLCM_MARK(2, &pt);
+      const int n = *nl;
+      // the other counter was last read before the previous barrier; the next angle uses it
+      if (threadIdx.x == 0) nlist[(a + 1) & 1] = 0;
+      glcm_walk(tab, list, n, acc[a]);
+      __syncthreads();
+      GLCM_MARK(3, &pt);
     }
+    glcm_finish(acc, tab, it.bh, it.bw, f);
+    GLCM_MARK(4, &pt);
   }
 }
 
@@ -698,10 +731,10 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
                       int H, int W, int max_label, int F, const cpx_object* objects_dev,
                       const cpx_fov_objects* hdr_dev, double* feats_dev, long long** crop_off_out) {
   static bool attr = false;
-  const size_t lds_t = sizeof(unsigned int) * (kTabW + kRedW + 4 + 256) + kCrop + 2 * kList;
-  static_assert(sizeof(unsigned int) * (kTabW + kRedW + 4 + 256) + kCrop + 2 * kList <= 160 * 1024,
+  const size_t lds_t = sizeof(unsigned int) * (kTabW + 4) + kCrop + 2 * kList;
+  static_assert(sizeof(unsigned int) * (kTabW + 4) + kCrop + 2 * kList <= 160 * 1024,
                 "GLCM LDS budget");
-  static_assert(kNG * kNW + 2 * kNW <= kRedW, "reduction scratch");
+  static_assert(kNW * 4 * kAccW <= kTabW, "reduction scratch inside the table");
   const size_t lds_s = sizeof(unsigned int) * 2 * kShapeW;
   if (!attr) {
     CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_tex_glcm,
