@@ -105,6 +105,9 @@ SIGNATURES = {
     "cpx_fov_features": (_I, [_P, _P, _I, _P, _P]),
     "cpx_fov_wait": (_I, [_P]),
     "cpx_cpnet_conv3x3": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P, _I, _P, _P, _I]),
+    "cpx_cpnet_conv3x3_head": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P, _I, _P,
+                                    _P, _P, _I, _P]),
+    "cpx_cpnet_stem": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
 }
 
 _lib = None

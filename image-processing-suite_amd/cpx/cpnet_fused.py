@@ -13,9 +13,11 @@ Further rewrites, all exact in real arithmetic:
   * the down path's 2x2 max-pool is fused with the next block's BatchNorm+ReLU
     (cpx_cpnet_pool).
 Every 3x3 convolution with 32..256 channels runs as ONE native launch (cpx_cpnet_conv3x3,
-k_conv.hip: MFMA implicit GEMM with the epilogue applied to the fp32 accumulators); the
-2-channel input convolution and the 1x1 convolutions stay on MIOpen.  Eager PyTorch runs ~9
-full-tensor passes per convolution; this runs one.
+k_conv.hip: MFMA implicit GEMM with the epilogue applied to the fp32 accumulators); the stem
+(input BatchNorm+ReLU, 2-channel 3x3 convolution + epilogue and the first 1x1 projection) is
+one native pass (cpx_cpnet_stem) and the output 1x1 convolution runs in the last 3x3
+convolution's epilogue (cpx_cpnet_conv3x3_head); only the inner blocks' 1x1 projections stay on
+MIOpen.  Eager PyTorch runs ~9 full-tensor passes per convolution; this runs one.
 """
 from __future__ import annotations
 
@@ -109,6 +111,16 @@ class FusedCPnet:
         self.bn_out = _bn_affine(net.output[0], td)
         self.w_out = _conv_w(net.output[-1], td)
         self.b_out = net.output[-1].bias.detach().to(td, torch.bfloat16)
+        # native stem (input BN+ReLU, 3x3 2->32 conv + epilogue, 1x1 projection in one pass) and
+        # output head (1x1 32->nout fused into the last conv's epilogue); operands are the
+        # bf16-rounded weights the MIOpen path uses, in fp32
+        d0 = self.down[0]
+        self.native = lib is not None and d0["w"][0].shape[1] == 2 and self.up[0]["pk"][3] is not None
+        if self.native:
+            self.stem_w = d0["w"][0].float().contiguous()                      # [32][2][3][3]
+            self.stem_wp = d0["wp"].float().reshape(d0["wp"].shape[0], -1).contiguous()  # [32][2]
+            self.head_w = self.w_out.float().reshape(self.w_out.shape[0], -1).contiguous()  # [nout][32]
+            self.head_b = self.b_out.float().contiguous()
 
     # -- libcpx passes -------------------------------------------------------------------------
     def _epi(self, conv, bias, res=None, res_up=False, style=None, bn=None, relu=True,
@@ -157,6 +169,28 @@ class FusedCPnet:
                                       C, _p(xo), _p(zo)), "cpx_cpnet_pool")
         return xo, zo
 
+    def _stem(self, x, d):
+        N, _, H, W = x.shape
+        p = torch.empty((N, 32, H, W), dtype=x.dtype, device=x.device, memory_format=CL)
+        z = torch.empty_like(p, memory_format=CL)
+        (s0, h0), (s1, h1) = d["bn"][0], d["bn"][1]
+        check(self.lib.cpx_cpnet_stem(self.dev.h, _p(x), N, H, W, _p(s0), _p(h0), _p(self.stem_w),
+                                      _p(d["b"][0]), _p(s1), _p(h1), _p(self.stem_wp), _p(p), _p(z)),
+              "cpx_cpnet_stem")
+        return p, z
+
+    def _head(self, z, u, x1):
+        """last up conv + output BatchNorm/ReLU + output 1x1 conv in one native launch."""
+        N, Cin, H, W = z.shape
+        nout = self.head_w.shape[0]
+        out = torch.empty((N, nout, H, W), dtype=z.dtype, device=z.device, memory_format=CL)
+        scale, shift = self.bn_out
+        check(self.lib.cpx_cpnet_conv3x3_head(self.dev.h, _p(z), N, H, W, Cin, u["w"][3].shape[0],
+                                              _p(u["pk"][3]), _p(u["b"][3]), _p(x1), 0, None,
+                                              _p(scale), _p(shift), 1, None, _p(self.head_w),
+                                              _p(self.head_b), nout, _p(out)), "cpx_cpnet_conv3x3_head")
+        return out
+
     # -- forward -------------------------------------------------------------------------------
     @torch.no_grad()
     def __call__(self, x):
@@ -166,13 +200,16 @@ class FusedCPnet:
         xd = []
         zu = None
         for n, d in enumerate(self.down):
-            if n == 0:
-                xin = x
-                _, z0 = self._epi(x, None, bn=d["bn"][0])
+            if n == 0 and self.native:
+                p, z = self._stem(x, d)
             else:
-                xin, z0 = self._pool(xd[-1], d["bn"][0])
-            p = F.conv2d(xin, d["wp"])
-            _, z = self._conv(z0, d, 0, d["b"][0], bn=d["bn"][1])
+                if n == 0:
+                    xin = x
+                    _, z0 = self._epi(x, None, bn=d["bn"][0])
+                else:
+                    xin, z0 = self._pool(xd[-1], d["bn"][0])
+                p = F.conv2d(xin, d["wp"])
+                _, z = self._conv(z0, d, 0, d["b"][0], bn=d["bn"][1])
             x1, z = self._conv(z, d, 1, d["b1p"], res=p, bn=d["bn"][2], y=True)
             _, z = self._conv(z, d, 2, d["b"][2], bn=d["bn"][3])
             if n < len(self.down) - 1:
@@ -195,6 +232,8 @@ class FusedCPnet:
             if n > 0:
                 x_small, z0 = self._conv(z, u, 3, u["b"][3], res=x1, bn=self.up[n - 1]["bn"][0],
                                          y=True, z_up=True)
+            elif self.native:
+                return self._head(z, u, x1)
             else:
                 _, out_in = self._conv(z, u, 3, u["b"][3], res=x1, bn=self.bn_out)
         return F.conv2d(out_in, self.w_out, self.b_out)

@@ -38,6 +38,12 @@ struct ConvEpi {
   unsigned short* y;
   unsigned short* z;
   int res_up, relu, z_up;
+  // optional CPnet output head on z (cout 32 only): head[pixel][j] = head_b[j] +
+  // sum_c head_w[j][c] * bf16(z[c]), j < n_head <= 4; z itself is then not stored
+  const float* head_w;
+  const float* head_b;
+  unsigned short* head;
+  int n_head;
 };
 
 // 16-byte chunk swizzle: chunk q of LDS row `row` (a pixel or an output channel) lives at
@@ -265,7 +271,7 @@ void k_conv3x3w(const unsigned short* __restrict__ in, const unsigned short* __r
     drain(ep.y);
     __syncthreads();
   }
-  if (!ep.z) return;
+  if (!ep.z && !ep.head) return;
   if (ep.style) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -297,6 +303,39 @@ void k_conv3x3w(const unsigned short* __restrict__ in, const unsigned short* __r
     for (int p = 0; p < NSH; ++p)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[p][r] = fmaxf(acc[p][r], 0.0f);
+  }
+  if constexpr (BM == 32) {
+    if (ep.head) {
+      // each lane holds 16 of its pixel's 32 channels (8 g + 4 h + k); the lane pair
+      // (l, l ^ 32) completes the dot products
+#pragma unroll
+      for (int p = 0; p < NSH; ++p) {
+        float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int c = 8 * g + 4 * h + k;
+            const float zb = (float)(__bf16)acc[p][4 * g + k];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (j < ep.n_head) o[j] += ep.head_w[j * 32 + c] * zb;
+          }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] += __shfl_xor(o[j], 32, 64);
+        const int px = (ph * NSH + p) * 32 + l32;
+        const long long gp = gpix(px);
+        if (h == 0 && p < nsub && gp >= 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < ep.n_head) {
+              const __bf16 v = (__bf16)(o[j] + ep.head_b[j]);
+              ep.head[gp * ep.n_head + j] = __builtin_bit_cast(unsigned short, v);
+            }
+        }
+      }
+      return;
+    }
   }
   stage();
   __syncthreads();
@@ -366,12 +405,12 @@ extern "C" int cpx_cpnet_conv_cfg(int cin, int cout, int* bn, int* ck) {
   return CPX_OK;
 }
 
-extern "C" int cpx_cpnet_conv3x3(cpx_ctx* ctx, const void* in, int N, int H, int W, int cin,
-                                 int cout, const void* wpk, const float* bias, const void* res,
-                                 int res_up, const float* style, const float* scale,
-                                 const float* shift, int relu, void* y_out, void* z_out,
-                                 int z_up) {
-  CPX_REQUIRE(ctx && in && wpk && (y_out || z_out), CPX_ERR_ARG,
+static int conv3x3_impl(cpx_ctx* ctx, const void* in, int N, int H, int W, int cin, int cout,
+                        const void* wpk, const float* bias, const void* res, int res_up,
+                        const float* style, const float* scale, const float* shift, int relu,
+                        void* y_out, void* z_out, int z_up, const float* head_w,
+                        const float* head_b, int n_head, void* head_out) {
+  CPX_REQUIRE(ctx && in && wpk && (y_out || z_out || head_out), CPX_ERR_ARG,
               "cpx_cpnet_conv3x3: null argument");
   CPX_REQUIRE(N > 0 && H > 0 && W > 0, CPX_ERR_ARG, "cpx_cpnet_conv3x3: bad sizes");
   CPX_REQUIRE(!(scale == nullptr) == !(shift == nullptr), CPX_ERR_ARG,
@@ -381,8 +420,12 @@ extern "C" int cpx_cpnet_conv3x3(cpx_ctx* ctx, const void* in, int N, int H, int
   CPX_REQUIRE(((uintptr_t)in | (uintptr_t)wpk) % 16 == 0 &&
                   ((uintptr_t)res | (uintptr_t)y_out | (uintptr_t)z_out) % 16 == 0,
               CPX_ERR_ARG, "cpx_cpnet_conv3x3: misaligned buffers");
+  CPX_REQUIRE(!head_out || (cout == 32 && !z_out && head_w && head_b && n_head >= 1 && n_head <= 4),
+              CPX_ERR_ARG, "cpx_cpnet_conv3x3_head: head needs cout 32, no z_out, 1..4 outputs");
   ConvEpi ep{bias, (const unsigned short*)res, style, scale, shift, (unsigned short*)y_out,
-             (unsigned short*)z_out, res_up, relu, z_up};
+             (unsigned short*)z_out, res_up, relu, z_up, head_w, head_b,
+             (unsigned short*)head_out, n_head};
+
 #define CPX_CONVW(CI, CO, BM_, TY_, TX_)                             \
   if (cin == CI && cout == CO)                                       \
     return launch_wide<CI, CO, BM_, TY_, TX_>(ctx, in, wpk, ep, N, H, W);
@@ -399,4 +442,24 @@ extern "C" int cpx_cpnet_conv3x3(cpx_ctx* ctx, const void* in, int N, int H, int
 #undef CPX_CONVW
   cpx_set_error("cpx_cpnet_conv3x3: unsupported channels %d -> %d", cin, cout);
   return CPX_ERR_SHAPE;
+}
+
+extern "C" int cpx_cpnet_conv3x3(cpx_ctx* ctx, const void* in, int N, int H, int W, int cin,
+                                 int cout, const void* wpk, const float* bias, const void* res,
+                                 int res_up, const float* style, const float* scale,
+                                 const float* shift, int relu, void* y_out, void* z_out,
+                                 int z_up) {
+  return conv3x3_impl(ctx, in, N, H, W, cin, cout, wpk, bias, res, res_up, style, scale, shift,
+                      relu, y_out, z_out, z_up, nullptr, nullptr, 0, nullptr);
+}
+
+extern "C" int cpx_cpnet_conv3x3_head(cpx_ctx* ctx, const void* in, int N, int H, int W, int cin,
+                                      int cout, const void* wpk, const float* bias,
+                                      const void* res, int res_up, const float* style,
+                                      const float* scale, const float* shift, int relu,
+                                      void* y_out, const float* head_w, const float* head_b,
+                                      int n_head, void* head_out) {
+  CPX_REQUIRE(head_out != nullptr, CPX_ERR_ARG, "cpx_cpnet_conv3x3_head: null head output");
+  return conv3x3_impl(ctx, in, N, H, W, cin, cout, wpk, bias, res, res_up, style, scale, shift,
+                      relu, y_out, nullptr, 0, head_w, head_b, n_head, head_out);
 }

@@ -258,3 +258,89 @@ extern "C" int cpx_cpnet_pool(cpx_ctx* ctx, const void* in, const float* scale,
   CPX_CHECK_LAUNCH("k_cpnet_pool8");
   return CPX_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// CPnet stem: the first down block's entry on the 2-channel network input x, one pass instead
+// of four (input BatchNorm+ReLU pass, MIOpen 3x3 2->32 conv + its epilogue pass, MIOpen 1x1
+// projection):  z0 = bf16(relu(scale0 * x + shift0)) is formed while the 18 x 18 halo tile is
+// staged in LDS, then per pixel 32 outputs of the 3x3 conv (K = 18, fp32 FMAs; the weights are
+// block-uniform scalar loads) with bias0 -> BatchNorm1 -> ReLU -> z_out, and the 1x1
+// projection of the raw x -> p_out.  Memory-bound: 4 B read, 128 B written per pixel.
+namespace {
+
+constexpr int kSTY = 16, kSTX = 16;
+
+__global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem(
+    const unsigned short* __restrict__ x, int N, int H, int W, const float* __restrict__ scale0,
+    const float* __restrict__ shift0, const float* __restrict__ w0, const float* __restrict__ bias0,
+    const float* __restrict__ scale1, const float* __restrict__ shift1,
+    const float* __restrict__ wp, unsigned short* __restrict__ p_out,
+    unsigned short* __restrict__ z_out, int tiles_x, int tiles_y) {
+  __shared__ float sz[2][kSTY + 2][kSTX + 2];
+  const int tiles = tiles_x * tiles_y;
+  const int n = blockIdx.x / tiles, t = blockIdx.x - n * tiles;
+  const int ty0 = (t / tiles_x) * kSTY, tx0 = (t % tiles_x) * kSTX;
+  const float s00 = scale0[0], s01 = scale0[1], h00 = shift0[0], h01 = shift0[1];
+  for (int i = threadIdx.x; i < (kSTY + 2) * (kSTX + 2); i += kSTY * kSTX) {
+    const int hy = i / (kSTX + 2), hx = i - hy * (kSTX + 2);
+    const int gy = ty0 + hy - 1, gx = tx0 + hx - 1;
+    float a = 0.0f, b = 0.0f;  // zero padding of z0 (the conv input)
+    if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+      const unsigned int v = *reinterpret_cast<const unsigned int*>(x + (((long long)n * H + gy) * W + gx) * 2);
+      a = bf2f(f2bf(fmaxf(s00 * __uint_as_float(v << 16) + h00, 0.0f)));
+      b = bf2f(f2bf(fmaxf(s01 * __uint_as_float(v & 0xffff0000u) + h01, 0.0f)));
+    }
+    sz[0][hy][hx] = a;
+    sz[1][hy][hx] = b;
+  }
+  __syncthreads();
+  const int ly = threadIdx.x / kSTX, lx = threadIdx.x - ly * kSTX;
+  const int gy = ty0 + ly, gx = tx0 + lx;
+  if (gy >= H || gx >= W) return;
+  const long long pix = ((long long)n * H + gy) * W + gx;
+  float in[18];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) in[c * 9 + k] = sz[c][ly + k / 3][lx + k % 3];
+  const unsigned int xv = *reinterpret_cast<const unsigned int*>(x + pix * 2);
+  const float x0 = __uint_as_float(xv << 16), x1 = __uint_as_float(xv & 0xffff0000u);
+  uint4* zo = reinterpret_cast<uint4*>(z_out + pix * 32);
+  uint4* po = reinterpret_cast<uint4*>(p_out + pix * 32);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float zf[8], pf[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int co = q * 8 + e;
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 18; ++k) acc += w0[co * 18 + k] * in[k];
+      zf[e] = fmaxf(scale1[co] * (acc + bias0[co]) + shift1[co], 0.0f);
+      pf[e] = wp[co * 2] * x0 + wp[co * 2 + 1] * x1;
+    }
+    zo[q] = pack8(zf);
+    po[q] = pack8(pf);
+  }
+}
+
+}  // namespace
+
+extern "C" int cpx_cpnet_stem(cpx_ctx* ctx, const void* x, int N, int H, int W,
+                              const float* scale0, const float* shift0, const float* w0,
+                              const float* bias0, const float* scale1, const float* shift1,
+                              const float* wp, void* p_out, void* z_out) {
+  CPX_REQUIRE(ctx && x && scale0 && shift0 && w0 && bias0 && scale1 && shift1 && wp && p_out && z_out,
+              CPX_ERR_ARG, "cpx_cpnet_stem: null argument");
+  CPX_REQUIRE(N > 0 && H > 0 && W > 0, CPX_ERR_ARG, "cpx_cpnet_stem: bad sizes");
+  CPX_REQUIRE(((uintptr_t)x % 4) == 0 && ((uintptr_t)p_out | (uintptr_t)z_out) % 16 == 0,
+              CPX_ERR_ARG, "cpx_cpnet_stem: misaligned buffers");
+  const int tx = cpx_div_up(W, kSTX), ty = cpx_div_up(H, kSTY);
+  const long long blocks = (long long)N * tx * ty;
+  CPX_REQUIRE(blocks < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_stem: too many tiles");
+  hipLaunchKernelGGL(k_cpnet_stem, dim3((unsigned)blocks), dim3(kSTY * kSTX), 0, ctx->stream,
+                     (const unsigned short*)x, N, H, W, scale0, shift0, w0, bias0, scale1, shift1,
+                     wp, (unsigned short*)p_out, (unsigned short*)z_out, tx, ty);
+  CPX_CHECK_LAUNCH("k_cpnet_stem");
+  return CPX_OK;
+}

@@ -289,6 +289,22 @@ int cpx_cpnet_conv3x3(cpx_ctx* ctx, const void* in, int N, int H, int W, int cin
                       const void* wpk, const float* bias, const void* res, int res_up,
                       const float* style, const float* scale, const float* shift, int relu,
                       void* y_out, void* z_out, int z_up);
+/* cpx_cpnet_conv3x3 (cout = 32) whose BatchNorm+ReLU output z feeds the CPnet output 1x1
+ * convolution directly (Cellpose resnet_torch.CPnet.output; z is never stored):
+ *   head_out [N,H,W,n_head] bf16 = head_b[j] + sum_c head_w[j][c] * bf16(z[c]),  n_head <= 4. */
+int cpx_cpnet_conv3x3_head(cpx_ctx* ctx, const void* in, int N, int H, int W, int cin, int cout,
+                           const void* wpk, const float* bias, const void* res, int res_up,
+                           const float* style, const float* scale, const float* shift, int relu,
+                           void* y_out, const float* head_w, const float* head_b, int n_head,
+                           void* head_out);
+/* CPnet stem (first down block's entry) on x [N,H,W,2] bf16, one pass:
+ *   z0 = bf16(relu(scale0 * x + shift0))        (input BatchNorm + ReLU, zero-padded conv input)
+ *   z_out [N,H,W,32] = relu(scale1 * (conv3x3(z0, w0) + bias0) + shift1)
+ *   p_out [N,H,W,32] = conv1x1(x, wp)           (block projection, BatchNorm folded into wp)
+ * w0 fp32 [32][2][3][3], wp fp32 [32][2]; fp32 arithmetic, bf16 (RNE) stores.                */
+int cpx_cpnet_stem(cpx_ctx* ctx, const void* x, int N, int H, int W, const float* scale0,
+                   const float* shift0, const float* w0, const float* bias0, const float* scale1,
+                   const float* shift1, const float* wp, void* p_out, void* z_out);
 
 /* ==== per-FOV drop-in boundary ============================================
  * Host planes in, host tables out, one context per GPU and one FOV at a time — the shape of the

@@ -308,3 +308,65 @@ def test_cpnet_conv3x3_native(dev, cin, cout, H, W, res_up, z_up):
     assert ((ty - t).abs() <= 1e-2 * t.abs() + 1e-2).all(), (ty - t).abs().max().item()
     tz = zo.float()
     assert ((tz - z).abs() <= 1e-2 * z.abs() + 3e-2).all(), (tz - z).abs().max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W", [(224, 224), (20, 36)])
+def test_cpnet_stem_native(dev, H, W):
+    """cpx_cpnet_stem vs torch fp32: BN+ReLU of x (bf16-rounded), 3x3 conv 2->32 + bias ->
+    BN -> ReLU, and the 1x1 projection of x."""
+    from cpx.cpnet_fused import _p
+    td = dev.torch_device
+    CL = torch.channels_last
+    g = torch.Generator().manual_seed(H + W)
+    N = 2
+    x = _bf(torch.randn(N, 2, H, W, generator=g) * 3).to(td).contiguous(memory_format=CL)
+    s0, h0 = torch.randn(2, generator=g).to(td), torch.randn(2, generator=g).to(td)
+    w0 = _bf(torch.randn(32, 2, 3, 3, generator=g) * 0.3).float().to(td)
+    b0 = torch.randn(32, generator=g).to(td)
+    s1, h1 = torch.randn(32, generator=g).to(td), torch.randn(32, generator=g).to(td)
+    wp = _bf(torch.randn(32, 2, generator=g)).float().to(td)
+    p = torch.empty((N, 32, H, W), dtype=torch.bfloat16, device=td, memory_format=CL)
+    z = torch.empty_like(p, memory_format=CL)
+    check(dev.lib.cpx_cpnet_stem(dev.h, _p(x), N, H, W, _p(s0), _p(h0), _p(w0.contiguous()), _p(b0),
+                                 _p(s1), _p(h1), _p(wp.contiguous()), _p(p), _p(z)), "stem")
+    xf = x.float()
+    z0 = torch.clamp_min(s0[None, :, None, None] * xf + h0[None, :, None, None], 0.0)
+    z0 = z0.to(torch.bfloat16).float()
+    c = torch.nn.functional.conv2d(z0, w0, padding=1) + b0[None, :, None, None]
+    zr = torch.clamp_min(s1[None, :, None, None] * c + h1[None, :, None, None], 0.0)
+    pr = torch.einsum("ok,nkhw->nohw", wp, xf)
+    dev.sync()
+    assert ((z.float() - zr).abs() <= 1e-2 * zr.abs() + 1e-2).all(), (z.float() - zr).abs().max().item()
+    assert ((p.float() - pr).abs() <= 1e-2 * pr.abs() + 1e-2).all(), (p.float() - pr).abs().max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,H,W", [(32, 40, 56), (64, 16, 32)])
+def test_cpnet_conv3x3_head(dev, cin, H, W):
+    """cpx_cpnet_conv3x3_head vs torch fp32: conv + bias + residual -> BN -> ReLU -> bf16 ->
+    output 1x1 conv (3 outputs) + bias."""
+    from cpx.cpnet_fused import _p, _pack3x3
+    td = dev.torch_device
+    CL = torch.channels_last
+    g = torch.Generator().manual_seed(cin + H)
+    N, cout = 2, 32
+    x = _bf(torch.randn(N, cin, H, W, generator=g)).to(td).contiguous(memory_format=CL)
+    w = _bf(torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (9 * cin)) ** 0.5)
+    pk = _pack3x3(dev.lib, w, td)
+    bias = torch.randn(cout, generator=g).to(td)
+    res = _bf(torch.randn(N, cout, H, W, generator=g)).to(td).contiguous(memory_format=CL)
+    scale, shift = torch.randn(cout, generator=g).to(td), torch.randn(cout, generator=g).to(td)
+    hw = torch.randn(3, cout, generator=g).to(td)
+    hb = torch.randn(3, generator=g).to(td)
+    out = torch.empty((N, 3, H, W), dtype=torch.bfloat16, device=td, memory_format=CL)
+    check(dev.lib.cpx_cpnet_conv3x3_head(dev.h, _p(x), N, H, W, cin, cout, _p(pk), _p(bias), _p(res), 0,
+                                         None, _p(scale), _p(shift), 1, None, _p(hw), _p(hb), 3,
+                                         _p(out)), "conv3x3_head")
+    t = torch.nn.functional.conv2d(x.float(), w.float().to(td), padding=1) + bias[None, :, None, None] + res.float()
+    zr = torch.clamp_min(scale[None, :, None, None] * t + shift[None, :, None, None], 0.0)
+    zr = zr.to(torch.bfloat16).float()
+    ref = torch.einsum("oc,nchw->nohw", hw, zr) + hb[None, :, None, None]
+    dev.sync()
+    err = (out.float() - ref).abs()
+    assert (err <= 2e-2 * ref.abs() + 5e-2).all(), err.max().item()
