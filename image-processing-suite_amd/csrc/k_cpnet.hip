@@ -39,12 +39,20 @@ __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   }
 }
 
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// two fp32 -> packed bf16 pair, round to nearest even (one v_cvt_pk_bf16_f32)
+__device__ __forceinline__ unsigned int pk2(float lo, float hi) {
+  const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(unsigned int, v);
+}
+
 __device__ __forceinline__ uint4 pack8(const float* f) {
   uint4 v;
-  v.x = (unsigned int)f2bf(f[0]) | ((unsigned int)f2bf(f[1]) << 16);
-  v.y = (unsigned int)f2bf(f[2]) | ((unsigned int)f2bf(f[3]) << 16);
-  v.z = (unsigned int)f2bf(f[4]) | ((unsigned int)f2bf(f[5]) << 16);
-  v.w = (unsigned int)f2bf(f[6]) | ((unsigned int)f2bf(f[7]) << 16);
+  v.x = pk2(f[0], f[1]);
+  v.y = pk2(f[2], f[3]);
+  v.z = pk2(f[4], f[5]);
+  v.w = pk2(f[6], f[7]);
   return v;
 }
 
@@ -287,8 +295,8 @@ __global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem(
     float a = 0.0f, b = 0.0f;  // zero padding of z0 (the conv input)
     if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
       const unsigned int v = *reinterpret_cast<const unsigned int*>(x + (((long long)n * H + gy) * W + gx) * 2);
-      a = bf2f(f2bf(fmaxf(s00 * __uint_as_float(v << 16) + h00, 0.0f)));
-      b = bf2f(f2bf(fmaxf(s01 * __uint_as_float(v & 0xffff0000u) + h01, 0.0f)));
+      a = (float)(__bf16)fmaxf(s00 * __uint_as_float(v << 16) + h00, 0.0f);
+      b = (float)(__bf16)fmaxf(s01 * __uint_as_float(v & 0xffff0000u) + h01, 0.0f);
     }
     sz[0][hy][hx] = a;
     sz[1][hy][hx] = b;
@@ -315,9 +323,9 @@ __global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem(
       const int co = q * 8 + e;
       float acc = 0.0f;
 #pragma unroll
-      for (int k = 0; k < 18; ++k) acc += w0[co * 18 + k] * in[k];
-      zf[e] = fmaxf(scale1[co] * (acc + bias0[co]) + shift1[co], 0.0f);
-      pf[e] = wp[co * 2] * x0 + wp[co * 2 + 1] * x1;
+      for (int k = 0; k < 18; ++k) acc = __builtin_fmaf(w0[co * 18 + k], in[k], acc);
+      zf[e] = fmaxf(__builtin_fmaf(scale1[co], acc + bias0[co], shift1[co]), 0.0f);
+      pf[e] = __builtin_fmaf(wp[co * 2], x0, wp[co * 2 + 1] * x1);
     }
     zo[q] = pack8(zf);
     po[q] = pack8(pf);
