@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU-box pass that produces the round's committed evidence (run via gpurun from the repo
+# root): the default bench line (with cpu_baseline), a rocprofv3 kernel-trace + stats run of
+# the same bench, and separate FETCH_SIZE / WRITE_SIZE counter passes (MI355X_MICROARCH.md:
+# they do not fit one pass).  Outputs land under gpurun_out/round/.
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/round
+mkdir -p $O
+cd $R
+timeout -k 10 420 python -u bench.py > $O/bench_default.log 2>&1
+cd /tmp && export TMPDIR=/tmp
+cd $R
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- \
+  python -u bench.py --steps 6 --warmup 2 --no-cpu-baseline --stage-steps 1 > $O/bench_kt.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- \
+  python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --stage-steps 1 > $O/bench_fetch.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- \
+  python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --stage-steps 1 > $O/bench_write.log 2>&1
+
+# summarise on the box (raw per-dispatch CSVs are too large to bring back)
+python tools/prof_summary.py $O/kt/run_kernel_trace.csv --steps 4 --md > $O/kernels_steady.md
+cp $O/kt/run_kernel_stats.csv $O/kernel_stats.csv
+python tools/pmc_traffic.py $O/fetch $O/write --out $O/pmc_traffic.json > $O/pmc_traffic.log
+rm -rf $O/kt $O/fetch $O/write
+echo done
