@@ -13,8 +13,9 @@
 //     row transform are kept (real-input pair trick: two rows per complex FFT), then a full
 //     column FFT over those R_max+1 columns; positions with j > W/2 are read from the conjugate
 //     symmetric partner X[(H-i)%H, W-j];
-//   * fp64 mixed-radix Stockham FFTs in LDS (radices 2,3,4,5,7,8,11,13), fp64 quotient
-//     recomputed from raw/illum (bit-identical to the reference's fp64 input);
+//   * fp64 mixed-radix Stockham FFTs in LDS (radices 2,3,4,5,7,8,11,13; the odd primes as
+//     symmetric-pair DFTs with compile-time roots, half the multiplies of a direct DFT), fp64
+//     quotient recomputed from raw/illum (bit-identical to the reference's fp64 input);
 //   * ring sums are fixed-order (one lane per ring per column, then a fixed-order column sum),
 //     the slope is computed on device exactly as scipy.stats.linregress (np.cov, bias=1).
 #include "cpx_internal.h"
@@ -43,22 +44,30 @@ __device__ __forceinline__ cplx cmul(cplx a, cplx b) {
 }
 __device__ __forceinline__ cplx mul_negi(cplx a) { return {a.y, -a.x}; }  // a * (-i)
 
+// cos / sin (2 pi k / R), k = 0 .. (R-1)/2, correctly rounded (50-digit evaluation)
+template <int R>
+struct PrimeRoots;
+template <> struct PrimeRoots<3> { static constexpr double c[2] = {1.0, -0.5}; static constexpr double s[2] = {0.0, 0.8660254037844386}; };
+template <> struct PrimeRoots<5> { static constexpr double c[3] = {1.0, 0.30901699437494745, -0.8090169943749475}; static constexpr double s[3] = {0.0, 0.9510565162951535, 0.5877852522924731}; };
+template <> struct PrimeRoots<7> { static constexpr double c[4] = {1.0, 0.6234898018587335, -0.2225209339563144, -0.9009688679024191}; static constexpr double s[4] = {0.0, 0.7818314824680298, 0.9749279121818236, 0.4338837391175581}; };
+template <> struct PrimeRoots<11> { static constexpr double c[6] = {1.0, 0.8412535328311812, 0.41541501300188644, -0.14231483827328514, -0.6548607339452851, -0.9594929736144974}; static constexpr double s[6] = {0.0, 0.5406408174555976, 0.9096319953545183, 0.9898214418809327, 0.7557495743542583, 0.28173255684142967}; };
+template <> struct PrimeRoots<13> { static constexpr double c[7] = {1.0, 0.8854560256532099, 0.5680647467311558, 0.12053668025532305, -0.3546048870425356, -0.7485107481711011, -0.970941817426052}; static constexpr double s[7] = {0.0, 0.46472317204376856, 0.8229838658936564, 0.992708874098054, 0.9350162426854148, 0.6631226582407952, 0.23931566428755777}; };
 // In-place R-point forward DFT (exp(-2 pi i / R) convention) of v[0..R-1].
 // root[m] = W_R^m (held in registers; only the odd radices use it).
 template <int R>
 __device__ __forceinline__ void dft(cplx* v, const cplx* root) {
-  if (R == 2) {
+  if constexpr (R == 2) {
     cplx a = v[0], b = v[1];
     v[0] = cadd(a, b);
     v[1] = csub(a, b);
-  } else if (R == 4) {
+  } else if constexpr (R == 4) {
     cplx t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
     cplx t2 = cadd(v[1], v[3]), t3 = mul_negi(csub(v[1], v[3]));
     v[0] = cadd(t0, t2);
     v[2] = csub(t0, t2);
     v[1] = cadd(t1, t3);
     v[3] = csub(t1, t3);
-  } else if (R == 8) {
+  } else if constexpr (R == 8) {
     cplx e[4] = {v[0], v[2], v[4], v[6]};
     cplx o[4] = {v[1], v[3], v[5], v[7]};
     dft<4>(e, root);
@@ -75,13 +84,38 @@ __device__ __forceinline__ void dft(cplx* v, const cplx* root) {
     v[3] = cadd(e[3], o3);
     v[7] = csub(e[3], o3);
   } else {
+    // odd prime R: pair r with R - r (W^(R-r)m = conj(W^rm)):
+    //   s_r = v_r + v_(R-r), d_r = v_r - v_(R-r)
+    //   A_m = v_0 + sum_r s_r cos(2 pi rm/R),  B_m = sum_r d_r sin(2 pi rm/R)
+    //   X_m = A_m - i B_m,  X_(R-m) = A_m + i B_m
+    // (R-1)^2/2 real-by-complex products instead of (R-1)^2 complex ones; the cosines and
+    // sines are compile-time constants (correctly rounded).
+    constexpr int H = (R - 1) / 2;
+    cplx sp[H + 1], dm[H + 1];
+    cplx x0 = v[0];
+#pragma unroll
+    for (int r = 1; r <= H; ++r) {
+      sp[r] = cadd(v[r], v[R - r]);
+      dm[r] = csub(v[r], v[R - r]);
+      x0 = cadd(x0, sp[r]);
+    }
     cplx out[R];
+    out[0] = x0;
 #pragma unroll
-    for (int m = 0; m < R; ++m) {
-      cplx acc = v[0];
+    for (int m = 1; m <= H; ++m) {
+      cplx A = v[0], B = {0.0, 0.0};
 #pragma unroll
-      for (int r = 1; r < R; ++r) acc = cadd(acc, cmul(v[r], root[(r * m) % R]));
-      out[m] = acc;
+      for (int r = 1; r <= H; ++r) {
+        const int k = (r * m) % R;
+        const double c = k <= H ? PrimeRoots<R>::c[k] : PrimeRoots<R>::c[R - k];
+        const double sn = k <= H ? PrimeRoots<R>::s[k] : -PrimeRoots<R>::s[R - k];
+        A.x += sp[r].x * c;
+        A.y += sp[r].y * c;
+        B.x += dm[r].x * sn;
+        B.y += dm[r].y * sn;
+      }
+      out[m] = cplx{A.x + B.y, A.y - B.x};      // A - iB
+      out[R - m] = cplx{A.x - B.y, A.y + B.x};  // A + iB
     }
 #pragma unroll
     for (int m = 0; m < R; ++m) v[m] = out[m];
@@ -95,7 +129,7 @@ __device__ __forceinline__ void stockham_stage(const cplx* __restrict__ in, cplx
   const int tstep = N / (Ns * R);
   cplx root[R];
 #pragma unroll
-  for (int m = 0; m < R; ++m) root[m] = (R == 2 || R == 4 || R == 8) ? cplx{0.0, 0.0} : tw[m * nb];
+  for (int m = 0; m < R; ++m) root[m] = cplx{0.0, 0.0};  // odd radices use PrimeRoots<R>
   for (int j = threadIdx.x; j < nb; j += blockDim.x) {
     const int k = j % Ns;
     cplx v[R];
