@@ -37,6 +37,9 @@ def parse():
     ap.add_argument("--weights", default=None, help="CPnet state_dict (default: seeded random init)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stage-steps", type=int, default=3, help="instrumented steps after timing")
+    ap.add_argument("--zstack", type=int, default=0,
+                    help="configs[4] variant: Z planes per channel, z-max projected on the GPU "
+                         "inside every step (default size 2048); not the headline workload")
     return ap.parse_args()
 
 
@@ -57,8 +60,11 @@ def main():
     from cpx.cpnet import count_flops
     from cpx.device import Device
     from cpx.pipeline import FovPipeline, PipelineConfig
-    from cpx.synth import synth_fovs, synth_illum
+    from cpx.synth import synth_fovs, synth_illum, synth_zstack
 
+    Z = a.zstack
+    if Z > 1 and a.size == 2080:
+        a.size = 2048  # configs[4]: 2048x2048x5ch x 7 z-planes
     H = W = a.size
     C, B = a.channels, a.batch
     dev = Device(local)
@@ -73,8 +79,19 @@ def main():
     # this rank's wells (well w -> rank w % world); the synthetic batches are seeded
     # by the rank's own FOV keys, so ranks never share inputs and exchange nothing
     mine = shard.shard(shard.plate_fovs(n_wells=384), rank, world)
-    pool = [synth_fovs(B, C, H, W, td, seed=shard.fov_seed(mine[(i * B) % len(mine)]))
-            for i in range(a.pool)]
+    if Z > 1:
+        pool = [synth_zstack(B, C, Z, H, W, td, seed=shard.fov_seed(mine[(i * B) % len(mine)]))
+                for i in range(a.pool)]
+    else:
+        pool = [synth_fovs(B, C, H, W, td, seed=shard.fov_seed(mine[(i * B) % len(mine)]))
+                for i in range(a.pool)]
+
+    def run_step(i):
+        if Z > 1:  # a5: z-max projection into the pipeline's raw planes, then the hot path
+            dev.zmax(pool[i % a.pool], pipe.raw)
+            pipe.run()
+        else:
+            pipe.run(pool[i % a.pool])
     torch.cuda.synchronize()
 
     def barrier():
@@ -83,13 +100,13 @@ def main():
 
     n_obj = []
     for i in range(a.warmup):
-        pipe.run(pool[i % a.pool])
+        run_step(i)
         pipe.fetch()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        pipe.run(pool[i % a.pool])
+        run_step(i)
         res = pipe.fetch()
         n_obj.append([int(res.hdr[s]["n_objects"].sum()) for s in ("Nuclei", "Cells", "Cytoplasm")])
     torch.cuda.synchronize()
@@ -103,12 +120,20 @@ def main():
     stages = ["illum_qc", "segment", "objects_features"]
     acc = {s: 0.0 for s in stages}
     sub = {"illum": 0.0, "qc_rps": 0.0, "seg_prep": 0.0, "cpnet": 0.0, "seg_post": 0.0}
+    if Z > 1:
+        sub["zmax"] = 0.0
     for i in range(a.stage_steps):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(9)]
+        if Z > 1:
+            ez = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ez[0].record()
+            dev.zmax(pool[i % a.pool], pipe.raw)
+            ez[1].record()
+        src = pipe.raw if Z > 1 else pool[i % a.pool]
         ev[0].record()
-        dev.illum_correct(pool[i % a.pool], pipe.illum, C, pipe.corr, pipe.stats)
+        dev.illum_correct(src, pipe.illum, C, pipe.corr, pipe.stats)
         ev[1].record()
-        dev.qc_rps(pool[i % a.pool], pipe.illum, C, pipe.stats, pipe.qc)
+        dev.qc_rps(src, pipe.illum, C, pipe.stats, pipe.qc)
         ev[2].record()
         pipe.seg.prepare(pipe.corr)
         ev[3].record()
@@ -127,6 +152,8 @@ def main():
         acc["illum_qc"] += ev[0].elapsed_time(ev[2])
         acc["segment"] += ev[2].elapsed_time(ev[5])
         acc["objects_features"] += ev[5].elapsed_time(ev[6])
+        if Z > 1:
+            sub["zmax"] += ez[0].elapsed_time(ez[1])
     per_step_ms = {k: v / a.stage_steps for k, v in acc.items()}
     sub_ms = {k: v / a.stage_steps for k, v in sub.items()}
     N = H * W
@@ -140,8 +167,11 @@ def main():
         "cpnet": dict(bound="mfma", work=cpnet_flops, ms=sub_ms["cpnet"]),
         "objects_features": dict(bound="hbm", work=feat_bytes, ms=per_step_ms["objects_features"]),
     }
+    if Z > 1:  # Z u16 planes in, one u16 plane out per channel group
+        kernels["zmax"] = dict(bound="hbm", work=B * C * N * (2 * Z + 2), ms=sub_ms["zmax"])
 
-    pmc, pmc_src = pmc_traffic(B)
+    # the committed PMC traffic was measured on the headline workload; not valid for variants
+    pmc, pmc_src = pmc_traffic(B) if (Z <= 1 and H == 2080) else ({}, None)
 
     def roof(k):
         d = kernels[k]
@@ -172,7 +202,9 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32 planes / fp64 QC+features / bf16 CPnet",
         "data": "synthetic (HBM-resident uint16 plates, Poisson background, Gaussian nuclei + halos)",
-        "config": {"workload": "configs[1]: 384-well plate, 1 FOV/well, 2080x2080x5ch, illum->seg->feat",
+        "config": {"workload": ("configs[1]: 384-well plate, 1 FOV/well, 2080x2080x5ch, illum->seg->feat"
+                                if Z <= 1 else
+                                f"configs[4] variant: {H}x{W}x{C}ch x {Z} z-planes, z-max->illum->seg->feat"),
                    "fovs_per_step": B * world, "batch_per_gpu": B, "H": H, "W": W, "C": C,
                    "cellpose_model": cfg.model, "diameter": cfg.diameter,
                    "cpnet_weights": os.path.basename(weights) if weights else "seeded-random-init",
@@ -184,7 +216,7 @@ def main():
         "roofline_all": {k: roof(k) for k in kernels},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(pool[0], illum, C, H, W, cfg)
+        line["cpu_baseline"] = cpu_baseline(pipe.raw if Z > 1 else pool[0], illum, C, H, W, cfg)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

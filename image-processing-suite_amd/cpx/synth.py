@@ -78,3 +78,27 @@ def synth_illum(C: int, H: int, W: int, seed: int = 0) -> np.ndarray:
 
 def to_uint16(planes_i16: torch.Tensor) -> np.ndarray:
     return planes_i16.cpu().numpy().view(np.uint16)
+
+
+def synth_zstack(B: int, C: int, Z: int, H: int, W: int, device, seed: int = 0) -> torch.Tensor:
+    """Z-stack variant (SURVEY.md 8(d), configs[4]): int16 [B*C, Z, H, W] uint16 bit patterns.
+    Plane z is the in-focus FOV (synth_fovs) blurred by a Gaussian of sigma 2|z - Z//2| plus
+    Poisson(20) read noise, so the per-pixel argmax over z varies across the plane."""
+    focus = synth_fovs(B, C, H, W, device, seed=seed)
+    g = torch.Generator(device=device).manual_seed(seed + 7)
+    out = torch.empty((B * C, Z, H, W), dtype=torch.int16, device=device)
+    for p in range(B * C):
+        img = focus[p].to(torch.int32)
+        img = torch.where(img < 0, img + 65536, img).to(torch.float32)
+        spec = torch.fft.rfft2(img)
+        for z in range(Z):
+            s = 2.0 * abs(z - Z // 2)
+            if s > 0:
+                tf = _gauss_tf(H, W, s, device) / (2 * math.pi * s * s)  # unit-gain blur
+                plane = torch.fft.irfft2(spec * tf, s=(H, W))
+            else:
+                plane = img
+            plane = plane + torch.poisson(torch.full_like(plane, 20.0), generator=g)
+            v = torch.clamp(plane, 0, 65535).to(torch.int32)
+            out[p, z] = torch.where(v > 32767, v - 65536, v).to(torch.int16)
+    return out
