@@ -25,6 +25,7 @@
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kFT = 512;  // FFT kernels: more threads -> fewer butterflies per thread in registers
 constexpr int kMaxN = 4096;
 constexpr int kMaxStages = 12;
 
@@ -122,53 +123,66 @@ __device__ __forceinline__ void dft(cplx* v, const cplx* root) {
   }
 }
 
+// One Stockham stage IN PLACE on buf (LDS): every thread first gathers, twiddles and
+// transforms all of its butterflies into registers, the block synchronises, then the outputs
+// are scattered back.  One N-point buffer per transform instead of a ping-pong pair halves the
+// LDS footprint (W = 2080: 33 KB per row pair, 4 blocks per CU instead of 2).
 template <int R>
-__device__ __forceinline__ void stockham_stage(const cplx* __restrict__ in, cplx* __restrict__ out,
-                                               const cplx* __restrict__ tw, int N, int Ns) {
+__device__ __forceinline__ void stockham_stage_ip(cplx* __restrict__ buf,
+                                                  const cplx* __restrict__ tw, int N, int Ns) {
+  constexpr int MB = (kMaxN / R + kFT - 1) / kFT;  // butterflies per thread (max)
   const int nb = N / R;
   const int tstep = N / (Ns * R);
   cplx root[R];
 #pragma unroll
   for (int m = 0; m < R; ++m) root[m] = cplx{0.0, 0.0};  // odd radices use PrimeRoots<R>
-  for (int j = threadIdx.x; j < nb; j += blockDim.x) {
-    const int k = j % Ns;
-    cplx v[R];
+  cplx v[MB][R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[r] = in[j + r * nb];
-    if (Ns > 1) {
+  for (int q = 0; q < MB; ++q) {
+    const int j = threadIdx.x + q * kFT;
+    if (j < nb) {
+      const int k = j % Ns;
 #pragma unroll
-      for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[k * r * tstep]);
+      for (int r = 0; r < R; ++r) v[q][r] = buf[j + r * nb];
+      if (Ns > 1) {
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[q][r] = cmul(v[q][r], tw[k * r * tstep]);
+      }
+      dft<R>(v[q], root);
     }
-    dft<R>(v, root);
-    const int d = (j / Ns) * Ns * R + k;
-#pragma unroll
-    for (int r = 0; r < R; ++r) out[d + r * Ns] = v[r];
   }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < MB; ++q) {
+    const int j = threadIdx.x + q * kFT;
+    if (j < nb) {
+      const int k = j % Ns;
+      const int d = (j / Ns) * Ns * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) buf[d + r * Ns] = v[q][r];
+    }
+  }
+  __syncthreads();
 }
 
-// Runs the planned FFT on a (in LDS), ping-ponging with b; returns the buffer holding the result.
-__device__ cplx* fft_lds(cplx* a, cplx* b, const cplx* __restrict__ tw, const Plan& p) {
+// Runs the planned FFT in place on buf (in LDS).
+__device__ void fft_lds(cplx* buf, const cplx* __restrict__ tw, const Plan& p) {
   int Ns = 1;
   for (int s = 0; s < p.nst; ++s) {
     const int R = p.radix[s];
     switch (R) {
-      case 2: stockham_stage<2>(a, b, tw, p.n, Ns); break;
-      case 3: stockham_stage<3>(a, b, tw, p.n, Ns); break;
-      case 4: stockham_stage<4>(a, b, tw, p.n, Ns); break;
-      case 5: stockham_stage<5>(a, b, tw, p.n, Ns); break;
-      case 7: stockham_stage<7>(a, b, tw, p.n, Ns); break;
-      case 8: stockham_stage<8>(a, b, tw, p.n, Ns); break;
-      case 11: stockham_stage<11>(a, b, tw, p.n, Ns); break;
-      case 13: stockham_stage<13>(a, b, tw, p.n, Ns); break;
+      case 2: stockham_stage_ip<2>(buf, tw, p.n, Ns); break;
+      case 3: stockham_stage_ip<3>(buf, tw, p.n, Ns); break;
+      case 4: stockham_stage_ip<4>(buf, tw, p.n, Ns); break;
+      case 5: stockham_stage_ip<5>(buf, tw, p.n, Ns); break;
+      case 7: stockham_stage_ip<7>(buf, tw, p.n, Ns); break;
+      case 8: stockham_stage_ip<8>(buf, tw, p.n, Ns); break;
+      case 11: stockham_stage_ip<11>(buf, tw, p.n, Ns); break;
+      case 13: stockham_stage_ip<13>(buf, tw, p.n, Ns); break;
       default: break;
     }
     Ns *= R;
-    __syncthreads();
-    cplx* t = a;
-    a = b;
-    b = t;
   }
-  return a;
 }
 
 struct QcAux {
@@ -186,13 +200,12 @@ __device__ __forceinline__ double qval(const unsigned short* rp, const void* il,
 
 // Row pass: one block per (row pair, plane).  rowspec[plane][row][k], k < KC, complex f64.
 template <int ILLUM>
-__global__ __launch_bounds__(kThreads) void k_qc_rows(
+__global__ __launch_bounds__(kFT) void k_qc_rows(
     const unsigned short* __restrict__ raw, const void* __restrict__ illum, int C, int H, int W,
     const cpx_plane_stats* __restrict__ stats, const cplx* __restrict__ twW, Plan pw, int KC,
     cplx* __restrict__ rowspec, QcAux* __restrict__ aux) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cplx* a = reinterpret_cast<cplx*>(smem);
-  cplx* b = a + W;
   const int plane = blockIdx.y;
   const int ch = plane % C;
   const int r0 = 2 * blockIdx.x, r1 = r0 + 1;
@@ -204,7 +217,7 @@ __global__ __launch_bounds__(kThreads) void k_qc_rows(
   const cpx_plane_stats st = stats[plane];
   const double mean = st.sum_q / (double)st.n;
   unsigned long long eq = 0;
-  for (int c = threadIdx.x; c < W; c += kThreads) {
+  for (int c = threadIdx.x; c < W; c += kFT) {
     double qa = qval<ILLUM>(rp, il, (long long)r0 * W + c);
     double qb = r1 < H ? qval<ILLUM>(rp, il, (long long)r1 * W + c) : mean;
     eq += (qa == mean) + (r1 < H && qb == mean);
@@ -214,11 +227,12 @@ __global__ __launch_bounds__(kThreads) void k_qc_rows(
   eq = wave_sum(eq);
   if ((threadIdx.x & 63) == 0 && eq) atomicAdd(&aux[plane].eq_count, eq);
   __syncthreads();
-  cplx* z = fft_lds(a, b, twW, pw);
+  fft_lds(a, twW, pw);
+  const cplx* z = a;
   // Unpack the two real transforms for k < KC:
   //   Xa[k] = (Z[k] + conj(Z[-k])) / 2 ;  Xb[k] = (Z[k] - conj(Z[-k])) / (2i)
   cplx* outa = rowspec + ((long long)plane * H + r0) * KC;
-  for (int k = threadIdx.x; k < KC; k += kThreads) {
+  for (int k = threadIdx.x; k < KC; k += kFT) {
     cplx zk = z[k];
     cplx zn = z[k == 0 ? 0 : W - k];
     cplx xa = {0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)};
@@ -271,28 +285,40 @@ __device__ __forceinline__ double ring_rows(const double* __restrict__ p, int H,
 }
 
 // Column pass: one block per (column j < KC, plane).  Writes ringpart[plane][j][ring].
-__global__ __launch_bounds__(kThreads) void k_qc_cols(const cplx* __restrict__ rowspec, int H,
+__global__ __launch_bounds__(kFT) void k_qc_cols(const cplx* __restrict__ rowspec, int H,
                                                       int W, int KC, const cplx* __restrict__ twH,
                                                       Plan ph, int n_rings,
                                                       double* __restrict__ ringpart) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cplx* a = reinterpret_cast<cplx*>(smem);
-  cplx* b = a + H;
   const int j = blockIdx.x;
   const int plane = blockIdx.y;
   const cplx* src = rowspec + (long long)plane * H * KC + j;
-  for (int r = threadIdx.x; r < H; r += kThreads) a[r] = src[(long long)r * KC];
+  for (int r = threadIdx.x; r < H; r += kFT) a[r] = src[(long long)r * KC];
   __syncthreads();
-  cplx* x = fft_lds(a, b, twH, ph);
-  // power in place (as doubles in the other buffer)
-  double* pw = reinterpret_cast<double*>(x == a ? b : a);
-  for (int r = threadIdx.x; r < H; r += kThreads) {
-    cplx v = x[r];
-    pw[r] = v.x * v.x + v.y * v.y;
+  fft_lds(a, twH, ph);
+  // power in place (doubles over the first half of the buffer: read all, sync, write)
+  constexpr int PR = kMaxN / kFT;
+  double pv[PR];
+#pragma unroll
+  for (int q = 0; q < PR; ++q) {
+    const int r = threadIdx.x + q * kFT;
+    pv[q] = 0.0;
+    if (r < H) {
+      const cplx v = a[r];
+      pv[q] = v.x * v.x + v.y * v.y;
+    }
+  }
+  __syncthreads();
+  double* pw = reinterpret_cast<double*>(a);
+#pragma unroll
+  for (int q = 0; q < PR; ++q) {
+    const int r = threadIdx.x + q * kFT;
+    if (r < H) pw[r] = pv[q];
   }
   __syncthreads();
   double* out = ringpart + ((long long)plane * KC + j) * n_rings;
-  for (int t = threadIdx.x; t < n_rings; t += kThreads) {
+  for (int t = threadIdx.x; t < n_rings; t += kFT) {
     const int R = t + 2;
     double s = 0.0;
     // direct positions (i, j): fj = min(j, W-1-j)
@@ -487,24 +513,24 @@ extern "C" int cpx_qc_rps(cpx_ctx* ctx, const uint16_t* raw_dev, const void* ill
       CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_qc_cols, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
       attrs = true;
     }
-    const size_t sh_rows = 2 * sizeof(cplx) * (size_t)W;
+    const size_t sh_rows = sizeof(cplx) * (size_t)W;
     dim3 grow((H + 1) / 2, n_planes);
     const void* il = illum_dtype == CPX_DTYPE_NONE ? nullptr : illum_dev;
     if (illum_dtype == CPX_DTYPE_F32)
-      hipLaunchKernelGGL(k_qc_rows<1>, grow, dim3(kThreads), sh_rows, ctx->stream, raw_dev, il, C,
+      hipLaunchKernelGGL(k_qc_rows<1>, grow, dim3(kFT), sh_rows, ctx->stream, raw_dev, il, C,
                          H, W, stats_dev, (const cplx*)twW, pw, KC, rowspec, aux);
     else if (illum_dtype == CPX_DTYPE_F64)
-      hipLaunchKernelGGL(k_qc_rows<2>, grow, dim3(kThreads), sh_rows, ctx->stream, raw_dev, il, C,
+      hipLaunchKernelGGL(k_qc_rows<2>, grow, dim3(kFT), sh_rows, ctx->stream, raw_dev, il, C,
                          H, W, stats_dev, (const cplx*)twW, pw, KC, rowspec, aux);
     else if (illum_dtype == CPX_DTYPE_IMAGE_F64)
-      hipLaunchKernelGGL(k_qc_rows<3>, grow, dim3(kThreads), sh_rows, ctx->stream, raw_dev, il, C,
+      hipLaunchKernelGGL(k_qc_rows<3>, grow, dim3(kFT), sh_rows, ctx->stream, raw_dev, il, C,
                          H, W, stats_dev, (const cplx*)twW, pw, KC, rowspec, aux);
     else
-      hipLaunchKernelGGL(k_qc_rows<0>, grow, dim3(kThreads), sh_rows, ctx->stream, raw_dev, il, C,
+      hipLaunchKernelGGL(k_qc_rows<0>, grow, dim3(kFT), sh_rows, ctx->stream, raw_dev, il, C,
                          H, W, stats_dev, (const cplx*)twW, pw, KC, rowspec, aux);
     CPX_CHECK_LAUNCH("k_qc_rows");
-    const size_t sh_cols = 2 * sizeof(cplx) * (size_t)H;
-    hipLaunchKernelGGL(k_qc_cols, dim3(KC, n_planes), dim3(kThreads), sh_cols, ctx->stream,
+    const size_t sh_cols = sizeof(cplx) * (size_t)H;
+    hipLaunchKernelGGL(k_qc_cols, dim3(KC, n_planes), dim3(kFT), sh_cols, ctx->stream,
                        (const cplx*)rowspec, H, W, KC, (const cplx*)twH, ph, n_rings, ringpart);
     CPX_CHECK_LAUNCH("k_qc_cols");
   }
