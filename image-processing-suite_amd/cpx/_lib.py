@@ -84,6 +84,7 @@ SIGNATURES = {
     "cpx_illum_correct": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "cpx_qc_rps": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cpx_zmax_u16": (_I, [_P, _P, _I, _I, _I64, _P]),
+    "cpx_rebin_u16": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "cpx_objects": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cpx_crops": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P]),
     "cpx_features": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),

@@ -126,6 +126,14 @@ class Device:
         self._bind_stream()
         check(self.lib.cpx_zmax_u16(self.h, _ptr(src), G, Z, N, _ptr(out)), "cpx_zmax_u16")
 
+    # ---- 8(f) rank 4: re-binning ------------------------------------------------------------
+    def rebin(self, src: torch.Tensor, out_h: int, out_w: int, out: torch.Tensor):
+        """src: uint16 bits (int16) [G, H, W] ; out: [G, out_h, out_w] (PIL LANCZOS resize)."""
+        G, H, W = src.shape
+        assert src.is_contiguous() and out.is_contiguous() and tuple(out.shape) == (G, out_h, out_w)
+        self._bind_stream()
+        check(self.lib.cpx_rebin_u16(self.h, _ptr(src), G, H, W, out_h, out_w, _ptr(out)), "cpx_rebin_u16")
+
     # ---- a7 ------------------------------------------------------------------------------
     def objects(self, labels: torch.Tensor, max_label: int, box: int, lstats: torch.Tensor,
                 objects: torch.Tensor, hdr: torch.Tensor):

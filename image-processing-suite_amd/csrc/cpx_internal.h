@@ -26,6 +26,8 @@ struct cpx_ctx {
   int seg_key[6] = {0, 0, 0, 0, 0, 0};
   void* seg_tab = nullptr;
   cpx_fov_state* fov = nullptr;
+  // re-binning coefficient tables currently uploaded (WS_REBIN): W, out_w, H, out_h
+  int rebin_key[4] = {0, 0, 0, 0};
 };
 
 void cpx_fov_free(cpx_ctx* ctx);
@@ -43,6 +45,8 @@ enum {
   WS_SEG_DYN = 8,    // dPs, p, h, M, M0, seeds, counts
   WS_SEG_OBJ = 9,    // label stats / objects for flow error + fill holes
   WS_SEG_FILL = 10,  // fill-hole owner map
+  WS_REBIN = 11,     // LANCZOS re-binning bounds + weights (both axes)
+  WS_REBIN_TMP = 12, // re-binning horizontal-pass intermediate (16-bit)
 };
 
 void cpx_set_error(const char* fmt, ...);

@@ -177,6 +177,13 @@ int cpx_qc_rps(cpx_ctx* ctx, const uint16_t* raw_dev, const void* illum_dev, int
 int cpx_zmax_u16(cpx_ctx* ctx, const uint16_t* src_dev, int G, int Z, int64_t N,
                  uint16_t* out_dev);
 
+/* ---- 8(f) rank 4: image re-binning ------------------------------------------------------- *
+ * Replaces Image_re-binning.py:12-22 (PIL Image.resize(target, LANCZOS) of a 16-bit TIFF plane)
+ * for G planes: src_dev uint16 [G][H][W] -> dst_dev uint16 [G][out_h][out_w], bit-identical to
+ * Pillow's separable LANCZOS-3 resampler (fp64 weights and sums, 16-bit intermediate).       */
+int cpx_rebin_u16(cpx_ctx* ctx, const uint16_t* src_dev, int G, int H, int W, int out_h,
+                  int out_w, uint16_t* dst_dev);
+
 /* ---- a7: object table (regionprops order, int centroids, edge filter, kept index) ------- *
  * Replaces Cellpose_GPU_s3fs.py:149-163 (regionprops(masks), map(int, centroid), box test).
  * labels_dev : int32 [B][H][W].  max_label: capacity per FOV (labels above it are flagged in
