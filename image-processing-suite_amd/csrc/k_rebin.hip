@@ -9,8 +9,10 @@
 //   * each output: fp64 sum of pixel * weight in index order (separate multiply and add, this TU
 //     is built with -ffp-contract=off), ROUND_UP, stored as low byte CLIP8(v % 256) and high
 //     byte CLIP8(v >> 8) (Pillow's 16-bit store: values above 65535 keep their low byte).
-// HBM-bound: 2 B read per source pixel (the ~2 * support / scale re-reads of neighbouring
-// pixels hit L1/L2), 2 B written per output pixel, the intermediate stays mostly in L2/MALL.
+// Not HBM-bound: Pillow's exact fp64 arithmetic (one multiply + one add per tap, ~2 * ksize /
+// scale taps per source pixel) and the per-tap LDS reads of the horizontal pass bound it; the
+// algorithmic traffic is 2 B per source pixel + 2 B per output pixel (the 16-bit intermediate
+// of the rows the vertical pass reads makes one HBM round trip).
 #include "cpx_internal.h"
 #include <math.h>
 #include <vector>
@@ -28,7 +30,8 @@ __device__ __forceinline__ unsigned short pil_store16(double ss) {
   return (unsigned short)(lo | (hi << 8));
 }
 
-// Horizontal pass: out[g][r][xx] = resample of src row (y0 + r) along x; src [G][H][W],
+// Horizontal pass, generic (kernel sizes > 25, i.e. downscales by more than 4):
+// out[g][r][xx] = resample of src row (y0 + r) along x; src [G][H][W],
 // out [G][rows][ow].  A block owns kRT consecutive output columns for kRB consecutive rows:
 // each thread loads its column's weights once (tap-major kT[x][xx], coalesced), and for every
 // row the block first stages the source segment its columns read (one coalesced pass) in LDS,
@@ -106,7 +109,9 @@ __global__ __launch_bounds__(kRT) void k_rebin_h(const unsigned short* __restric
 // Vertical pass: out[g][yy][xx] = resample of column xx of src [G][rows][w] along y (bounds
 // relative to row 0).  A row's weights are wave-uniform; each thread computes VW adjacent
 // columns from VW-wide loads (VW = 4 when w % 4 == 0).
-template <int KM, int VW>
+// EX: KM is the exact kernel size; every tap is read (rows clamped into the image) and taps
+// past an output's count carry weight +0.0, which leaves the sum unchanged.
+template <int KM, int VW, bool EX = false>
 __global__ __launch_bounds__(kRT) void k_rebin_v(const unsigned short* __restrict__ src,
                                                  int rows, int w, int oh,
                                                  const int2* __restrict__ bnd,
@@ -125,8 +130,8 @@ __global__ __launch_bounds__(kRT) void k_rebin_v(const unsigned short* __restric
   double ss[VW];
 #pragma unroll
   for (int v = 0; v < VW; ++v) ss[v] = 0.0;
-  auto tap = [&](int y) {
-    const VT pv = *reinterpret_cast<const VT*>(col + (long long)y * w);
+  auto tap = [&](int y, int row) {
+    const VT pv = *reinterpret_cast<const VT*>(col + (long long)row * w);
     const double ky = k[y];
     if constexpr (VW == 4) {
       ss[0] += (double)(pv.x & 0xffffu) * ky;
@@ -137,12 +142,16 @@ __global__ __launch_bounds__(kRT) void k_rebin_v(const unsigned short* __restric
       ss[0] += (double)pv * ky;
     }
   };
-  if constexpr (KM == 0) {
-    for (int y = 0; y < b.y; ++y) tap(y);
+  if constexpr (EX) {
+    const int ylast = rows - 1 - b.x;
+#pragma unroll
+    for (int y = 0; y < KM; ++y) tap(y, min(y, ylast));
+  } else if constexpr (KM == 0) {
+    for (int y = 0; y < b.y; ++y) tap(y, y);
   } else {
 #pragma unroll
     for (int y = 0; y < KM; ++y)
-      if (y < b.y) tap(y);
+      if (y < b.y) tap(y, y);
   }
   unsigned short* o = out + (long long)g * oh * w + (long long)yy * w + (long long)xv * VW;
   if constexpr (VW == 4) {
@@ -152,6 +161,80 @@ __global__ __launch_bounds__(kRT) void k_rebin_v(const unsigned short* __restric
     *reinterpret_cast<uint2*>(o) = st;
   } else {
     o[0] = pil_store16(ss[0]);
+  }
+}
+
+// Horizontal pass, kernel sizes up to 25 (scale <= 4): every wave works on its own: it owns
+// 64 consecutive output columns and a run of rows, stages kHR source rows of its column span
+// in a wave-private LDS strip (no block barrier: LDS ops of one wave complete in order), and
+// issues the loads of the next kHR rows before resampling the current ones, so global latency
+// hides behind the fp64 work.  K (the exact kernel size) is a template constant: all taps
+// are read unconditionally — taps past an output's count have weight +0.0 and read finite
+// pixels of the strip — which leaves Pillow's left-to-right sum unchanged.
+constexpr int kHR = 4;      // rows per staging step
+// strip chunks a kernel size needs: K = 2 ceil(3 scale) + 1 bounds scale <= (K - 1) / 6, so a
+// 64-column group spans < 64 (K - 1) / 6 + K source pixels; + K pad
+__host__ __device__ constexpr int hw_chunks(int K) { return (64 * (K - 1) / 6 + 2 * K + 63) / 64; }
+constexpr int kHRows = 64;  // rows per block
+
+template <int K>
+__global__ __launch_bounds__(kRT) void k_rebin_hw(const unsigned short* __restrict__ src, int H,
+                                                  int W, int y0, int rows, int ow,
+                                                  const int2* __restrict__ bnd,
+                                                  const double* __restrict__ kT,
+                                                  unsigned short* __restrict__ out) {
+  constexpr int NL = hw_chunks(K);
+  __shared__ double strip[kRT / 64][kHR][NL * 64];  // fp64: each pixel converted once
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int xg = (blockIdx.x * (kRT / 64) + wv) * 64;
+  if (xg >= ow) return;  // whole wave
+  const int xx = min(xg + lane, ow - 1);
+  const bool act = xg + lane < ow;
+  const int2 bl = bnd[min(ow, xg + 64) - 1];
+  const int s0 = bnd[xg].x, span = bl.x + bl.y - s0;
+  const int bx = bnd[xx].x - s0;
+  double kw[K];
+#pragma unroll
+  for (int x = 0; x < K; ++x) kw[x] = kT[(long long)x * ow + xx];
+  const int g = blockIdx.z;
+  const int r0 = blockIdx.y * kHRows, nr = min(kHRows, rows - r0);
+  const unsigned short* base = src + ((long long)g * H + y0 + r0) * W + s0;
+  unsigned short* o = out + ((long long)g * rows + r0) * ow + xx;
+  // strip columns past the span load the span's last pixel (in bounds, finite)
+  int col[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) col[l] = min(l * 64 + lane, span - 1);
+  unsigned short v[kHR][NL];
+  auto load = [&](int r) {
+#pragma unroll
+    for (int rr = 0; rr < kHR; ++rr) {
+      const unsigned short* rp = base + (long long)min(r + rr, nr - 1) * W;
+#pragma unroll
+      for (int l = 0; l < NL; ++l) v[rr][l] = rp[col[l]];
+    }
+  };
+  load(0);
+  double(*st)[NL * 64] = strip[wv];
+  for (int r = 0; r < nr; r += kHR) {
+#pragma unroll
+    for (int rr = 0; rr < kHR; ++rr)
+#pragma unroll
+      for (int l = 0; l < NL; ++l) st[rr][l * 64 + lane] = (double)v[rr][l];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (r + kHR < nr) load(r + kHR);
+    double ss[kHR];
+#pragma unroll
+    for (int rr = 0; rr < kHR; ++rr) ss[rr] = 0.0;
+#pragma unroll
+    for (int x = 0; x < K; ++x)  // kHR independent chains, each in Pillow's tap order
+#pragma unroll
+      for (int rr = 0; rr < kHR; ++rr) ss[rr] += st[rr][bx + x] * kw[x];
+#pragma unroll
+    for (int rr = 0; rr < kHR; ++rr)
+      if (act && r + rr < nr) o[(long long)(r + rr) * ow] = pil_store16(ss[rr]);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   }
 }
 
@@ -255,17 +338,38 @@ extern "C" int cpx_rebin_u16(cpx_ctx* ctx, const uint16_t* src_dev, int G, int H
       out = (unsigned short*)cpx_ws(ctx, WS_REBIN_TMP, sizeof(uint16_t) * (size_t)G * rows * out_w);
       if (!out) return CPX_ERR_OOM;
     }
+    // strip chunks of the widest 64-column group (+ K pad for the unconditional taps)
+    int nl = 0;
+    for (int a = 0; a < out_w; a += 64) {
+      const int e = std::min(out_w, a + 64) - 1;
+      nl = std::max(nl, cpx_div_up(bh[2 * (size_t)e] + bh[2 * (size_t)e + 1] - bh[2 * (size_t)a] + ksh, 64));
+    }
+    if (ksh <= 25 && nl <= hw_chunks(ksh)) {
+      CPX_REQUIRE(cpx_div_up(rows, kHRows) <= 65535, CPX_ERR_ARG, "cpx_rebin_u16: plane too large");
+      const dim3 grid(cpx_div_up(out_w, kRT), cpx_div_up(rows, kHRows), G);
+#define CPX_REBIN_HW(KK)                                                                       \
+  case KK:                                                                                     \
+    hipLaunchKernelGGL(k_rebin_hw<KK>, grid, dim3(kRT), 0, ctx->stream,                         \
+                       (const unsigned short*)src_dev, H, W, y0, rows, out_w, dbh, dkh, out);     \
+    break;
+      switch (ksh) {
+        CPX_REBIN_HW(7) CPX_REBIN_HW(9) CPX_REBIN_HW(11) CPX_REBIN_HW(13) CPX_REBIN_HW(15)
+        CPX_REBIN_HW(17) CPX_REBIN_HW(19) CPX_REBIN_HW(21) CPX_REBIN_HW(23) CPX_REBIN_HW(25)
+        default: CPX_REQUIRE(false, CPX_ERR_ARG, "cpx_rebin_u16: kernel size");
+      }
+#undef CPX_REBIN_HW
+      CPX_CHECK_LAUNCH("k_rebin_hw");
+    } else {
     CPX_REQUIRE(cpx_div_up(rows, kRB) <= 65535, CPX_ERR_ARG, "cpx_rebin_u16: plane too large");
     const dim3 grid(cpx_div_up(out_w, kRT), cpx_div_up(rows, kRB), G);
 #define CPX_REBIN_H(KM)                                                                        \
   hipLaunchKernelGGL(k_rebin_h<KM>, grid, dim3(kRT), 0, ctx->stream,                          \
                      (const unsigned short*)src_dev, H, W, y0, rows, out_w, dbh, dkh, ksh, out)
-    if (ksh <= 8) CPX_REBIN_H(8);
-    else if (ksh <= 16) CPX_REBIN_H(16);
-    else if (ksh <= 32) CPX_REBIN_H(32);
+    if (ksh <= 32) CPX_REBIN_H(32);
     else CPX_REBIN_H(0);
 #undef CPX_REBIN_H
     CPX_CHECK_LAUNCH("k_rebin_h");
+    }
     vsrc = out;
     vrows = rows;
   }
@@ -278,17 +382,28 @@ extern "C" int cpx_rebin_u16(cpx_ctx* ctx, const uint16_t* src_dev, int G, int H
 #define CPX_REBIN_V(KM, VW)                                                                    \
   hipLaunchKernelGGL((k_rebin_v<KM, VW>), grid, dim3(kRT), 0, ctx->stream, vsrc, vrows, w,    \
                      out_h, dbv, dkv, ksv, (unsigned short*)dst_dev)
-    if (v4) {
-      if (ksv <= 8) CPX_REBIN_V(8, 4);
-      else if (ksv <= 16) CPX_REBIN_V(16, 4);
-      else if (ksv <= 32) CPX_REBIN_V(32, 4);
-      else CPX_REBIN_V(0, 4);
-    } else {
-      if (ksv <= 8) CPX_REBIN_V(8, 1);
-      else if (ksv <= 16) CPX_REBIN_V(16, 1);
-      else if (ksv <= 32) CPX_REBIN_V(32, 1);
-      else CPX_REBIN_V(0, 1);
+#define CPX_REBIN_VX(KK)                                                                       \
+  case KK:                                                                                     \
+    if (v4)                                                                                    \
+      hipLaunchKernelGGL((k_rebin_v<KK, 4, true>), grid, dim3(kRT), 0, ctx->stream, vsrc, vrows, \
+                         w, out_h, dbv, dkv, ksv, (unsigned short*)dst_dev);                   \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_rebin_v<KK, 1, true>), grid, dim3(kRT), 0, ctx->stream, vsrc, vrows, \
+                         w, out_h, dbv, dkv, ksv, (unsigned short*)dst_dev);                   \
+    break;
+    switch (ksv) {  // exact kernel sizes up to 25 (scale <= 4)
+      CPX_REBIN_VX(7) CPX_REBIN_VX(9) CPX_REBIN_VX(11) CPX_REBIN_VX(13) CPX_REBIN_VX(15)
+      CPX_REBIN_VX(17) CPX_REBIN_VX(19) CPX_REBIN_VX(21) CPX_REBIN_VX(23) CPX_REBIN_VX(25)
+      default:
+        if (v4) {
+          if (ksv <= 32) CPX_REBIN_V(32, 4);
+          else CPX_REBIN_V(0, 4);
+        } else {
+          if (ksv <= 32) CPX_REBIN_V(32, 1);
+          else CPX_REBIN_V(0, 1);
+        }
     }
+#undef CPX_REBIN_VX
 #undef CPX_REBIN_V
     CPX_CHECK_LAUNCH("k_rebin_v");
   }

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--size", type=int, default=2080)
     ap.add_argument("--res", type=int, default=1080)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--cpu", type=int, default=0,
+                    help="also time Pillow's own resize (what the reference calls) on this many planes")
     a = ap.parse_args()
     dev = Device(0)
     td = dev.torch_device
@@ -36,9 +38,20 @@ def main():
     ms = e0.elapsed_time(e1) / a.reps
     G = src.shape[0]
     byt = G * (a.size * a.size * 2 + a.res * a.res * 2)
-    print(json.dumps({"planes": G, "ms_per_call": round(ms, 4), "planes_per_s": round(G / ms * 1e3, 1),
-                      "fovs_per_s_5ch": round(G / 5 / ms * 1e3, 1), "achieved_GBs": round(byt / ms / 1e6, 1),
-                      "hbm_frac": round(byt / ms / 1e6 / 8000.0, 4)}))
+    res = {"planes": G, "ms_per_call": round(ms, 4), "planes_per_s": round(G / ms * 1e3, 1),
+           "fovs_per_s_5ch": round(G / 5 / ms * 1e3, 1), "achieved_GBs": round(byt / ms / 1e6, 1),
+           "hbm_frac": round(byt / ms / 1e6 / 8000.0, 4)}
+    if a.cpu:
+        import time
+        from PIL import Image
+        host = src[:a.cpu].cpu().numpy().view("uint16")
+        t0 = time.perf_counter()
+        for p in host:
+            Image.fromarray(p).resize((a.res, a.res), Image.LANCZOS)
+        dt = time.perf_counter() - t0
+        res["cpu_pillow"] = {"planes_per_s": round(a.cpu / dt, 2), "cores": 1, "kind": "reference",
+                             "sample": f"{a.cpu} planes {a.size}^2 -> {a.res}^2, PIL Image.resize LANCZOS"}
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":
