@@ -65,7 +65,12 @@ class FovObjects(ct.Structure):
                 ("overflow", ct.c_int32)]
 
 
-SIZES = {"cpx_plane_stats": 64, "cpx_qc_result": 24, "cpx_label_stats": 64, "cpx_object": 56,
+class ColumnStat(ct.Structure):
+    _fields_ = [("na_count", ct.c_int64), ("nunique", ct.c_int64), ("top_count", ct.c_int64),
+                ("second_count", ct.c_int64), ("max", ct.c_double), ("min", ct.c_double)]
+
+
+SIZES = {"cpx_column_stat": 48, "cpx_plane_stats": 64, "cpx_qc_result": 24, "cpx_label_stats": 64, "cpx_object": 56,
          "cpx_fov_objects": 16}
 
 _P = ct.c_void_p
@@ -85,6 +90,13 @@ SIGNATURES = {
     "cpx_qc_rps": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cpx_zmax_u16": (_I, [_P, _P, _I, _I, _I64, _P]),
     "cpx_rebin_u16": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
+    "cpx_group_kahan_accumulate": (_I, [_P, _P, _I, _I, ct.c_longlong, _P, _P, _I, _P, _P, _P]),
+    "cpx_group_mean_finalize": (_I, [_P, _P, _P, _I, _I, _P]),
+    "cpx_nancorr": (_I, [_P, _P, _I, _I, _P]),
+    "cpx_robust_mad": (_I, [_P, _P, _I, _I, _P, _I, ct.c_double, _P, _P]),
+    "cpx_mad_sigmoid": (_I, [_P, _P, _I, _I, _P, _P, ct.c_double, ct.c_double, _P]),
+    "cpx_column_stats": (_I, [_P, _P, _I, _I, _P]),
+    "cpx_cosine_groups": (_I, [_P, _P, _I, _I, _P, _P, _I, ct.c_longlong, _P, _P]),
     "cpx_objects": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cpx_crops": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P]),
     "cpx_features": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),

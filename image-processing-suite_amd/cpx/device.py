@@ -134,6 +134,65 @@ class Device:
         self._bind_stream()
         check(self.lib.cpx_rebin_u16(self.h, _ptr(src), G, H, W, out_h, out_w, _ptr(out)), "cpx_rebin_u16")
 
+    # ---- 8(f) rank 1: per-time profiles ------------------------------------------------------
+    def group_kahan(self, values: torch.Tensor, order: torch.Tensor, offs: torch.Tensor,
+                    sumx: torch.Tensor, comp: torch.Tensor, nobs: torch.Tensor):
+        """values fp64 [n, ld] (first K = sumx.shape[1] columns); order/offs int32; state [G, K]."""
+        n, ld = values.shape
+        G, K = sumx.shape
+        assert values.dtype == torch.float64 and values.is_contiguous() and K <= ld
+        assert order.dtype == torch.int32 and offs.dtype == torch.int32 and offs.numel() == G + 1
+        assert comp.shape == sumx.shape and nobs.shape == sumx.shape and nobs.dtype == torch.int64
+        self._bind_stream()
+        check(self.lib.cpx_group_kahan_accumulate(self.h, _ptr(values), n, K, ld, _ptr(order),
+                                                  _ptr(offs), G, _ptr(sumx), _ptr(comp), _ptr(nobs)),
+              "cpx_group_kahan_accumulate")
+
+    def group_finalize(self, sumx: torch.Tensor, nobs: torch.Tensor, out: torch.Tensor):
+        G, K = sumx.shape
+        assert out.shape == sumx.shape and out.dtype == torch.float64
+        self._bind_stream()
+        check(self.lib.cpx_group_mean_finalize(self.h, _ptr(sumx), _ptr(nobs), G, K, _ptr(out)),
+              "cpx_group_mean_finalize")
+
+    def nancorr(self, colmajor: torch.Tensor, out: torch.Tensor):
+        """colmajor fp64 [K, N] (one row per feature) -> out [K, K]."""
+        K, N = colmajor.shape
+        assert colmajor.is_contiguous() and out.shape == (K, K)
+        self._bind_stream()
+        check(self.lib.cpx_nancorr(self.h, _ptr(colmajor), N, K, _ptr(out)), "cpx_nancorr")
+
+    def robust_mad(self, colmajor: torch.Tensor, fit_rows: torch.Tensor, scale: float,
+                   med: torch.Tensor, mad: torch.Tensor):
+        K, N = colmajor.shape
+        assert colmajor.is_contiguous() and fit_rows.dtype == torch.int32
+        self._bind_stream()
+        check(self.lib.cpx_robust_mad(self.h, _ptr(colmajor), N, K, _ptr(fit_rows), fit_rows.numel(),
+                                      float(scale), _ptr(med), _ptr(mad)), "cpx_robust_mad")
+
+    def mad_sigmoid(self, colmajor: torch.Tensor, med, mad, eps: float, alpha: float, out):
+        K, N = colmajor.shape
+        assert colmajor.is_contiguous() and out.shape == colmajor.shape
+        self._bind_stream()
+        check(self.lib.cpx_mad_sigmoid(self.h, _ptr(colmajor), N, K, _ptr(med), _ptr(mad),
+                                       float(eps), float(alpha), _ptr(out)), "cpx_mad_sigmoid")
+
+    def column_stats(self, colmajor: torch.Tensor, stats: torch.Tensor):
+        """stats: uint8 [K * 48] (cpx_column_stat[K])."""
+        K, N = colmajor.shape
+        assert colmajor.is_contiguous() and stats.numel() >= 48 * K
+        self._bind_stream()
+        check(self.lib.cpx_column_stats(self.h, _ptr(colmajor), N, K, _ptr(stats)), "cpx_column_stats")
+
+    def cosine_groups(self, x: torch.Tensor, offs: torch.Tensor, pair_offs: torch.Tensor,
+                      norms: torch.Tensor, out: torch.Tensor):
+        N, F = x.shape
+        G = offs.numel() - 1
+        assert x.is_contiguous() and offs.dtype == torch.int32 and pair_offs.dtype == torch.int64
+        self._bind_stream()
+        check(self.lib.cpx_cosine_groups(self.h, _ptr(x), N, F, _ptr(offs), _ptr(pair_offs), G,
+                                         out.numel(), _ptr(norms), _ptr(out)), "cpx_cosine_groups")
+
     # ---- a7 ------------------------------------------------------------------------------
     def objects(self, labels: torch.Tensor, max_label: int, box: int, lstats: torch.Tensor,
                 objects: torch.Tensor, hdr: torch.Tensor):

@@ -184,6 +184,56 @@ int cpx_zmax_u16(cpx_ctx* ctx, const uint16_t* src_dev, int G, int Z, int64_t N,
 int cpx_rebin_u16(cpx_ctx* ctx, const uint16_t* src_dev, int G, int H, int W, int out_h,
                   int out_w, uint16_t* dst_dev);
 
+/* ---- 8(f) rank 1: per-time profiles (Pycyto_pertime.py:29-172) --------------------------- *
+ * Per-well aggregation, normalisation, feature-selection statistics and cosine similarities,
+ * each bit-identical to the library call the reference makes (oracle/profiles_oracle.py).   */
+
+/* pandas `groupby(keys).mean()` (Pycyto_pertime.py:69-72; pandas group_mean: Kahan sum per
+ * group and column in row order, NaN skipped).  values_dev: fp64 rows [n_rows][ld] (first K
+ * columns used); order_dev: int32 row indices grouped by group, original order within a group;
+ * offs_dev: int32 [G+1] group starts in order_dev.  sum/comp/nobs [G][K] carry the state
+ * (zero them first), so a table may be streamed in row order over several calls.           */
+int cpx_group_kahan_accumulate(cpx_ctx* ctx, const double* values_dev, int n_rows, int K,
+                               long long ld, const int32_t* order_dev, const int32_t* offs_dev,
+                               int G, double* sum_dev, double* comp_dev, int64_t* nobs_dev);
+/* out_dev [G][K] = sum / nobs (NaN where nobs == 0).                                          */
+int cpx_group_mean_finalize(cpx_ctx* ctx, const double* sum_dev, const int64_t* nobs_dev, int G,
+                            int K, double* out_dev);
+
+/* pandas DataFrame.corr(method="pearson") (pycytominer correlation_threshold,
+ * Pycyto_pertime.py:93-104): mat_dev column-major [K][N] (N <= 8192), out_dev [K][K].         */
+int cpx_nancorr(cpx_ctx* ctx, const double* mat_dev, int N, int K, double* out_dev);
+
+/* pycytominer RobustMAD.fit (normalize(method="mad_robustize"), Pycyto_pertime.py:83-88):
+ * per column of mat_dev (column-major [K][N]) over the rows fit_rows_dev[n_fit] (n_fit <= 4096):
+ * med = median of the non-NaN values, mad = median(|x - med|) / scale (scale = 1/1.4826).     */
+int cpx_robust_mad(cpx_ctx* ctx, const double* mat_dev, int N, int K, const int32_t* fit_rows_dev,
+                   int n_fit, double scale, double* med_dev, double* mad_dev);
+
+/* RobustMAD.transform + double_sigmoid + abs (Pycyto_pertime.py:13-16, 89-91), column-major:
+ * out = |s((x - med[j]) / (mad[j] + eps))|, s(z) = (z/alpha)^3 / sqrt(1 + (z/alpha)^6).      */
+int cpx_mad_sigmoid(cpx_ctx* ctx, const double* mat_dev, int N, int K, const double* med_dev,
+                    const double* mad_dev, double eps, double alpha, double* out_dev);
+
+/* feature_select statistics (variance_threshold, drop_na_columns, drop_outliers) per column of
+ * mat_dev (column-major [K][N], N <= 4096).                                                  */
+typedef struct cpx_column_stat {
+  int64_t na_count;      /* NaN rows */
+  int64_t nunique;       /* distinct non-NaN values */
+  int64_t top_count;     /* largest value count */
+  int64_t second_count;  /* second largest value count (0 if one distinct value) */
+  double max, min;       /* over non-NaN values (NaN if none) */
+} cpx_column_stat;
+int cpx_column_stats(cpx_ctx* ctx, const double* mat_dev, int N, int K, cpx_column_stat* stats_dev);
+
+/* sklearn cosine_similarity within groups of consecutive rows, upper triangle only
+ * (Pycyto_pertime.py:115-140; NaN read as 0 = fillna(0)).  x_dev row-major [N][F]; offs_dev
+ * int32 [G+1] row starts; pair_offs_dev int64 [G+1] output starts (group g has n(n-1)/2 pairs in
+ * np.triu_indices(n, 1) order); norms_dev [N] scratch; out_dev [n_pairs].                     */
+int cpx_cosine_groups(cpx_ctx* ctx, const double* x_dev, int N, int F, const int32_t* offs_dev,
+                      const int64_t* pair_offs_dev, int G, long long n_pairs, double* norms_dev,
+                      double* out_dev);
+
 /* ---- a7: object table (regionprops order, int centroids, edge filter, kept index) ------- *
  * Replaces Cellpose_GPU_s3fs.py:149-163 (regionprops(masks), map(int, centroid), box test).
  * labels_dev : int32 [B][H][W].  max_label: capacity per FOV (labels above it are flagged in

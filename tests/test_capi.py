@@ -37,6 +37,7 @@ def test_struct_sizes_match_header():
     assert ct.sizeof(_lib.LabelStats) == 64
     assert ct.sizeof(_lib.Object) == 56
     assert ct.sizeof(_lib.FovObjects) == 16
+    assert ct.sizeof(_lib.ColumnStat) == 48
 
 
 def test_error_paths_without_gpu():

@@ -1,0 +1,264 @@
+"""Per-time profiles (Pycyto_pertime.py:29-172).
+
+CPU: the restatement in oracle/profiles_oracle.py is pinned bit-exactly to the libraries the
+reference calls (pandas groupby mean / corr / median, scipy median_abs_deviation, sklearn
+cosine_similarity), and its feature_select shortcut to a literal pandas restatement of the
+pycytominer operations.  GPU: every libcpx kernel against those, then the whole CLI against the
+oracle pipeline.  pycytominer itself is absent (and unpinned by the reference), so the
+composition of normalize / feature_select is "parity unpinned" beyond the pinned pieces.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(0, os.path.join(REPO, "image-processing-suite_amd"))
+import profiles_oracle as po  # noqa: E402
+
+pd = pytest.importorskip("pandas")
+
+
+def _matrix(seed, n=300, K=9, nan=0.03, inf=True):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, K)) * rng.choice([1e-3, 1.0, 1e5], size=(n, K))
+    X[:, 2] = np.round(X[:, 2])            # ties
+    X[:, 4] = 3.0                          # constant
+    X[:, 5] = X[:, 1] * 2.0 + 1e-7 * rng.normal(size=n)   # near-collinear
+    X[rng.random((n, K)) < nan] = np.nan
+    if inf:
+        X[3, 0], X[7, 6] = np.inf, -np.inf
+    return X
+
+
+# ------------------------------------------------------------------------------------ CPU
+def test_oracle_group_mean_is_pandas():
+    rng = np.random.default_rng(1)
+    X = _matrix(1, n=2000, K=7)
+    g = rng.integers(0, 17, len(X))
+    ref = pd.DataFrame(X).assign(g=g).groupby("g").mean().to_numpy()
+    assert np.array_equal(po.group_kahan_mean(X, g, 17), ref, equal_nan=True)
+
+
+def test_oracle_corr_is_pandas():
+    X = _matrix(2, n=150, K=10)
+    assert np.array_equal(po.nancorr(X), pd.DataFrame(X).corr().to_numpy(), equal_nan=True)
+
+
+def test_oracle_robust_mad_is_pandas_scipy():
+    from scipy.stats import median_abs_deviation
+    for seed in (3, 4):
+        X = _matrix(seed, n=41 + seed, K=8, inf=False)
+        med, mad = po.robust_mad_fit(X)
+        assert np.array_equal(med, pd.DataFrame(X).median().to_numpy(), equal_nan=True)
+        ref = median_abs_deviation(X, nan_policy="omit", scale=1 / 1.4826)
+        assert np.array_equal(mad, ref, equal_nan=True)
+
+
+def test_oracle_cosine_matches_sklearn():
+    from sklearn.metrics.pairwise import cosine_similarity
+    X = np.nan_to_num(_matrix(5, n=12, K=30, inf=False))
+    X[3] = 0.0
+    np.testing.assert_allclose(po.cosine_similarity(X), cosine_similarity(X), rtol=0, atol=1e-14)
+
+
+def _pycytominer_exclusions(df, features):
+    """Literal pandas restatement of pycytominer's variance_threshold / get_na_columns /
+    correlation_threshold / drop_outlier_features (defaults), for pinning the oracle's
+    statistics shortcut."""
+    pop = df.loc[:, features]
+
+    def freq(col):
+        vc = col.value_counts()
+        if len(vc) < 2:
+            return np.nan
+        f = vc.iloc[1] / vc.iloc[0]
+        return np.nan if f < 0.05 else col.name
+    ex = pop.apply(freq, axis="rows")
+    out = set(ex[ex.isna()].index)
+    ratio = pop.nunique() / pop.shape[0]
+    out |= set(ratio[ratio < 0.01].index)
+    na = pop.isna().sum() / pop.shape[0]
+    out |= set(na[na > 0.05].index)
+    cor = pop.corr(method="pearson")
+    tri = cor.where(np.tril(np.ones(cor.shape), k=-1).astype(bool))
+    pairs = tri.stack().reset_index()
+    pairs.columns = ["pair_a", "pair_b", "correlation"]
+    pairs = pairs.query("correlation > 0.9")
+    order = cor.abs().sum().sort_values().index
+    for a, b in zip(pairs.pair_a, pairs.pair_b):
+        out.add(a if order.get_loc(a) > order.get_loc(b) else b)
+    mx, mn = pop.max().abs(), pop.min().abs()
+    out |= set(mx[(mx > 500) | (mn > 500)].index)
+    return out
+
+
+def test_oracle_feature_select_matches_pandas_restatement():
+    X = _matrix(6, n=60, K=12, nan=0.02, inf=False)
+    X[:, 7] = np.where(np.arange(60) < 59, 1.0, 2.0)      # freq ratio 1/59 < 0.05
+    X[:, 8] *= 1e4                                         # outliers
+    X[np.arange(60) % 7 == 0, 9] = np.nan                  # > 5 % NaN
+    feats = [f"F{i}" for i in range(12)]
+    df = pd.DataFrame(X, columns=feats)
+    assert po.excluded_features(df, feats) == _pycytominer_exclusions(df, feats)
+
+
+def test_oracle_pipeline_runs(tmp_path):
+    from cpx.synth_tables import plate_tables
+    tb = plate_tables(n_wells=16, sites=2, objects=12, n_feat=10, seed=2)
+    sel, avg, sims = po.pycyto_pertime(tb["Image"], tb["Nuclei"], tb["Cells"], tb["Cytoplasm"],
+                                       "Plate_1", "T1", str(tmp_path / "sel.csv"))
+    assert len(sel) == 16 and sel.columns[0] == "Metadata_Plate"
+    assert set(avg.Metadata_compound_code) == {"DMSO", "CmpA", "CmpB", "CmpC"}
+    assert avg.average_cosine_similarity.notna().all()
+
+
+# ------------------------------------------------------------------------------------ GPU
+@pytest.fixture(scope="module")
+def eng():
+    from cpx.profiles import ProfileEngine
+    return ProfileEngine()
+
+
+@pytest.mark.gpu
+def test_gpu_group_mean_bit_exact(eng):
+    from cpx.synth_tables import plate_tables
+    tb = plate_tables(n_wells=40, sites=3, objects=30, n_feat=None, seed=7)
+    nuc = tb["Nuclei"].merge(tb["Image"][po.IMAGE_META], on="ImageNumber")
+    nuc.loc[5, "AreaShape_Area"] = np.inf
+    nuc.loc[9, "AreaShape_Perimeter"] = -np.inf
+    nuc["flag"] = nuc.ObjectNumber % 2 == 0          # bool column
+    nuc["label"] = "x"                               # nuisance column (dropped)
+    ref = nuc.groupby(po.KEYS, as_index=False).mean(numeric_only=True)
+    got = eng.group_mean(nuc)
+    assert list(got.columns) == list(ref.columns)
+    for c in ref.columns:
+        if c in po.KEYS:
+            assert (got[c].to_numpy() == ref[c].to_numpy()).all()
+        else:
+            assert np.array_equal(got[c].to_numpy(), ref[c].to_numpy(), equal_nan=True), c
+
+
+@pytest.mark.gpu
+def test_gpu_object_means_without_merge(eng):
+    """The merge-free path == merge(Image metadata) -> drop -> groupby mean, including a well
+    whose images have no objects and a bool column."""
+    from cpx.profiles import object_means_applies
+    from cpx.synth_tables import plate_tables
+    tb = plate_tables(n_wells=20, sites=2, objects=15, n_feat=12, seed=13)
+    img, nuc = tb["Image"], tb["Nuclei"]
+    nuc = nuc[~nuc.ImageNumber.isin([3, 4])].reset_index(drop=True)   # well 2 has no objects
+    nuc["flag"] = nuc.ObjectNumber % 3 == 0
+    assert object_means_applies(img, nuc)
+    ref = (nuc.merge(img[po.IMAGE_META], on="ImageNumber", how="left")
+           .drop(["ImageNumber", "Metadata_Site", "Metadata_ConcLevel"], axis=1)
+           .groupby(po.KEYS, as_index=False).mean(numeric_only=True))
+    got = eng.object_means(nuc, img)
+    assert list(got.columns) == list(ref.columns) and len(got) == len(ref)
+    for c in ref.columns:
+        if c in po.KEYS:
+            assert (got[c].to_numpy() == ref[c].to_numpy()).all()
+        else:
+            assert np.array_equal(got[c].to_numpy(), ref[c].to_numpy(), equal_nan=True), c
+
+
+@pytest.mark.gpu
+def test_gpu_nancorr_bit_exact(eng):
+    X = _matrix(8, n=384, K=70)
+    assert np.array_equal(eng.corr(X), pd.DataFrame(X).corr().to_numpy(), equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_gpu_robust_mad_and_sigmoid(eng):
+    import torch
+    from scipy.stats import median_abs_deviation
+    X = _matrix(9, n=384, K=40, inf=False)
+    fit = np.nonzero(np.arange(384) % 4 == 0)[0]
+    X[fit, 3] = 5.0          # mad 0: (x - 5) / 1e-18 overflows the powers -> NaN, as numpy
+    X[1, 6] = 1e60           # x^3 finite, x^6 overflows -> 0, as numpy
+    med_ref = pd.DataFrame(X[fit]).median().to_numpy()
+    mad_ref = median_abs_deviation(X[fit], nan_policy="omit", scale=1 / 1.4826)
+    col = torch.from_numpy(np.ascontiguousarray(X.T)).to(eng.td)
+    med = torch.empty(40, dtype=torch.float64, device=eng.td)
+    mad = torch.empty_like(med)
+    eng.dev.robust_mad(col, torch.from_numpy(fit.astype(np.int32)).to(eng.td), po.MAD_SCALE, med, mad)
+    assert np.array_equal(med.cpu().numpy(), med_ref, equal_nan=True)
+    assert np.array_equal(mad.cpu().numpy(), mad_ref, equal_nan=True)
+    # transform + double sigmoid + abs.  The kernel forms x**3 and x**6 correctly rounded;
+    # numpy's array power is host-dependent (AVX-512 builds use a SIMD pow within 1 ulp), so
+    # against numpy the tolerance is 4 ulp, and against the correctly rounded powers (exact
+    # rational arithmetic) the result is bit-identical.
+    got = eng.mad_sigmoid(X, fit)
+    ref = po.mad_sigmoid_abs(X, med_ref, mad_ref)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    np.testing.assert_allclose(got[ok], ref[ok], rtol=4 * 2.0 ** -52, atol=0)
+    print(f"mad_sigmoid bit-identical to numpy: {np.mean(got[ok] == ref[ok]):.6f}")
+    from fractions import Fraction
+    Z = (X - med_ref) / (mad_ref + po.MAD_EPS)
+    T = Z / po.ALPHA
+    sample = ok & (np.arange(384)[:, None] % 3 == 0) & (np.abs(T) < 1e30)
+    for i, j in zip(*np.nonzero(sample)):
+        t = Fraction(float(T[i, j]))
+        p3, p6 = float(t ** 3), float(t ** 6)
+        cr = abs(p3 / np.sqrt(1.0 + p6))
+        assert got[i, j] == cr, (i, j)
+
+
+@pytest.mark.gpu
+def test_gpu_column_stats_and_exclusions(eng):
+    X = _matrix(10, n=200, K=16, nan=0.02, inf=False)
+    X[:, 7] = np.where(np.arange(200) < 199, 1.0, 2.0)
+    X[np.arange(200) % 9 == 0, 9] = np.nan
+    X[:, 11] = np.nan
+    for a, b in zip(eng.column_stats(X), po.column_stats(X)):
+        assert tuple(a[:4]) == tuple(b[:4])
+        assert np.array_equal(np.array(a[4:]), np.array(b[4:]), equal_nan=True)
+    feats = [f"F{i}" for i in range(16)]
+    df = pd.DataFrame(X, columns=feats)
+    assert eng.excluded_features(df, feats) == po.excluded_features(df, feats)
+
+
+@pytest.mark.gpu
+def test_gpu_group_cosine(eng):
+    from sklearn.metrics.pairwise import cosine_similarity
+    rng = np.random.default_rng(11)
+    groups = [rng.normal(size=(n, 57)) for n in (1, 2, 5, 9)]
+    groups[2][1] = 0.0
+    groups[3][0, 3] = np.nan
+    got = eng.group_cosine(groups)
+    for g, v in zip(groups, got):
+        s = cosine_similarity(np.nan_to_num(g, nan=0.0))
+        ref = s[np.triu_indices_from(s, k=1)]
+        assert v.shape == ref.shape
+        np.testing.assert_allclose(v, ref, rtol=0, atol=1e-13)
+
+
+@pytest.mark.gpu
+def test_gpu_pertime_cli_matches_oracle(eng, tmp_path):
+    """python -m cpx.profiles over a CSV tree == the oracle pipeline on the same tables."""
+    from cpx.profiles import main
+    from cpx.synth_tables import plate_tables, write_tree
+    tb = plate_tables(n_wells=32, sites=3, objects=25, n_feat=None, seed=12)
+    write_tree(str(tmp_path / "in"), "Exp/Plate_1", "T1", tb)
+    main(["--bucket_name", str(tmp_path / "in"), "--base_folder", "Exp/Plate_1", "--times", "T1",
+          "--output_bucket", str(tmp_path / "out"), "--output_prefix", "res/Plate_1",
+          "--local_dir", str(tmp_path / "tmp")])
+    d = tmp_path / "out" / "res" / "Plate_1" / "T1"
+    sel = pd.read_csv(d / "CP_features_selected.csv")
+    avg = pd.read_csv(d / "CPfeatures_average_cosine_similarity.csv")
+    rd = {n: po.read_table(str(tmp_path / "in" / "Exp" / "Plate_1" / "T1" / f"{n}.csv"))
+          for n in ("Image", "Nuclei", "Cells", "Cytoplasm")}
+    rsel, ravg, _ = po.pycyto_pertime(rd["Image"], rd["Nuclei"], rd["Cells"], rd["Cytoplasm"],
+                                      "Plate_1", "T1", str(tmp_path / "ref.csv"))
+    assert list(sel.columns) == list(rsel.columns)
+    meta = [c for c in sel.columns if c.startswith("Metadata_")]
+    assert sel[meta].equals(rsel[meta])
+    feats = [c for c in sel.columns if c not in meta]
+    # numpy's SIMD array pow (oracle side) strays up to a few tens of ulp from the correctly
+    # rounded powers the kernel forms at small magnitudes: rtol 1e-13
+    np.testing.assert_allclose(sel[feats].to_numpy(), rsel[feats].to_numpy(), rtol=1e-13, atol=0)
+    assert (avg.iloc[:, :3].astype(str).to_numpy() == ravg.iloc[:, :3].astype(str).to_numpy()).all()
+    np.testing.assert_allclose(avg.average_cosine_similarity, ravg.average_cosine_similarity, atol=1e-13)
