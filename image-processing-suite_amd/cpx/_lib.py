@@ -90,11 +90,12 @@ SIGNATURES = {
     "cpx_qc_rps": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cpx_zmax_u16": (_I, [_P, _P, _I, _I, _I64, _P]),
     "cpx_rebin_u16": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
-    "cpx_group_kahan_accumulate": (_I, [_P, _P, _I, _I, ct.c_longlong, _P, _P, _I, _P, _P, _P]),
+    "cpx_group_kahan_accumulate": (_I, [_P, _P, _I, _I, ct.c_longlong, _P, _P, _I, _P, _P, _P, _P, _P]),
     "cpx_group_mean_finalize": (_I, [_P, _P, _P, _I, _I, _P]),
+    "cpx_group_median": (_I, [_P, _P, _I, _I, ct.c_longlong, _P, _P, _I, _I, _P, _P, _P]),
     "cpx_nancorr": (_I, [_P, _P, _I, _I, _P]),
     "cpx_robust_mad": (_I, [_P, _P, _I, _I, _P, _I, ct.c_double, _P, _P]),
-    "cpx_mad_sigmoid": (_I, [_P, _P, _I, _I, _P, _P, ct.c_double, ct.c_double, _P]),
+    "cpx_mad_transform": (_I, [_P, _P, _I, _I, _P, _P, ct.c_double, _I, ct.c_double, _P]),
     "cpx_column_stats": (_I, [_P, _P, _I, _I, _P]),
     "cpx_cosine_groups": (_I, [_P, _P, _I, _I, _P, _P, _I, ct.c_longlong, _P, _P]),
     "cpx_objects": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),

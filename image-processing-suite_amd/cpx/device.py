@@ -136,17 +136,34 @@ class Device:
 
     # ---- 8(f) rank 1: per-time profiles ------------------------------------------------------
     def group_kahan(self, values: torch.Tensor, order: torch.Tensor, offs: torch.Tensor,
-                    sumx: torch.Tensor, comp: torch.Tensor, nobs: torch.Tensor):
-        """values fp64 [n, ld] (first K = sumx.shape[1] columns); order/offs int32; state [G, K]."""
+                    sumx: torch.Tensor, comp: torch.Tensor, nobs: torch.Tensor,
+                    row_scale: torch.Tensor | None = None, col_scaled: torch.Tensor | None = None):
+        """values fp64 [n, ld] (first K = sumx.shape[1] columns); order/offs int32; state [G, K];
+        optional fp64 row_scale [n] applied to the columns where uint8 col_scaled [K] != 0."""
         n, ld = values.shape
         G, K = sumx.shape
         assert values.dtype == torch.float64 and values.is_contiguous() and K <= ld
         assert order.dtype == torch.int32 and offs.dtype == torch.int32 and offs.numel() == G + 1
         assert comp.shape == sumx.shape and nobs.shape == sumx.shape and nobs.dtype == torch.int64
         self._bind_stream()
+        if row_scale is not None:
+            assert row_scale.dtype == torch.float64 and row_scale.numel() == n
+            assert col_scaled is not None and col_scaled.dtype == torch.uint8 and col_scaled.numel() == K
         check(self.lib.cpx_group_kahan_accumulate(self.h, _ptr(values), n, K, ld, _ptr(order),
-                                                  _ptr(offs), G, _ptr(sumx), _ptr(comp), _ptr(nobs)),
+                                                  _ptr(offs), G, _ptr(row_scale), _ptr(col_scaled),
+                                                  _ptr(sumx), _ptr(comp), _ptr(nobs)),
               "cpx_group_kahan_accumulate")
+
+    def group_median(self, values: torch.Tensor, order: torch.Tensor, offs: torch.Tensor,
+                     max_group_rows: int, out: torch.Tensor, row_scale: torch.Tensor | None = None,
+                     col_scaled: torch.Tensor | None = None):
+        n, ld = values.shape
+        G, K = out.shape
+        assert values.dtype == torch.float64 and values.is_contiguous() and K <= ld
+        self._bind_stream()
+        check(self.lib.cpx_group_median(self.h, _ptr(values), n, K, ld, _ptr(order), _ptr(offs), G,
+                                        int(max_group_rows), _ptr(row_scale), _ptr(col_scaled), _ptr(out)),
+              "cpx_group_median")
 
     def group_finalize(self, sumx: torch.Tensor, nobs: torch.Tensor, out: torch.Tensor):
         G, K = sumx.shape
@@ -170,12 +187,14 @@ class Device:
         check(self.lib.cpx_robust_mad(self.h, _ptr(colmajor), N, K, _ptr(fit_rows), fit_rows.numel(),
                                       float(scale), _ptr(med), _ptr(mad)), "cpx_robust_mad")
 
-    def mad_sigmoid(self, colmajor: torch.Tensor, med, mad, eps: float, alpha: float, out):
+    def mad_transform(self, colmajor: torch.Tensor, med, mad, eps: float, out,
+                      double_sigmoid: bool = False, alpha: float = 1.0):
         K, N = colmajor.shape
         assert colmajor.is_contiguous() and out.shape == colmajor.shape
         self._bind_stream()
-        check(self.lib.cpx_mad_sigmoid(self.h, _ptr(colmajor), N, K, _ptr(med), _ptr(mad),
-                                       float(eps), float(alpha), _ptr(out)), "cpx_mad_sigmoid")
+        check(self.lib.cpx_mad_transform(self.h, _ptr(colmajor), N, K, _ptr(med), _ptr(mad), float(eps),
+                                         int(bool(double_sigmoid)), float(alpha), _ptr(out)),
+              "cpx_mad_transform")
 
     def column_stats(self, colmajor: torch.Tensor, stats: torch.Tensor):
         """stats: uint8 [K * 48] (cpx_column_stat[K])."""

@@ -39,7 +39,16 @@ def parse_args(argv=None):
     ap.add_argument("--threads", type=int, default=16, help="TIFF decode threads")
     ap.add_argument("--weights", default=None, help="CPnet state_dict (default: packaged synthetic-trained weights)")
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--csv-image-key", default=None,
+                    help="folder with an Image.csv whose ImageQC_* flags exclude FOVs (Cellpose_GPU_s3fs.py:252-255)")
     return ap.parse_args(argv)
+
+
+def qc_filter(load_data, image_df):
+    """Cellpose_GPU_s3fs.py:252-255: keep the LoadData rows whose ImageQC_* flags sum below 1
+    (boolean indexing aligned on the row index, as the reference)."""
+    not_failing = image_df.filter(like="ImageQC_").sum(axis=1) < 1
+    return load_data[not_failing].copy()
 
 
 def _illum(illum_path, channels, H, W):
@@ -69,6 +78,12 @@ def run(argv=None):
     a = parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s: %(message)s")
     table = pd.read_csv(a.load_data)
+    if a.csv_image_key:
+        n0 = len(table)
+        table = qc_filter(table, pd.read_csv(os.path.join(a.csv_image_key, "Image.csv")))
+        log.info("image QC filter: %d of %d sites kept", len(table), n0)
+    else:
+        log.info("No csv_image_key provided — skipping image QC filtering.")
     chans = list(a.channels)
     C = len(chans)
     plate = a.plate or (str(table["Metadata_Plate"].iloc[0]) if "Metadata_Plate" in table else "plate")
@@ -114,7 +129,7 @@ def run(argv=None):
             pipe.run()
             res = pipe.fetch()
             for k, row_i in enumerate(idx):
-                img_no = row_i + 1
+                img_no = int(table.index[row_i]) + 1   # the LoadData row, also after QC filtering
                 meta = table.iloc[row_i].to_dict()
                 q = res.qc[k * C:(k + 1) * C]
                 counts = {s: int(res.hdr[s][k]["n_objects"]) for s in OBJECT_SETS}

@@ -9,7 +9,7 @@ libcpx (include/cpx.h, k_profiles.hip) with the arithmetic of the library call i
   reference call (file:line)                                  libcpx
   `groupby(keys, as_index=False).mean()` (:69-72)             cpx_group_kahan_accumulate/_finalize
   pycytominer normalize(mad_robustize) fit (:83-88)           cpx_robust_mad
-  RobustMAD transform + double_sigmoid + abs (:13-16, 89-91)  cpx_mad_sigmoid
+  RobustMAD transform + double_sigmoid + abs (:13-16, 89-91)  cpx_mad_transform
   feature_select stats (:93-104)                              cpx_column_stats, cpx_nancorr
   cosine_similarity within treatment groups (:115-140)        cpx_cosine_groups
 
@@ -55,18 +55,7 @@ class ProfileEngine:
     def group_mean(self, df, keys=KEYS):
         """`df.groupby(keys, as_index=False).mean()` (sorted keys, NaN keys dropped, numeric
         columns only) with pandas' Kahan group mean on the GPU."""
-        import pandas as pd
-        torch = self.torch
-        gb = df.groupby(keys, sort=True)
-        codes = gb.ngroup().to_numpy()
-        key_df = gb.size().reset_index()[keys]
-        G = len(key_df)
-        cols = [c for c in df.columns if c not in keys and
-                (pd.api.types.is_numeric_dtype(df[c]) or pd.api.types.is_bool_dtype(df[c]))]
-        if G == 0 or not cols:
-            return pd.concat([key_df, pd.DataFrame(index=key_df.index, columns=cols, dtype=float)], axis=1)
-        means = self._kahan_means(df, cols, codes, G)
-        return pd.concat([key_df, pd.DataFrame(means, columns=cols, index=key_df.index)], axis=1)
+        return self.group_agg(df, keys, "mean")
 
     def _upload_rows(self, df, cols):
         """fp64 [n, K] row-major device copy of df[cols].  pandas keeps each column contiguous
@@ -80,8 +69,9 @@ class ProfileEngine:
             cm[i].copy_(torch.from_numpy(np.ascontiguousarray(v)))
         return cm.t().contiguous()
 
-    def _kahan_means(self, df, cols, codes, G) -> np.ndarray:
-        """Per-group Kahan means of df[cols] for row group codes in [0, G) (-1: row dropped)."""
+    def _kahan_means(self, df, cols, codes, G, func="mean", row_scale=None, scaled_cols=()) -> np.ndarray:
+        """Per-group means (pandas Kahan) or medians of df[cols] for row group codes in [0, G)
+        (-1: row dropped); `row_scale` [n] multiplies the columns named in `scaled_cols`."""
         torch = self.torch
         keep = codes >= 0
         rows = np.nonzero(keep)[0]
@@ -90,13 +80,40 @@ class ProfileEngine:
         offs = np.zeros(G + 1, dtype=np.int32)
         np.cumsum(counts, out=offs[1:])
         K = len(cols)
-        sumx = torch.zeros((G, K), dtype=torch.float64, device=self.td)
-        comp = torch.zeros_like(sumx)
-        nobs = torch.zeros((G, K), dtype=torch.int64, device=self.td)
-        out = torch.empty_like(sumx)
-        self.dev.group_kahan(self._upload_rows(df, cols), self._t(order), self._t(offs), sumx, comp, nobs)
-        self.dev.group_finalize(sumx, nobs, out)
+        vals = self._upload_rows(df, cols)
+        rs = cs = None
+        if row_scale is not None and len(scaled_cols):
+            rs = self._t(np.asarray(row_scale, dtype=np.float64))
+            sc = set(scaled_cols)
+            cs = self._t(np.array([c in sc for c in cols], dtype=np.uint8))
+        out = torch.empty((G, K), dtype=torch.float64, device=self.td)
+        if func == "mean":
+            sumx = torch.zeros((G, K), dtype=torch.float64, device=self.td)
+            comp = torch.zeros_like(sumx)
+            nobs = torch.zeros((G, K), dtype=torch.int64, device=self.td)
+            self.dev.group_kahan(vals, self._t(order), self._t(offs), sumx, comp, nobs, rs, cs)
+            self.dev.group_finalize(sumx, nobs, out)
+        elif func == "median":
+            self.dev.group_median(vals, self._t(order), self._t(offs), int(counts.max(initial=0)), out, rs, cs)
+        else:
+            raise NotImplementedError(f"well aggregation {func!r}: libcpx implements 'mean' and 'median'")
         return out.cpu().numpy()
+
+    def group_agg(self, df, keys, func="mean", row_scale=None, scaled_cols=()):
+        """`df.groupby(keys, as_index=False).agg(func)` for func in {"mean", "median"} (pandas
+        1.5.3: non-numeric columns dropped), optionally with per-row scaling of some columns
+        fused into the reduction (the values pandas would have multiplied first)."""
+        import pandas as pd
+        gb = df.groupby(keys, sort=True)
+        codes = gb.ngroup().to_numpy()
+        key_df = gb.size().reset_index()[keys]
+        G = len(key_df)
+        cols = [c for c in df.columns if c not in keys and
+                (pd.api.types.is_numeric_dtype(df[c]) or pd.api.types.is_bool_dtype(df[c]))]
+        if G == 0 or not cols:
+            return pd.concat([key_df, pd.DataFrame(index=key_df.index, columns=cols, dtype=float)], axis=1)
+        vals = self._kahan_means(df, cols, codes, G, func, row_scale, scaled_cols)
+        return pd.concat([key_df, pd.DataFrame(vals, columns=cols, index=key_df.index)], axis=1)
 
     def object_means(self, obj, image, keys=KEYS):
         """`obj.merge(image[IMAGE_META], on="ImageNumber", how="left").drop(ImageNumber, Site,
@@ -122,8 +139,9 @@ class ProfileEngine:
 
 
     # -- Pycyto_pertime.py:83-91 -----------------------------------------------------------
-    def mad_sigmoid(self, X: np.ndarray, fit_rows: np.ndarray) -> np.ndarray:
-        """normalize(mad_robustize) fitted on X[fit_rows], then |double_sigmoid|; X [N, K]."""
+    def mad_sigmoid(self, X: np.ndarray, fit_rows: np.ndarray, sigmoid: bool = True) -> np.ndarray:
+        """normalize(mad_robustize) fitted on X[fit_rows], then (sigmoid=True) |double_sigmoid|;
+        X [N, K]."""
         torch = self.torch
         N, K = X.shape
         if K == 0:
@@ -133,7 +151,7 @@ class ProfileEngine:
         mad = torch.empty_like(med)
         self.dev.robust_mad(col, self._t(np.asarray(fit_rows, dtype=np.int32)), MAD_SCALE, med, mad)
         out = torch.empty_like(col)
-        self.dev.mad_sigmoid(col, med, mad, MAD_EPS, ALPHA, out)
+        self.dev.mad_transform(col, med, mad, MAD_EPS, out, double_sigmoid=sigmoid, alpha=ALPHA)
         return out.cpu().numpy().T.copy()
 
     # -- Pycyto_pertime.py:93-104 (pycytominer feature_select) ------------------------------
@@ -219,7 +237,7 @@ def object_means_applies(image, *objs) -> bool:
 
 
 def double_sigmoid_host(x):
-    """Pycyto_pertime.py:13-16 (reporting helper; the pipeline uses cpx_mad_sigmoid)."""
+    """Pycyto_pertime.py:13-16 (reporting helper; the pipeline uses cpx_mad_transform)."""
     return (x / ALPHA) ** K_SIG / np.sqrt(1 + (x / ALPHA) ** (2 * K_SIG))
 
 

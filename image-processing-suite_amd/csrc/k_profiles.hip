@@ -7,7 +7,8 @@
 //     (_libs/groupby.pyx group_mean: Kahan sum per group and column in row order, NaN skipped);
 //   * cpx_nancorr: pandas DataFrame.corr(pearson) (_libs/algos.pyx nancorr, Welford);
 //   * cpx_robust_mad: pycytominer RobustMAD.fit = pandas median + scipy median_abs_deviation;
-//   * cpx_mad_sigmoid: (x - median) / (mad + eps), Pycyto_pertime.py:13-16 double_sigmoid, abs
+//   * cpx_mad_transform: (x - median) / (mad + eps) (RobustMAD.transform), optionally followed by
+//     Pycyto_pertime.py:13-16 double_sigmoid and abs
 //     (x**3 and x**6 rounded once from double-double products, as a correctly rounded pow);
 //   * cpx_column_stats: value-count / nunique / NaN / extreme statistics of feature_select;
 //   * cpx_cosine_groups: sklearn cosine_similarity within row groups (tolerance-level parity:
@@ -39,11 +40,16 @@ __device__ __forceinline__ void load_idx(const int* order, int r, int r1, int* i
   for (int u = 0; u < kGU; ++u) idx[u] = r + u < r1 ? order[r + u] : -1;
 }
 
+// value of row idx[u] (times its row scale when the column is scaled: Normalize_CP_ami's
+// site scaling of integer features, one rounding as pandas' multiply)
 __device__ __forceinline__ void load_vals(const double* values, long long ld, int j,
-                                          const int* idx, double* v) {
+                                          const int* idx, const double* row_scale, bool scaled,
+                                          double* v) {
 #pragma unroll
-  for (int u = 0; u < kGU; ++u)
+  for (int u = 0; u < kGU; ++u) {
     v[u] = idx[u] >= 0 ? values[(long long)idx[u] * ld + j] : __builtin_nan("");
+    if (scaled && idx[u] >= 0) v[u] = v[u] * row_scale[idx[u]];
+  }
 }
 
 __device__ __forceinline__ void kahan_chunk(const double* v, double& s, double& c, long long& n) {
@@ -62,12 +68,15 @@ __device__ __forceinline__ void kahan_chunk(const double* v, double& s, double& 
 __global__ __launch_bounds__(kGT) void k_group_kahan(const double* __restrict__ values, int K,
                                                      long long ld, const int* __restrict__ order,
                                                      const int* __restrict__ offs,
+                                                     const double* __restrict__ row_scale,
+                                                     const unsigned char* __restrict__ col_scaled,
                                                      double* __restrict__ sumx,
                                                      double* __restrict__ comp,
                                                      long long* __restrict__ nobs) {
   const int g = blockIdx.y;
   const int j = blockIdx.x * kGT + threadIdx.x;
   if (j >= K) return;
+  const bool scaled = row_scale != nullptr && col_scaled != nullptr && col_scaled[j] != 0;
   const long long sidx = (long long)g * K + j;
   double s = sumx[sidx], c = comp[sidx];
   long long n = nobs[sidx];
@@ -75,14 +84,14 @@ __global__ __launch_bounds__(kGT) void k_group_kahan(const double* __restrict__ 
   GroupChunk A, B;
   load_idx(order, r0, r1, A.idx);
   load_idx(order, r0 + kGU, r1, B.idx);
-  load_vals(values, ld, j, A.idx, A.v);
+  load_vals(values, ld, j, A.idx, row_scale, scaled, A.v);
   for (int r = r0; r < r1; r += 2 * kGU) {
     // A: values of rows r.. in flight; B: indices of rows r+kGU..
-    load_vals(values, ld, j, B.idx, B.v);
+    load_vals(values, ld, j, B.idx, row_scale, scaled, B.v);
     load_idx(order, r + 2 * kGU, r1, A.idx);
     kahan_chunk(A.v, s, c, n);
     if (r + kGU >= r1) break;
-    load_vals(values, ld, j, A.idx, A.v);
+    load_vals(values, ld, j, A.idx, row_scale, scaled, A.v);
     load_idx(order, r + 3 * kGU, r1, B.idx);
     kahan_chunk(B.v, s, c, n);
   }
@@ -187,6 +196,38 @@ __device__ __forceinline__ double median_sorted(const double* a, int m) {
   return (m & 1) ? a[m / 2] : (a[m / 2 - 1] + a[m / 2]) / 2.0;
 }
 
+// pandas groupby median (well_agg_func="median", Normalize_CP_ami.py:113): one block per
+// (group, column), the group's non-NaN values sorted in (dynamic) LDS.
+__global__ __launch_bounds__(kST) void k_group_median(const double* __restrict__ values, int K,
+                                                      long long ld,
+                                                      const int* __restrict__ order,
+                                                      const int* __restrict__ offs,
+                                                      const double* __restrict__ row_scale,
+                                                      const unsigned char* __restrict__ col_scaled,
+                                                      double* __restrict__ out) {
+  extern __shared__ double a_dyn[];
+  __shared__ int cnt;
+  const int j = blockIdx.x, g = blockIdx.y;
+  const int r0 = offs[g], n = offs[g + 1] - r0;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  const bool scaled = row_scale != nullptr && col_scaled != nullptr && col_scaled[j] != 0;
+  for (int i = threadIdx.x; i < n; i += kST) {
+    const int row = order[r0 + i];
+    double v = values[(long long)row * ld + j];
+    if (scaled) v = v * row_scale[row];
+    if (v == v) a_dyn[atomicAdd(&cnt, 1)] = v;
+  }
+  __syncthreads();
+  const int m = cnt;
+  int n2 = 1;
+  while (n2 < m) n2 <<= 1;
+  for (int i = m + threadIdx.x; i < n2; i += kST) a_dyn[i] = __builtin_inf();
+  __syncthreads();
+  block_sort(a_dyn, n2);
+  if (threadIdx.x == 0) out[(long long)g * K + j] = median_sorted(a_dyn, m);
+}
+
 // RobustMAD.fit: one block per feature column over the fit rows.
 __global__ __launch_bounds__(kST) void k_robust_mad(const double* __restrict__ mat, int N,
                                                     const int* __restrict__ fit, int n_fit,
@@ -229,14 +270,18 @@ __device__ __forceinline__ void pow36(double t, double& p3, double& p6) {
   p6 = isfinite(q) ? q + q_lo : q;
 }
 
-// (x - median) / (mad + eps) -> double sigmoid -> abs; column-major [K][N].
-__global__ void k_mad_sigmoid(const double* __restrict__ mat, int N, int K,
-                              const double* __restrict__ med, const double* __restrict__ mad,
-                              double eps, double alpha, double* __restrict__ out) {
+// (x - median) / (mad + eps) [-> double sigmoid -> abs]; column-major [K][N].
+__global__ void k_mad_transform(const double* __restrict__ mat, int N, int K,
+                                const double* __restrict__ med, const double* __restrict__ mad,
+                                double eps, int sigmoid, double alpha, double* __restrict__ out) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long long)N * K) return;
   const int j = (int)(i / N);
   const double z = (mat[i] - med[j]) / (mad[j] + eps);
+  if (!sigmoid) {
+    out[i] = z;
+    return;
+  }
   const double t = z / alpha;
   double p3, p6;
   pow36(t, p3, p6);
@@ -329,7 +374,9 @@ __global__ void k_cosine_pairs(const double* __restrict__ x, int F, const int* _
 
 extern "C" int cpx_group_kahan_accumulate(cpx_ctx* ctx, const double* values_dev, int n_rows,
                                           int K, long long ld, const int32_t* order_dev,
-                                          const int32_t* offs_dev, int G, double* sum_dev,
+                                          const int32_t* offs_dev, int G,
+                                          const double* row_scale_dev,
+                                          const uint8_t* col_scaled_dev, double* sum_dev,
                                           double* comp_dev, int64_t* nobs_dev) {
   CPX_REQUIRE(ctx && values_dev && order_dev && offs_dev && sum_dev && comp_dev && nobs_dev,
               CPX_ERR_ARG, "cpx_group_kahan_accumulate: null argument");
@@ -337,9 +384,25 @@ extern "C" int cpx_group_kahan_accumulate(cpx_ctx* ctx, const double* values_dev
               "cpx_group_kahan_accumulate: bad sizes");
   if (n_rows == 0) return CPX_OK;
   hipLaunchKernelGGL(k_group_kahan, dim3(cpx_div_up(K, kGT), G), dim3(kGT), 0, ctx->stream,
-                     values_dev, K, ld, (const int*)order_dev, (const int*)offs_dev, sum_dev,
-                     comp_dev, (long long*)nobs_dev);
+                     values_dev, K, ld, (const int*)order_dev, (const int*)offs_dev, row_scale_dev,
+                     (const unsigned char*)col_scaled_dev, sum_dev, comp_dev, (long long*)nobs_dev);
   CPX_CHECK_LAUNCH("k_group_kahan");
+  return CPX_OK;
+}
+
+extern "C" int cpx_group_median(cpx_ctx* ctx, const double* values_dev, int n_rows, int K,
+                                long long ld, const int32_t* order_dev, const int32_t* offs_dev,
+                                int G, int max_group_rows, const double* row_scale_dev,
+                                const uint8_t* col_scaled_dev, double* out_dev) {
+  CPX_REQUIRE(ctx && values_dev && order_dev && offs_dev && out_dev && n_rows >= 0 && K > 0 &&
+                  ld >= K && G > 0 && G <= 65535 && max_group_rows >= 0 && max_group_rows <= 16384,
+              CPX_ERR_ARG, "cpx_group_median: bad argument (at most 16384 rows per group)");
+  int n2 = 1;
+  while (n2 < max_group_rows) n2 <<= 1;
+  hipLaunchKernelGGL(k_group_median, dim3(K, G), dim3(kST), sizeof(double) * n2, ctx->stream,
+                     values_dev, K, ld, (const int*)order_dev, (const int*)offs_dev, row_scale_dev,
+                     (const unsigned char*)col_scaled_dev, out_dev);
+  CPX_CHECK_LAUNCH("k_group_median");
   return CPX_OK;
 }
 
@@ -376,16 +439,16 @@ extern "C" int cpx_robust_mad(cpx_ctx* ctx, const double* mat_dev, int N, int K,
   return CPX_OK;
 }
 
-extern "C" int cpx_mad_sigmoid(cpx_ctx* ctx, const double* mat_dev, int N, int K,
-                               const double* med_dev, const double* mad_dev, double eps,
-                               double alpha, double* out_dev) {
+extern "C" int cpx_mad_transform(cpx_ctx* ctx, const double* mat_dev, int N, int K,
+                                 const double* med_dev, const double* mad_dev, double eps,
+                                 int double_sigmoid, double alpha, double* out_dev) {
   CPX_REQUIRE(ctx && mat_dev && med_dev && mad_dev && out_dev && N >= 0 && K > 0, CPX_ERR_ARG,
-              "cpx_mad_sigmoid: bad argument");
+              "cpx_mad_transform: bad argument");
   const long long total = (long long)N * K;
   if (total == 0) return CPX_OK;
-  hipLaunchKernelGGL(k_mad_sigmoid, dim3(cpx_div_up(total, 256)), dim3(256), 0, ctx->stream,
-                     mat_dev, N, K, med_dev, mad_dev, eps, alpha, out_dev);
-  CPX_CHECK_LAUNCH("k_mad_sigmoid");
+  hipLaunchKernelGGL(k_mad_transform, dim3(cpx_div_up(total, 256)), dim3(256), 0, ctx->stream,
+                     mat_dev, N, K, med_dev, mad_dev, eps, double_sigmoid, alpha, out_dev);
+  CPX_CHECK_LAUNCH("k_mad_transform");
   return CPX_OK;
 }
 

@@ -191,11 +191,20 @@ int cpx_rebin_u16(cpx_ctx* ctx, const uint16_t* src_dev, int G, int H, int W, in
 /* pandas `groupby(keys).mean()` (Pycyto_pertime.py:69-72; pandas group_mean: Kahan sum per
  * group and column in row order, NaN skipped).  values_dev: fp64 rows [n_rows][ld] (first K
  * columns used); order_dev: int32 row indices grouped by group, original order within a group;
- * offs_dev: int32 [G+1] group starts in order_dev.  sum/comp/nobs [G][K] carry the state
- * (zero them first), so a table may be streamed in row order over several calls.           */
+ * offs_dev: int32 [G+1] group starts in order_dev.  Optional site scaling
+ * (Normalize_CP_ami.py:95-111): where col_scaled_dev[j] != 0, value * row_scale_dev[row] is
+ * summed (both NULL: no scaling).  sum/comp/nobs [G][K] carry the state (zero them first), so
+ * a table may be streamed in row order over several calls.                                   */
 int cpx_group_kahan_accumulate(cpx_ctx* ctx, const double* values_dev, int n_rows, int K,
                                long long ld, const int32_t* order_dev, const int32_t* offs_dev,
-                               int G, double* sum_dev, double* comp_dev, int64_t* nobs_dev);
+                               int G, const double* row_scale_dev, const uint8_t* col_scaled_dev,
+                               double* sum_dev, double* comp_dev, int64_t* nobs_dev);
+/* pandas `groupby(...).median()` (Normalize_CP_ami.py:113, well_agg_func="median"): same row
+ * layout and optional site scaling as cpx_group_kahan_accumulate, out_dev [G][K]; groups of at
+ * most 16384 rows (max_group_rows = the largest group).                                       */
+int cpx_group_median(cpx_ctx* ctx, const double* values_dev, int n_rows, int K, long long ld,
+                     const int32_t* order_dev, const int32_t* offs_dev, int G, int max_group_rows,
+                     const double* row_scale_dev, const uint8_t* col_scaled_dev, double* out_dev);
 /* out_dev [G][K] = sum / nobs (NaN where nobs == 0).                                          */
 int cpx_group_mean_finalize(cpx_ctx* ctx, const double* sum_dev, const int64_t* nobs_dev, int G,
                             int K, double* out_dev);
@@ -210,10 +219,12 @@ int cpx_nancorr(cpx_ctx* ctx, const double* mat_dev, int N, int K, double* out_d
 int cpx_robust_mad(cpx_ctx* ctx, const double* mat_dev, int N, int K, const int32_t* fit_rows_dev,
                    int n_fit, double scale, double* med_dev, double* mad_dev);
 
-/* RobustMAD.transform + double_sigmoid + abs (Pycyto_pertime.py:13-16, 89-91), column-major:
- * out = |s((x - med[j]) / (mad[j] + eps))|, s(z) = (z/alpha)^3 / sqrt(1 + (z/alpha)^6).      */
-int cpx_mad_sigmoid(cpx_ctx* ctx, const double* mat_dev, int N, int K, const double* med_dev,
-                    const double* mad_dev, double eps, double alpha, double* out_dev);
+/* RobustMAD.transform (Normalize_CP_ami.py:119-124, Pycyto_pertime.py:83-88), column-major:
+ * z = (x - med[j]) / (mad[j] + eps); with double_sigmoid != 0 also Pycyto_pertime.py:13-16,
+ * 89-91: out = |(z/alpha)^3 / sqrt(1 + (z/alpha)^6)|, powers correctly rounded.              */
+int cpx_mad_transform(cpx_ctx* ctx, const double* mat_dev, int N, int K, const double* med_dev,
+                      const double* mad_dev, double eps, int double_sigmoid, double alpha,
+                      double* out_dev);
 
 /* feature_select statistics (variance_threshold, drop_na_columns, drop_outliers) per column of
  * mat_dev (column-major [K][N], N <= 4096).                                                  */
