@@ -98,17 +98,27 @@ def main():
         if world > 1:
             dist.barrier()
 
+    def run_steps(n, record=None):
+        """n steps with every step's results fetched to the host; step i + 1 is enqueued before
+        step i is fetched, so the result copies (side stream) overlap the next step's work."""
+        slots = [None] * n
+        if n:
+            run_step(0)
+            slots[0] = pipe.cur
+        for i in range(n):
+            if i + 1 < n:
+                run_step(i + 1)
+                slots[i + 1] = pipe.cur
+            res = pipe.fetch(slots[i])
+            if record is not None:
+                record.append([int(res.hdr[s]["n_objects"].sum()) for s in ("Nuclei", "Cells", "Cytoplasm")])
+
     n_obj = []
-    for i in range(a.warmup):
-        run_step(i)
-        pipe.fetch()
+    run_steps(a.warmup)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        run_step(i)
-        res = pipe.fetch()
-        n_obj.append([int(res.hdr[s]["n_objects"].sum()) for s in ("Nuclei", "Cells", "Cytoplasm")])
+    run_steps(a.steps, n_obj)
     torch.cuda.synchronize()
     barrier()
     dt = shard.max_over_ranks(time.perf_counter() - t0, device=td)

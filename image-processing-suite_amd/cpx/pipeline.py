@@ -9,7 +9,10 @@ for a batch of B FOVs that are already resident in HBM (uint16 planes [B*C, H, W
   B  Segmenter (libcpx normalise/tiles -> CPnet bf16 -> libcpx tile average/dynamics/masks)
   C  libcpx cpx_expand_labels (Cells, Cytoplasm) + cpx_objects for Nuclei / Cells / Cytoplasm
   D  libcpx cpx_features for the three object sets (+ optional a7 crops)
-Everything is enqueued on one HIP stream; `fetch()` is the only synchronisation.
+Everything is enqueued on one HIP stream.  Results (QC, object tables, features) live in
+`slots` alternating buffer sets: `run()` writes slot i % slots and records an event, and
+`fetch(slot)` copies that slot to pinned host memory on a separate copy stream after waiting
+for the event only — so the host can fetch step i while the GPU already runs step i + 1.
 """
 from __future__ import annotations
 
@@ -41,6 +44,7 @@ class PipelineConfig:
     seed: int = 0
     use_graph: bool = True
     crops: bool = False              # a7 crops for the embedding consumer (off in the bench)
+    slots: int = 2                   # result buffer sets (fetch of step i overlaps step i + 1)
 
 
 @dataclasses.dataclass
@@ -61,21 +65,41 @@ class FovPipeline:
         self.illum = None if illum is None else torch.from_numpy(np.ascontiguousarray(illum)).to(td)
         self.corr = torch.empty((B, C, H, W), dtype=torch.float32, device=td)
         self.stats = dev.empty_bytes(64 * B * C)
-        self.qc = dev.empty_bytes(24 * B * C)
         ML = cfg.max_objects
         self.labels = {s: torch.empty((B, H, W), dtype=torch.int32, device=td) for s in OBJECT_SETS}
         self.lstats = dev.empty_bytes(64 * B * (ML + 1))
-        self.objects = {s: dev.empty_bytes(56 * B * ML) for s in OBJECT_SETS}
-        self.hdr = {s: dev.empty_bytes(16 * B) for s in OBJECT_SETS}
         self.F = n_features(C)
-        self.feats = {s: torch.zeros((B, ML, self.F), dtype=torch.float64, device=td) for s in OBJECT_SETS}
         self.seg = Segmenter(dev, H, W, B, model=cfg.model, diameter=cfg.diameter, weights=cfg.weights,
                              seed=cfg.seed, use_graph=cfg.use_graph, max_objects=ML)
+        # result slots (device) and their pinned host mirrors
+        self._slots = []
+        for _ in range(max(1, cfg.slots)):
+            self._slots.append({
+                "qc": dev.empty_bytes(24 * B * C),
+                "hdr": {s: dev.empty_bytes(16 * B) for s in OBJECT_SETS},
+                "objects": {s: dev.empty_bytes(56 * B * ML) for s in OBJECT_SETS},
+                "feats": {s: torch.zeros((B, ML, self.F), dtype=torch.float64, device=td) for s in OBJECT_SETS},
+                "seg_stats": torch.empty_like(self.seg.stats),
+                "event": None})
+        self._host = {
+            "qc": torch.empty(24 * B * C, dtype=torch.uint8, pin_memory=True),
+            "hdr": {s: torch.empty(16 * B, dtype=torch.uint8, pin_memory=True) for s in OBJECT_SETS},
+            "objects": {s: torch.empty(56 * B * ML, dtype=torch.uint8, pin_memory=True) for s in OBJECT_SETS},
+            "feats": {s: torch.empty(B * ML * self.F, dtype=torch.float64, pin_memory=True) for s in OBJECT_SETS},
+            "seg_stats": torch.empty(self.seg.stats.shape, dtype=self.seg.stats.dtype, pin_memory=True)}
+        self._copy_stream = torch.cuda.Stream(device=td)
+        self._step = 0
+        self._use_slot(0)
         self.crops = None
         if cfg.crops:
             self.crops = torch.zeros((B, ML, cfg.box, cfg.box, C), dtype=torch.float32, device=td)
             self.crops8 = torch.zeros((B, ML, C, cfg.box, cfg.box), dtype=torch.uint8, device=td)
         dev.reserve(B * C, H, W, B, ML)
+
+    def _use_slot(self, k: int):
+        sl = self._slots[k]
+        self.cur = k
+        self.qc, self.hdr, self.objects, self.feats = sl["qc"], sl["hdr"], sl["objects"], sl["feats"]
 
     # ---- stages ---------------------------------------------------------------------------
     def stage_illum_qc(self):
@@ -110,21 +134,53 @@ class FovPipeline:
         if raw is not None:
             assert raw.shape == self.raw.shape and raw.dtype == torch.int16 and raw.is_contiguous()
             self.raw = raw
+        k = self._step % len(self._slots)
+        self._step += 1
+        sl = self._slots[k]
+        stream = torch.cuda.current_stream(self.dev.torch_device)
+        # (a slot's previous fetch() returned only after its copies completed)
+        self._use_slot(k)
         self.stage_illum_qc()
         self.stage_segment()
         self.stage_objects()
+        sl["seg_stats"].copy_(self.seg.stats)
+        sl["event"] = torch.cuda.Event()
+        sl["event"].record(stream)
+        return k
 
-    def fetch(self) -> FovResults:
-        """Synchronise and copy the per-FOV results to the host (only the valid object rows)."""
-        B = self.cfg.batch
-        hdrs = {s: as_numpy(self.hdr[s], "hdr") for s in OBJECT_SETS}  # syncs
-        qc = as_numpy(self.qc, "qc")
+    def fetch(self, slot: int | None = None) -> FovResults:
+        """Copy one slot's results to the host (default: the last run) and return them.  Waits
+        only for that slot's step (its recorded event), with the copies on a side stream, so a
+        step enqueued after it keeps the GPU busy meanwhile."""
+        from .segment import SEG_STATS_DTYPE
+        k = self.cur if slot is None else slot
+        sl, hb = self._slots[k], self._host
+        B, ML, F = self.cfg.batch, self.cfg.max_objects, self.F
+        cs = self._copy_stream
+        cs.wait_event(sl["event"])
+        with torch.cuda.stream(cs):
+            hb["qc"].copy_(sl["qc"], non_blocking=True)
+            hb["seg_stats"].copy_(sl["seg_stats"], non_blocking=True)
+            for s in OBJECT_SETS:
+                hb["hdr"][s].copy_(sl["hdr"][s], non_blocking=True)
+        cs.synchronize()
+        hdrs = {s: as_numpy(hb["hdr"][s], "hdr").copy() for s in OBJECT_SETS}
+        qc = as_numpy(hb["qc"], "qc").copy()
+        nmax = {s: max(int(hdrs[s]["n_objects"].max()) if B else 0, 1) for s in OBJECT_SETS}
+        with torch.cuda.stream(cs):
+            for s in OBJECT_SETS:
+                n = nmax[s]
+                hb["feats"][s][:B * n * F].view(B, n, F).copy_(sl["feats"][s][:, :n], non_blocking=True)
+                hb["objects"][s][:B * n * 56].view(B, n * 56).copy_(
+                    sl["objects"][s].view(B, ML * 56)[:, :n * 56], non_blocking=True)
+        cs.synchronize()
         objs, feats = {}, {}
         for s in OBJECT_SETS:
-            n = hdrs[s]["n_objects"].astype(int)
-            nmax = int(n.max()) if B else 0
-            f = self.feats[s][:, :max(nmax, 1)].cpu().numpy()
-            o = as_numpy(self.objects[s], "object").reshape(B, self.cfg.max_objects)[:, :max(nmax, 1)]
-            feats[s] = [f[b, : n[b]] for b in range(B)]
-            objs[s] = [o[b, : n[b]] for b in range(B)]
-        return FovResults(qc=qc, hdr=hdrs, objects=objs, feats=feats, seg_stats=self.seg.seg_stats())
+            n_b = hdrs[s]["n_objects"].astype(int)
+            n = nmax[s]
+            f = hb["feats"][s][:B * n * F].view(B, n, F).numpy()
+            o = as_numpy(hb["objects"][s][:B * n * 56], "object").reshape(B, n)
+            feats[s] = [f[b, : n_b[b]].copy() for b in range(B)]
+            objs[s] = [o[b, : n_b[b]].copy() for b in range(B)]
+        seg_stats = hb["seg_stats"].numpy().view(SEG_STATS_DTYPE).copy()
+        return FovResults(qc=qc, hdr=hdrs, objects=objs, feats=feats, seg_stats=seg_stats)
