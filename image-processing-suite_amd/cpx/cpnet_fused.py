@@ -191,6 +191,15 @@ class FusedCPnet:
                                               _p(self.head_b), nout, _p(out)), "cpx_cpnet_conv3x3_head")
         return out
 
+    @staticmethod
+    def _proj(x, w):
+        """1x1 projection of an NHWC (channels_last) tensor as one GEMM [pixels, cin] x [cin, cout]
+        (hipBLASLt, fixed reduction order).  MIOpen's fast 1x1 solvers split K with atomic
+        accumulation, which makes the bf16 outputs — and so the masks — differ run to run."""
+        N, C, H, W = x.shape
+        y = torch.matmul(x.permute(0, 2, 3, 1).reshape(-1, C), w.reshape(w.shape[0], C).t())
+        return y.view(N, H, W, -1).permute(0, 3, 1, 2)
+
     # -- forward -------------------------------------------------------------------------------
     @torch.no_grad()
     def __call__(self, x):
@@ -208,7 +217,7 @@ class FusedCPnet:
                     _, z0 = self._epi(x, None, bn=d["bn"][0])
                 else:
                     xin, z0 = self._pool(xd[-1], d["bn"][0])
-                p = F.conv2d(xin, d["wp"])
+                p = self._proj(xin, d["wp"])
                 _, z = self._conv(z0, d, 0, d["b"][0], bn=d["bn"][1])
             x1, z = self._conv(z, d, 1, d["b1p"], res=p, bn=d["bn"][2], y=True)
             _, z = self._conv(z, d, 2, d["b"][2], bn=d["bn"][3])
@@ -224,7 +233,7 @@ class FusedCPnet:
         for n in range(len(self.up) - 1, -1, -1):
             u = self.up[n]
             s = [(style @ w.t() + b).contiguous() for (w, b) in u["full"]]
-            p = F.conv2d(x_small, u["wp"])
+            p = self._proj(x_small, u["wp"])
             _, z = self._conv(z0, u, 0, u["b"][0], res=xd[n], style=s[0], bn=u["bn"][1])
             x1, z = self._conv(z, u, 1, u["b1p"], res=p, res_up=(n < len(self.up) - 1), style=s[1],
                                bn=u["bn"][2], y=True)
