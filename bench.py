@@ -37,6 +37,9 @@ def parse():
     ap.add_argument("--weights", default=None, help="CPnet state_dict (default: seeded random init)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stage-steps", type=int, default=3, help="instrumented steps after timing")
+    ap.add_argument("--pipes", type=int, default=2,
+                    help="pipelines (own libcpx context, buffers and HIP stream) per GPU: step i "
+                         "runs on pipeline i %% pipes, so that many batches are in flight")
     ap.add_argument("--zstack", type=int, default=0,
                     help="configs[4] variant: Z planes per channel, z-max projected on the GPU "
                          "inside every step (default size 2048); not the headline workload")
@@ -75,7 +78,15 @@ def main():
         weights = cand if os.path.exists(cand) else None
     cfg = PipelineConfig(H=H, W=W, C=C, batch=B, weights=weights)
     illum = synth_illum(C, H, W, seed=1)
-    pipe = FovPipeline(dev, cfg, illum)
+    # P pipelines, each with its own libcpx context (workspaces), buffers and HIP stream: the
+    # kernels of one batch fill the gaps of the other (many post-processing / feature kernels
+    # do not fill 256 CUs on their own)
+    streams = [torch.cuda.Stream(device=td) for _ in range(max(1, a.pipes))]
+    pipes = []
+    for p_i, st in enumerate(streams):
+        with torch.cuda.stream(st):
+            pipes.append(FovPipeline(dev if p_i == 0 else Device(local), cfg, illum))
+    pipe = pipes[0]
     # this rank's wells (well w -> rank w % world); the synthetic batches are seeded
     # by the rank's own FOV keys, so ranks never share inputs and exchange nothing
     mine = shard.shard(shard.plate_fovs(n_wells=384), rank, world)
@@ -87,11 +98,15 @@ def main():
                 for i in range(a.pool)]
 
     def run_step(i):
-        if Z > 1:  # a5: z-max projection into the pipeline's raw planes, then the hot path
-            dev.zmax(pool[i % a.pool], pipe.raw)
-            pipe.run()
-        else:
-            pipe.run(pool[i % a.pool])
+        """Enqueue step i on pipeline i % P (its stream); returns (pipeline, result slot)."""
+        q = pipes[i % len(pipes)]
+        with torch.cuda.stream(streams[i % len(pipes)]):
+            if Z > 1:  # a5: z-max projection into the pipeline's raw planes, then the hot path
+                q.dev.zmax(pool[i % a.pool], q.raw)
+                slot = q.run()
+            else:
+                slot = q.run(pool[i % a.pool])
+        return q, slot
     torch.cuda.synchronize()
 
     def barrier():
@@ -99,19 +114,22 @@ def main():
             dist.barrier()
 
     def run_steps(n, record=None):
-        """n steps with every step's results fetched to the host; step i + 1 is enqueued before
-        step i is fetched, so the result copies (side stream) overlap the next step's work."""
-        slots = [None] * n
-        if n:
-            run_step(0)
-            slots[0] = pipe.cur
-        for i in range(n):
-            if i + 1 < n:
-                run_step(i + 1)
-                slots[i + 1] = pipe.cur
-            res = pipe.fetch(slots[i])
+        """n steps with every step's results fetched to the host.  Up to P + 1 steps are
+        enqueued ahead of the oldest unfetched one; a fetch waits for its own step only and
+        copies on a side stream, so the GPU never idles on the host."""
+        pend = []
+
+        def fetch_oldest():
+            q, slot = pend.pop(0)
+            res = q.fetch(slot)
             if record is not None:
                 record.append([int(res.hdr[s]["n_objects"].sum()) for s in ("Nuclei", "Cells", "Cytoplasm")])
+        for i in range(n):
+            pend.append(run_step(i))
+            if len(pend) > len(pipes):
+                fetch_oldest()
+        while pend:
+            fetch_oldest()
 
     n_obj = []
     run_steps(a.warmup)
@@ -218,7 +236,8 @@ def main():
                    "fovs_per_step": B * world, "batch_per_gpu": B, "H": H, "W": W, "C": C,
                    "cellpose_model": cfg.model, "diameter": cfg.diameter,
                    "cpnet_weights": os.path.basename(weights) if weights else "seeded-random-init",
-                   "tiles_per_fov": n_tiles, "parallelism": f"fov-sharded x{world}"},
+                   "tiles_per_fov": n_tiles, "parallelism": f"fov-sharded x{world}",
+                   "batches_in_flight_per_gpu": len(pipes)},
         "objects_per_fov": ([round(x / (B * world) * world, 1) for x in np.mean(np.array(n_obj), axis=0)]
                             if n_obj else None),
         "stage_ms_per_step": {k: round(v, 3) for k, v in {**per_step_ms, **sub_ms}.items()},
