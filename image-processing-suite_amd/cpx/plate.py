@@ -39,6 +39,8 @@ def parse_args(argv=None):
     ap.add_argument("--threads", type=int, default=16, help="TIFF decode threads")
     ap.add_argument("--weights", default=None, help="CPnet state_dict (default: packaged synthetic-trained weights)")
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--pipes", type=int, default=2,
+                    help="pipelines (libcpx context + HIP stream) on the GPU: batches in flight")
     ap.add_argument("--csv-image-key", default=None,
                     help="folder with an Image.csv whose ImageQC_* flags exclude FOVs (Cellpose_GPU_s3fs.py:252-255)")
     return ap.parse_args(argv)
@@ -95,10 +97,16 @@ def run(argv=None):
     if weights is None:
         cand = os.path.join(os.path.dirname(__file__), "weights", "cpnet_nuclei_synth.pt")
         weights = cand if os.path.exists(cand) else None
-    dev = Device(a.device)
     B = max(1, min(a.batch, len(files)))
     cfg = PipelineConfig(H=H, W=W, C=C, batch=B, channels=tuple(chans), weights=weights)
-    pipe = FovPipeline(dev, cfg, _illum(a.illum_path, chans, H, W))
+    illum = _illum(a.illum_path, chans, H, W)
+    n_pipes = max(1, min(a.pipes, (len(files) + B - 1) // B))
+    streams, pipes = [], []
+    for _ in range(n_pipes):
+        st = torch.cuda.Stream(device=torch.device("cuda", a.device))
+        with torch.cuda.stream(st):
+            pipes.append(FovPipeline(Device(a.device), cfg, illum))
+        streams.append(st)
     out = PlateTables(chans)
 
     def read_fov(paths):
@@ -114,29 +122,49 @@ def run(argv=None):
                 planes.append(np.zeros((H, W), np.uint16))
         return np.stack(planes)
 
-    host = torch.empty((B * C, H, W), dtype=torch.int16, pin_memory=True)
+    hosts = [torch.empty((B * C, H, W), dtype=torch.int16, pin_memory=True) for _ in range(n_pipes)]
     batches = [list(range(i, min(i + B, len(files)))) for i in range(0, len(files), B)]
+    inflight = []  # (batch index, pipeline, slot, upload event)
+
+    def record(bi, res):
+        idx = batches[bi]
+        for k, row_i in enumerate(idx):
+            img_no = int(table.index[row_i]) + 1   # the LoadData row, also after QC filtering
+            meta = table.iloc[row_i].to_dict()
+            q = res.qc[k * C:(k + 1) * C]
+            counts = {s: int(res.hdr[s][k]["n_objects"]) for s in OBJECT_SETS}
+            out.add_image(img_no, meta, q["slope"], q["pct_max"], counts)
+            for s in OBJECT_SETS:
+                out.add_objects(s, img_no, res.objects[s][k]["label"], res.feats[s][k])
+        log.info("batch %d/%d: %d FOVs", bi + 1, len(batches), len(idx))
+
     with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, a.threads)) as pool:
         pending = [pool.submit(read_fov, files[i]) for i in batches[0]]
         for bi, idx in enumerate(batches):
             fovs = [f.result() for f in pending]
             if bi + 1 < len(batches):  # decode the next batch while this one runs
                 pending = [pool.submit(read_fov, files[i]) for i in batches[bi + 1]]
+            p_i = bi % n_pipes
+            # the pinned staging buffer of this pipeline is free once its last upload completed
+            for _, q, _, up in inflight:
+                if q is pipes[p_i]:
+                    up.synchronize()
+            host = hosts[p_i]
             hn = host.numpy().view(np.uint16).reshape(B, C, H, W)
             hn[:len(fovs)] = np.stack(fovs)
             hn[len(fovs):] = 0
-            pipe.raw.copy_(host, non_blocking=True)
-            pipe.run()
-            res = pipe.fetch()
-            for k, row_i in enumerate(idx):
-                img_no = int(table.index[row_i]) + 1   # the LoadData row, also after QC filtering
-                meta = table.iloc[row_i].to_dict()
-                q = res.qc[k * C:(k + 1) * C]
-                counts = {s: int(res.hdr[s][k]["n_objects"]) for s in OBJECT_SETS}
-                out.add_image(img_no, meta, q["slope"], q["pct_max"], counts)
-                for s in OBJECT_SETS:
-                    out.add_objects(s, img_no, res.objects[s][k]["label"], res.feats[s][k])
-            log.info("batch %d/%d: %d FOVs", bi + 1, len(batches), len(idx))
+            with torch.cuda.stream(streams[p_i]):
+                pipes[p_i].raw.copy_(host, non_blocking=True)
+                up = torch.cuda.Event()
+                up.record(streams[p_i])
+                slot = pipes[p_i].run()
+            inflight.append((bi, pipes[p_i], slot, up))
+            if len(inflight) > n_pipes:   # results in batch order, one step behind the GPU
+                obi, q, sl, _ = inflight.pop(0)
+                record(obi, q.fetch(sl))
+        while inflight:
+            obi, q, sl, _ = inflight.pop(0)
+            record(obi, q.fetch(sl))
     d = out.write(a.out, plate, time)
     log.info("tables written to %s", d)
     return d
