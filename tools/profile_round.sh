@@ -11,16 +11,23 @@ cd $R
 timeout -k 10 420 python -u bench.py > $O/bench_default.log 2>&1
 cd /tmp && export TMPDIR=/tmp
 cd $R
+# per-kernel durations: one pipeline (steps run back to back, as the bench's instrumented
+# stage timing that the roofline uses); the default two-pipeline run overlaps batches, so its
+# kernel durations include co-resident work (kernels_concurrent.md)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- \
-  python -u bench.py --steps 6 --warmup 2 --no-cpu-baseline --stage-steps 1 > $O/bench_kt.log 2>&1
+  python -u bench.py --pipes 1 --steps 6 --warmup 2 --no-cpu-baseline --stage-steps 1 > $O/bench_kt.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt2 -o run -- \
+  python -u bench.py --steps 6 --warmup 2 --no-cpu-baseline --stage-steps 1 > $O/bench_kt2.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- \
-  python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --stage-steps 1 > $O/bench_fetch.log 2>&1
+  python -u bench.py --pipes 1 --steps 3 --warmup 1 --no-cpu-baseline --stage-steps 1 > $O/bench_fetch.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- \
-  python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --stage-steps 1 > $O/bench_write.log 2>&1
+  python -u bench.py --pipes 1 --steps 3 --warmup 1 --no-cpu-baseline --stage-steps 1 > $O/bench_write.log 2>&1
 
 # summarise on the box (raw per-dispatch CSVs are too large to bring back)
 python tools/prof_summary.py $O/kt/run_kernel_trace.csv --steps 4 --md > $O/kernels_steady.md
+python tools/prof_summary.py $O/kt2/run_kernel_trace.csv --steps 4 --md > $O/kernels_concurrent.md
 cp $O/kt/run_kernel_stats.csv $O/kernel_stats.csv
+cp $O/kt2/run_kernel_stats.csv $O/kernel_stats_concurrent.csv
 python tools/pmc_traffic.py $O/fetch $O/write --out $O/pmc_traffic.json > $O/pmc_traffic.log
-rm -rf $O/kt $O/fetch $O/write
+rm -rf $O/kt $O/kt2 $O/fetch $O/write
 echo done
