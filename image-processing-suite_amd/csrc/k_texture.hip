@@ -72,6 +72,29 @@ __device__ __forceinline__ unsigned int wave_sum_u32(unsigned int v) {
   return (unsigned int)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// The same scan for a u64 (both halves moved by DPP, 64-bit adds): no LDS round trips, where
+// the generic __shfl_xor sum costs twelve ds_bpermute.
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#define CPX_U64_DPP_STEP(CTRL, ROWMASK)                                                         \
+  {                                                                                            \
+    const unsigned int lo_ = (unsigned int)__builtin_amdgcn_update_dpp(0, (int)(unsigned int)v, \
+                                                                       CTRL, ROWMASK, 0xf, false); \
+    const unsigned int hi_ = (unsigned int)__builtin_amdgcn_update_dpp(                        \
+        0, (int)(unsigned int)(v >> 32), CTRL, ROWMASK, 0xf, false);                           \
+    v += ((unsigned long long)hi_ << 32) | lo_;                                                \
+  }
+  CPX_U64_DPP_STEP(0x111, 0xf)
+  CPX_U64_DPP_STEP(0x112, 0xf)
+  CPX_U64_DPP_STEP(0x114, 0xf)
+  CPX_U64_DPP_STEP(0x118, 0xf)
+  CPX_U64_DPP_STEP(0x142, 0xa)
+  CPX_U64_DPP_STEP(0x143, 0xc)
+#undef CPX_U64_DPP_STEP
+  const unsigned int lo = (unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)v, 63);
+  const unsigned int hi = (unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)(v >> 32), 63);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
 // GLCM of one (object, channel) item: skimage graycomatrix offsets (dr, dc) for angles
 // 0, pi/4, pi/2, 3pi/4 at distance 3, symmetric=False, normed, then greycoprops.
 //  1. count (per angle): every pixel pair adds 1 to its packed-u16 counter in a 64K-key LDS
@@ -233,7 +256,7 @@ __device__ void glcm_finish(const GlcmAcc (&A)[4], unsigned int* red, int bh, in
       const unsigned int t = wave_sum_u32(w[k]);
       if (lane == 0) red[(wid * 4 + a) * kAccW + k] = t;
     }
-    const unsigned long long hs = wave_sum(A[a].hom);
+    const unsigned long long hs = wave_sum_u64(A[a].hom);
     if (lane == 0) {
       red[(wid * 4 + a) * kAccW + 9] = (unsigned int)hs;
       red[(wid * 4 + a) * kAccW + 10] = (unsigned int)(hs >> 32);
