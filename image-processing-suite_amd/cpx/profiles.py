@@ -38,6 +38,13 @@ MAD_EPS = 1e-18        # pycytominer normalize(mad_robustize_epsilon=1e-18)
 FEATURE_SELECT_OPS = ["variance_threshold", "drop_na_columns", "correlation_threshold", "drop_outliers"]
 
 
+def _group_codes(gb) -> np.ndarray:
+    """Row -> group index in sorted-key order; -1 for rows whose keys hold NaN (pandas drops
+    them; ngroup() reports NaN for them)."""
+    c = gb.ngroup().to_numpy(dtype=np.float64)
+    return np.where(np.isnan(c), -1, c).astype(np.int64)
+
+
 class ProfileEngine:
     """GPU numerics of the profile step on one device (cpx.device.Device)."""
 
@@ -105,7 +112,7 @@ class ProfileEngine:
         fused into the reduction (the values pandas would have multiplied first)."""
         import pandas as pd
         gb = df.groupby(keys, sort=True)
-        codes = gb.ngroup().to_numpy()
+        codes = _group_codes(gb)
         key_df = gb.size().reset_index()[keys]
         G = len(key_df)
         cols = [c for c in df.columns if c not in keys and
@@ -121,7 +128,7 @@ class ProfileEngine:
         object row takes the well group of its image.  Callers check `object_means_applies`."""
         import pandas as pd
         igb = image.groupby(keys, sort=True)
-        icode = igb.ngroup().to_numpy()
+        icode = _group_codes(igb)
         ikeys = igb.size().reset_index()[keys]
         lut = pd.Series(icode, index=image["ImageNumber"].to_numpy())
         codes = lut.reindex(obj["ImageNumber"].to_numpy()).to_numpy()

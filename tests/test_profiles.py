@@ -131,6 +131,7 @@ def test_gpu_group_mean_bit_exact(eng):
     nuc.loc[9, "AreaShape_Perimeter"] = -np.inf
     nuc["flag"] = nuc.ObjectNumber % 2 == 0          # bool column
     nuc["label"] = "x"                               # nuisance column (dropped)
+    nuc.loc[[3, 17], "Metadata_Well"] = None          # NaN keys: rows dropped
     ref = nuc.groupby(po.KEYS, as_index=False).mean(numeric_only=True)
     got = eng.group_mean(nuc)
     assert list(got.columns) == list(ref.columns)
