@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--channels", type=int, default=5)
     ap.add_argument("--weights", default=None, help="CPnet state_dict (default: seeded random init)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--stage-steps", type=int, default=3, help="instrumented steps after timing")
+    ap.add_argument("--stage-steps", type=int, default=3, help="instrumented steps after timing (>= 1)")
     ap.add_argument("--pipes", type=int, default=2,
                     help="pipelines (own libcpx context, buffers and HIP stream) per GPU: step i "
                          "runs on pipeline i %% pipes, so that many batches are in flight")
@@ -48,6 +48,7 @@ def parse():
 
 def main():
     a = parse()
+    a.stage_steps = max(1, a.stage_steps)
     import numpy as np
     import torch
     import torch.distributed as dist
