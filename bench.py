@@ -217,6 +217,20 @@ def main():
                 "traffic_source": pmc_src if traffic else None,
                 "algorithmic_flops_per_launch": d["work"], "avg_launch_ms": round(d["ms"], 4)}
 
+    # measured copy bandwidth of this HBM (report next to the vendor peak):
+    # 2 GiB device-to-device copy, read + write bytes over the mean copy time
+    src_b = torch.empty(1 << 31, dtype=torch.uint8, device=td)
+    dst_b = torch.empty_like(src_b)
+    dst_b.copy_(src_b)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        dst_b.copy_(src_b)
+    e1.record()
+    torch.cuda.synchronize()
+    copy_gbs = 2 * (1 << 31) * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del src_b, dst_b
+
     dominant = max(kernels, key=lambda k: kernels[k]["ms"])
     line = {
         "metric": "fields-of-view/sec, 2080x2080x5ch illum+seg+feat pipe",
@@ -244,6 +258,7 @@ def main():
         "stage_ms_per_step": {k: round(v, 3) for k, v in {**per_step_ms, **sub_ms}.items()},
         "roofline": roof(dominant),
         "roofline_all": {k: roof(k) for k in kernels},
+        "hbm_copy_measured_GBs": round(copy_gbs, 1),
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(pipe.raw if Z > 1 else pool[0], illum, C, H, W, cfg)
