@@ -431,10 +431,33 @@ __global__ __launch_bounds__(kAT) void k_tex_stage(const int* __restrict__ label
     const bool flat = !(mmax != mmin);
     unsigned char* dst = scratch + (long long)fov * scratch_per_fov + off +
                          (long long)ch * (((long long)bh * bw + 15) / 16 * 16);
-    for (int r = ty; r < bh; r += 8)
-      for (int c = tx; c < bw; c += 32)
-        dst[r * bw + c] = (unsigned char)quantize(img[(long long)r * W + c],
-                                                  lb[(long long)r * W + c] == L, mmin, rng, flat);
+    // the crop is written as a flat row-major byte array, four pixels per thread per step
+    // packed into one 32-bit store (slots are 16-byte aligned): all lanes busy whatever bw is,
+    // and a wave stores 256 contiguous bytes instead of 64 single bytes
+    const int nb = bh * bw;
+    for (int f0 = 4 * threadIdx.x; f0 < nb; f0 += 4 * kAT) {
+      int r = f0 / bw, c = f0 - r * bw;
+      float vv[4];
+      int ll[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        vv[u] = 0.0f;
+        ll[u] = -1;
+        if (f0 + u < nb) {
+          vv[u] = img[(long long)r * W + c];
+          ll[u] = lb[(long long)r * W + c];
+        }
+        if (++c == bw) {
+          c = 0;
+          ++r;
+        }
+      }
+      unsigned int word = 0u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        word |= (unsigned int)quantize(vv[u], ll[u] == L, mmin, rng, flat) << (8 * u);
+      *reinterpret_cast<unsigned int*>(dst + f0) = word;
+    }
   }
 }
 
