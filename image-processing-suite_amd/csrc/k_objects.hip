@@ -119,19 +119,27 @@ __global__ __launch_bounds__(kThreads) void k_label_stats(const int* __restrict_
   if (c < W) {
     const int* col = labels + (long long)fov * H * W + c;
     int cur = 0, start = 0;
-    for (int r = r0; r < r1; ++r) {
-      int l = col[(long long)r * W];
-      if (l > 0) {
-        seen_max = max(seen_max, l);
-        if (l > max_label) {
-          overflow = true;
-          l = 0;
+    for (int rb = r0; rb < r1; rb += 8) {  // eight label loads in flight, then the run scan
+      int lv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) lv[u] = rb + u < r1 ? col[(long long)(rb + u) * W] : 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = rb + u;
+        if (r >= r1) break;
+        int l = lv[u];
+        if (l > 0) {
+          seen_max = max(seen_max, l);
+          if (l > max_label) {
+            overflow = true;
+            l = 0;
+          }
         }
-      }
-      if (l != cur) {
-        if (cur > 0) lds_flush_run(tab, st, cur, c, start, r - 1);
-        cur = l;
-        start = r;
+        if (l != cur) {
+          if (cur > 0) lds_flush_run(tab, st, cur, c, start, r - 1);
+          cur = l;
+          start = r;
+        }
       }
     }
     if (cur > 0) lds_flush_run(tab, st, cur, c, start, r1 - 1);
