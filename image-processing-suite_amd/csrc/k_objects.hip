@@ -43,7 +43,7 @@ __global__ void k_stats_init(cpx_label_stats* __restrict__ st, long long n,
 // Labels are compact, so a tile holds a handful of them: global atomics drop from one set per
 // run to one per tile and label.  A full table (pathological label images) spills runs
 // straight to global memory, so results never depend on the table size.
-constexpr int kTileR = 32;
+constexpr int kTileR = 128;  // rows per thread: longer runs, fewer table flushes (32: 172 us, 128: 92 us per call)
 constexpr int kHash = 256;
 
 struct LdsStat {
