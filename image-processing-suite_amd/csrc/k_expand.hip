@@ -13,7 +13,7 @@
 // within `distance` of the pixel when the result is kept (distance <= D), so both passes are
 // bounded-window here:
 //   pass 1 (one thread per column and 64-row tile, coalesced): signed offset to the nearest
-//          feature row in the column within D (int8; none = -128);
+//          feature row in the column within D (none = -128), packed with that feature's label;
 //   pass 2 (one thread per pixel, row segment + halo staged in LDS): scan the 2D+1 columns in
 //          ascending order with a strict `<` (smaller column wins ties), threshold d^2 <= D^2.
 // Bit-identical to skimage/scipy (tests/test_gpu_parity.py, including equidistant ties).
@@ -25,70 +25,99 @@ constexpr int kT = 256;
 constexpr signed char kNone = -128;
 
 // pass 1: per column and tile of kColTile rows, nearest feature row within +-D (down sweep from
-// D rows above the tile, then up sweep from D rows below it)
+// D rows above the tile, then up sweep from D rows below it).  Stored packed per pixel:
+// (label of that feature << 8) | (uint8)row offset, offset kNone (label 0) when none — so pass 2
+// reads the winning label from its staged row segment instead of gathering it from the labels.
 constexpr int kColTile = 64;
 
+__device__ __forceinline__ int pack_ft(int dr, int lab) { return (lab << 8) | (dr & 0xff); }
+__device__ __forceinline__ int ft_dr(int v) { return (int)(signed char)(v & 0xff); }
+
 __global__ __launch_bounds__(kT) void k_edt_cols(const int* __restrict__ labels, int H, int W,
-                                                 int D, signed char* __restrict__ off) {
+                                                 int D, int* __restrict__ off) {
   const int fov = blockIdx.z;
   const int col = blockIdx.x * kT + threadIdx.x;
   if (col >= W) return;
   const int r0 = blockIdx.y * kColTile, r1 = min(H, r0 + kColTile);
   const long long base = (long long)fov * H * W + col;
   const int* lab = labels + base;
-  signed char* o = off + base;
+  int* o = off + base;
   // down sweep: distance to the last feature at or above (stored), capped at D+1
-  int last = -0x40000000;
-  for (int r = max(0, r0 - D); r < r1; ++r) {
-    if (lab[(long long)r * W] != 0) last = r;
-    if (r < r0) continue;
-    const int du = r - last;
-    o[(long long)r * W] = du <= D ? (signed char)(-du) : kNone;  // feature above (or here)
+  int last = -0x40000000, last_l = 0;
+  for (int rb = max(0, r0 - D); rb < r1; rb += 8) {  // eight label loads in flight
+    int lv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) lv[u] = rb + u < r1 ? lab[(long long)(rb + u) * W] : 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = rb + u;
+      if (r >= r1) break;
+      if (lv[u] != 0) {
+        last = r;
+        last_l = lv[u];
+      }
+      if (r < r0) continue;
+      const int du = r - last;
+      o[(long long)r * W] = du <= D ? pack_ft(-du, last_l) : pack_ft(kNone, 0);  // feature above (or here)
+    }
   }
   // up sweep: next feature at or below; keep the above one on ties (smaller row)
-  int next = 0x40000000;
+  int next = 0x40000000, next_l = 0;
   for (int r = min(H, r1 + D) - 1; r >= r0; --r) {
-    if (lab[(long long)r * W] != 0) next = r;
+    const int l = lab[(long long)r * W];
+    if (l != 0) {
+      next = r;
+      next_l = l;
+    }
     if (r >= r1) continue;
     const int dd = next - r;
     if (dd > D) continue;
-    const signed char cur = o[(long long)r * W];
-    const int du = cur == kNone ? 0x7fffffff : -(int)cur;
-    if (dd < du) o[(long long)r * W] = (signed char)dd;
+    const int cur = ft_dr(o[(long long)r * W]);
+    const int du = cur == kNone ? 0x7fffffff : -cur;
+    if (dd < du) o[(long long)r * W] = pack_ft(dd, next_l);
   }
 }
 
-// pass 2: per pixel, lexicographic min of (d^2, column) over the 2D+1 columns
+// pass 2: per pixel, lexicographic min of (d^2, column) over the 2D+1 columns.  A block owns
+// kRowsPB rows of a kT-column segment (fewer, fuller blocks: one block per row was
+// dispatch-bound); all its rows' candidate segments are staged in LDS at once.
+constexpr int kRowsPB = 8;
+
 __global__ __launch_bounds__(kT) void k_edt_rows(const int* __restrict__ nuc, int H, int W, int D,
-                                                 const signed char* __restrict__ off,
+                                                 const int* __restrict__ off,
                                                  int* __restrict__ cells, int* __restrict__ cyto) {
-  extern __shared__ signed char seg[];  // kT + 2D
-  const int fov = blockIdx.z, r = blockIdx.y;
+  extern __shared__ int seg[];  // kRowsPB x (kT + 2D) packed candidates
+  const int fov = blockIdx.z, r0 = blockIdx.y * kRowsPB;
+  const int nr = min(kRowsPB, H - r0);
   const int c0 = blockIdx.x * kT;
-  const long long rowbase = ((long long)fov * H + r) * W;
-  for (int i = threadIdx.x; i < kT + 2 * D; i += kT) {
-    const int c = c0 - D + i;
-    seg[i] = (c >= 0 && c < W) ? off[rowbase + c] : kNone;
+  const int sw = kT + 2 * D;
+  for (int i = threadIdx.x; i < nr * sw; i += kT) {
+    const int rr = i / sw, k = i - rr * sw;
+    const int c = c0 - D + k;
+    seg[i] = (c >= 0 && c < W) ? off[((long long)fov * H + r0 + rr) * W + c] : pack_ft(kNone, 0);
   }
   __syncthreads();
   const int c = c0 + threadIdx.x;
   if (c >= W) return;
-  int best = 0x7fffffff, bc = -1, br = 0;
-  for (int k = 0; k <= 2 * D; ++k) {
-    const signed char dr = seg[threadIdx.x + k];
-    if (dr == kNone) continue;
-    const int dc = k - D;
-    const int d2 = (int)dr * (int)dr + dc * dc;
-    if (d2 < best) {
-      best = d2;
-      bc = c + dc;
-      br = r + dr;
+  for (int rr = 0; rr < nr; ++rr) {
+    const int* sr = seg + rr * sw + threadIdx.x;
+    int best = 0x7fffffff, blab = 0;
+    for (int k = 0; k <= 2 * D; ++k) {
+      const int v = sr[k];
+      const int dr = ft_dr(v);
+      if (dr == kNone) continue;
+      const int dc = k - D;
+      const int d2 = dr * dr + dc * dc;
+      if (d2 < best) {
+        best = d2;
+        blab = v >> 8;
+      }
     }
+    const int lab = best <= D * D ? blab : 0;
+    const long long px = ((long long)fov * H + r0 + rr) * W + c;
+    if (cells) cells[px] = lab;
+    if (cyto) cyto[px] = (nuc[px] == 0) ? lab : 0;
   }
-  int lab = 0;
-  if (bc >= 0 && best <= D * D) lab = nuc[((long long)fov * H + br) * W + bc];
-  if (cells) cells[rowbase + c] = lab;
-  if (cyto) cyto[rowbase + c] = (nuc[rowbase + c] == 0) ? lab : 0;
 }
 
 }  // namespace
@@ -99,15 +128,15 @@ extern "C" int cpx_expand_labels(cpx_ctx* ctx, const int32_t* nuclei_dev, int B,
               "cpx_expand_labels: null argument");
   CPX_REQUIRE(B > 0 && B <= 65535 && H > 0 && H <= 65535 && W > 0 && distance >= 0 && distance <= 127,
               CPX_ERR_ARG, "cpx_expand_labels: bad sizes (distance must be <= 127)");
-  signed char* off = (signed char*)cpx_ws(ctx, WS_FEAT, (size_t)B * H * W + 256);
+  int* off = (int*)cpx_ws(ctx, WS_FEAT, sizeof(int) * (size_t)B * H * W + 256);
   if (!off) return CPX_ERR_OOM;
   hipLaunchKernelGGL(k_edt_cols, dim3(cpx_div_up(W, kT), cpx_div_up(H, kColTile), B), dim3(kT),
                      0, ctx->stream,
                      (const int*)nuclei_dev, H, W, distance, off);
   CPX_CHECK_LAUNCH("k_edt_cols");
-  hipLaunchKernelGGL(k_edt_rows, dim3(cpx_div_up(W, kT), H, B), dim3(kT), kT + 2 * distance,
-                     ctx->stream, (const int*)nuclei_dev, H, W, distance, (const signed char*)off,
-                     cells_dev, cyto_dev);
+  hipLaunchKernelGGL(k_edt_rows, dim3(cpx_div_up(W, kT), cpx_div_up(H, kRowsPB), B), dim3(kT),
+                     sizeof(int) * kRowsPB * (kT + 2 * distance), ctx->stream,
+                     (const int*)nuclei_dev, H, W, distance, (const int*)off, cells_dev, cyto_dev);
   CPX_CHECK_LAUNCH("k_edt_rows");
   return CPX_OK;
 }

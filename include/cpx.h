@@ -279,7 +279,7 @@ int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev,
  * cells = skimage.segmentation.expand_labels(nuclei, distance) (0.18.3: nearest label pixel by
  * scipy's exact Euclidean feature transform, kept where the distance <= `distance`);
  * cyto = cells where nuclei == 0 (Cytoplasm shares the Cells/Nuclei ObjectNumber).  Either
- * output may be NULL.  All int32 [B][H][W].                                                  */
+ * output may be NULL.  All int32 [B][H][W]; label values below 2^23.                        */
 int cpx_expand_labels(cpx_ctx* ctx, const int32_t* nuclei_dev, int B, int H, int W, int distance,
                       int32_t* cells_dev, int32_t* cyto_dev);
 
