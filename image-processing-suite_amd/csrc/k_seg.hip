@@ -716,15 +716,18 @@ __global__ void k_count_bad(int max_label, const unsigned char* __restrict__ bad
 }
 
 // nearest-neighbour resize to full resolution
+constexpr int kUpRows = 8;
 __global__ __launch_bounds__(kT) void k_upsample(const int* __restrict__ m0, int Ly, int Lx, int H,
                                                  int W, const int* __restrict__ ysrc,
                                                  const int* __restrict__ xsrc,
                                                  int* __restrict__ out) {
   const int fov = blockIdx.z;
-  const int y = blockIdx.y;
   const int x = blockIdx.x * kT + threadIdx.x;
   if (x >= W) return;
-  out[((long long)fov * H + y) * W + x] = m0[((long long)fov * Ly + ysrc[y]) * Lx + xsrc[x]];
+  const int xs = xsrc[x];
+  const int y0 = blockIdx.y * kUpRows, y1 = min(H, y0 + kUpRows);  // rows per block
+  for (int y = y0; y < y1; ++y)
+    out[((long long)fov * H + y) * W + x] = m0[((long long)fov * Ly + ysrc[y]) * Lx + xs];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -866,18 +869,35 @@ __global__ __launch_bounds__(kT) void k_fill_apply(int* __restrict__ labels, lon
                                                    const int* __restrict__ fillidx,
                                                    const int* __restrict__ newlab) {
   const int fov = blockIdx.y;
-  for (long long q = (long long)blockIdx.x * kT + threadIdx.x; q < n; q += (long long)gridDim.x * kT) {
-    int* lp = labels + (long long)fov * n + q;
-    const int l = *lp;
-    int cand = 0;
-    if (l > 0 && l <= max_label) {
-      const int k = lab2idx[(long long)fov * (max_label + 1) + l];
-      if (newlab[(long long)fov * max_label + k]) cand = k + 1;
+  const int* l2i = lab2idx + (long long)fov * (max_label + 1);
+  const int* nl = newlab + (long long)fov * max_label;
+  // four independent pixels per iteration: their dependent lookups (label -> index -> new
+  // label) overlap instead of one chain of loads at a time
+  const long long stride = (long long)gridDim.x * kT;
+  for (long long q0 = (long long)blockIdx.x * kT + threadIdx.x; q0 < n; q0 += 4 * stride) {
+    int l[4], f[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long q = q0 + u * stride;
+      l[u] = q < n ? labels[(long long)fov * n + q] : 0;
+      f[u] = q < n ? fillidx[(long long)fov * n + q] : 0;
     }
-    int f = fillidx[(long long)fov * n + q];
-    if (f && !newlab[(long long)fov * max_label + f - 1]) f = 0;
-    const int best = max(cand, f);
-    *lp = best ? newlab[(long long)fov * max_label + best - 1] : 0;
+    int k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) k[u] = (l[u] > 0 && l[u] <= max_label) ? l2i[l[u]] : -1;
+    int cand[4], fk[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      cand[u] = (k[u] >= 0 && nl[k[u]]) ? k[u] + 1 : 0;
+      fk[u] = (f[u] && nl[f[u] - 1]) ? f[u] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long q = q0 + u * stride;
+      if (q >= n) continue;
+      const int best = max(cand[u], fk[u]);
+      labels[(long long)fov * n + q] = best ? nl[best - 1] : 0;
+    }
   }
 }
 
@@ -1106,7 +1126,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
                        (const unsigned char*)bad, stats_dev);
     CPX_CHECK_LAUNCH("cpx_seg_masks flow error");
   }
-  hipLaunchKernelGGL(k_upsample, dim3(cpx_div_up(W, kT), H, B), dim3(kT), 0, ctx->stream,
+  hipLaunchKernelGGL(k_upsample, dim3(cpx_div_up(W, kT), cpx_div_up(H, kUpRows), B), dim3(kT), 0, ctx->stream,
                      (const int*)d.m0, Ly, Lx, H, W, tabs.ynear, tabs.xnear, labels_dev);
   CPX_CHECK_LAUNCH("k_upsample");
   // ---- fill holes + remove small at full resolution
