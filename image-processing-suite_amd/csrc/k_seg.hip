@@ -554,6 +554,7 @@ __global__ __launch_bounds__(kT) void k_apply_newlab(int Ly, int Lx, DynBufs d) 
 // and per-mask mean squared difference against dP/5; one block per mask.
 constexpr int kFlowThreads = 256;
 constexpr int kFlowMaxCells = 8192;  // 2 x (ly+2)*(lx+2) doubles in LDS; larger masks: BIG pass
+constexpr int kFlowPP = 4;           // bbox pixels per thread kept in registers for the diffusion
 
 // BIG = false: grid-stride over the masks that fit in LDS; BIG = true: one block per FOV walks
 // the oversize masks with a per-FOV global scratch (no two blocks share a scratch area).
@@ -637,20 +638,43 @@ __global__ __launch_bounds__(kFlowThreads) void k_flow_error(
   const int pbest = (int)(bsel & 0xffffffffu);
   const int ym = pbest / bw + 1, xm = pbest % bw + 1;
   const int niter = 2 * ((bw - 1) + (bh - 1));  // 2 * (ptp(x) + ptp(y))
-  // Jacobi heat diffusion over mask pixels (T outside the mask stays 0)
+  // Jacobi heat diffusion over mask pixels (T outside the mask stays 0).  Objects of at most
+  // kFlowPP pixels per thread keep their in-mask cell indices in registers, so the iterations
+  // touch LDS only (no label re-reads per iteration).
+  const bool small = nb <= kFlowPP * kFlowThreads;  // block-uniform
+  int myi[kFlowPP];
+#pragma unroll
+  for (int j = 0; j < kFlowPP; ++j) {
+    const int p = threadIdx.x + j * kFlowThreads;
+    myi[j] = -1;
+    if (small && p < nb) {
+      const int rr = p / bw, cc = p - rr * bw;
+      if (lab[(r0 + rr) * Lx + c0 + cc] == L) myi[j] = (rr + 1) * lx + cc + 1;
+    }
+  }
   double* Tc = T0;
   double* Tn = T1;
   for (int it = 0; it < niter; ++it) {
     if (threadIdx.x == 0) Tc[ym * lx + xm] += 1.0;
     __syncthreads();
-    for (int p = threadIdx.x; p < nb; p += kFlowThreads) {
-      const int rr = p / bw, cc = p - rr * bw;
-      if (lab[(r0 + rr) * Lx + c0 + cc] != L) continue;
-      const int y = rr + 1, x = cc + 1;
-      Tn[y * lx + x] = 1 / 9. * (Tc[y * lx + x] + Tc[(y - 1) * lx + x] + Tc[(y + 1) * lx + x] +
-                                 Tc[y * lx + x - 1] + Tc[y * lx + x + 1] + Tc[(y - 1) * lx + x - 1] +
-                                 Tc[(y - 1) * lx + x + 1] + Tc[(y + 1) * lx + x - 1] +
-                                 Tc[(y + 1) * lx + x + 1]);
+    if (small) {
+#pragma unroll
+      for (int j = 0; j < kFlowPP; ++j) {
+        const int i = myi[j];
+        if (i < 0) continue;
+        Tn[i] = 1 / 9. * (Tc[i] + Tc[i - lx] + Tc[i + lx] + Tc[i - 1] + Tc[i + 1] + Tc[i - lx - 1] +
+                          Tc[i - lx + 1] + Tc[i + lx - 1] + Tc[i + lx + 1]);
+      }
+    } else {
+      for (int p = threadIdx.x; p < nb; p += kFlowThreads) {
+        const int rr = p / bw, cc = p - rr * bw;
+        if (lab[(r0 + rr) * Lx + c0 + cc] != L) continue;
+        const int y = rr + 1, x = cc + 1;
+        Tn[y * lx + x] = 1 / 9. * (Tc[y * lx + x] + Tc[(y - 1) * lx + x] + Tc[(y + 1) * lx + x] +
+                                   Tc[y * lx + x - 1] + Tc[y * lx + x + 1] + Tc[(y - 1) * lx + x - 1] +
+                                   Tc[(y - 1) * lx + x + 1] + Tc[(y + 1) * lx + x - 1] +
+                                   Tc[(y + 1) * lx + x + 1]);
+      }
     }
     __syncthreads();
     double* t = Tc;
