@@ -553,8 +553,9 @@ __global__ __launch_bounds__(kT) void k_apply_newlab(int Ly, int Lx, DynBufs d) 
 // flow-error filter: masks_to_flows (heat diffusion from the pixel nearest the median, fp64)
 // and per-mask mean squared difference against dP/5; one block per mask.
 constexpr int kFlowThreads = 256;
-constexpr int kFlowMaxCells = 8192;  // 2 x (ly+2)*(lx+2) doubles in LDS; larger masks: BIG pass
-constexpr int kFlowPP = 4;           // bbox pixels per thread kept in registers for the diffusion
+constexpr int kFlowMaxCells = 2048;  // 2 x (ly+2)*(lx+2) doubles in LDS (48 KiB with the median
+                                     // histograms: 3 blocks per CU); larger masks: BIG pass
+constexpr int kFlowPP = 8;           // bbox pixels per thread kept in registers for the diffusion
 
 // BIG = false: grid-stride over the masks that fit in LDS; BIG = true: one block per FOV walks
 // the oversize masks with a per-FOV global scratch (no two blocks share a scratch area).
@@ -1137,7 +1138,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       attr = true;
     }
-    const int per_fov = std::max(1, std::min(ML, (2 * ctx->n_cu + B - 1) / B));
+    const int per_fov = std::max(1, std::min(ML, (6 * ctx->n_cu + B - 1) / B));
     hipLaunchKernelGGL(k_flow_error<false>, dim3(per_fov, B), dim3(kFlowThreads), lds, ctx->stream,
                        (const int*)d.m0, yf_dev, Ly, Lx, ML, (const cpx_object*)obj,
                        (const cpx_fov_objects*)hdr, flow_threshold, gscr, (long long)gscr_per, bad);
