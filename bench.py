@@ -30,7 +30,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=16, help="FOVs per step per GPU")
+    ap.add_argument("--batch", type=int, default=32, help="FOVs per step per GPU (384-well plate = 12 steps)")
     ap.add_argument("--pool", type=int, default=2, help="distinct synthetic batches cycled per GPU")
     ap.add_argument("--size", type=int, default=2080)
     ap.add_argument("--channels", type=int, default=5)

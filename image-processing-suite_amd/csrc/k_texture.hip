@@ -559,6 +559,9 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
       __syncthreads();
       GLCM_MARK(2, &pt);
       const int n = *nl;
+#ifdef CPX_GLCM_PROF
+      if (threadIdx.x == 0 && n > kList) atomicAdd(&g_glcm_prof[0], 1ull);  // dense walks
+#endif
       // the other counter was last read before the previous barrier; the next angle uses it
       if (threadIdx.x == 0) nlist[(a + 1) & 1] = 0;
       glcm_walk(tab, list, n, acc[a]);
