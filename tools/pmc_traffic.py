@@ -52,7 +52,8 @@ def load(d, counter):
     per_fam = collections.defaultdict(float)
     for r in step:
         v = float(r["Counter_Value"]) * 1024.0  # KB -> bytes
-        short = r["Kernel_Name"].split("(")[0].replace("void ", "")[:80]
+        short = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+        short = short.replace("void ", "")[:80]
         per_kernel[short] += v
         per_fam[family(r["Kernel_Name"])] += v
     return per_kernel, per_fam, len(step)
@@ -63,7 +64,7 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--out", required=True)
-    ap.add_argument("--batch", type=int, default=16, help="FOVs per bench step")
+    ap.add_argument("--batch", type=int, default=32, help="FOVs per bench step (bench.py --batch)")
     a = ap.parse_args()
     fk, ff, n1 = load(a.fetch_dir, "FETCH_SIZE")
     wk, wf, n2 = load(a.write_dir, "WRITE_SIZE")

@@ -6,6 +6,7 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/round
+BATCH=${BATCH:-32}  # bench.py's default --batch
 mkdir -p $O
 cd $R
 timeout -k 10 420 python -u bench.py > $O/bench_default.log 2>&1
@@ -28,6 +29,6 @@ python tools/prof_summary.py $O/kt/run_kernel_trace.csv --steps 4 --md > $O/kern
 python tools/prof_summary.py $O/kt2/run_kernel_trace.csv --steps 4 --md > $O/kernels_concurrent.md
 cp $O/kt/run_kernel_stats.csv $O/kernel_stats.csv
 cp $O/kt2/run_kernel_stats.csv $O/kernel_stats_concurrent.csv
-python tools/pmc_traffic.py $O/fetch $O/write --out $O/pmc_traffic.json > $O/pmc_traffic.log
+python tools/pmc_traffic.py $O/fetch $O/write --batch $BATCH --out $O/pmc_traffic.json > $O/pmc_traffic.log
 rm -rf $O/kt $O/kt2 $O/fetch $O/write
 echo done
