@@ -291,8 +291,18 @@ __global__ __launch_bounds__(kFT) void k_qc_cols(const cplx* __restrict__ rowspe
                                                       double* __restrict__ ringpart) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cplx* a = reinterpret_cast<cplx*>(smem);
-  const int j = blockIdx.x;
-  const int plane = blockIdx.y;
+  // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs (linear id % 8), so
+  // virtual index V puts consecutive columns of one plane on one XCD at the same time; their
+  // strided 16-byte reads (row stride KC * 16 B) then share each fetched line in that XCD's L2
+  // instead of every column block pulling its own line from HBM.
+  int j = blockIdx.x, plane = blockIdx.y;
+  const int total = gridDim.x * gridDim.y;
+  if ((total & 7) == 0) {
+    const int L = blockIdx.y * gridDim.x + blockIdx.x;
+    const int V = (L & 7) * (total >> 3) + (L >> 3);
+    plane = V / KC;
+    j = V - plane * KC;
+  }
   const cplx* src = rowspec + (long long)plane * H * KC + j;
   for (int r = threadIdx.x; r < H; r += kFT) a[r] = src[(long long)r * KC];
   __syncthreads();
