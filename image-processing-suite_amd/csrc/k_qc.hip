@@ -25,7 +25,10 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kFT = 512;  // FFT kernels: more threads -> fewer butterflies per thread in registers
+#ifndef CPX_QC_FT
+#define CPX_QC_FT 512
+#endif
+constexpr int kFT = CPX_QC_FT;  // FFT kernels: more threads -> fewer butterflies per thread in registers
 constexpr int kMaxN = 4096;
 constexpr int kMaxStages = 12;
 
@@ -308,7 +311,7 @@ __global__ __launch_bounds__(kFT) void k_qc_cols(const cplx* __restrict__ rowspe
   __syncthreads();
   fft_lds(a, twH, ph);
   // power in place (doubles over the first half of the buffer: read all, sync, write)
-  constexpr int PR = kMaxN / kFT;
+  constexpr int PR = (kMaxN + kFT - 1) / kFT;
   double pv[PR];
 #pragma unroll
   for (int q = 0; q < PR; ++q) {
