@@ -462,20 +462,40 @@ __global__ __launch_bounds__(kAT) void k_tex_stage(const int* __restrict__ label
 }
 
 struct GlcmItem {
-  int k, ch, bh, bw, nb;  // nb <= 0: nothing to do (past the end, no slot, or > 65535 px)
+  int fov, k, ch, bh, bw, nb;  // nb <= 0: nothing to do (no slot, > 65535 px, or queue drained)
   const unsigned char* src;
 };
+
+// Work queue of k_tex_glcm (thread 0 only): items of FOV f are handed out by one atomic
+// counter per FOV; a block starts on its own FOV and moves to the next FOV when that queue is
+// drained, so blocks of light FOVs help heavy ones and the launch ends within about one item
+// of balance.  Returns fov * 2^20 + item, or -1 when every queue has been drained (each block
+// visits each FOV at most once, so every block reaches the exit).
+__device__ __forceinline__ int glcm_grab(int& f, int& visited, int B, int C,
+                                         const cpx_fov_objects* __restrict__ hdr,
+                                         int* __restrict__ next) {
+  while (visited < B) {
+    const int n_items = hdr[f].n_objects * C;
+    const int v = atomicAdd(&next[f], 1);
+    if (v < n_items) return (f << 20) | v;
+    ++visited;
+    f = f + 1 == B ? 0 : f + 1;
+  }
+  return -1;
+}
 
 constexpr int kPre = (kCrop / 16 + kTT - 1) / kTT;  // uint4 prefetch registers per thread
 static_assert(kPre == 2, "glcm_prefetch holds two uint4 per thread");
 
-__device__ __forceinline__ GlcmItem glcm_item(int item, int n_items, int C, int fov,
-                                              int max_label, const cpx_object* objects,
+__device__ __forceinline__ GlcmItem glcm_item(int code, int C, int max_label,
+                                              const cpx_object* objects,
                                               const long long* crop_off,
                                               const unsigned char* scratch,
                                               long long scratch_per_fov) {
-  GlcmItem g{0, 0, 0, 0, 0, nullptr};
-  if (item >= n_items) return g;
+  GlcmItem g{0, 0, 0, 0, 0, 0, nullptr};
+  if (code < 0) return g;
+  const int fov = code >> 20, item = code & 0xfffff;
+  g.fov = fov;
   g.k = item / C;
   g.ch = item - g.k * C;
   const long long off = crop_off[(long long)fov * max_label + g.k];
@@ -504,38 +524,48 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
                                                  const long long* __restrict__ crop_off,
                                                  const unsigned char* __restrict__ scratch,
                                                  long long scratch_per_fov,
+                                                 int* __restrict__ glcm_next,
                                                  double* __restrict__ feats) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int s_code[2];  // queue codes (see glcm_grab), double-buffered by iteration parity
   unsigned int* tab = reinterpret_cast<unsigned int*>(smem);
   int* nlist = reinterpret_cast<int*>(tab + kTabW);  // two counters: angle a uses a & 1
   unsigned char* crop = reinterpret_cast<unsigned char*>(nlist + 4);
   unsigned short* list = reinterpret_cast<unsigned short*>(crop + kCrop);
-  const int fov = blockIdx.y;
-  const int n_items = hdr[fov].n_objects * C;
-  if ((int)blockIdx.x >= n_items) return;
+  const int B = gridDim.y;
+  int q_fov = blockIdx.y, q_visited = 0;  // thread 0's queue position
   for (int x = threadIdx.x; x < kTabW; x += kTT) tab[x] = 0u;
   if (threadIdx.x < 4) nlist[threadIdx.x] = 0;
+  if (threadIdx.x == 0) {
+    s_code[0] = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next);
+    s_code[1] = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next);
+  }
   __syncthreads();
   // software pipeline: the next item's metadata and LDS-sized crop are loaded into registers
   // while the current item runs its four angles (the crop was written by k_tex_stage, possibly
-  // on another XCD, so the loads are HBM/MALL latency).
-  GlcmItem cur = glcm_item(blockIdx.x, n_items, C, fov, max_label, objects, crop_off, scratch,
-                           scratch_per_fov);
+  // on another XCD, so the loads are HBM/MALL latency); thread 0 grabs the item after that one
+  // from the queue during the current item, so the atomic's latency is hidden too.
+  GlcmItem cur = glcm_item(s_code[0], C, max_label, objects, crop_off, scratch, scratch_per_fov);
   uint4 p0 = {0u, 0u, 0u, 0u}, p1 = {0u, 0u, 0u, 0u};
   glcm_prefetch(cur, p0, p1);
-  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+  int ahead = -2;  // -2: nothing grabbed yet
+  for (int par = 1; s_code[par ^ 1] >= 0; par ^= 1) {
+    // s_code[par ^ 1] holds the current item (cur), s_code[par] receives the next one
     if (cur.nb > 0 && cur.nb <= kCrop) {
       const int n16 = (cur.nb + 15) / 16;
       if ((int)threadIdx.x < n16) reinterpret_cast<uint4*>(crop)[threadIdx.x] = p0;
       if ((int)threadIdx.x + kTT < n16) reinterpret_cast<uint4*>(crop)[threadIdx.x + kTT] = p1;
     }
+    // s_code[par] was last read by the previous iteration's loop test (before its barrier); it
+    // receives the item grabbed during the previous item
+    if (threadIdx.x == 0 && ahead != -2) s_code[par] = ahead;
     __syncthreads();
     const GlcmItem it = cur;
-    cur = glcm_item(item + gridDim.x, n_items, C, fov, max_label, objects, crop_off, scratch,
-                    scratch_per_fov);
+    cur = glcm_item(s_code[par], C, max_label, objects, crop_off, scratch, scratch_per_fov);
     glcm_prefetch(cur, p0, p1);
+    if (threadIdx.x == 0) ahead = s_code[par] >= 0 ? glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next) : -1;
     if (it.nb <= 0) continue;
-    double* f = feats + ((long long)fov * max_label + it.k) * F + CPX_N_SHAPE +
+    double* f = feats + ((long long)it.fov * max_label + it.k) * F + CPX_N_SHAPE +
                 (long long)it.ch * CPX_FEATURES_PER_CHANNEL + CPX_N_INT;
     long long pt = 0;
 #ifdef CPX_GLCM_PROF
@@ -578,9 +608,11 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
 __global__ __launch_bounds__(1024) void k_crop_offsets(int C, int max_label,
                                                       const cpx_object* __restrict__ objects,
                                                       const cpx_fov_objects* __restrict__ hdr,
-                                                      long long cap, long long* __restrict__ crop_off) {
+                                                      long long cap, long long* __restrict__ crop_off,
+                                                      int* __restrict__ glcm_next) {
   const int fov = blockIdx.x;
   const int n = hdr[fov].n_objects;
+  if (threadIdx.x == 0) glcm_next[fov] = 0;  // k_tex_glcm's work queue of this FOV
   __shared__ long long wsum[16];
   __shared__ long long base;
   if (threadIdx.x == 0) base = 0;
@@ -794,14 +826,18 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   }
   // workspace: crop offsets [B][max_label] + scratch (2 bytes per pixel-channel per FOV)
   const long long per_fov = ((2LL * H * W * C + 255) / 256) * 256;
-  const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + 255) / 256) * 256;
+  // + one GLCM work-queue counter per FOV (zeroed by k_crop_offsets)
+  const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + sizeof(int) * (size_t)B + 255) / 256) * 256;
   unsigned char* ws = (unsigned char*)cpx_ws(ctx, WS_MISC, off_bytes + (size_t)B * per_fov + 256);  // +256: GLCM key read-ahead
   if (!ws) return CPX_ERR_OOM;
+  CPX_REQUIRE(B < 2048 && (long long)max_label * C < (1 << 20), CPX_ERR_SHAPE,
+              "GLCM queue codes hold fov < 2048 and items < 2^20");
   long long* crop_off = (long long*)ws;
+  int* glcm_next = (int*)(crop_off + (size_t)B * max_label);
   unsigned char* scratch = ws + off_bytes;
   *crop_off_out = crop_off;
   hipLaunchKernelGGL(k_crop_offsets, dim3(B), dim3(1024), 0, ctx->stream, C, max_label,
-                     objects_dev, hdr_dev, per_fov, crop_off);
+                     objects_dev, hdr_dev, per_fov, crop_off, glcm_next);
   CPX_CHECK_LAUNCH("k_crop_offsets");
   const int per_fov_s = std::max(1, std::min(max_label, (8 * ctx->n_cu + B - 1) / B));
   hipLaunchKernelGGL(k_shape_fast, dim3(per_fov_s, B), dim3(kST), lds_s, ctx->stream,
@@ -815,7 +851,7 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   const int per_fov_t = std::max(1, std::min(max_label * C, (ctx->n_cu + B - 1) / B));
   hipLaunchKernelGGL(k_tex_glcm, dim3(per_fov_t, B), dim3(kTT), lds_t, ctx->stream, C, max_label,
                      F, objects_dev, hdr_dev, (const long long*)crop_off,
-                     (const unsigned char*)scratch, per_fov, feats_dev);
+                     (const unsigned char*)scratch, per_fov, glcm_next, feats_dev);
   CPX_CHECK_LAUNCH("k_tex_glcm");
   return CPX_OK;
 }
