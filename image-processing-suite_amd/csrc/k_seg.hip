@@ -293,6 +293,7 @@ struct DynBufs {
   int* first;      // [B][kMaxSeeds + 1]
   int* newlab;     // [B][kMaxSeeds + 1]
   unsigned char* mark;  // [B][Ly*Lx]
+  int* act;        // [B][Ly*Lx]: indices of the moving pixels (first n_moving entries per FOV)
   cpx_seg_stats* st;
 };
 
@@ -314,18 +315,25 @@ __global__ __launch_bounds__(kT) void k_dyn_prep(const float* __restrict__ yf, i
     d.p[(long long)fov * 2 * n + n + q] = (float)x;
     moving = (double)fabsf(dy) > 1e-3;
   }
-  moving = wave_sum(moving);
-  if ((threadIdx.x & 63) == 0 && moving) atomicAdd(&d.st[fov].n_moving, moving);
+  // compact the moving pixels (wave-aggregated slots; the list order does not matter, every
+  // pixel writes only its own position) so k_dyn_follow runs full waves
+  const unsigned long long mask = __ballot(moving);
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (lane == 0 && mask) base = atomicAdd(&d.st[fov].n_moving, __popcll(mask));
+  base = __shfl(base, 0);
+  if (moving) d.act[(long long)fov * n + base + __popcll(mask & ((1ull << lane) - 1ull))] = q;
 }
 
 __global__ __launch_bounds__(kT) void k_dyn_follow(int Ly, int Lx, int niter, DynBufs d) {
   const int fov = blockIdx.y;
-  const int q = blockIdx.x * kT + threadIdx.x;
+  const int t = blockIdx.x * kT + threadIdx.x;
   const int n = Ly * Lx;
-  if (q >= n) return;
-  if (d.st[fov].n_moving < 5) return;  // follow_flows returns inds=None -> no masks
+  const int n_moving = d.st[fov].n_moving;
+  if (n_moving < 5) return;  // follow_flows returns inds=None -> no masks
+  if (t >= n_moving) return;
+  const int q = d.act[(long long)fov * n + t];  // a pixel with |dY| > 1e-3 (k_dyn_prep)
   const float* I = d.dps + (long long)fov * 2 * n;
-  if (!((double)fabsf(I[q]) > 1e-3)) return;
   float py = (float)(q / Lx), px = (float)(q % Lx);
   const float fLy = (float)(Ly - 1), fLx = (float)(Lx - 1);
   for (int it = 0; it < niter; ++it) {
@@ -1071,7 +1079,8 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   const size_t sz_seeds = al(sizeof(int) * (size_t)B * kMaxSeeds);
   const size_t sz_cnt = al(sizeof(int) * (size_t)B * (kMaxSeeds + 1));
   const size_t sz_mark = al((size_t)B * n);
-  const size_t total = sz_dps + sz_p + sz_h + sz_M + sz_m0 + sz_seeds + 3 * sz_cnt + sz_mark;
+  const size_t sz_act = al(sizeof(int) * B * n);
+  const size_t total = sz_dps + sz_p + sz_h + sz_M + sz_m0 + sz_seeds + 3 * sz_cnt + sz_mark + sz_act;
   unsigned char* w = (unsigned char*)cpx_ws(ctx, WS_SEG_DYN, total);
   if (!w) return CPX_ERR_OOM;
   DynBufs d;
@@ -1085,6 +1094,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   d.first = (int*)w; w += sz_cnt;
   d.newlab = (int*)w; w += sz_cnt;
   d.mark = (unsigned char*)w; w += sz_mark;
+  d.act = (int*)w; w += sz_act;
   d.st = stats_dev;
   CPX_CHECK_HIP(hipMemsetAsync(stats_dev, 0, sizeof(cpx_seg_stats) * B, ctx->stream));
   CPX_CHECK_HIP(hipMemsetAsync(d.h, 0, sz_h, ctx->stream));
