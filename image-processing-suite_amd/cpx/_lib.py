@@ -105,7 +105,7 @@ SIGNATURES = {
     "cpx_seg_percentiles": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "cpx_seg_tiles": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P]),
     "cpx_seg_average": (_I, [_P, _P, _I, _I, _I, _P, _P, _P]),
-    "cpx_seg_masks": (_I, [_P, _P, _I, _P, _I, _I, _I, ct.c_double, _I, _I, _P, _P]),
+    "cpx_seg_masks": (_I, [_P, _P, _I, _P, _I, _I, _I, ct.c_double, _I, _I, _I, _P, _P]),
     "cpx_cpnet_epilogue": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I]),
     "cpx_cpnet_pool": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "cpx_cpnet_conv_cfg": (_I, [_I, _I, _P, _P]),
@@ -114,7 +114,7 @@ SIGNATURES = {
     "cpx_fov_qc": (_I, [_P, _P, _P, _P]),
     "cpx_fov_planes": (_I, [_P, _P, _P]),
     "cpx_fov_read_plane": (_I, [_P, _I, _P]),
-    "cpx_fov_segment_post": (_I, [_P, _P, _I, _P, _P, _I, ct.c_double, _I, _I, _P, _P]),
+    "cpx_fov_segment_post": (_I, [_P, _P, _I, _P, _P, _I, ct.c_double, _I, _I, _I, _P, _P]),
     "cpx_fov_object_table": (_I, [_P, _P, _I, _I, _P, _P]),
     "cpx_fov_features": (_I, [_P, _P, _I, _P, _P]),
     "cpx_fov_wait": (_I, [_P]),

@@ -37,6 +37,7 @@ class PipelineConfig:
     channels: tuple = ("DNA", "ER", "RNA", "AGP", "Mito")
     model: str = CELLPOSE_MODEL
     diameter: float = DIAMETER
+    resample: bool = True            # CellposeModel.eval default: dynamics at full resolution
     cell_expand: int = 15            # Cells = expand_labels(Nuclei, cell_expand)
     max_objects: int = 2048          # per FOV and object set
     box: int = 200                   # Cellpose_GPU_s3fs.py:30 BOX_SIZE
@@ -70,7 +71,8 @@ class FovPipeline:
         self.lstats = dev.empty_bytes(64 * B * (ML + 1))
         self.F = n_features(C)
         self.seg = Segmenter(dev, H, W, B, model=cfg.model, diameter=cfg.diameter, weights=cfg.weights,
-                             seed=cfg.seed, use_graph=cfg.use_graph, max_objects=ML)
+                             seed=cfg.seed, use_graph=cfg.use_graph, max_objects=ML,
+                             resample=cfg.resample)
         # result slots (device) and their pinned host mirrors
         self._slots = []
         for _ in range(max(1, cfg.slots)):

@@ -2,8 +2,11 @@
 (Cellpose_GPU_s3fs.py:108,143), Cellpose <= v3 semantics as pinned in DESIGN.md §Segmentation.
 
 Pipeline per batch of FOVs (all device-resident, one HIP stream):
-  libcpx cpx_seg_percentiles -> cpx_seg_tiles (bf16 NHWC) -> CPnet forward (PyTorch-ROCm, bf16
-  channels_last, HIP-graph captured) -> cpx_seg_average -> cpx_seg_masks -> int32 labels [B,H,W].
+  libcpx cpx_seg_percentiles -> cpx_seg_tiles (bf16 NHWC) -> CPnet forward (native MFMA
+  convolutions, HIP-graph captured) -> cpx_seg_average -> cpx_seg_masks -> int32 labels [B,H,W].
+Every other eval() argument is at Cellpose's default: resample=True (the averaged flows are
+resized to H x W and the dynamics run at full resolution) with niter = uint32(1 / rescale * 200)
+(_run_cp; 1176 for the nuclei model at diameter 100).  resample=False is a named option.
 """
 from __future__ import annotations
 
@@ -24,7 +27,17 @@ CELLPOSE_MODEL = "nuclei"  # Cellpose_GPU_s3fs.py:28
 DIAMETER = 100.0           # Cellpose_GPU_s3fs.py:143
 BSIZE = 224
 TILE_OVERLAP = 0.1
-NITER = 200
+RESAMPLE = True           # CellposeModel.eval default (the reference passes only diameter)
+NITER_NET = 200           # Cellpose 2.x's steps when the dynamics run at network size
+
+
+def default_niter(model: str = CELLPOSE_MODEL, diameter: float = DIAMETER, resample: bool = RESAMPLE) -> int:
+    """CellposeModel._run_cp: niter = 1 / rescale * 200 (rescale = diam_mean / diameter), cast
+    to uint32 by dynamics.follow_flows."""
+    if not resample:
+        return NITER_NET
+    rescale = DIAM_MEAN[model] / diameter
+    return int(np.uint32(1 / rescale * 200))
 FLOW_THRESHOLD = 0.4
 MIN_SIZE = 15
 NET_CHANNELS = 2
@@ -99,15 +112,17 @@ class Segmenter:
     def __init__(self, dev: Device, H: int, W: int, batch: int, model: str = CELLPOSE_MODEL,
                  diameter: float = DIAMETER, weights: str | None = None, seed: int = 0,
                  use_graph: bool = True, max_objects: int = 4096, net_dtype=torch.bfloat16,
-                 fused: bool = True,
-                 niter: int = NITER, flow_threshold: float = FLOW_THRESHOLD, min_size: int = MIN_SIZE):
+                 fused: bool = True, resample: bool = RESAMPLE,
+                 niter: int | None = None, flow_threshold: float = FLOW_THRESHOLD, min_size: int = MIN_SIZE):
         self.dev = dev
         self.H, self.W, self.B = H, W, batch
         self.geom = make_geom(H, W, model, diameter)
         g = self.geom
         td = dev.torch_device
         self.max_objects = max_objects
-        self.niter, self.flow_threshold, self.min_size = niter, flow_threshold, min_size
+        self.resample = bool(resample)
+        self.niter = default_niter(model, diameter, self.resample) if niter is None else int(niter)
+        self.flow_threshold, self.min_size = flow_threshold, min_size
         self.net_dtype = net_dtype
         self.net = build_cpnet(seed=seed, model=model, state_dict_path=weights).to(td)
         self.layout = 1 if net_dtype == torch.bfloat16 else 0
@@ -178,7 +193,7 @@ class Segmenter:
                                   ct.c_void_p(ct.addressof(self.geom)), _ptr(self.taper), _ptr(self.yf)), "cpx_seg_average")
         check(lib.cpx_seg_masks(self.dev.h, _ptr(self.yf), self.B, ct.c_void_p(ct.addressof(self.geom)), self.H, self.W,
                                 self.niter, float(self.flow_threshold), self.min_size, self.max_objects,
-                                _ptr(labels), _ptr(self.stats)), "cpx_seg_masks")
+                                int(self.resample), _ptr(labels), _ptr(self.stats)), "cpx_seg_masks")
 
     def segment(self, corr: torch.Tensor, labels: torch.Tensor | None = None) -> torch.Tensor:
         if labels is None:

@@ -229,7 +229,8 @@ int cpx_fov_read_plane(cpx_ctx* ctx, int ch, uint16_t* host) {
 
 int cpx_fov_segment_post(cpx_ctx* ctx, const void* net_dev, int layout, const cpx_seg_geom* geom,
                          const float* taper_dev, int niter, double flow_threshold, int min_size,
-                         int max_objects, int32_t* labels_dev, cpx_seg_stats* stats_dev) {
+                         int max_objects, int resample, int32_t* labels_dev,
+                         cpx_seg_stats* stats_dev) {
   CPX_REQUIRE(ctx && net_dev && geom && taper_dev && labels_dev && stats_dev, CPX_ERR_ARG,
               "cpx_fov_segment_post: null argument");
   CPX_REQUIRE(ctx->fov && ctx->fov->have, CPX_ERR_STATE, "cpx_fov_segment_post: no FOV submitted");
@@ -239,7 +240,7 @@ int cpx_fov_segment_post(cpx_ctx* ctx, const void* net_dev, int layout, const cp
   if ((rc = grow(ctx, (void**)&f->yf, &f->yf_cap, need, "fov flows")) != CPX_OK) return rc;
   if ((rc = cpx_seg_average(ctx, net_dev, layout, 1, 3, geom, taper_dev, f->yf)) != CPX_OK) return rc;
   return cpx_seg_masks(ctx, f->yf, 1, geom, f->H, f->W, niter, flow_threshold, min_size,
-                       max_objects, labels_dev, stats_dev);
+                       max_objects, resample, labels_dev, stats_dev);
 }
 
 int cpx_fov_object_table(cpx_ctx* ctx, const int32_t* labels_dev, int box, int max_objects,

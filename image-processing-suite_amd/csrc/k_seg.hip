@@ -281,174 +281,410 @@ __global__ __launch_bounds__(kT) void k_seg_average(const void* __restrict__ net
 }
 
 // ---------------------------------------------------------------------------------------------
-// dynamics
+// dynamics (dynamics.compute_masks) at the dynamics resolution Dy x Dx: the full H x W with
+// resample=True (CellposeModel.eval's default, the reference call), Ly x Lx with resample=False.
 struct DynBufs {
-  float* dps;      // [B][2][Ly][Lx]
-  float* p;        // [B][2][Ly][Lx]
-  int* h;          // [B][Lyh][Lxh]
-  unsigned int* M; // [B][Lyh][Lxh]
-  int* m0;         // [B][Ly][Lx]
-  int* seeds;      // [B][kMaxSeeds]
-  int* cnt;        // [B][kMaxSeeds + 1]
-  int* first;      // [B][kMaxSeeds + 1]
-  int* newlab;     // [B][kMaxSeeds + 1]
-  unsigned char* mark;  // [B][Ly*Lx]
-  int* act;        // [B][Ly*Lx]: indices of the moving pixels (first n_moving entries per FOV)
+  float2* dps;           // [B][n] (dY, dX) * cp_mask / 5: the follow_flows field
+  float2* dpf;           // [B][n] (dY, dX) network flows (flow-error input)
+  float2* p;             // [B][n] final positions (written for moving pixels only)
+  unsigned char* mov;    // [B][n] pixel follows the flow (|dY * cp / 5| > 1e-3)
+  int* h;                // [B][nh] histogram of final positions, padded by kRpad
+  unsigned int* M;       // [B][nh] seed-expansion label map
+  unsigned char* sflag;  // [B][nh] seed flags
+  int* m0;               // [B][n] get_masks labels (the caller's labels buffer at full res)
+  int* seeds;            // [B][kMaxSeeds] seed pixels (padded grid), row-major
+  int* cnt;              // [B][kMaxSeeds + 1] pixels per seed label
+  int* first;            // [B][kMaxSeeds + 1] first pixel (raster order) per seed label
+  int* newlab;           // [B][kMaxSeeds + 1] renumbered label (0: removed)
+  unsigned char* mark;   // [B][n] first-occurrence pixels of the kept labels
+  int* marklist;         // [B][kMaxSeeds] marked pixels in raster order
+  int* act;              // [B][n] moving pixels (first n_moving entries per FOV, any order)
+  void* fitems0;         // [B][n] FollowItem ping
+  void* fitems1;         // [B][n] FollowItem pong
+  int* fcnt;             // [rounds + 1][B] items per FOV entering each follow round
+  int* tiles;            // [B][ntile] ordered-compaction tile counts -> offsets
+  int* totals;           // [B] ordered-compaction totals
   cpx_seg_stats* st;
 };
 
+// Dynamics pixels -> dps, dpf, moving flag; the moving pixels are compacted into `act` in
+// tile order (one atomic per block; inside a tile the raster order is kept) so a wave of
+// k_dyn_follow starts on 64 neighbouring pixels.  RESAMPLE: cv2 INTER_LINEAR of the Ly x Lx
+// averaged output to Dy x Dx (transforms.resize_image), fp32, row pass then column pass.
+constexpr int kPrepPer = 8;  // pixels per thread (thread t: pixels t, t + kT, ...)
+
+template <bool RESAMPLE>
 __global__ __launch_bounds__(kT) void k_dyn_prep(const float* __restrict__ yf, int Ly, int Lx,
+                                                 int Dy, int Dx, AxisTab uy, AxisTab ux,
                                                  DynBufs d) {
   const int fov = blockIdx.y;
-  const int q = blockIdx.x * kT + threadIdx.x;
-  const int n = Ly * Lx;
-  int moving = 0;
-  if (q < n) {
-    const float* f = yf + (long long)fov * 3 * n;
-    const bool cp = f[2 * n + q] > 0.0f;  // cellprob > cellprob_threshold (0.0)
-    const float dy = (f[q] * (cp ? 1.0f : 0.0f)) / 5.0f;
-    const float dx = (f[n + q] * (cp ? 1.0f : 0.0f)) / 5.0f;
-    d.dps[(long long)fov * 2 * n + q] = dy;
-    d.dps[(long long)fov * 2 * n + n + q] = dx;
-    const int y = q / Lx, x = q - y * Lx;
-    d.p[(long long)fov * 2 * n + q] = (float)y;
-    d.p[(long long)fov * 2 * n + n + q] = (float)x;
-    moving = (double)fabsf(dy) > 1e-3;
+  const long long n = (long long)Dy * Dx;
+  const long long nl = (long long)Ly * Lx;
+  const long long q0 = (long long)blockIdx.x * kT * kPrepPer;
+  const float* f = yf + (long long)fov * 3 * nl;
+  unsigned int movbits = 0;
+#pragma unroll
+  for (int k = 0; k < kPrepPer; ++k) {
+    const long long q = q0 + k * kT + threadIdx.x;
+    if (q >= n) break;
+    float v[3];
+    if (RESAMPLE) {
+      const int y = (int)(q / Dx), x = (int)(q - (long long)y * Dx);
+      const int y0 = uy.i0[y], y1 = uy.i1[y], x0 = ux.i0[x], x1 = ux.i1[x];
+      const float wy = uy.w[y], wx = ux.w[x];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float* P = f + c * nl;
+        const float r0 = P[y0 * Lx + x0] * (1.0f - wx) + P[y0 * Lx + x1] * wx;
+        const float r1 = P[y1 * Lx + x0] * (1.0f - wx) + P[y1 * Lx + x1] * wx;
+        v[c] = r0 * (1.0f - wy) + r1 * wy;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[c] = f[c * nl + q];
+    }
+    const float cp = v[2] > 0.0f ? 1.0f : 0.0f;  // cellprob > cellprob_threshold (0.0)
+    const float dy = (v[0] * cp) / 5.0f, dx = (v[1] * cp) / 5.0f;
+    d.dps[(long long)fov * n + q] = make_float2(dy, dx);
+    d.dpf[(long long)fov * n + q] = make_float2(v[0], v[1]);
+    // np.abs(dP[0]) > 1e-3: numpy compares the float32 array with the scalar cast to float32
+    const bool moving = fabsf(dy) > 1e-3f;
+    d.mov[(long long)fov * n + q] = (unsigned char)moving;
+    movbits |= (unsigned int)moving << k;
   }
-  // compact the moving pixels (wave-aggregated slots; the list order does not matter, every
-  // pixel writes only its own position) so k_dyn_follow runs full waves
-  const unsigned long long mask = __ballot(moving);
-  const int lane = threadIdx.x & 63;
-  int base = 0;
-  if (lane == 0 && mask) base = atomicAdd(&d.st[fov].n_moving, __popcll(mask));
-  base = __shfl(base, 0);
-  if (moving) d.act[(long long)fov * n + base + __popcll(mask & ((1ull << lane) - 1ull))] = q;
+  // block-wide exclusive ranks in (k, thread) order, one atomic per block
+  __shared__ int wsum[kPrepPer][kT / 64];
+  __shared__ int sbase;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long bal[kPrepPer];
+#pragma unroll
+  for (int k = 0; k < kPrepPer; ++k) {
+    bal[k] = __ballot((movbits >> k) & 1u);
+    if (lane == 0) wsum[k][wid] = __popcll(bal[k]);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int k = 0; k < kPrepPer; ++k)
+      for (int w = 0; w < kT / 64; ++w) {
+        const int c = wsum[k][w];
+        wsum[k][w] = s;
+        s += c;
+      }
+    sbase = s ? atomicAdd(&d.st[fov].n_moving, s) : 0;
+  }
+  __syncthreads();
+  const unsigned long long lower = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int k = 0; k < kPrepPer; ++k)
+    if ((movbits >> k) & 1u)
+      d.act[(long long)fov * n + sbase + wsum[k][wid] + __popcll(bal[k] & lower)] =
+          (int)(q0 + k * kT + threadIdx.x);
 }
 
-__global__ __launch_bounds__(kT) void k_dyn_follow(int Ly, int Lx, int niter, DynBufs d) {
+// follow_flows: every moving pixel runs niter Euler steps of the map_coordinates update (fp64
+// bilinear expression of the fp32 field, rounded to fp32, fp32 add, clamp).  The update depends
+// on the position alone, so a pixel whose position does not change in a step sits on an exact
+// fixed point and keeps it for the remaining steps: it stops there and its final position is
+// bit-identical to the full loop (>= 99.9 % of the synthetic plates' pixels reach one within a
+// few hundred of the 1176 steps, 82 on average).  The steps run in rounds of K: round r takes
+// the pixels still moving after r rounds (positions carried in a compact item list), runs K
+// steps, writes the finished ones and appends the rest to the next round's list in block order
+// — so the 64 lanes of a wave stay spatial neighbours and their bilinear gathers share lines.
+struct FollowItem {
+  int q;
+  float py, px;
+  int pad;
+};
+
+__global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, int step0, int K,
+                                                   int from_act, const FollowItem* __restrict__ in,
+                                                   const int* __restrict__ in_cnt,
+                                                   FollowItem* __restrict__ out,
+                                                   int* __restrict__ out_cnt, DynBufs d) {
   const int fov = blockIdx.y;
-  const int t = blockIdx.x * kT + threadIdx.x;
-  const int n = Ly * Lx;
+  const long long n = (long long)Dy * Dx;
   const int n_moving = d.st[fov].n_moving;
   if (n_moving < 5) return;  // follow_flows returns inds=None -> no masks
-  if (t >= n_moving) return;
-  const int q = d.act[(long long)fov * n + t];  // a pixel with |dY| > 1e-3 (k_dyn_prep)
-  const float* I = d.dps + (long long)fov * 2 * n;
-  float py = (float)(q / Lx), px = (float)(q % Lx);
-  const float fLy = (float)(Ly - 1), fLx = (float)(Lx - 1);
-  for (int it = 0; it < niter; ++it) {
-    const int yi = (int)py, xi = (int)px;
-    const double yy = (double)py - (double)yi, xx = (double)px - (double)xi;
-    const int y0 = min(Ly - 1, max(0, yi)), x0 = min(Lx - 1, max(0, xi));
-    const int y1 = min(Ly - 1, y0 + 1), x1 = min(Lx - 1, x0 + 1);
-    float dv[2];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const float* Ic = I + (long long)c * n;
-      const double v = (double)Ic[y0 * Lx + x0] * (1.0 - yy) * (1.0 - xx) +
-                       (double)Ic[y0 * Lx + x1] * (1.0 - yy) * xx +
-                       (double)Ic[y1 * Lx + x0] * yy * (1.0 - xx) +
-                       (double)Ic[y1 * Lx + x1] * yy * xx;
-      dv[c] = (float)v;
+  const int n_in = from_act ? n_moving : in_cnt[fov];
+  const int steps = min(K, niter - step0);
+  const float2* __restrict__ I = d.dps + (long long)fov * n;
+  float2* __restrict__ P = d.p + (long long)fov * n;
+  const FollowItem* src = in + (long long)fov * n;
+  FollowItem* dst = out + (long long)fov * n;
+  const float fLy = (float)(Dy - 1), fLx = (float)(Dx - 1);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __shared__ int wsum[kT / 64];
+  __shared__ int sbase;
+  for (int i0 = blockIdx.x * kT; i0 < n_in; i0 += gridDim.x * kT) {  // block-uniform
+    const int i = i0 + threadIdx.x;
+    bool active = i < n_in;
+    int q = 0;
+    float py = 0.0f, px = 0.0f;
+    if (active) {
+      if (from_act) {
+        q = d.act[(long long)fov * n + i];
+        py = (float)(q / Dx);
+        px = (float)(q % Dx);
+      } else {
+        const FollowItem it = src[i];
+        q = it.q;
+        py = it.py;
+        px = it.px;
+      }
     }
-    py = fminf(fLy, fmaxf(0.0f, py + dv[0]));
-    px = fminf(fLx, fmaxf(0.0f, px + dv[1]));
+    bool done = !active;
+    for (int s = 0; s < steps; ++s) {
+      if (done) continue;
+      const int yi = (int)py, xi = (int)px;
+      const double yy = (double)py - (double)yi, xx = (double)px - (double)xi;
+      const int y0 = min(Dy - 1, max(0, yi)), x0 = min(Dx - 1, max(0, xi));
+      const int y1 = min(Dy - 1, y0 + 1), x1 = min(Dx - 1, x0 + 1);
+      const float2 a = I[(long long)y0 * Dx + x0], b = I[(long long)y0 * Dx + x1];
+      const float2 c = I[(long long)y1 * Dx + x0], e = I[(long long)y1 * Dx + x1];
+      const double vy = (double)a.x * (1.0 - yy) * (1.0 - xx) + (double)b.x * (1.0 - yy) * xx +
+                        (double)c.x * yy * (1.0 - xx) + (double)e.x * yy * xx;
+      const double vx = (double)a.y * (1.0 - yy) * (1.0 - xx) + (double)b.y * (1.0 - yy) * xx +
+                        (double)c.y * yy * (1.0 - xx) + (double)e.y * yy * xx;
+      const float ny = fminf(fLy, fmaxf(0.0f, py + (float)vy));
+      const float nx = fminf(fLx, fmaxf(0.0f, px + (float)vx));
+      if (ny == py && nx == px) done = true;  // exact fixed point
+      py = ny;
+      px = nx;
+    }
+    const bool last = step0 + steps >= niter;
+    if (active && (done || last)) P[q] = make_float2(py, px);
+    const bool carry = active && !done && !last;
+    const unsigned long long bal = __ballot(carry);
+    if (lane == 0) wsum[wid] = __popcll(bal);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int s = 0;
+      for (int w = 0; w < kT / 64; ++w) {
+        const int c = wsum[w];
+        wsum[w] = s;
+        s += c;
+      }
+      sbase = s ? atomicAdd(&out_cnt[fov], s) : 0;
+    }
+    __syncthreads();
+    if (carry) {
+      FollowItem it;
+      it.q = q;
+      it.py = py;
+      it.px = px;
+      it.pad = 0;
+      dst[sbase + wsum[wid] + __popcll(bal & ((1ull << lane) - 1ull))] = it;
+    }
+    __syncthreads();
   }
-  d.p[(long long)fov * 2 * n + q] = py;
-  d.p[(long long)fov * 2 * n + n + q] = px;
 }
 
-__global__ __launch_bounds__(kT) void k_dyn_hist(int Ly, int Lx, DynBufs d) {
+// histogram of final positions (get_masks: np.add.at(h, (p + rpad)), padded grid Dyh x Dxh).
+// Pixels that did not move sit at their own coordinate: one plain store per padded cell covers
+// them (and clears the rest); the moving pixels then add with wave-aggregated atomics (the
+// pixels of one cell mostly end in the same bin).
+__global__ __launch_bounds__(kT) void k_hist_init(int Dy, int Dx, DynBufs d) {
   const int fov = blockIdx.y;
-  const int q = blockIdx.x * kT + threadIdx.x;
-  const int n = Ly * Lx;
-  if (q >= n) return;
-  const int Lxh = Lx + 2 * kRpad, Lyh = Ly + 2 * kRpad;
-  const int iy = (int)d.p[(long long)fov * 2 * n + q] + kRpad;
-  const int ix = (int)d.p[(long long)fov * 2 * n + n + q] + kRpad;
-  atomicAdd(&d.h[(long long)fov * Lyh * Lxh + iy * Lxh + ix], 1);
+  const int Dxh = Dx + 2 * kRpad, Dyh = Dy + 2 * kRpad;
+  const long long nh = (long long)Dyh * Dxh;
+  const long long b = (long long)blockIdx.x * kT + threadIdx.x;
+  if (b >= nh) return;
+  const int y = (int)(b / Dxh) - kRpad, x = (int)(b % Dxh) - kRpad;
+  int v = 0;
+  if (y >= 0 && y < Dy && x >= 0 && x < Dx) v = d.mov[(long long)fov * Dy * Dx + (long long)y * Dx + x] ? 0 : 1;
+  d.h[(long long)fov * nh + b] = v;
+}
+
+__device__ __forceinline__ void agg_add(int* base, int key, bool valid) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long pend = __ballot(valid);
+  while (pend) {
+    const int leader = __ffsll((long long)pend) - 1;
+    const int k0 = __shfl(key, leader);
+    const unsigned long long m = __ballot(valid && key == k0);
+    if (lane == leader) atomicAdd(&base[k0], __popcll(m));
+    pend &= ~m;
+  }
+}
+
+__global__ __launch_bounds__(kT) void k_hist_moving(int Dy, int Dx, DynBufs d) {
+  const int fov = blockIdx.y;
+  const long long n = (long long)Dy * Dx;
+  const int i = blockIdx.x * kT + threadIdx.x;
+  const int n_moving = d.st[fov].n_moving;
+  if ((long long)blockIdx.x * kT >= n_moving) return;  // block-uniform
+  const int Dxh = Dx + 2 * kRpad;
+  const bool valid = i < n_moving;
+  int key = 0;
+  if (valid) {
+    const int q = d.act[(long long)fov * n + i];
+    // moving pixels of an FOV with < 5 of them never followed: their own coordinate
+    float2 pp = n_moving >= 5 ? d.p[(long long)fov * n + q] : make_float2((float)(q / Dx), (float)(q % Dx));
+    key = ((int)pp.x + kRpad) * Dxh + (int)pp.y + kRpad;
+  }
+  agg_add(d.h + (long long)fov * (Dy + 2 * kRpad) * Dxh, key, valid);
 }
 
 // seeds: h > 10 and h == 5x5 max (maximum_filter1d size 5 on both axes)
-__global__ __launch_bounds__(kT) void k_seed_flags(int Lyh, int Lxh, DynBufs d) {
+__global__ __launch_bounds__(kT) void k_seed_flags(int Dyh, int Dxh, DynBufs d) {
   const int fov = blockIdx.y;
-  const int q = blockIdx.x * kT + threadIdx.x;
-  if (q >= Lyh * Lxh) return;
-  const int* h = d.h + (long long)fov * Lyh * Lxh;
+  const long long nh = (long long)Dyh * Dxh;
+  const long long q = (long long)blockIdx.x * kT + threadIdx.x;
+  if (q >= nh) return;
+  const int* h = d.h + (long long)fov * nh;
   const int v = h[q];
   unsigned char f = 0;
   if (v > 10) {
-    const int y = q / Lxh, x = q - y * Lxh;
+    const int y = (int)(q / Dxh), x = (int)(q % Dxh);
     int mx = v;
     for (int dy = -2; dy <= 2; ++dy)
       for (int dx = -2; dx <= 2; ++dx) {
         int yy = y + dy, xx = x + dx;  // scipy 'reflect' boundary (never reached by seeds)
-        yy = yy < 0 ? -yy - 1 : (yy >= Lyh ? 2 * Lyh - yy - 1 : yy);
-        xx = xx < 0 ? -xx - 1 : (xx >= Lxh ? 2 * Lxh - xx - 1 : xx);
-        mx = max(mx, h[yy * Lxh + xx]);
+        yy = yy < 0 ? -yy - 1 : (yy >= Dyh ? 2 * Dyh - yy - 1 : yy);
+        xx = xx < 0 ? -xx - 1 : (xx >= Dxh ? 2 * Dxh - xx - 1 : xx);
+        mx = max(mx, h[(long long)yy * Dxh + xx]);
       }
     f = (v >= mx);
   }
-  // reuse the seed map M as the flag array until compaction
-  d.M[(long long)fov * Lyh * Lxh + q] = f;
+  d.sflag[(long long)fov * nh + q] = f;
 }
 
-// one block per FOV: row-major compaction of seed flags into the seed list; clears M
-__global__ __launch_bounds__(1024) void k_seed_compact(int Lyh, int Lxh, DynBufs d) {
+// ---- ordered compaction of byte flags: indices of the set flags in increasing order ---------
+// (tile counts -> per-FOV exclusive scan -> in-tile ranks).  Three launches; every block works
+// on one 8 KiB tile, so a 2080^2 FOV's flags spread over ~550 blocks instead of one.
+constexpr int kOcThreads = 256;
+constexpr int kOcPer = 32;                       // flags per thread (two 16-byte loads)
+constexpr int kOcTile = kOcThreads * kOcPer;     // 8192
+
+__device__ __forceinline__ int oc_load(const unsigned char* f, long long n, long long i0,
+                                       unsigned int* bits) {
+  // bit j of *bits = flag i0 + j (j < 32); returns the count
+  unsigned int b = 0;
+  if (i0 + kOcPer <= n && (((uintptr_t)(f + i0)) & 15u) == 0) {
+    const uint4* v = reinterpret_cast<const uint4*>(f + i0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint4 t = v[h];
+      const unsigned int w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int by = 0; by < 4; ++by)
+          b |= (((w[k] >> (8 * by)) & 0xffu) ? 1u : 0u) << (h * 16 + k * 4 + by);
+    }
+  } else {
+    for (int j = 0; j < kOcPer; ++j)
+      if (i0 + j < n && f[i0 + j]) b |= 1u << j;
+  }
+  *bits = b;
+  return __popc(b);
+}
+
+__global__ __launch_bounds__(kOcThreads) void k_oc_count(const unsigned char* __restrict__ flags,
+                                                         long long n, int ntile, int* __restrict__ tiles) {
+  const int fov = blockIdx.y, t = blockIdx.x;
+  const unsigned char* f = flags + (long long)fov * n;
+  unsigned int bits;
+  int c = oc_load(f, n, (long long)t * kOcTile + (long long)threadIdx.x * kOcPer, &bits);
+  c = wave_sum(c);
+  __shared__ int ws[kOcThreads / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int w = 0; w < kOcThreads / 64; ++w) s += ws[w];
+    tiles[(long long)fov * ntile + t] = s;
+  }
+}
+
+// one block per FOV: exclusive scan of the tile counts in place; total -> totals[fov]
+__global__ __launch_bounds__(1024) void k_oc_scan(int ntile, int* __restrict__ tiles,
+                                                  int* __restrict__ totals) {
   const int fov = blockIdx.x;
-  unsigned int* M = d.M + (long long)fov * Lyh * Lxh;
-  int* seeds = d.seeds + (long long)fov * kMaxSeeds;
+  int* t = tiles + (long long)fov * ntile;
   __shared__ int wsum[16];
   __shared__ int base;
   if (threadIdx.x == 0) base = 0;
   __syncthreads();
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int n = Lyh * Lxh;
-  for (int i0 = 0; i0 < n; i0 += blockDim.x) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int i0 = 0; i0 < ntile; i0 += 1024) {
     const int i = i0 + threadIdx.x;
-    const int f = (i < n) ? (int)M[i] : 0;
-    if (i < n) M[i] = 0u;
-    const unsigned long long b = __ballot(f);
-    const unsigned long long lower = lane ? (~0ull >> (64 - lane)) : 0ull;
-    if (lane == 0) wsum[wid] = __popcll(b);
+    const int v = i < ntile ? t[i] : 0;
+    int inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) wsum[wid] = inc;
     __syncthreads();
     int off = base;
     for (int w = 0; w < wid; ++w) off += wsum[w];
-    const int k = off + __popcll(b & lower);
-    if (f && k < kMaxSeeds) seeds[k] = i;
+    if (i < ntile) t[i] = off + inc - v;
     __syncthreads();
     if (threadIdx.x == 0) {
-      int tot = 0;
-      for (int w = 0; w < nw; ++w) tot += wsum[w];
-      base += tot;
+      int s = 0;
+      for (int w = 0; w < 16; ++w) s += wsum[w];
+      base += s;
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    d.st[fov].n_seeds = min(base, kMaxSeeds);
-    if (base > kMaxSeeds) d.st[fov].overflow = 1;
+  if (threadIdx.x == 0) totals[fov] = base;
+}
+
+__global__ __launch_bounds__(kOcThreads) void k_oc_emit(const unsigned char* __restrict__ flags,
+                                                        long long n, int ntile,
+                                                        const int* __restrict__ tiles, int cap,
+                                                        int* __restrict__ out, long long out_stride) {
+  const int fov = blockIdx.y, t = blockIdx.x;
+  const int off0 = tiles[(long long)fov * ntile + t];
+  if (off0 >= cap) return;
+  const unsigned char* f = flags + (long long)fov * n;
+  const long long i0 = (long long)t * kOcTile + (long long)threadIdx.x * kOcPer;
+  unsigned int bits;
+  const int c = oc_load(f, n, i0, &bits);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int inc = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  __shared__ int wsum[kOcThreads / 64];
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  int k = off0 + inc - c;
+  for (int w = 0; w < wid; ++w) k += wsum[w];
+  int* o = out + (long long)fov * out_stride;
+  while (bits) {
+    const int j = __ffs(bits) - 1;
+    bits &= bits - 1;
+    if (k < cap) o[k] = (int)(i0 + j);
+    ++k;
   }
 }
 
 // one wave per seed: geodesic 8-connected ball of radius 5 through h > 2 (get_masks expansion)
-__global__ __launch_bounds__(kT) void k_seed_expand(int Lyh, int Lxh, DynBufs d) {
+__global__ __launch_bounds__(kT) void k_seed_expand(int Dyh, int Dxh, DynBufs d) {
   const int fov = blockIdx.y;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   __shared__ unsigned char cur[kT / 64][2][169];
   const int ns = d.st[fov].n_seeds;
+  const long long nh = (long long)Dyh * Dxh;
   for (int kb = blockIdx.x * (kT / 64); kb < ns; kb += gridDim.x * (kT / 64)) {  // block-uniform
   const int k = kb + wid;
   const bool active = k < ns;
   const int s = active ? d.seeds[(long long)fov * kMaxSeeds + k] : 0;
-  const int sy = s / Lxh, sx = s - sy * Lxh;
-  const int* h = d.h + (long long)fov * Lyh * Lxh;
+  const int sy = s / Dxh, sx = s - sy * Dxh;
+  const int* h = d.h + (long long)fov * nh;
   bool good[3];
   for (int u = 0; u < 3; ++u) {
     const int c = lane + 64 * u;
     good[u] = false;
     if (c < 169 && active) {
       const int yy = sy - 6 + c / 13, xx = sx - 6 + c % 13;
-      good[u] = yy >= 0 && yy < Lyh && xx >= 0 && xx < Lxh && h[yy * Lxh + xx] > 2;
+      good[u] = yy >= 0 && yy < Dyh && xx >= 0 && xx < Dxh && h[(long long)yy * Dxh + xx] > 2;
       cur[wid][0][c] = (c == 84);  // the seed (window centre)
     }
   }
@@ -471,12 +707,12 @@ __global__ __launch_bounds__(kT) void k_seed_expand(int Lyh, int Lxh, DynBufs d)
     src ^= 1;
   }
   if (active) {
-    unsigned int* M = d.M + (long long)fov * Lyh * Lxh;
+    unsigned int* M = d.M + (long long)fov * nh;
     for (int u = 0; u < 3; ++u) {
       const int c = lane + 64 * u;
       if (c < 169 && cur[wid][src][c]) {
         const int yy = sy - 6 + c / 13, xx = sx - 6 + c % 13;
-        atomicMax(&M[yy * Lxh + xx], (unsigned int)(k + 1));  // later seeds win (M[pix[k]] = 1+k)
+        atomicMax(&M[(long long)yy * Dxh + xx], (unsigned int)(k + 1));  // later seeds win (M[pix[k]] = 1+k)
       }
     }
   }
@@ -484,73 +720,66 @@ __global__ __launch_bounds__(kT) void k_seed_expand(int Lyh, int Lxh, DynBufs d)
   }  // seed loop
 }
 
-__global__ __launch_bounds__(kT) void k_assign(int Ly, int Lx, DynBufs d) {
+// M0 = M[pflows]: every pixel's label at its final position; per label its pixel count and
+// first pixel, aggregated per wave (lanes are consecutive pixels, mostly of one label)
+__global__ __launch_bounds__(kT) void k_assign(int Dy, int Dx, DynBufs d) {
   const int fov = blockIdx.y;
+  const long long n = (long long)Dy * Dx;
   const int q = blockIdx.x * kT + threadIdx.x;
-  const int n = Ly * Lx;
-  if (q >= n) return;
-  const int Lxh = Lx + 2 * kRpad, Lyh = Ly + 2 * kRpad;
-  const int iy = (int)d.p[(long long)fov * 2 * n + q] + kRpad;
-  const int ix = (int)d.p[(long long)fov * 2 * n + n + q] + kRpad;
-  const int l = (int)d.M[(long long)fov * Lyh * Lxh + iy * Lxh + ix];
-  d.m0[(long long)fov * n + q] = l;
-  if (l) {
-    atomicAdd(&d.cnt[(long long)fov * (kMaxSeeds + 1) + l], 1);
-    atomicMin(&d.first[(long long)fov * (kMaxSeeds + 1) + l], q);
+  const int Dxh = Dx + 2 * kRpad;
+  int l = 0;
+  if (q < n) {
+    int iy = q / Dx, ix = q - iy * Dx;
+    if (d.mov[(long long)fov * n + q] && d.st[fov].n_moving >= 5) {
+      const float2 pp = d.p[(long long)fov * n + q];
+      iy = (int)pp.x;
+      ix = (int)pp.y;
+    }
+    l = (int)d.M[(long long)fov * (Dy + 2 * kRpad) * Dxh + (long long)(iy + kRpad) * Dxh + ix + kRpad];
+    d.m0[(long long)fov * n + q] = l;
+  }
+  const int lane = threadIdx.x & 63;
+  unsigned long long pend = __ballot(l != 0);
+  while (pend) {
+    const int leader = __ffsll((long long)pend) - 1;
+    const int l0 = __shfl(l, leader);
+    const unsigned long long m = __ballot(l == l0);
+    if (lane == leader) {
+      atomicAdd(&d.cnt[(long long)fov * (kMaxSeeds + 1) + l0], __popcll(m));
+      atomicMin(&d.first[(long long)fov * (kMaxSeeds + 1) + l0], q);  // lowest lane = first pixel
+    }
+    pend &= ~m;
   }
 }
 
-// big-mask removal + first-occurrence renumbering (fastremap.renumber)
-__global__ __launch_bounds__(kT) void k_relabel_mark(int Ly, int Lx, DynBufs d) {
+// big-mask removal (> 40 % of the image) + first-occurrence marks for fastremap.renumber
+__global__ __launch_bounds__(kT) void k_relabel_mark(int Dy, int Dx, DynBufs d) {
   const int fov = blockIdx.y;
   const int l = blockIdx.x * kT + threadIdx.x + 1;
   if (l > d.st[fov].n_seeds) return;
   const long long o = (long long)fov * (kMaxSeeds + 1) + l;
   const int c = d.cnt[o];
-  const double big = (double)Ly * (double)Lx * 0.4;
-  if (c > 0 && !((double)c > big)) d.mark[(long long)fov * Ly * Lx + d.first[o]] = 1;
+  const double big = (double)Dy * (double)Dx * 0.4;
+  if (c > 0 && !((double)c > big)) d.mark[(long long)fov * Dy * Dx + d.first[o]] = 1;
 }
 
-// one block per FOV: exclusive scan of marks over pixel order -> rank of each label
-__global__ __launch_bounds__(1024) void k_relabel_scan(int Ly, int Lx, DynBufs d) {
-  const int fov = blockIdx.x;
-  const int n = Ly * Lx;
-  unsigned char* mark = d.mark + (long long)fov * n;
-  __shared__ int wsum[16];
-  __shared__ int base;
-  if (threadIdx.x == 0) base = 0;
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  // pass: rank for each marked pixel, written back as rank+1 into `first`-indexed newlab via m0
-  for (int i0 = 0; i0 < n; i0 += blockDim.x) {
-    const int i = i0 + threadIdx.x;
-    const int f = (i < n) ? (int)mark[i] : 0;
-    const unsigned long long b = __ballot(f);
-    const unsigned long long lower = lane ? (~0ull >> (64 - lane)) : 0ull;
-    if (lane == 0) wsum[wid] = __popcll(b);
-    __syncthreads();
-    int off = base;
-    for (int w = 0; w < wid; ++w) off += wsum[w];
-    if (f) {
-      const int l = d.m0[(long long)fov * n + i];  // the label whose first pixel this is
-      d.newlab[(long long)fov * (kMaxSeeds + 1) + l] = off + __popcll(b & lower) + 1;
-      mark[i] = 0;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int tot = 0;
-      for (int w = 0; w < nw; ++w) tot += wsum[w];
-      base += tot;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) d.st[fov].n_masks = base;
-}
-
-__global__ __launch_bounds__(kT) void k_apply_newlab(int Ly, int Lx, DynBufs d) {
+// the j-th marked pixel (raster order) carries the label that becomes j + 1
+__global__ __launch_bounds__(kT) void k_relabel_apply(int Dy, int Dx, DynBufs d) {
   const int fov = blockIdx.y;
-  const int q = blockIdx.x * kT + threadIdx.x;
-  const int n = Ly * Lx;
+  const int n_masks = min(d.totals[fov], kMaxSeeds);
+  const long long n = (long long)Dy * Dx;
+  for (int j = blockIdx.x * kT + threadIdx.x; j < n_masks; j += gridDim.x * kT) {
+    const int pix = d.marklist[(long long)fov * kMaxSeeds + j];
+    d.mark[(long long)fov * n + pix] = 0;
+    d.newlab[(long long)fov * (kMaxSeeds + 1) + d.m0[(long long)fov * n + pix]] = j + 1;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.st[fov].n_masks = n_masks;
+}
+
+__global__ __launch_bounds__(kT) void k_apply_newlab(int Dy, int Dx, DynBufs d) {
+  const int fov = blockIdx.y;
+  const long long n = (long long)Dy * Dx;
+  const long long q = (long long)blockIdx.x * kT + threadIdx.x;
   if (q >= n) return;
   int* m = d.m0 + (long long)fov * n + q;
   const int l = *m;
@@ -558,41 +787,262 @@ __global__ __launch_bounds__(kT) void k_apply_newlab(int Ly, int Lx, DynBufs d) 
 }
 
 // ---------------------------------------------------------------------------------------------
-// flow-error filter: masks_to_flows (heat diffusion from the pixel nearest the median, fp64)
-// and per-mask mean squared difference against dP/5; one block per mask.
-constexpr int kFlowThreads = 256;
-constexpr int kFlowMaxCells = 2048;  // 2 x (ly+2)*(lx+2) doubles in LDS (48 KiB with the median
-                                     // histograms: 3 blocks per CU); larger masks: BIG pass
-constexpr int kFlowPP = 8;           // bbox pixels per thread kept in registers for the diffusion
+// flow-error filter (dynamics.remove_bad_flow_masks / metrics.flow_error): per mask the 2.x CPU
+// masks_to_flows heat diffusion from the pixel nearest the median, 2 * (ptp x + ptp y) Jacobi
+// iterations in fp64, normalised central differences, mean squared difference to dP / 5.
+//
+// k_flow_error_lds: one block per mask (dynamic queue over all masks of the batch).  The
+// diffusion grid T ((bh+2) x (bw+2) fp64, zero outside the mask, padded below to whole strips)
+// lives in LDS as ONE buffer: a work unit is 8 consecutive rows of one column; the thread that
+// owns it slides a 3 x 3 window down the unit (3 LDS reads per row instead of 9 per pixel),
+// keeps the 8 new values in registers and writes them back after a barrier.  Every thread owns
+// up to U units (consecutive threads: consecutive columns, so LDS accesses are conflict-free).
+// Sums keep the reference's term order; rows are computed unconditionally (compile-time loop)
+// and only mask cells are written.
+constexpr int kFeKS = 12;
+static_assert(kFeKS <= 32, "unit mask bits");
 
-// BIG = false: grid-stride over the masks that fit in LDS; BIG = true: one block per FOV walks
-// the oversize masks with a per-FOV global scratch (no two blocks share a scratch area).
-template <bool BIG>
-__global__ __launch_bounds__(kFlowThreads) void k_flow_error(
-    const int* __restrict__ m0, const float* __restrict__ yf, int Ly, int Lx, int max_label,
-    const cpx_object* __restrict__ objects, const cpx_fov_objects* __restrict__ hdr,
-    double thr, double* __restrict__ gscratch, long long gscratch_per_fov,
-    unsigned char* __restrict__ bad) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  int* rowc = reinterpret_cast<int*>(smem + (BIG ? 0 : sizeof(double) * 2 * kFlowMaxCells));
-  int* colc = rowc + 2048;
+__host__ __device__ inline bool fe_fits(int bh, int bw, int threads, int units, int cells) {
+  const int nsr = (bh + kFeKS - 1) / kFeKS;
+  return (long long)(bh + 2) * (bw + 2) <= cells && (long long)bw * nsr <= (long long)threads * units;
+}
+
+// exclusive prefix of the per-FOV object counts (queue item -> (fov, object))
+__global__ void k_obj_prefix(int B, const cpx_fov_objects* __restrict__ hdr, int* __restrict__ off) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    int s = 0;
+    for (int b = 0; b < B; ++b) {
+      off[b] = s;
+      s += hdr[b].n_objects;
+    }
+    off[B] = s;
+  }
+}
+
+template <int THREADS, int CELLS, int U>
+__global__ __launch_bounds__(THREADS) void k_flow_error_lds(
+    const int* __restrict__ m0, const float2* __restrict__ dpf, int Dy, int Dx, int B, int max_label,
+    const cpx_object* __restrict__ objects, const int* __restrict__ off, int* __restrict__ ctr,
+    int lo_threads, int lo_units, int lo_cells, double thr, unsigned char* __restrict__ bad) {
+  __shared__ double T[CELLS];
+  __shared__ double sred[THREADS / 64][2];
+  __shared__ unsigned long long sbest[THREADS / 64];
+  __shared__ double smed[2];
+  __shared__ int sitem;
+  const long long n = (long long)Dy * Dx;
+  const int total = off[B];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  while (true) {
+    if (tid == 0) sitem = atomicAdd(ctr, 1);
+    __syncthreads();
+    const int item = sitem;
+    __syncthreads();
+    if (item >= total) break;
+    int fov = 0;
+    while (fov + 1 < B && off[fov + 1] <= item) ++fov;
+    const int kobj = item - off[fov];
+    const cpx_object o = objects[(long long)fov * max_label + kobj];
+    const int L = o.label;
+    const int r0 = o.bbox[0], c0 = o.bbox[1];
+    const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
+    // block-uniform: objects of the smaller variant or of k_flow_error_big are skipped
+    if (!fe_fits(bh, bw, THREADS, U, CELLS)) continue;
+    if (lo_threads > 0 && fe_fits(bh, bw, lo_threads, lo_units, lo_cells)) continue;
+    const int nsr = (bh + kFeKS - 1) / kFeKS;
+    const int ly = bh + 2, lx = bw + 2;
+    const int nunits = bw * nsr;
+    const int* lab = m0 + (long long)fov * n;
+    // ---- medians of the pixel coordinates (row / column counts in the T area, as ints)
+    int* rowc = reinterpret_cast<int*>(T);
+    int* colc = rowc + bh;
+    for (int i = tid; i < bh + bw; i += THREADS) rowc[i] = 0;
+    __syncthreads();
+    const int nb = bh * bw;
+    for (int p = tid; p < nb; p += THREADS) {
+      const int rr = p / bw, cc = p - rr * bw;
+      if (lab[(long long)(r0 + rr) * Dx + c0 + cc] == L) {
+        atomicAdd(&rowc[rr], 1);
+        atomicAdd(&colc[cc], 1);
+      }
+    }
+    __syncthreads();
+    if (tid < 2) {
+      const int* hc = tid == 0 ? rowc : colc;
+      const int len = tid == 0 ? bh : bw;
+      const long long cntn = o.area;
+      const long long ka = (cntn - 1) / 2, kb = cntn / 2;
+      long long cum = 0;
+      int va = -1, vb = -1;
+      for (int i = 0; i < len; ++i) {
+        cum += hc[i];
+        if (va < 0 && cum > ka) va = i;
+        if (vb < 0 && cum > kb) { vb = i; break; }
+      }
+      smed[tid] = ((double)(va + 1) + (double)(vb + 1)) / 2.0;
+    }
+    __syncthreads();
+    // ---- argmin of (x-xmed)^2 + (y-ymed)^2, first in row-major order on ties
+    const double ymed = smed[0], xmed = smed[1];
+    unsigned long long best = ~0ull;
+    for (int p = tid; p < nb; p += THREADS) {
+      const int rr = p / bw, cc = p - rr * bw;
+      if (lab[(long long)(r0 + rr) * Dx + c0 + cc] != L) continue;
+      const double dy = (double)(rr + 1) - ymed, dx = (double)(cc + 1) - xmed;
+      const double dist = dx * dx + dy * dy;
+      // medians are multiples of 1/2, so 4*dist is an exact integer: order-preserving key
+      const unsigned long long key = ((unsigned long long)(dist * 4.0) << 32) | (unsigned int)p;
+      best = key < best ? key : best;
+    }
+    best = wave_min(best);
+    if (lane == 0) sbest[wid] = best;
+    __syncthreads();
+    unsigned long long bsel = sbest[0];
+    for (int w = 1; w < THREADS / 64; ++w) bsel = sbest[w] < bsel ? sbest[w] : bsel;
+    const int pbest = (int)(bsel & 0xffffffffu);
+    const int ym = pbest / bw + 1, xm = pbest % bw + 1;
+    const int niter = 2 * ((bw - 1) + (bh - 1));  // 2 * (ptp(x) + ptp(y))
+    // ---- this thread's units: column X, rows Y0 .. Y0 + 7
+    int ux[U], uy0[U], ujc[U];
+    unsigned int um[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      const int u = tid + i * THREADS;
+      um[i] = 0u;
+      ux[i] = 1;
+      uy0[i] = 1;
+      ujc[i] = -1;
+      if (u < nunits) {
+        const int X = u % bw + 1, Y0 = 1 + (u / bw) * kFeKS;
+        ux[i] = X;
+        uy0[i] = Y0;
+        unsigned int m = 0u;
+        for (int j = 0; j < kFeKS && Y0 + j <= bh; ++j)
+          if (lab[(long long)(r0 + Y0 - 1 + j) * Dx + c0 + X - 1] == L) m |= 1u << j;
+        um[i] = m;
+        if (X == xm && ym >= Y0 && ym < Y0 + kFeKS) ujc[i] = ym - Y0;
+      }
+    }
+    __syncthreads();  // rowc / colc / sbest reads done before T is cleared
+    for (int i = tid; i < ly * lx; i += THREADS) T[i] = 0.0;
+    __syncthreads();
+    if (tid == 0 && niter > 0) T[ym * lx + xm] = 1.0;  // the first iteration's T[centre] += 1
+    __syncthreads();
+    double nv[U][kFeKS];
+    for (int it = 0; it < niter; ++it) {
+#pragma unroll
+      for (int i = 0; i < U; ++i) {
+        if (!um[i]) continue;  // no mask cell in this unit (or no unit)
+        // opaque per-iteration base: stops the compiler from keeping every row address of
+        // every unit live across the iteration loop (it hoisted ~90 of them and spilled)
+        int tb = (uy0[i] - 1) * lx + ux[i];
+        int lim = ly - uy0[i];
+        asm volatile("" : "+v"(tb), "+v"(lim));
+        const double* Tu = T + tb;
+        double ul = Tu[-1], uc = Tu[0], ur = Tu[1];
+        double cl = Tu[lx - 1], cc = Tu[lx], cr = Tu[lx + 1];
+        const double* T2 = Tu + min(2, lim) * lx;
+        double dl = T2[-1], dc = T2[0], dr = T2[1];
+#pragma unroll
+        for (int j = 0; j < kFeKS; ++j) {
+          // the next row's loads are issued before this row's sum, which hides their latency;
+          // the scheduling barrier keeps the compiler from hoisting more rows (register budget)
+          // rows past the last strip's object rows read the zero border row (clamped): their
+          // sums are never written
+          double nl = 0.0, nc = 0.0, nr = 0.0;
+          if (j + 1 < kFeKS) {
+            const double* Tn = Tu + min(j + 3, lim) * lx;
+            nl = Tn[-1];
+            nc = Tn[0];
+            nr = Tn[1];
+          }
+          nv[i][j] = 1 / 9. * (cc + uc + dc + cl + cr + ul + ur + dl + dr);
+          ul = cl; uc = cc; ur = cr;
+          cl = dl; cc = dc; cr = dr;
+          dl = nl; dc = nc; dr = nr;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      __syncthreads();
+      const bool last = it + 1 == niter;
+#pragma unroll
+      for (int i = 0; i < U; ++i) {
+        if (!um[i]) continue;
+        int wb = uy0[i] * lx + ux[i];
+        asm volatile("" : "+v"(wb));
+        double* Tw = T + wb;
+#pragma unroll
+        for (int j = 0; j < kFeKS; ++j)
+          if ((um[i] >> j) & 1u) Tw[j * lx] = (j == ujc[i] && !last) ? nv[i][j] + 1.0 : nv[i][j];
+      }
+      __syncthreads();
+    }
+    // ---- gradients, normalisation, error vs dP/5
+    const float2* F = dpf + (long long)fov * n;
+    double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      for (int j = 0; j < kFeKS; ++j) {
+        if (!((um[i] >> j) & 1u)) continue;
+        const int Y = uy0[i] + j, X = ux[i];
+        const double dy = T[(Y + 1) * lx + X] - T[(Y - 1) * lx + X];
+        const double dx = T[Y * lx + X + 1] - T[Y * lx + X - 1];
+        const double nrm = 1e-20 + sqrt(dy * dy + dx * dx);
+        const double my = dy / nrm, mx = dx / nrm;
+        const float2 f = F[(long long)(r0 + Y - 1) * Dx + c0 + X - 1];
+        const double ty = my - (double)(f.x / 5.0f);
+        const double tx = mx - (double)(f.y / 5.0f);
+        e0 += ty * ty;
+        e1 += tx * tx;
+      }
+    }
+    e0 = wave_sum(e0);
+    e1 = wave_sum(e1);
+    if (lane == 0) {
+      sred[wid][0] = e0;
+      sred[wid][1] = e1;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int w = 0; w < THREADS / 64; ++w) {
+        s0 += sred[w][0];
+        s1 += sred[w][1];
+      }
+      const double err = 0.0 + s0 / (double)o.area + s1 / (double)o.area;
+      bad[(long long)fov * (max_label + 1) + L] = err > thr ? 1 : 0;
+    }
+    __syncthreads();
+  }
+}
+
+// masks too large for either LDS kernel: one block per FOV walks them with a two-buffer Jacobi
+// in a per-FOV global scratch (no two blocks share a scratch area)
+constexpr int kFlowThreads = 256;
+
+__global__ __launch_bounds__(kFlowThreads) void k_flow_error_big(
+    const int* __restrict__ m0, const float2* __restrict__ dpf, int Dy, int Dx, int max_label,
+    const cpx_object* __restrict__ objects, const cpx_fov_objects* __restrict__ hdr, int lds_threads,
+    int lds_units, int lds_cells, double thr, double* __restrict__ gscratch,
+    long long gscratch_per_fov, unsigned char* __restrict__ bad) {
+  __shared__ int rowc[2048];
+  __shared__ int colc[2048];
   __shared__ double sred[kFlowThreads / 64][2];
   __shared__ unsigned long long sbest[kFlowThreads / 64];
   __shared__ double smed[2];
-  const int fov = blockIdx.y;
-  const int n = Ly * Lx;
+  const int fov = blockIdx.x;
+  const long long n = (long long)Dy * Dx;
   const int* lab = m0 + (long long)fov * n;
   const int nobj = hdr[fov].n_objects;
-  for (int k = blockIdx.x; k < nobj; k += gridDim.x) {
+  for (int k = 0; k < nobj; ++k) {
   const cpx_object o = objects[(long long)fov * max_label + k];
   const int L = o.label;
   const int r0 = o.bbox[0], c0 = o.bbox[1];
   const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
+  if (fe_fits(bh, bw, lds_threads, lds_units, lds_cells)) continue;  // block-uniform: an LDS kernel's
   const int ly = bh + 2, lx = bw + 2;
   const int ncell = ly * lx;
-  if ((ncell > kFlowMaxCells) != BIG) continue;  // block-uniform
-  double* T0 = BIG ? gscratch + (long long)fov * gscratch_per_fov : reinterpret_cast<double*>(smem);
-  double* T1 = T0 + (BIG ? ncell : kFlowMaxCells);
+  double* T0 = gscratch + (long long)fov * gscratch_per_fov;
+  double* T1 = T0 + ncell;
   for (int i = threadIdx.x; i < ncell; i += kFlowThreads) {
     T0[i] = 0.0;
     T1[i] = 0.0;
@@ -605,13 +1055,12 @@ __global__ __launch_bounds__(kFlowThreads) void k_flow_error(
   const int nb = bh * bw;
   for (int p = threadIdx.x; p < nb; p += kFlowThreads) {
     const int rr = p / bw, cc = p - rr * bw;
-    if (lab[(r0 + rr) * Lx + c0 + cc] == L) {
+    if (lab[(long long)(r0 + rr) * Dx + c0 + cc] == L) {
       atomicAdd(&rowc[min(rr, 2047)], 1);
       atomicAdd(&colc[min(cc, 2047)], 1);
     }
   }
   __syncthreads();
-  // medians of y and x (np.median of the pixel coordinates, local +1 offset)
   if (threadIdx.x < 2) {
     const int* hc = threadIdx.x == 0 ? rowc : colc;
     const int len = min(threadIdx.x == 0 ? bh : bw, 2048);
@@ -628,14 +1077,12 @@ __global__ __launch_bounds__(kFlowThreads) void k_flow_error(
   }
   __syncthreads();
   const double ymed = smed[0], xmed = smed[1];
-  // argmin of (x-xmed)^2 + (y-ymed)^2 over mask pixels, first in row-major order on ties
   unsigned long long best = ~0ull;
   for (int p = threadIdx.x; p < nb; p += kFlowThreads) {
     const int rr = p / bw, cc = p - rr * bw;
-    if (lab[(r0 + rr) * Lx + c0 + cc] != L) continue;
+    if (lab[(long long)(r0 + rr) * Dx + c0 + cc] != L) continue;
     const double dy = (double)(rr + 1) - ymed, dx = (double)(cc + 1) - xmed;
     const double dist = dx * dx + dy * dy;
-    // medians are multiples of 1/2, so 4*dist is an exact integer: order-preserving key
     const unsigned long long key = ((unsigned long long)(dist * 4.0) << 32) | (unsigned int)p;
     best = key < best ? key : best;
   }
@@ -646,65 +1093,40 @@ __global__ __launch_bounds__(kFlowThreads) void k_flow_error(
   for (int w = 1; w < kFlowThreads / 64; ++w) bsel = sbest[w] < bsel ? sbest[w] : bsel;
   const int pbest = (int)(bsel & 0xffffffffu);
   const int ym = pbest / bw + 1, xm = pbest % bw + 1;
-  const int niter = 2 * ((bw - 1) + (bh - 1));  // 2 * (ptp(x) + ptp(y))
-  // Jacobi heat diffusion over mask pixels (T outside the mask stays 0).  Objects of at most
-  // kFlowPP pixels per thread keep their in-mask cell indices in registers, so the iterations
-  // touch LDS only (no label re-reads per iteration).
-  const bool small = nb <= kFlowPP * kFlowThreads;  // block-uniform
-  int myi[kFlowPP];
-#pragma unroll
-  for (int j = 0; j < kFlowPP; ++j) {
-    const int p = threadIdx.x + j * kFlowThreads;
-    myi[j] = -1;
-    if (small && p < nb) {
-      const int rr = p / bw, cc = p - rr * bw;
-      if (lab[(r0 + rr) * Lx + c0 + cc] == L) myi[j] = (rr + 1) * lx + cc + 1;
-    }
-  }
+  const int niter = 2 * ((bw - 1) + (bh - 1));
   double* Tc = T0;
   double* Tn = T1;
   for (int it = 0; it < niter; ++it) {
     if (threadIdx.x == 0) Tc[ym * lx + xm] += 1.0;
     __syncthreads();
-    if (small) {
-#pragma unroll
-      for (int j = 0; j < kFlowPP; ++j) {
-        const int i = myi[j];
-        if (i < 0) continue;
-        Tn[i] = 1 / 9. * (Tc[i] + Tc[i - lx] + Tc[i + lx] + Tc[i - 1] + Tc[i + 1] + Tc[i - lx - 1] +
-                          Tc[i - lx + 1] + Tc[i + lx - 1] + Tc[i + lx + 1]);
-      }
-    } else {
-      for (int p = threadIdx.x; p < nb; p += kFlowThreads) {
-        const int rr = p / bw, cc = p - rr * bw;
-        if (lab[(r0 + rr) * Lx + c0 + cc] != L) continue;
-        const int y = rr + 1, x = cc + 1;
-        Tn[y * lx + x] = 1 / 9. * (Tc[y * lx + x] + Tc[(y - 1) * lx + x] + Tc[(y + 1) * lx + x] +
-                                   Tc[y * lx + x - 1] + Tc[y * lx + x + 1] + Tc[(y - 1) * lx + x - 1] +
-                                   Tc[(y - 1) * lx + x + 1] + Tc[(y + 1) * lx + x - 1] +
-                                   Tc[(y + 1) * lx + x + 1]);
-      }
+    for (int p = threadIdx.x; p < nb; p += kFlowThreads) {
+      const int rr = p / bw, cc = p - rr * bw;
+      if (lab[(long long)(r0 + rr) * Dx + c0 + cc] != L) continue;
+      const int y = rr + 1, x = cc + 1;
+      Tn[y * lx + x] = 1 / 9. * (Tc[y * lx + x] + Tc[(y - 1) * lx + x] + Tc[(y + 1) * lx + x] +
+                                 Tc[y * lx + x - 1] + Tc[y * lx + x + 1] + Tc[(y - 1) * lx + x - 1] +
+                                 Tc[(y - 1) * lx + x + 1] + Tc[(y + 1) * lx + x - 1] +
+                                 Tc[(y + 1) * lx + x + 1]);
     }
     __syncthreads();
     double* t = Tc;
     Tc = Tn;
     Tn = t;
   }
-  // gradients, normalisation, error vs dP/5
-  const float* dY = yf + (long long)fov * 3 * n;
-  const float* dX = dY + n;
+  const float2* F = dpf + (long long)fov * n;
   double e0 = 0.0, e1 = 0.0;
   for (int p = threadIdx.x; p < nb; p += kFlowThreads) {
     const int rr = p / bw, cc = p - rr * bw;
     const int gy = r0 + rr, gx = c0 + cc;
-    if (lab[gy * Lx + gx] != L) continue;
+    if (lab[(long long)gy * Dx + gx] != L) continue;
     const int y = rr + 1, x = cc + 1;
     const double dy = Tc[(y + 1) * lx + x] - Tc[(y - 1) * lx + x];
     const double dx = Tc[y * lx + x + 1] - Tc[y * lx + x - 1];
     const double nrm = 1e-20 + sqrt(dy * dy + dx * dx);
     const double my = dy / nrm, mx = dx / nrm;
-    const double ty = my - (double)(dY[gy * Lx + gx] / 5.0f);
-    const double tx = mx - (double)(dX[gy * Lx + gx] / 5.0f);
+    const float2 f = F[(long long)gy * Dx + gx];
+    const double ty = my - (double)(f.x / 5.0f);
+    const double tx = mx - (double)(f.y / 5.0f);
     e0 += ty * ty;
     e1 += tx * tx;
   }
@@ -728,11 +1150,11 @@ __global__ __launch_bounds__(kFlowThreads) void k_flow_error(
   }  // object loop
 }
 
-__global__ __launch_bounds__(kT) void k_apply_bad(int n, int max_label,
+__global__ __launch_bounds__(kT) void k_apply_bad(long long n, int max_label,
                                                   const unsigned char* __restrict__ bad,
                                                   int* __restrict__ m0) {
   const int fov = blockIdx.y;
-  const int q = blockIdx.x * kT + threadIdx.x;
+  const long long q = (long long)blockIdx.x * kT + threadIdx.x;
   if (q >= n) return;
   int* m = m0 + (long long)fov * n + q;
   const int l = *m;
@@ -935,7 +1357,8 @@ __global__ __launch_bounds__(kT) void k_fill_apply(int* __restrict__ labels, lon
 }
 
 void axis_coeffs(int n_src, int n_dst, int* i0, int* i1, float* w) {
-  const double scale = (double)n_src / (double)n_dst;
+  // cv2.resize INTER_LINEAR: scale = 1 / (dst / src), fx = (float)((d + 0.5) * scale - 0.5)
+  const double scale = 1.0 / ((double)n_dst / (double)n_src);
   for (int d = 0; d < n_dst; ++d) {
     float f = (float)((d + 0.5) * scale - 0.5);
     int s = (int)floorf(f);
@@ -954,15 +1377,17 @@ void axis_coeffs(int n_src, int n_dst, int* i0, int* i1, float* w) {
   }
 }
 
-// host-side coefficient tables (bilinear for H,W -> Ly,Lx and nearest for Ly,Lx -> H,W)
+// host-side coefficient tables: bilinear H,W -> Ly,Lx (network input), bilinear Ly,Lx -> H,W
+// (resample=True flows) and nearest Ly,Lx -> H,W (resample=False masks)
 struct SegTabs {
   AxisTab ty, tx;
+  AxisTab uy, ux;
   const int* ynear;
   const int* xnear;
 };
 
 int seg_tables(cpx_ctx* ctx, int H, int W, int Ly, int Lx, SegTabs& t) {
-  const size_t words = (size_t)3 * Ly + 3 * Lx + H + W;
+  const size_t words = (size_t)3 * Ly + 3 * Lx + H + W + 3 * (size_t)H + 3 * (size_t)W;
   void* buf = cpx_ws(ctx, WS_SEG_TAB, words * 4 + 256);
   if (!buf) return CPX_ERR_OOM;
   int* base = (int*)buf;
@@ -974,7 +1399,14 @@ int seg_tables(cpx_ctx* ctx, int H, int W, int Ly, int Lx, SegTabs& t) {
   t.tx.w = (const float*)(base + 3 * Ly + 2 * Lx);
   t.ynear = base + 3 * Ly + 3 * Lx;
   t.xnear = base + 3 * Ly + 3 * Lx + H;
-  const int key[6] = {H, W, Ly, Lx, 1, 0};
+  int* up = base + 3 * Ly + 3 * Lx + H + W;
+  t.uy.i0 = up;
+  t.uy.i1 = up + H;
+  t.uy.w = (const float*)(up + 2 * H);
+  t.ux.i0 = up + 3 * H;
+  t.ux.i1 = up + 3 * H + W;
+  t.ux.w = (const float*)(up + 3 * H + 2 * W);
+  const int key[6] = {H, W, Ly, Lx, 2, 0};
   bool same = ctx->seg_tab == buf;
   for (int i = 0; i < 6; ++i) same = same && ctx->seg_key[i] == key[i];
   if (same) return CPX_OK;
@@ -984,6 +1416,9 @@ int seg_tables(cpx_ctx* ctx, int H, int W, int Ly, int Lx, SegTabs& t) {
   const double ify = 1.0 / ((double)H / (double)Ly), ifx = 1.0 / ((double)W / (double)Lx);
   for (int y = 0; y < H; ++y) h[3 * Ly + 3 * Lx + y] = std::min((int)floor(y * ify), Ly - 1);
   for (int x = 0; x < W; ++x) h[3 * Ly + 3 * Lx + H + x] = std::min((int)floor(x * ifx), Lx - 1);
+  const size_t u = (size_t)3 * Ly + 3 * Lx + H + W;
+  axis_coeffs(Ly, H, &h[u], &h[u + H], (float*)&h[u + 2 * H]);
+  axis_coeffs(Lx, W, &h[u + 3 * H], &h[u + 3 * H + W], (float*)&h[u + 3 * H + 2 * W]);
   CPX_CHECK_HIP(hipMemcpyAsync(buf, h.data(), words * 4, hipMemcpyHostToDevice, ctx->stream));
   CPX_CHECK_HIP(hipStreamSynchronize(ctx->stream));
   for (int i = 0; i < 6; ++i) ctx->seg_key[i] = key[i];
@@ -1058,64 +1493,136 @@ extern "C" int cpx_seg_average(cpx_ctx* ctx, const void* net_dev, int layout, in
   return CPX_OK;
 }
 
+// ordered compaction launches (flags [B][n] bytes -> out [B][out_stride] indices, totals [B])
+static int ordered_compact(cpx_ctx* ctx, const unsigned char* flags, long long n, int B, int* tiles,
+                           int* totals, int cap, int* out, long long out_stride) {
+  const int ntile = cpx_div_up(n, kOcTile);
+  hipLaunchKernelGGL(k_oc_count, dim3(ntile, B), dim3(kOcThreads), 0, ctx->stream, flags, n, ntile, tiles);
+  hipLaunchKernelGGL(k_oc_scan, dim3(B), dim3(1024), 0, ctx->stream, ntile, tiles, totals);
+  hipLaunchKernelGGL(k_oc_emit, dim3(ntile, B), dim3(kOcThreads), 0, ctx->stream, flags, n, ntile,
+                     (const int*)tiles, cap, out, out_stride);
+  CPX_CHECK_LAUNCH("ordered_compact");
+  return CPX_OK;
+}
+
+__global__ void k_seed_count(int B, const int* __restrict__ totals, cpx_seg_stats* __restrict__ st) {
+  const int fov = blockIdx.x * blockDim.x + threadIdx.x;
+  if (fov >= B) return;
+  const int t = totals[fov];
+  st[fov].n_seeds = min(t, kMaxSeeds);
+  if (t > kMaxSeeds) st[fov].overflow = 1;
+}
+
+constexpr int kFeSmallThreads = 256, kFeSmallCells = 5000;    // 40 KiB: 4 blocks per CU
+constexpr int kFeLargeThreads = 1024, kFeLargeCells = 20224;  // 158 KiB: 1 block per CU
+constexpr int kFeU = 2;                                        // 12-row units per thread
+
 extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx_seg_geom* geom,
                              int H, int W, int niter, double flow_threshold, int min_size,
-                             int max_objects, int32_t* labels_dev, cpx_seg_stats* stats_dev) {
+                             int max_objects, int resample, int32_t* labels_dev,
+                             cpx_seg_stats* stats_dev) {
   CPX_REQUIRE(ctx && yf_dev && labels_dev && stats_dev, CPX_ERR_ARG, "cpx_seg_masks: null argument");
   CPX_REQUIRE(geom_ok(geom), CPX_ERR_ARG, "cpx_seg_masks: bad geometry");
-  CPX_REQUIRE(B > 0 && B <= 65535 && H > 0 && W > 0 && niter >= 0 && max_objects > 0, CPX_ERR_ARG,
-              "cpx_seg_masks: bad sizes");
+  CPX_REQUIRE(B > 0 && B <= 65535 && H > 0 && W > 0 && niter >= 0 && max_objects > 0 &&
+                  (long long)(H + 2 * kRpad) * (W + 2 * kRpad) < (1LL << 31),
+              CPX_ERR_ARG, "cpx_seg_masks: bad sizes");
   const int Ly = geom->Ly, Lx = geom->Lx;
-  const int Lyh = Ly + 2 * kRpad, Lxh = Lx + 2 * kRpad;
-  const long long n = (long long)Ly * Lx, nh = (long long)Lyh * Lxh;
+  const int Dy = resample ? H : Ly, Dx = resample ? W : Lx;  // dynamics resolution
+  const int Dyh = Dy + 2 * kRpad, Dxh = Dx + 2 * kRpad;
+  const long long n = (long long)Dy * Dx, nh = (long long)Dyh * Dxh;
   SegTabs tabs;
   int rc = seg_tables(ctx, H, W, Ly, Lx, tabs);
   if (rc) return rc;
   // ---- workspace carve (WS_SEG_DYN)
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-  const size_t sz_dps = al(sizeof(float) * B * 2 * n), sz_p = sz_dps;
-  const size_t sz_h = al(sizeof(int) * B * nh), sz_M = sz_h;
-  const size_t sz_m0 = al(sizeof(int) * B * n);
+  const int ntile = cpx_div_up(std::max(n, nh), kOcTile);
+  const size_t sz_f2 = al(sizeof(float2) * B * n);
+  const size_t sz_b = al((size_t)B * n);
+  const size_t sz_h = al(sizeof(int) * B * nh), sz_hb = al((size_t)B * nh);
+  const size_t sz_m0 = resample ? 0 : al(sizeof(int) * B * n);
   const size_t sz_seeds = al(sizeof(int) * (size_t)B * kMaxSeeds);
   const size_t sz_cnt = al(sizeof(int) * (size_t)B * (kMaxSeeds + 1));
-  const size_t sz_mark = al((size_t)B * n);
   const size_t sz_act = al(sizeof(int) * B * n);
-  const size_t total = sz_dps + sz_p + sz_h + sz_M + sz_m0 + sz_seeds + 3 * sz_cnt + sz_mark + sz_act;
+  const size_t sz_small = al(sizeof(int) * (size_t)B);
+  const int rounds = 24 + cpx_div_up(std::max(0, niter - 384), 128) + 2;
+  const size_t sz_fcnt = al(sizeof(int) * (size_t)B * (rounds + 1));
+  const size_t sz_items = al((size_t)16 * B * n);
+  const size_t sz_tiles = al(sizeof(int) * (size_t)B * ntile);
+  const size_t total = 3 * sz_f2 + 2 * sz_b + 2 * sz_h + sz_hb + sz_m0 + 2 * sz_seeds + 3 * sz_cnt +
+                       sz_act + sz_small + sz_tiles + sz_fcnt + 2 * sz_items;
   unsigned char* w = (unsigned char*)cpx_ws(ctx, WS_SEG_DYN, total);
   if (!w) return CPX_ERR_OOM;
   DynBufs d;
-  d.dps = (float*)w; w += sz_dps;
-  d.p = (float*)w; w += sz_p;
+  d.dps = (float2*)w; w += sz_f2;
+  d.dpf = (float2*)w; w += sz_f2;
+  d.p = (float2*)w; w += sz_f2;
+  d.mov = w; w += sz_b;
+  d.mark = w; w += sz_b;
   d.h = (int*)w; w += sz_h;
-  d.M = (unsigned int*)w; w += sz_M;
-  d.m0 = (int*)w; w += sz_m0;
+  d.M = (unsigned int*)w; w += sz_h;
+  d.sflag = w; w += sz_hb;
+  d.m0 = resample ? labels_dev : (int*)w; w += sz_m0;
   d.seeds = (int*)w; w += sz_seeds;
+  d.marklist = (int*)w; w += sz_seeds;
   d.cnt = (int*)w; w += sz_cnt;
   d.first = (int*)w; w += sz_cnt;
   d.newlab = (int*)w; w += sz_cnt;
-  d.mark = (unsigned char*)w; w += sz_mark;
   d.act = (int*)w; w += sz_act;
+  d.fcnt = (int*)w; w += sz_fcnt;
+  d.fitems0 = w; w += sz_items;
+  d.fitems1 = w; w += sz_items;
+  d.totals = (int*)w; w += sz_small;
+  d.tiles = (int*)w; w += sz_tiles;
   d.st = stats_dev;
   CPX_CHECK_HIP(hipMemsetAsync(stats_dev, 0, sizeof(cpx_seg_stats) * B, ctx->stream));
-  CPX_CHECK_HIP(hipMemsetAsync(d.h, 0, sz_h, ctx->stream));
+  CPX_CHECK_HIP(hipMemsetAsync(d.M, 0, sz_h, ctx->stream));
+  CPX_CHECK_HIP(hipMemsetAsync(d.mark, 0, sz_b, ctx->stream));
   CPX_CHECK_HIP(hipMemsetAsync(d.cnt, 0, sz_cnt, ctx->stream));
   CPX_CHECK_HIP(hipMemsetAsync(d.first, 0x7f, sz_cnt, ctx->stream));
   CPX_CHECK_HIP(hipMemsetAsync(d.newlab, 0, sz_cnt, ctx->stream));
-  CPX_CHECK_HIP(hipMemsetAsync(d.mark, 0, sz_mark, ctx->stream));
+  CPX_CHECK_HIP(hipMemsetAsync(d.fcnt, 0, sz_fcnt, ctx->stream));
   const dim3 gp(cpx_div_up(n, kT), B), gh(cpx_div_up(nh, kT), B);
-  hipLaunchKernelGGL(k_dyn_prep, gp, dim3(kT), 0, ctx->stream, yf_dev, Ly, Lx, d);
-  hipLaunchKernelGGL(k_dyn_follow, gp, dim3(kT), 0, ctx->stream, Ly, Lx, niter, d);
-  hipLaunchKernelGGL(k_dyn_hist, gp, dim3(kT), 0, ctx->stream, Ly, Lx, d);
-  hipLaunchKernelGGL(k_seed_flags, gh, dim3(kT), 0, ctx->stream, Lyh, Lxh, d);
-  hipLaunchKernelGGL(k_seed_compact, dim3(B), dim3(1024), 0, ctx->stream, Lyh, Lxh, d);
+  const dim3 gprep(cpx_div_up(n, (long long)kT * kPrepPer), B);
+  if (resample)
+    hipLaunchKernelGGL(k_dyn_prep<true>, gprep, dim3(kT), 0, ctx->stream, yf_dev, Ly, Lx, Dy, Dx,
+                       tabs.uy, tabs.ux, d);
+  else
+    hipLaunchKernelGGL(k_dyn_prep<false>, gprep, dim3(kT), 0, ctx->stream, yf_dev, Ly, Lx, Dy, Dx,
+                       tabs.uy, tabs.ux, d);
+  // follow rounds: K = 16 steps while most pixels still move, then 128 for the long tail
+  const int fblk = std::max(1, std::min(cpx_div_up(n, kT), (16 * ctx->n_cu + B - 1) / B));
+  {
+    int step = 0, r = 0;
+    do {  // at least one round: with niter = 0 it only records the start positions
+      const int K = step < 384 ? 16 : 128;
+      const FollowItem* in = (const FollowItem*)(r & 1 ? d.fitems1 : d.fitems0);
+      FollowItem* out = (FollowItem*)(r & 1 ? d.fitems0 : d.fitems1);
+      hipLaunchKernelGGL(k_dyn_follow, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step,
+                         K, r == 0 ? 1 : 0, in, (const int*)(d.fcnt + (size_t)B * r), out,
+                         d.fcnt + (size_t)B * (r + 1), d);
+      step += K;
+      ++r;
+    } while (step < niter);
+  }
+  hipLaunchKernelGGL(k_hist_init, gh, dim3(kT), 0, ctx->stream, Dy, Dx, d);
+  hipLaunchKernelGGL(k_hist_moving, gp, dim3(kT), 0, ctx->stream, Dy, Dx, d);
+  hipLaunchKernelGGL(k_seed_flags, gh, dim3(kT), 0, ctx->stream, Dyh, Dxh, d);
+  CPX_CHECK_LAUNCH("cpx_seg_masks follow");
+  rc = ordered_compact(ctx, d.sflag, nh, B, d.tiles, d.totals, kMaxSeeds, d.seeds, kMaxSeeds);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_seed_count, dim3(cpx_div_up(B, 256)), dim3(256), 0, ctx->stream, B,
+                     (const int*)d.totals, stats_dev);
   hipLaunchKernelGGL(k_seed_expand, dim3(std::max(1, (4 * ctx->n_cu + B - 1) / B), B), dim3(kT), 0,
-                     ctx->stream, Lyh, Lxh, d);
-  hipLaunchKernelGGL(k_assign, gp, dim3(kT), 0, ctx->stream, Ly, Lx, d);
-  hipLaunchKernelGGL(k_relabel_mark, dim3(cpx_div_up(kMaxSeeds, kT), B), dim3(kT), 0, ctx->stream, Ly, Lx, d);
-  hipLaunchKernelGGL(k_relabel_scan, dim3(B), dim3(1024), 0, ctx->stream, Ly, Lx, d);
-  hipLaunchKernelGGL(k_apply_newlab, gp, dim3(kT), 0, ctx->stream, Ly, Lx, d);
-  CPX_CHECK_LAUNCH("cpx_seg_masks dynamics");
-  // ---- object workspaces (WS_SEG_OBJ): net-res and full-res object tables share it
+                     ctx->stream, Dyh, Dxh, d);
+  hipLaunchKernelGGL(k_assign, gp, dim3(kT), 0, ctx->stream, Dy, Dx, d);
+  hipLaunchKernelGGL(k_relabel_mark, dim3(cpx_div_up(kMaxSeeds, kT), B), dim3(kT), 0, ctx->stream, Dy, Dx, d);
+  CPX_CHECK_LAUNCH("cpx_seg_masks seeds");
+  rc = ordered_compact(ctx, d.mark, n, B, d.tiles, d.totals, kMaxSeeds, d.marklist, kMaxSeeds);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_relabel_apply, dim3(4, B), dim3(kT), 0, ctx->stream, Dy, Dx, d);
+  hipLaunchKernelGGL(k_apply_newlab, gp, dim3(kT), 0, ctx->stream, Dy, Dx, d);
+  CPX_CHECK_LAUNCH("cpx_seg_masks relabel");
+  // ---- object workspaces (WS_SEG_OBJ): the flow-error and fill-holes object tables share it
   const int ML = max_objects;
   const size_t sz_lst = al(sizeof(cpx_label_stats) * (size_t)B * (ML + 1));
   const size_t sz_obj = al(sizeof(cpx_object) * (size_t)B * ML);
@@ -1124,10 +1631,11 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   const size_t sz_l2i = al(sizeof(int) * (size_t)B * (ML + 1));
   const size_t sz_abs = al(sizeof(int) * (size_t)B * ML);
   const size_t sz_nl = sz_abs;
-  const size_t gscr_per = (size_t)2 * (Ly + 2) * (Lx + 2);  // doubles per FOV (oversize masks)
+  const size_t sz_off = al(sizeof(int) * (size_t)(B + 1 + 2));
+  const size_t gscr_per = (size_t)2 * (Dy + 2) * (Dx + 2);  // doubles per FOV (oversize masks)
   const size_t sz_gscr = al(sizeof(double) * B * gscr_per);
   unsigned char* o = (unsigned char*)cpx_ws(ctx, WS_SEG_OBJ,
-      sz_lst + sz_obj + sz_hdr + sz_bad + sz_l2i + sz_abs + sz_nl + sz_gscr);
+      sz_lst + sz_obj + sz_hdr + sz_bad + sz_l2i + sz_abs + sz_nl + sz_off + sz_gscr);
   if (!o) return CPX_ERR_OOM;
   cpx_label_stats* lst = (cpx_label_stats*)o; o += sz_lst;
   cpx_object* obj = (cpx_object*)o; o += sz_obj;
@@ -1136,34 +1644,38 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   int* l2i = (int*)o; o += sz_l2i;
   int* absorber = (int*)o; o += sz_abs;
   int* newlab = (int*)o; o += sz_nl;
+  int* off = (int*)o; o += sz_off;
   double* gscr = (double*)o;
   if (flow_threshold > 0.0) {
-    rc = cpx_objects(ctx, d.m0, B, Ly, Lx, ML, 0, lst, obj, hdr);
+    rc = cpx_objects(ctx, d.m0, B, Dy, Dx, ML, 0, lst, obj, hdr);
     if (rc) return rc;
     CPX_CHECK_HIP(hipMemsetAsync(bad, 0, sz_bad, ctx->stream));
-    static bool attr = false;
-    const size_t lds = sizeof(double) * 2 * kFlowMaxCells + sizeof(int) * 4096;
-    if (!attr) {
-      CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_flow_error<false>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      attr = true;
-    }
-    const int per_fov = std::max(1, std::min(ML, (6 * ctx->n_cu + B - 1) / B));
-    hipLaunchKernelGGL(k_flow_error<false>, dim3(per_fov, B), dim3(kFlowThreads), lds, ctx->stream,
-                       (const int*)d.m0, yf_dev, Ly, Lx, ML, (const cpx_object*)obj,
-                       (const cpx_fov_objects*)hdr, flow_threshold, gscr, (long long)gscr_per, bad);
-    hipLaunchKernelGGL(k_flow_error<true>, dim3(1, B), dim3(kFlowThreads), sizeof(int) * 4096,
-                       ctx->stream, (const int*)d.m0, yf_dev, Ly, Lx, ML, (const cpx_object*)obj,
-                       (const cpx_fov_objects*)hdr, flow_threshold, gscr, (long long)gscr_per, bad);
-    hipLaunchKernelGGL(k_apply_bad, gp, dim3(kT), 0, ctx->stream, (int)n, ML,
+    CPX_CHECK_HIP(hipMemsetAsync(off + B + 1, 0, 2 * sizeof(int), ctx->stream));
+    hipLaunchKernelGGL(k_obj_prefix, dim3(1), dim3(64), 0, ctx->stream, B,
+                       (const cpx_fov_objects*)hdr, off);
+    hipLaunchKernelGGL((k_flow_error_lds<kFeSmallThreads, kFeSmallCells, kFeU>), dim3(4 * ctx->n_cu),
+                       dim3(kFeSmallThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
+                       Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 1, 0, 0, 0,
+                       flow_threshold, bad);
+    hipLaunchKernelGGL((k_flow_error_lds<kFeLargeThreads, kFeLargeCells, kFeU>), dim3(ctx->n_cu),
+                       dim3(kFeLargeThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
+                       Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 2,
+                       kFeSmallThreads, kFeU, kFeSmallCells, flow_threshold, bad);
+    hipLaunchKernelGGL(k_flow_error_big, dim3(B), dim3(kFlowThreads), 0, ctx->stream,
+                       (const int*)d.m0, (const float2*)d.dpf, Dy, Dx, ML, (const cpx_object*)obj,
+                       (const cpx_fov_objects*)hdr, kFeLargeThreads, kFeU, kFeLargeCells,
+                       flow_threshold, gscr, (long long)gscr_per, bad);
+    hipLaunchKernelGGL(k_apply_bad, gp, dim3(kT), 0, ctx->stream, n, ML,
                        (const unsigned char*)bad, d.m0);
     hipLaunchKernelGGL(k_count_bad, dim3(B), dim3(256), 0, ctx->stream, ML,
                        (const unsigned char*)bad, stats_dev);
     CPX_CHECK_LAUNCH("cpx_seg_masks flow error");
   }
-  hipLaunchKernelGGL(k_upsample, dim3(cpx_div_up(W, kT), cpx_div_up(H, kUpRows), B), dim3(kT), 0, ctx->stream,
-                     (const int*)d.m0, Ly, Lx, H, W, tabs.ynear, tabs.xnear, labels_dev);
-  CPX_CHECK_LAUNCH("k_upsample");
+  if (!resample) {
+    hipLaunchKernelGGL(k_upsample, dim3(cpx_div_up(W, kT), cpx_div_up(H, kUpRows), B), dim3(kT), 0,
+                       ctx->stream, (const int*)d.m0, Ly, Lx, H, W, tabs.ynear, tabs.xnear, labels_dev);
+    CPX_CHECK_LAUNCH("k_upsample");
+  }
   // ---- fill holes + remove small at full resolution
   rc = cpx_objects(ctx, labels_dev, B, H, W, ML, 0, lst, obj, hdr);
   if (rc) return rc;

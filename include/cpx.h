@@ -323,12 +323,17 @@ int cpx_seg_tiles(cpx_ctx* ctx, const float* corr_dev, int B, int C, int H, int 
  * yf_dev float32 [B][nout][Ly][Lx] (dy, dx, cellprob).                                       */
 int cpx_seg_average(cpx_ctx* ctx, const void* net_dev, int layout, int B, int nout,
                     const cpx_seg_geom* geom, const float* taper_dev, float* yf_dev);
-/* compute_masks at network resolution (follow_flows, get_masks, flow-error filter), nearest
- * resize to (H, W), fill_holes_and_remove_small_masks.  labels_dev int32 [B][H][W];
- * stats_dev cpx_seg_stats [B].  max_objects bounds labels per FOV.                           */
+/* dynamics.compute_masks on the averaged network output yf_dev (Ly x Lx): follow_flows
+ * (niter Euler steps, CPU map_coordinates arithmetic), get_masks, flow-error filter,
+ * fill_holes_and_remove_small_masks.  resample = 1 (CellposeModel.eval's default, the
+ * reference call Cellpose_GPU_s3fs.py:143): the flows are first resized to H x W
+ * (transforms.resize_image, cv2 INTER_LINEAR) and everything runs at full resolution, with
+ * niter = uint32(200 / rescale) (1176 for nuclei at diameter 100; the host passes it).
+ * resample = 0: dynamics at Ly x Lx, masks nearest-resized to H x W (Cellpose's resize=).
+ * labels_dev int32 [B][H][W]; stats_dev cpx_seg_stats [B].  max_objects bounds labels per FOV.*/
 int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx_seg_geom* geom, int H,
                   int W, int niter, double flow_threshold, int min_size, int max_objects,
-                  int32_t* labels_dev, cpx_seg_stats* stats_dev);
+                  int resample, int32_t* labels_dev, cpx_seg_stats* stats_dev);
 
 /* ---- a4 CPnet glue (bf16 NHWC activations around MIOpen convolutions) ----------------------
  * Cellpose resnet_torch.CPnet forward (used at Cellpose_GPU_s3fs.py:108-110 through
@@ -404,11 +409,12 @@ int cpx_fov_planes(cpx_ctx* ctx, const float** corr_dev, const uint16_t** plane_
 /* Copy channel `ch` of the (z-max'd) uint16 planes to host [H][W] (MaxProjection output).   */
 int cpx_fov_read_plane(cpx_ctx* ctx, int ch, uint16_t* host);
 /* a6 post-processing of one FOV from the CPnet output tiles (net_dev in `layout`, geom as for
- * cpx_seg_average): tile average, flow dynamics, masks, resize, fill holes
+ * cpx_seg_average): tile average, then cpx_seg_masks (resample as there)
  * (Cellpose_GPU_s3fs.py:108,143-147, models.CellposeModel.eval).  labels_dev int32 [H][W].  */
 int cpx_fov_segment_post(cpx_ctx* ctx, const void* net_dev, int layout, const cpx_seg_geom* geom,
                          const float* taper_dev, int niter, double flow_threshold, int min_size,
-                         int max_objects, int32_t* labels_dev, cpx_seg_stats* stats_dev);
+                         int max_objects, int resample, int32_t* labels_dev,
+                         cpx_seg_stats* stats_dev);
 /* a7 object table of a label image (int32 [H][W], device) for the submitted FOV's shape:
  * regionprops order, int centroids, `box` edge filter, kept index (Cellpose_GPU_s3fs.py:
  * 149-163).  host_out: cpx_object [max_objects] (may be NULL, then only *n_out is set).

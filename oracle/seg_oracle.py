@@ -13,14 +13,22 @@ libcpx must match bit-exactly on identical network outputs.  Choices (DESIGN.md 
   * channels=None with C > 2 -> the first nchan=2 channels are used;
   * normalize99 per channel: exact order statistics, fp64 linear interpolation (numpy's lerp
     formula), x' = fp32(((double)x - p1) / (p99 - p1));
-  * rescale = diam_mean / diameter (nuclei 17 / 100); resize = half-pixel bilinear (OpenCV
-    INTER_LINEAR coordinate rule), fp32, no FMA;
-  * resample=False: dynamics at network resolution (niter=200), masks resized to full resolution
-    by nearest neighbour before fill-holes / remove-small (Cellpose's `resize` path);
+  * rescale = diam_mean / diameter (nuclei 17 / 100); resize = cv2.resize INTER_LINEAR
+    (scale = 1 / (dst / src), half-pixel centres, clamped edges), fp32, no FMA;
+  * resample=True (CellposeModel.eval's default): the averaged network output is resized back
+    to H x W before the dynamics, so follow_flows / get_masks / the flow-error filter /
+    fill-holes all run at full resolution; niter = uint32(1 / rescale * 200) (1176 for the
+    reference's nuclei model at diameter 100; `_run_cp`).  resample=False (dynamics at network
+    resolution, masks nearest-resized) is kept as a named option;
+  * follow_flows uses the CPU map_coordinates step (numba: fp64 expression, fp32 storage);
   * get_masks keeps Cellpose's seed order (the `for s in seeds: s = s[isort]` no-op leaves seeds
     in row-major order) and renumbers labels by first occurrence (fastremap.renumber);
-  * flow-error filter (threshold 0.4) with the 2.x masks_to_flows heat diffusion (median centre,
-    niter = 2*(ptp x + ptp y), no log), fp64.
+  * flow-error filter (threshold 0.4) with the 2.x CPU masks_to_flows heat diffusion (median
+    centre, niter = 2*(ptp x + ptp y), no log), fp64.
+The literal numpy loops of follow_flows and masks_to_flows take minutes per 2080^2 FOV at
+niter 1176; oracle/seg_oracle_c.c repeats them statement by statement in C (liboracle_seg.so,
+built by oracle/Makefile) and is used when present (`impl="auto"`); tests/test_seg_oracle_c.py
+checks the two implementations against each other.
 """
 from __future__ import annotations
 
@@ -33,7 +41,7 @@ NET_CHANNELS = 2
 DIAM_MEAN = {"nuclei": 17.0, "cyto": 30.0, "cyto2": 30.0, "cyto3": 30.0}
 BSIZE = 224
 TILE_OVERLAP = 0.1
-NITER = 200
+NITER_NET = 200          # resample=False keeps Cellpose 2.x's fixed 200 steps at network size
 CELLPROB_THRESHOLD = 0.0
 FLOW_THRESHOLD = 0.4
 MIN_SIZE = 15
@@ -75,8 +83,39 @@ def net_size(H: int, W: int, model: str = "nuclei", diameter: float = 100.0):
     return int(H * rescale), int(W * rescale)
 
 
+def default_niter(model: str = "nuclei", diameter: float = 100.0, resample: bool = True) -> int:
+    """CellposeModel._run_cp: niter = 1 / rescale * 200, cast by follow_flows to uint32."""
+    if not resample:
+        return NITER_NET
+    rescale = DIAM_MEAN[model] / diameter
+    return int(np.uint32(1 / rescale * 200))
+
+
+_CLIB = None
+
+
+def clib():
+    """liboracle_seg.so (oracle/seg_oracle_c.c) or None when it has not been built."""
+    global _CLIB
+    if _CLIB is None:
+        import ctypes as ct
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liboracle_seg.so")
+        if not os.path.exists(path):
+            _CLIB = False
+        else:
+            lib = ct.CDLL(path)
+            P = ct.c_void_p
+            lib.follow_flows_c.argtypes = [P, ct.c_int, ct.c_int, ct.c_int64, ct.c_int, P, P]
+            lib.follow_flows_c.restype = None
+            lib.flow_error_c.argtypes = [P, P, ct.c_int, ct.c_int, ct.c_int, P]
+            lib.flow_error_c.restype = None
+            _CLIB = lib
+    return _CLIB or None
+
+
 def _axis_coeffs(n_src: int, n_dst: int):
-    scale = n_src / n_dst
+    scale = 1.0 / (n_dst / n_src)  # cv2.resize: scale_x = 1. / inv_scale_x, inv = dst / src
     i0 = np.zeros(n_dst, np.int64)
     w = np.zeros(n_dst, np.float32)
     for d in range(n_dst):
@@ -92,7 +131,7 @@ def _axis_coeffs(n_src: int, n_dst: int):
 
 
 def resize_bilinear(img32: np.ndarray, Ly: int, Lx: int) -> np.ndarray:
-    """Half-pixel bilinear (cv2 INTER_LINEAR coordinate rule), fp32 arithmetic, row pass
+    """cv2.resize INTER_LINEAR (half-pixel centres, clamped edges), fp32 arithmetic, row pass
     h = a*(1-wx) + b*wx then column pass h0*(1-wy) + h1*wy."""
     H, W = img32.shape
     y0, y1, wy = _axis_coeffs(H, Ly)
@@ -169,9 +208,10 @@ def average_tiles(y: np.ndarray, g: TileGeom) -> np.ndarray:
 # dynamics
 # ---------------------------------------------------------------------------------------------
 
-def follow_flows(dP: np.ndarray, cp_mask: np.ndarray, niter: int = NITER):
+def follow_flows(dP: np.ndarray, cp_mask: np.ndarray, niter: int, impl: str = "auto"):
     """dynamics.follow_flows(dP * cp_mask / 5., niter, interp=True) with the CPU map_coordinates
-    step (numba: fp64 expression, fp32 storage); returns p [2,Ly,Lx] fp32 and n_moving."""
+    step (numba: fp64 expression, fp32 storage); returns p [2,Ly,Lx] fp32 and n_moving.
+    impl: "numpy" (the literal loop below), "c" (seg_oracle_c.c, same statements) or "auto"."""
     Ly, Lx = dP.shape[1:]
     dPs = (dP * cp_mask / np.float32(5.0)).astype(np.float32)
     p = np.array(np.meshgrid(np.arange(Ly), np.arange(Lx), indexing="ij")).astype(np.float32)
@@ -180,23 +220,32 @@ def follow_flows(dP: np.ndarray, cp_mask: np.ndarray, niter: int = NITER):
         return p, int(inds.shape[0])
     py = p[0][inds[:, 0], inds[:, 1]].copy()
     px = p[1][inds[:, 0], inds[:, 1]].copy()
-    I = dPs.astype(np.float64)
-    for _ in range(niter):
-        yf = py.astype(np.int32)
-        xf = px.astype(np.int32)
-        y = (py - yf).astype(np.float32).astype(np.float64)
-        x = (px - xf).astype(np.float32).astype(np.float64)
-        y0 = np.minimum(Ly - 1, np.maximum(0, yf))
-        x0 = np.minimum(Lx - 1, np.maximum(0, xf))
-        y1 = np.minimum(Ly - 1, y0 + 1)
-        x1 = np.minimum(Lx - 1, x0 + 1)
-        d = []
-        for c in range(2):
-            v = (I[c, y0, x0] * (1 - y) * (1 - x) + I[c, y0, x1] * (1 - y) * x +
-                 I[c, y1, x0] * y * (1 - x) + I[c, y1, x1] * y * x)
-            d.append(v.astype(np.float32))
-        py = np.minimum(np.float32(Ly - 1), np.maximum(np.float32(0), (py + d[0]).astype(np.float32)))
-        px = np.minimum(np.float32(Lx - 1), np.maximum(np.float32(0), (px + d[1]).astype(np.float32)))
+    lib = clib() if impl in ("auto", "c") else None
+    if impl == "c" and lib is None:
+        raise RuntimeError("liboracle_seg.so not built (make -C oracle)")
+    if lib is not None:
+        import ctypes as ct
+        dpc = np.ascontiguousarray(dPs)
+        lib.follow_flows_c(dpc.ctypes.data_as(ct.c_void_p), Ly, Lx, py.size, int(niter),
+                           py.ctypes.data_as(ct.c_void_p), px.ctypes.data_as(ct.c_void_p))
+    else:
+        I = dPs.astype(np.float64)
+        for _ in range(niter):
+            yf = py.astype(np.int32)
+            xf = px.astype(np.int32)
+            y = (py - yf).astype(np.float32).astype(np.float64)
+            x = (px - xf).astype(np.float32).astype(np.float64)
+            y0 = np.minimum(Ly - 1, np.maximum(0, yf))
+            x0 = np.minimum(Lx - 1, np.maximum(0, xf))
+            y1 = np.minimum(Ly - 1, y0 + 1)
+            x1 = np.minimum(Lx - 1, x0 + 1)
+            d = []
+            for c in range(2):
+                v = (I[c, y0, x0] * (1 - y) * (1 - x) + I[c, y0, x1] * (1 - y) * x +
+                     I[c, y1, x0] * y * (1 - x) + I[c, y1, x1] * y * x)
+                d.append(v.astype(np.float32))
+            py = np.minimum(np.float32(Ly - 1), np.maximum(np.float32(0), (py + d[0]).astype(np.float32)))
+            px = np.minimum(np.float32(Lx - 1), np.maximum(np.float32(0), (px + d[1]).astype(np.float32)))
     p[0][inds[:, 0], inds[:, 1]] = py
     p[1][inds[:, 0], inds[:, 1]] = px
     return p, int(inds.shape[0])
@@ -220,14 +269,15 @@ def get_masks(p: np.ndarray, iscell: np.ndarray, rpad: int = RPAD) -> np.ndarray
     M = np.zeros(shape, np.uint32)
     good = h > 2
     for k, (sy, sx) in enumerate(zip(*seeds)):
-        cur = np.zeros(shape, bool)
-        cur[sy, sx] = True
+        # the expansion never leaves the 13 x 13 window (pix within +-6 after 5 dilations that
+        # are clipped to it), so it is computed on the window alone; seeds sit >= 20 px inside
         y0, y1, x0, x1 = sy - 6, sy + 7, sx - 6, sx + 7
+        cur = np.zeros((13, 13), bool)
+        cur[6, 6] = True
         for _ in range(5):
-            win = cur[y0:y1, x0:x1]
-            dil = ndi.binary_dilation(win, structure=np.ones((3, 3), bool))
-            cur[y0:y1, x0:x1] = dil & good[y0:y1, x0:x1]
-        M[cur] = k + 1
+            dil = ndi.binary_dilation(cur, structure=np.ones((3, 3), bool))
+            cur = dil & good[y0:y1, x0:x1]
+        M[y0:y1, x0:x1][cur] = k + 1
     M0 = M[pflows[0] + rpad, pflows[1] + rpad]
     # remove big masks (> 40% of the image)
     uniq, counts = np.unique(M0, return_counts=True)
@@ -275,17 +325,38 @@ def masks_to_flows(masks: np.ndarray) -> np.ndarray:
     return mu
 
 
-def remove_bad_flow_masks(masks: np.ndarray, dP: np.ndarray, threshold: float = FLOW_THRESHOLD):
-    """dynamics.remove_bad_flow_masks / metrics.flow_error restated."""
+def flow_errors(masks: np.ndarray, dP: np.ndarray, impl: str = "auto") -> np.ndarray:
+    """metrics.flow_error: per label 1..max, mean over its pixels of (mu - dP/5)^2 summed over
+    the two flow components (masks_to_flows of the masks vs the network flows)."""
     n = int(masks.max())
-    if n == 0:
-        return masks
+    lib = clib() if impl in ("auto", "c") else None
+    if impl == "c" and lib is None:
+        raise RuntimeError("liboracle_seg.so not built (make -C oracle)")
+    if lib is not None:
+        import ctypes as ct
+        m = np.ascontiguousarray(masks, dtype=np.int32)
+        d = np.ascontiguousarray(dP, dtype=np.float32)
+        err = np.zeros(n, np.float64)
+        with np.errstate(all="ignore"):
+            lib.flow_error_c(m.ctypes.data_as(ct.c_void_p), d.ctypes.data_as(ct.c_void_p),
+                             m.shape[0], m.shape[1], n, err.ctypes.data_as(ct.c_void_p))
+        return err
     mu = masks_to_flows(masks)
     err = np.zeros(n)
     idx = np.arange(1, n + 1)
     for i in range(2):
         with np.errstate(all="ignore"):
             err += ndi.mean((mu[i] - dP[i].astype(np.float32) / np.float32(5.0)) ** 2, masks, index=idx)
+    return err
+
+
+def remove_bad_flow_masks(masks: np.ndarray, dP: np.ndarray, threshold: float = FLOW_THRESHOLD,
+                          impl: str = "auto"):
+    """dynamics.remove_bad_flow_masks / metrics.flow_error restated."""
+    n = int(masks.max())
+    if n == 0:
+        return masks
+    err = flow_errors(masks, dP, impl)
     bad = 1 + np.nonzero(err > threshold)[0]
     out = masks.copy()
     out[np.isin(out, bad)] = 0
@@ -320,18 +391,34 @@ def fill_holes_and_remove_small_masks(masks: np.ndarray, min_size: int = MIN_SIZ
     return masks
 
 
-def compute_masks(yf: np.ndarray, H: int, W: int, niter: int = NITER,
-                  flow_threshold: float = FLOW_THRESHOLD, min_size: int = MIN_SIZE) -> np.ndarray:
-    """dynamics.compute_masks(dP, cellprob, resize=(H, W)) at network resolution."""
+def upsample_flows(yf: np.ndarray, H: int, W: int) -> np.ndarray:
+    """CellposeModel._run_cp with resample=True: transforms.resize_image(yf, H, W) of the
+    averaged network output (cv2 INTER_LINEAR per channel)."""
+    return np.stack([resize_bilinear(yf[c], H, W) for c in range(yf.shape[0])])
+
+
+def compute_masks(yf: np.ndarray, H: int, W: int, niter: int | None = None,
+                  flow_threshold: float = FLOW_THRESHOLD, min_size: int = MIN_SIZE,
+                  resample: bool = True, model: str = "nuclei", diameter: float = 100.0,
+                  impl: str = "auto") -> np.ndarray:
+    """masks of one FOV from the averaged network output yf [3, Ly, Lx] (dy, dx, cellprob).
+    resample=True (the reference call's default): flows resized to H x W, then
+    dynamics.compute_masks at full resolution with niter = default_niter(model, diameter).
+    resample=False: compute_masks at network resolution (niter 200) with resize=(H, W)."""
+    if niter is None:
+        niter = default_niter(model, diameter, resample)
+    if resample:
+        yf = upsample_flows(yf, H, W)
     dP, cellprob = yf[:2], yf[2]
     cp_mask = cellprob > CELLPROB_THRESHOLD
     if not np.any(cp_mask):
         return np.zeros((H, W), np.int32)
-    p, nmov = follow_flows(dP, cp_mask, niter)
+    p, nmov = follow_flows(dP, cp_mask, niter, impl)
     if nmov < 5:
         return np.zeros((H, W), np.int32)
     m = get_masks(p, cp_mask)
     if m.max() > 0 and flow_threshold > 0:
-        m = remove_bad_flow_masks(m, dP, flow_threshold)
-    m = resize_nearest(m, H, W)
+        m = remove_bad_flow_masks(m, dP, flow_threshold, impl)
+    if not resample:
+        m = resize_nearest(m, H, W)
     return fill_holes_and_remove_small_masks(m, min_size).astype(np.int32)

@@ -81,8 +81,8 @@ def test_multi_tile_geometry_2080():
     assert t.tiles == [(int(g.ys[i // 3]), int(g.xs[i % 3])) for i in range(9)]
 
 
-def _synthetic_yf(Ly, Lx, seed, noise=0.05):
-    lab = sg.labels(seed, Ly, Lx, n=18, rmin=3, rmax=10, skip_every=0)
+def _synthetic_yf(Ly, Lx, seed, noise=0.05, rmin=3, rmax=10, n=18):
+    lab = sg.labels(seed, Ly, Lx, n=n, rmin=rmin, rmax=rmax, skip_every=0)
     mu = so.masks_to_flows(lab)
     rng = np.random.default_rng(seed)
     yf = np.zeros((3, Ly, Lx), np.float32)
@@ -92,24 +92,33 @@ def _synthetic_yf(Ly, Lx, seed, noise=0.05):
     return yf, lab
 
 
-def _gpu_masks(dev, yf, g, H, W, flow_threshold=0.4, min_size=15):
+def _gpu_masks(dev, yf, g, H, W, flow_threshold=0.4, min_size=15, resample=True, niter=None):
     B = yf.shape[0]
+    if niter is None:
+        niter = so.default_niter(resample=resample)
     yft = torch.from_numpy(np.ascontiguousarray(yf)).to(dev.torch_device)
     labels = torch.empty((B, H, W), dtype=torch.int32, device=dev.torch_device)
     stats = torch.zeros(32 * B, dtype=torch.uint8, device=dev.torch_device)
-    check(dev.lib.cpx_seg_masks(dev.h, _ptr(yft), B, _geom_ptr(g), H, W, 200, float(flow_threshold),
-                                min_size, 1024, _ptr(labels), _ptr(stats)), "masks")
+    check(dev.lib.cpx_seg_masks(dev.h, _ptr(yft), B, _geom_ptr(g), H, W, niter, float(flow_threshold),
+                                min_size, 1024, int(resample), _ptr(labels), _ptr(stats)), "masks")
     dev.sync()
     return labels.cpu().numpy(), stats.cpu().numpy().view(SEG_STATS_DTYPE)
 
 
-def test_masks_bit_exact_vs_oracle(dev):
-    H, W = 700, 760
+def _oracle_nmoving(yf, H, W, resample=True):
+    f = so.upsample_flows(yf, H, W) if resample else yf
+    dps = (f[:2] * (f[2] > 0) / np.float32(5.0)).astype(np.float32)
+    return int((np.abs(dps[0]) > 1e-3).sum())
+
+
+@pytest.mark.parametrize("H,W,rmax", [(700, 760, 10), (1040, 1100, 10), (1040, 1100, 16)])
+def test_masks_full_resolution_bit_exact_vs_oracle(dev, H, W, rmax):
+    """resample=True (Cellpose's default): flows resized to H x W, 1176 follow steps (the
+    kernel stops each pixel at its exact fixed point), get_masks / flow error / fill holes at
+    full resolution — labels bit-identical to the restatement's plain loops.  rmax 16 (up to
+    ~190 px masks) sends masks through all three flow-error kernels (LDS small / large, global)."""
     g = make_geom(H, W)
-    yfs = []
-    for s in (1, 2, 3):
-        yf, _ = _synthetic_yf(g.Ly, g.Lx, s)
-        yfs.append(yf)
+    yfs = [_synthetic_yf(g.Ly, g.Lx, s, rmax=rmax, n=18 if rmax <= 10 else 10)[0] for s in (1, 2)]
     yfs.append(np.full((3, g.Ly, g.Lx), -1.0, np.float32))  # no cells at all
     yf = np.stack(yfs)
     got, st = _gpu_masks(dev, yf, g, H, W)
@@ -117,8 +126,21 @@ def test_masks_bit_exact_vs_oracle(dev):
         ref = so.compute_masks(yf[b], H, W)
         np.testing.assert_array_equal(got[b], ref, err_msg=f"fov {b}")
         assert st[b]["n_final"] == ref.max()
+        assert st[b]["n_moving"] == _oracle_nmoving(yf[b], H, W)
     assert st[0]["n_final"] >= 8  # the synthetic objects were recovered
-    assert st[3]["n_final"] == 0 and st[3]["n_moving"] == 0
+    assert st[2]["n_final"] == 0 and st[2]["n_moving"] == 0
+
+
+def test_masks_network_resolution_bit_exact_vs_oracle(dev):
+    """resample=False (named option): dynamics at network size (200 steps), nearest resize."""
+    H, W = 700, 760
+    g = make_geom(H, W)
+    yf = np.stack([_synthetic_yf(g.Ly, g.Lx, s)[0] for s in (1, 3)])
+    got, st = _gpu_masks(dev, yf, g, H, W, resample=False)
+    for b in range(yf.shape[0]):
+        ref = so.compute_masks(yf[b], H, W, resample=False)
+        np.testing.assert_array_equal(got[b], ref, err_msg=f"fov {b}")
+        assert st[b]["n_moving"] == _oracle_nmoving(yf[b], H, W, resample=False)
 
 
 def test_masks_without_flow_filter_and_min_size(dev):
@@ -128,6 +150,22 @@ def test_masks_without_flow_filter_and_min_size(dev):
     got, _ = _gpu_masks(dev, yf[None], g, H, W, flow_threshold=0.0, min_size=400)
     ref = so.compute_masks(yf, H, W, flow_threshold=0.0, min_size=400)
     np.testing.assert_array_equal(got[0], ref)
+
+
+def test_moving_threshold_is_float32(dev):
+    """|dY * cp / 5| == float32(1e-3) exactly does not move (numpy compares in float32)."""
+    H, W = 700, 760
+    g = make_geom(H, W)
+    yf, _ = _synthetic_yf(g.Ly, g.Lx, 4)
+    t = np.float32(1e-3)
+    v = np.float32(t * np.float32(5.0))
+    while np.float32(v / np.float32(5.0)) != t:
+        v = np.nextafter(v, np.float32(1.0))
+    yf[0, :6, :6] = v            # exactly at the threshold: not moving
+    yf[0, :6, 6:12] = np.nextafter(v, np.float32(1.0))  # just above: moving
+    yf[2, :6, :12] = 5.0
+    _, st = _gpu_masks(dev, yf[None], g, H, W, resample=False)
+    assert st[0]["n_moving"] == _oracle_nmoving(yf, H, W, resample=False)
 
 
 def test_cpnet_forward_gpu_vs_cpu_fp32(dev):
