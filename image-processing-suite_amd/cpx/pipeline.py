@@ -38,6 +38,9 @@ class PipelineConfig:
     model: str = CELLPOSE_MODEL
     diameter: float = DIAMETER
     resample: bool = True            # CellposeModel.eval default: dynamics at full resolution
+    cpnet_precision: str = "bf16"    # "bf16": native MFMA convolutions (headline); "fp32": the
+                                     # same network in fp32 (PyTorch eager), masks identical to
+                                     # the fp32 CPU network on the e2e plates
     cell_expand: int = 15            # Cells = expand_labels(Nuclei, cell_expand)
     max_objects: int = 2048          # per FOV and object set
     box: int = 200                   # Cellpose_GPU_s3fs.py:30 BOX_SIZE
@@ -71,8 +74,10 @@ class FovPipeline:
         self.lstats = dev.empty_bytes(64 * B * (ML + 1))
         self.F = n_features(C)
         self.seg = Segmenter(dev, H, W, B, model=cfg.model, diameter=cfg.diameter, weights=cfg.weights,
-                             seed=cfg.seed, use_graph=cfg.use_graph, max_objects=ML,
-                             resample=cfg.resample)
+                             seed=cfg.seed, use_graph=cfg.use_graph and cfg.cpnet_precision == "bf16",
+                             max_objects=ML, resample=cfg.resample,
+                             net_dtype=torch.bfloat16 if cfg.cpnet_precision == "bf16" else torch.float32,
+                             fused=cfg.cpnet_precision == "bf16")
         # result slots (device) and their pinned host mirrors
         self._slots = []
         for _ in range(max(1, cfg.slots)):

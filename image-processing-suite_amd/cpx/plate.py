@@ -1,4 +1,4 @@
-"""Plate/time measurement run on one GPU: LoadData CSV + TIFF planes -> the four CSV tables.
+"""Plate/time measurement run: LoadData CSV + TIFF planes -> the four CSV tables.
 
 Replaces the CellProfiler job that Feature_extraction_opt.py:159-177 launches per (plate, time)
 (LoadData CSV in, per-object tables synced to `<base>/<plate>/<time>/`), with the GPU pipeline
@@ -6,29 +6,39 @@ of cpx.pipeline: flat-field + QC -> Cellpose-restated segmentation -> Cells/Cyto
 tables -> features, in batches of FOVs resident in HBM.  Host threads decode the next batch's
 TIFFs while the GPU works on the current one.
 
-  python -m cpx.plate --load-data load_data_P01_24_illum.csv --data-path IMAGES \\
-      --illum-path ILLUM --channels DNA ER RNA AGP Mito --out RESULTS [--batch 8]
+  python -m cpx.plate --load-data load_data_P01_24_illum.csv [more LoadData files ...] \
+      --data-path IMAGES --illum-path ILLUM --channels DNA ER RNA AGP Mito --out RESULTS
 
 Channel files come from FileName_<ch> (relative to --data-path); flat-fields from
 <ch>_illum.npy or Illum<ch>.npy (as the QC tool); plate and time from Metadata_Plate /
-Metadata_Timepoint unless given.  Multi-GPU: run one process per GPU on a well shard
-(cpx.shard.shard) and concatenate the tables (rows are keyed by ImageNumber).
+Metadata_Timepoint unless given.  Every LoadData file is one (plate, time) job.
+
+Multi-GPU (the reference's per-GPU consumers Cellpose_GPU_s3fs.py:269-300 and
+per-(plate, time) jobs Feature_extraction_opt.py:63-76): one process per GPU (`cpx.launch`, or
+torchrun with RANK / WORLD_SIZE), each draining its own queue of (plate, time, well shard)
+jobs — wells are dealt round-robin in first-appearance order, so all sites of a well stay on one
+GPU — and writing its rows as parquet parts; the parts are merged into the final CSVs sorted by
+(ImageNumber, ObjectNumber), byte-identical for any number of processes.  No collective touches
+the data path.  Batches always hold --batch FOVs (the tail is zero-padded), so every process runs
+the same kernels on the same batch shape.
 """
 from __future__ import annotations
 
 import argparse
 import concurrent.futures
+import glob
+import json
 import logging
 import os
+import shutil
 
 import numpy as np
 
 log = logging.getLogger("cpx.plate")
-
-
+PARTS = ".parts"
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(prog="python -m cpx.plate", description="GPU per-object measurement of one plate/time")
-    ap.add_argument("--load-data", required=True)
+    ap.add_argument("--load-data", required=True, nargs="+", help="one LoadData CSV per (plate, time) job")
     ap.add_argument("--data-path", required=True)
     ap.add_argument("--illum-path", default=None)
     ap.add_argument("--channels", nargs="+", required=True)
@@ -43,7 +53,59 @@ def parse_args(argv=None):
                     help="pipelines (libcpx context + HIP stream) on the GPU: batches in flight")
     ap.add_argument("--csv-image-key", default=None,
                     help="folder with an Image.csv whose ImageQC_* flags exclude FOVs (Cellpose_GPU_s3fs.py:252-255)")
+    ap.add_argument("--rank", type=int, default=int(os.environ.get("RANK", "0")),
+                    help="this process's rank (well shard); default $RANK")
+    ap.add_argument("--world", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
+                    help="processes (GPUs) sharing the jobs; default $WORLD_SIZE")
+    ap.add_argument("--no-merge", action="store_true",
+                    help="with --world > 1: leave the parts for cpx.launch / merge_parts")
     return ap.parse_args(argv)
+
+
+def shard_rows(table, rank: int, world: int):
+    """Row positions of `rank`: wells dealt round-robin in first-appearance order (all sites of
+    a well on one rank); rows without Metadata_Well are dealt one by one."""
+    if world <= 1:
+        return list(range(len(table)))
+    if "Metadata_Well" in table:
+        order = {}
+        wells = [order.setdefault(w, len(order)) for w in table["Metadata_Well"].astype(str)]
+        return [i for i, w in enumerate(wells) if w % world == rank]
+    return [i for i in range(len(table)) if i % world == rank]
+
+
+def job_dir(out, plate, time):
+    return os.path.join(out, str(plate), str(time))
+
+
+def write_part(d, rank, world, frames: dict):
+    """One rank's rows of one (plate, time) job as parquet (exact dtypes and floats)."""
+    pdir = os.path.join(d, PARTS, f"r{rank:04d}of{world:04d}")
+    os.makedirs(pdir, exist_ok=True)
+    for name, df in frames.items():
+        df.to_parquet(os.path.join(pdir, f"{name}.parquet"), index=False)
+    return pdir
+
+
+def merge_parts(d, world=None):
+    """Concatenate the ranks' parts of job directory d into the final CSVs (rows sorted by
+    ImageNumber, then ObjectNumber) and remove the parts."""
+    import pandas as pd
+    parts = sorted(glob.glob(os.path.join(d, PARTS, "r*of*")))
+    if world is not None and len(parts) != world:
+        raise RuntimeError(f"{d}: {len(parts)} parts, expected {world}")
+    names = sorted({os.path.splitext(f)[0] for p in parts for f in os.listdir(p)})
+    for name in names:
+        blocks = [pd.read_parquet(os.path.join(p, name + ".parquet")) for p in parts
+                  if os.path.exists(os.path.join(p, name + ".parquet"))]
+        blocks = [b for b in blocks if len(b)] or blocks[:1]
+        df = pd.concat(blocks, ignore_index=True)
+        keys = [k for k in ("ImageNumber", "ObjectNumber") if k in df.columns]
+        if keys and len(df):
+            df = df.sort_values(keys, kind="stable").reset_index(drop=True)
+        df.to_csv(os.path.join(d, f"{name}.csv"), index=False)
+    shutil.rmtree(os.path.join(d, PARTS), ignore_errors=True)
+    return d
 
 
 def qc_filter(load_data, image_df):
@@ -69,73 +131,149 @@ def _illum(illum_path, channels, H, W):
     return np.stack(planes)
 
 
-def run(argv=None):
+def _job_meta(a, load_data):
+    """(table after the QC filter, plate, time) of one LoadData job."""
     import pandas as pd
-    import torch
-    from . import tiffio
-    from .csvout import PlateTables
-    from .device import Device
-    from .pipeline import OBJECT_SETS, FovPipeline, PipelineConfig
-
-    a = parse_args(argv)
-    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s: %(message)s")
-    table = pd.read_csv(a.load_data)
+    table = pd.read_csv(load_data)
     if a.csv_image_key:
         n0 = len(table)
         table = qc_filter(table, pd.read_csv(os.path.join(a.csv_image_key, "Image.csv")))
         log.info("image QC filter: %d of %d sites kept", len(table), n0)
     else:
         log.info("No csv_image_key provided — skipping image QC filtering.")
-    chans = list(a.channels)
-    C = len(chans)
     plate = a.plate or (str(table["Metadata_Plate"].iloc[0]) if "Metadata_Plate" in table else "plate")
     time = a.time or (str(table["Metadata_Timepoint"].iloc[0]) if "Metadata_Timepoint" in table else "0")
-    files = [[os.path.join(a.data_path, str(r[f"FileName_{ch}"])) for ch in chans] for _, r in table.iterrows()]
-    first = tiffio.imread(files[0][0])
-    H, W = first.shape
-    weights = a.weights
-    if weights is None:
-        cand = os.path.join(os.path.dirname(__file__), "weights", "cpnet_nuclei_synth.pt")
-        weights = cand if os.path.exists(cand) else None
-    B = max(1, min(a.batch, len(files)))
-    cfg = PipelineConfig(H=H, W=W, C=C, batch=B, channels=tuple(chans), weights=weights)
-    illum = _illum(a.illum_path, chans, H, W)
-    n_pipes = max(1, min(a.pipes, (len(files) + B - 1) // B))
-    streams, pipes = [], []
-    for _ in range(n_pipes):
-        st = torch.cuda.Stream(device=torch.device("cuda", a.device))
-        with torch.cuda.stream(st):
-            pipes.append(FovPipeline(Device(a.device), cfg, illum))
-        streams.append(st)
-    out = PlateTables(chans)
+    return table, plate, time
+
+
+def run(argv=None):
+    """Run every LoadData job's share of this rank; returns the job directories."""
+    import pandas as pd
+    from . import tiffio
+    from .csvout import PlateTables
+    from .pipeline import OBJECT_SETS
+
+    a = parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s: %(message)s")
+    chans = list(a.channels)
+    C = len(chans)
+    state = {}  # pipelines, created for the first job's plane geometry and reused
+    dirs = []
+    for load_data in a.load_data:
+        table, plate, time = _job_meta(a, load_data)
+        mine = shard_rows(table, a.rank, a.world)
+        files = [[os.path.join(a.data_path, str(table.iloc[i][f"FileName_{ch}"])) for ch in chans] for i in mine]
+        out = PlateTables(chans)
+        status = []  # per site: the reference's results_dict entry (Cellpose_GPU_s3fs.py:123-125,219-223)
+        if files:
+            _run_sites(a, table, mine, files, chans, state, out, status)
+        d = job_dir(a.out, plate, time)
+        frames = out.frames()
+        frames["site_status"] = pd.DataFrame(status, columns=["ImageNumber", "status", "n_cells"]) \
+            .sort_values("ImageNumber", kind="stable").reset_index(drop=True)
+        if a.world > 1:
+            write_part(d, a.rank, a.world, frames)
+        else:
+            os.makedirs(d, exist_ok=True)
+            for name, df in frames.items():
+                df.to_csv(os.path.join(d, f"{name}.csv"), index=False)
+        log.info("rank %d/%d: %d sites of %s/%s -> %s", a.rank, a.world, len(files), plate, time, d)
+        dirs.append(d)
+    if a.world > 1:
+        with open(os.path.join(a.out, f".cpx_jobs_r{a.rank:04d}.json"), "w") as f:
+            json.dump(dirs, f)
+        if not a.no_merge:
+            _torchrun_merge(a, dirs)
+    return dirs[0] if len(dirs) == 1 else dirs
+
+
+def _torchrun_merge(a, dirs):
+    """Under torchrun (a process group can be formed): barrier on gloo, rank 0 merges."""
+    import torch.distributed as dist
+    if not dist.is_available() or "MASTER_ADDR" not in os.environ:
+        return
+    if not dist.is_initialized():
+        dist.init_process_group("gloo")
+    dist.barrier()
+    if a.rank == 0:
+        for d in dirs:
+            merge_parts(d, a.world)
+    dist.barrier()
+
+
+def _run_sites(a, table, mine, files, chans, state, out, status):
+    import torch
+    from . import tiffio
+    from .device import Device
+    from .pipeline import OBJECT_SETS, FovPipeline, PipelineConfig
+    C = len(chans)
+    if "pipes" not in state:
+        H = W = None
+        for fs in files:  # the plane geometry from the first readable plane
+            try:
+                H, W = tiffio.imread(fs[0]).shape
+                break
+            except Exception:  # noqa: BLE001
+                continue
+        if H is None:
+            raise RuntimeError("no readable plane in this job")
+        weights = a.weights
+        if weights is None:
+            cand = os.path.join(os.path.dirname(__file__), "weights", "cpnet_nuclei_synth.pt")
+            weights = cand if os.path.exists(cand) else None
+        B = max(1, a.batch)
+        cfg = PipelineConfig(H=H, W=W, C=C, batch=B, channels=tuple(chans), weights=weights)
+        illum = _illum(a.illum_path, chans, H, W)
+        streams, pipes = [], []
+        for _ in range(max(1, a.pipes)):
+            st = torch.cuda.Stream(device=torch.device("cuda", a.device))
+            with torch.cuda.stream(st):
+                pipes.append(FovPipeline(Device(a.device), cfg, illum))
+            streams.append(st)
+        hosts = [torch.empty((B * C, H, W), dtype=torch.int16, pin_memory=True) for _ in pipes]
+        state.update(pipes=pipes, streams=streams, hosts=hosts, B=B, H=H, W=W)
+    pipes, streams, hosts = state["pipes"], state["streams"], state["hosts"]
+    B, H, W = state["B"], state["H"], state["W"]
+    n_pipes = len(pipes)
 
     def read_fov(paths):
-        planes = []
-        for p in paths:
-            if os.path.exists(p):
+        """The site's C planes, or None when any of them cannot be read (missing, undecodable,
+        other shape): the reference's producer then sends (site_id, None) and the consumer
+        records the site as {'status': 'empty', 'n_cells': 0} (Cellpose_GPU_s3fs.py:76-87,
+        123-136)."""
+        try:
+            planes = []
+            for p in paths:
                 x = tiffio.imread(p)
                 if x.shape != (H, W):
                     raise ValueError(f"{p}: shape {x.shape}, expected {(H, W)}")
                 planes.append(x.astype(np.uint16, copy=False))
-            else:
-                log.warning("missing plane %s: zeros used", p)
-                planes.append(np.zeros((H, W), np.uint16))
-        return np.stack(planes)
+            return np.stack(planes)
+        except Exception as e:  # noqa: BLE001
+            log.error("failed on site %s: %s", paths, e)
+            return None
 
-    hosts = [torch.empty((B * C, H, W), dtype=torch.int16, pin_memory=True) for _ in range(n_pipes)]
     batches = [list(range(i, min(i + B, len(files)))) for i in range(0, len(files), B)]
-    inflight = []  # (batch index, pipeline, slot, upload event)
+    inflight = []  # (batch index, pipeline, slot, upload event, empty flags)
 
-    def record(bi, res):
+    def record(bi, res, empty):
         idx = batches[bi]
-        for k, row_i in enumerate(idx):
+        for k, j in enumerate(idx):
+            row_i = mine[j]
             img_no = int(table.index[row_i]) + 1   # the LoadData row, also after QC filtering
             meta = table.iloc[row_i].to_dict()
+            if empty[k]:  # unreadable site: no measurements, no object rows
+                nan = [float("nan")] * C
+                out.add_image(img_no, meta, nan, nan, {s: 0 for s in OBJECT_SETS})
+                status.append({"ImageNumber": img_no, "status": "empty", "n_cells": 0})
+                continue
             q = res.qc[k * C:(k + 1) * C]
             counts = {s: int(res.hdr[s][k]["n_objects"]) for s in OBJECT_SETS}
             out.add_image(img_no, meta, q["slope"], q["pct_max"], counts)
             for s in OBJECT_SETS:
                 out.add_objects(s, img_no, res.objects[s][k]["label"], res.feats[s][k])
+            n = counts["Nuclei"]
+            status.append({"ImageNumber": img_no, "status": "success" if n else "empty", "n_cells": n})
         log.info("batch %d/%d: %d FOVs", bi + 1, len(batches), len(idx))
 
     with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, a.threads)) as pool:
@@ -146,28 +284,27 @@ def run(argv=None):
                 pending = [pool.submit(read_fov, files[i]) for i in batches[bi + 1]]
             p_i = bi % n_pipes
             # the pinned staging buffer of this pipeline is free once its last upload completed
-            for _, q, _, up in inflight:
+            for _, q, _, up, _ in inflight:
                 if q is pipes[p_i]:
                     up.synchronize()
             host = hosts[p_i]
             hn = host.numpy().view(np.uint16).reshape(B, C, H, W)
-            hn[:len(fovs)] = np.stack(fovs)
+            empty = [f is None for f in fovs]
+            for k, f in enumerate(fovs):
+                hn[k] = 0 if f is None else f
             hn[len(fovs):] = 0
             with torch.cuda.stream(streams[p_i]):
                 pipes[p_i].raw.copy_(host, non_blocking=True)
                 up = torch.cuda.Event()
                 up.record(streams[p_i])
                 slot = pipes[p_i].run()
-            inflight.append((bi, pipes[p_i], slot, up))
+            inflight.append((bi, pipes[p_i], slot, up, empty))
             if len(inflight) > n_pipes:   # results in batch order, one step behind the GPU
-                obi, q, sl, _ = inflight.pop(0)
-                record(obi, q.fetch(sl))
+                obi, q, sl, _, em = inflight.pop(0)
+                record(obi, q.fetch(sl), em)
         while inflight:
-            obi, q, sl, _ = inflight.pop(0)
-            record(obi, q.fetch(sl))
-    d = out.write(a.out, plate, time)
-    log.info("tables written to %s", d)
-    return d
+            obi, q, sl, _, em = inflight.pop(0)
+            record(obi, q.fetch(sl), em)
 
 
 if __name__ == "__main__":

@@ -76,16 +76,21 @@ def process_images(root: str, image_folder: str, resolution: int, dev=None, batc
     keys.sort()
 
     def load(k):
-        with open(os.path.join(root, k), "rb") as fh:
-            return _decode(fh.read())
+        # Image_re-binning.py:56-58: a file that fails is logged and skipped, the loop continues
+        try:
+            with open(os.path.join(root, k), "rb") as fh:
+                return _decode(fh.read())
+        except Exception:  # noqa: BLE001
+            log.error("Failed to process '%s'", k, exc_info=True)
+            return None
 
     n = 0
     with concurrent.futures.ThreadPoolExecutor(threads) as ex:
         for i in range(0, len(keys), batch):
             chunk = keys[i:i + batch]
             planes = list(ex.map(load, chunk))
-            shapes = {p.shape for p in planes}
-            groups = {s: [j for j, p in enumerate(planes) if p.shape == s] for s in shapes}
+            shapes = {p.shape for p in planes if p is not None}
+            groups = {s: [j for j, p in enumerate(planes) if p is not None and p.shape == s] for s in shapes}
             for s, idx in groups.items():
                 out = rebin_planes(dev, np.stack([planes[j] for j in idx]), resolution, resolution)
                 host = out.cpu().numpy().view(np.uint16)

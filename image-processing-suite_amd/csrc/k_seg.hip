@@ -820,7 +820,7 @@ __global__ void k_obj_prefix(int B, const cpx_fov_objects* __restrict__ hdr, int
 }
 
 template <int THREADS, int CELLS, int U>
-__global__ __launch_bounds__(THREADS) void k_flow_error_lds(
+__global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per SIMD: <= 128 VGPRs
     const int* __restrict__ m0, const float2* __restrict__ dpf, int Dy, int Dx, int B, int max_label,
     const cpx_object* __restrict__ objects, const int* __restrict__ off, int* __restrict__ ctr,
     int lo_threads, int lo_units, int lo_cells, double thr, unsigned char* __restrict__ bad) {
@@ -928,6 +928,11 @@ __global__ __launch_bounds__(THREADS) void k_flow_error_lds(
     if (tid == 0 && niter > 0) T[ym * lx + xm] = 1.0;  // the first iteration's T[centre] += 1
     __syncthreads();
     double nv[U][kFeKS];
+    double nvc = 0.0;  // the centre cell's new value (owner thread only)
+    int ci = -1;       // its unit
+#pragma unroll
+    for (int i = 0; i < U; ++i)
+      if (ujc[i] >= 0) ci = i;
     for (int it = 0; it < niter; ++it) {
 #pragma unroll
       for (int i = 0; i < U; ++i) {
@@ -956,6 +961,7 @@ __global__ __launch_bounds__(THREADS) void k_flow_error_lds(
             nr = Tn[1];
           }
           nv[i][j] = 1 / 9. * (cc + uc + dc + cl + cr + ul + ur + dl + dr);
+          if (j == ujc[i]) nvc = nv[i][j];
           ul = cl; uc = cc; ur = cr;
           cl = dl; cc = dc; cr = dr;
           dl = nl; dc = nc; dr = nr;
@@ -972,8 +978,10 @@ __global__ __launch_bounds__(THREADS) void k_flow_error_lds(
         double* Tw = T + wb;
 #pragma unroll
         for (int j = 0; j < kFeKS; ++j)
-          if ((um[i] >> j) & 1u) Tw[j * lx] = (j == ujc[i] && !last) ? nv[i][j] + 1.0 : nv[i][j];
+          if ((um[i] >> j) & 1u) Tw[j * lx] = nv[i][j];
       }
+      // the next iteration's T[centre] += 1, by the centre's owner after its own store
+      if (ci >= 0 && !last) T[ym * lx + xm] = nvc + 1.0;
       __syncthreads();
     }
     // ---- gradients, normalisation, error vs dP/5
@@ -1514,6 +1522,7 @@ __global__ void k_seed_count(int B, const int* __restrict__ totals, cpx_seg_stat
 }
 
 constexpr int kFeSmallThreads = 256, kFeSmallCells = 5000;    // 40 KiB: 4 blocks per CU
+constexpr int kFeMidThreads = 512, kFeMidCells = 10176;       // 80 KiB: 2 blocks per CU
 constexpr int kFeLargeThreads = 1024, kFeLargeCells = 20224;  // 158 KiB: 1 block per CU
 constexpr int kFeU = 2;                                        // 12-row units per thread
 
@@ -1631,7 +1640,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   const size_t sz_l2i = al(sizeof(int) * (size_t)B * (ML + 1));
   const size_t sz_abs = al(sizeof(int) * (size_t)B * ML);
   const size_t sz_nl = sz_abs;
-  const size_t sz_off = al(sizeof(int) * (size_t)(B + 1 + 2));
+  const size_t sz_off = al(sizeof(int) * (size_t)(B + 1 + 3));
   const size_t gscr_per = (size_t)2 * (Dy + 2) * (Dx + 2);  // doubles per FOV (oversize masks)
   const size_t sz_gscr = al(sizeof(double) * B * gscr_per);
   unsigned char* o = (unsigned char*)cpx_ws(ctx, WS_SEG_OBJ,
@@ -1650,17 +1659,21 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
     rc = cpx_objects(ctx, d.m0, B, Dy, Dx, ML, 0, lst, obj, hdr);
     if (rc) return rc;
     CPX_CHECK_HIP(hipMemsetAsync(bad, 0, sz_bad, ctx->stream));
-    CPX_CHECK_HIP(hipMemsetAsync(off + B + 1, 0, 2 * sizeof(int), ctx->stream));
+    CPX_CHECK_HIP(hipMemsetAsync(off + B + 1, 0, 3 * sizeof(int), ctx->stream));
     hipLaunchKernelGGL(k_obj_prefix, dim3(1), dim3(64), 0, ctx->stream, B,
                        (const cpx_fov_objects*)hdr, off);
     hipLaunchKernelGGL((k_flow_error_lds<kFeSmallThreads, kFeSmallCells, kFeU>), dim3(4 * ctx->n_cu),
                        dim3(kFeSmallThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
                        Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 1, 0, 0, 0,
                        flow_threshold, bad);
-    hipLaunchKernelGGL((k_flow_error_lds<kFeLargeThreads, kFeLargeCells, kFeU>), dim3(ctx->n_cu),
-                       dim3(kFeLargeThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
+    hipLaunchKernelGGL((k_flow_error_lds<kFeMidThreads, kFeMidCells, kFeU>), dim3(2 * ctx->n_cu),
+                       dim3(kFeMidThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
                        Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 2,
                        kFeSmallThreads, kFeU, kFeSmallCells, flow_threshold, bad);
+    hipLaunchKernelGGL((k_flow_error_lds<kFeLargeThreads, kFeLargeCells, kFeU>), dim3(ctx->n_cu),
+                       dim3(kFeLargeThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
+                       Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 3,
+                       kFeMidThreads, kFeU, kFeMidCells, flow_threshold, bad);
     hipLaunchKernelGGL(k_flow_error_big, dim3(B), dim3(kFlowThreads), 0, ctx->stream,
                        (const int*)d.m0, (const float2*)d.dpf, Dy, Dx, ML, (const cpx_object*)obj,
                        (const cpx_fov_objects*)hdr, kFeLargeThreads, kFeU, kFeLargeCells,

@@ -7,9 +7,9 @@ on the same inputs.
     GPU's own tile-averaged flows gives bit-identical Nuclei labels at 2080^2;
   * Cells / Cytoplasm bit-identical to cpx_oracle.secondary_objects of those Nuclei;
   * object tables bit-exact and all three feature tables within rtol 1e-5 of cpx_oracle.features;
-  * the bf16 CPnet's masks vs the same network in fp32 on the CPU (then the oracle's dynamics):
-    the fraction of objects with an identical mask and label (north_star asks for identical IDs;
-    the number is recorded in DESIGN.md §6 and written to gpurun_out/e2e_seg_agreement.json).
+  * the bf16 CPnet's (and an fp32 GPU CPnet's) masks vs the same network in fp32 on the CPU,
+    then the oracle's dynamics: identical-mask and IoU-matched fractions (north_star asks for
+    identical IDs; recorded in DESIGN.md §6 and gpurun_out/e2e_seg_agreement.json).
 """
 import json
 import os
@@ -92,40 +92,65 @@ def test_e2e_objects_and_features(e2e, objset):
         np.testing.assert_allclose(res.feats[objset][b], ref, rtol=1e-5, atol=1e-9)
 
 
-def _match(a, b):
-    """Objects of label image a with an identical pixel set and identical label in b."""
+def _agreement(a, b):
+    """Objects of label image a vs b: identical pixel set AND label; one-to-one matches by
+    IoU >= 0.5 (with the matched label's id equal or not) and their mean IoU."""
     ids = np.unique(a[a > 0])
-    same = 0
+    same = matched = same_id = 0
+    ious = []
     for l in ids:
         m = a == l
-        same += bool(np.array_equal(m, b == l))
-    return same, len(ids)
+        if np.array_equal(m, b == l):
+            same += 1
+        cand = b[m]
+        cand = cand[cand > 0]
+        if cand.size == 0:
+            continue
+        k = np.bincount(cand).argmax()
+        mb = b == k
+        iou = np.logical_and(m, mb).sum() / np.logical_or(m, mb).sum()
+        if iou >= 0.5:
+            matched += 1
+            same_id += int(k == l)
+            ious.append(iou)
+    n = max(len(ids), 1)
+    return {"objects": int(len(ids)), "identical_mask_and_id": int(same), "fraction_identical": same / n,
+            "matched_iou50": int(matched), "fraction_matched": matched / n,
+            "matched_same_id": int(same_id), "mean_iou_matched": float(np.mean(ious)) if ious else 0.0}
 
 
-def test_e2e_bf16_vs_fp32_network_agreement(e2e):
-    """Masks of the bf16 MFMA CPnet vs the same weights in fp32 on the CPU (same tiles, same
-    restated dynamics): report the fraction of identical objects; require most of them."""
+def test_e2e_network_precision_agreement(e2e, dev):
+    """Masks of the bf16 MFMA CPnet and of the same weights in fp32 on the GPU (eager PyTorch)
+    vs fp32 on the CPU, all followed by the same restated dynamics.  The dynamics amplify any
+    flow difference at mask boundaries, so identical masks need identical flows; the numbers
+    are recorded in DESIGN.md §6 (gpurun_out/e2e_seg_agreement.json).  Required: >= 90 % of the
+    fp32-CPU objects matched one-to-one (IoU >= 0.5) by the bf16 masks."""
     from cpx.cpnet import build_cpnet
+    from cpx.segment import Segmenter
     torch.set_num_threads(16)
     cfg = e2e["cfg"]
     net = build_cpnet(seed=cfg.seed, model=cfg.model, state_dict_path=cfg.weights)
     H, W = cfg.H, cfg.W
+    B = e2e["yf"].shape[0]
     Ly, Lx = so.net_size(H, W, cfg.model, cfg.diameter)
+    seg32 = Segmenter(dev, H, W, B, model=cfg.model, diameter=cfg.diameter, weights=cfg.weights,
+                      seed=cfg.seed, use_graph=False, max_objects=cfg.max_objects,
+                      net_dtype=torch.float32, fused=False)
+    lab32 = seg32.segment(torch.from_numpy(e2e["corr"]).to(dev.torch_device)).cpu().numpy()
     rows = []
-    for b in range(e2e["yf"].shape[0]):
+    for b in range(B):
         tiles, g = so.make_net_input(e2e["corr"][b], Ly, Lx)
         with torch.no_grad():
             y = net(torch.from_numpy(tiles)).numpy()
         yf32 = so.average_tiles(y, g)
-        m32 = so.compute_masks(yf32, H, W)
-        mbf = e2e["labels"]["Nuclei"][b]
-        same, n = _match(m32, mbf)
-        rows.append({"fov": b, "objects_fp32": int(n), "objects_bf16": int(mbf.max()),
-                     "identical_mask_and_id": int(same), "fraction": same / max(n, 1),
-                     "max_abs_flow_diff": float(np.abs(yf32 - e2e["yf"][b]).max())})
+        m_cpu = so.compute_masks(yf32, H, W)
+        r = {"fov": b, "max_abs_flow_diff_bf16": float(np.abs(yf32 - e2e["yf"][b]).max()),
+             "bf16_gpu_vs_fp32_cpu": _agreement(m_cpu, e2e["labels"]["Nuclei"][b]),
+             "fp32_gpu_vs_fp32_cpu": _agreement(m_cpu, lab32[b])}
+        rows.append(r)
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     with open(os.path.join(REPO, "gpurun_out", "e2e_seg_agreement.json"), "w") as f:
         json.dump(rows, f, indent=1)
     print(json.dumps(rows))
     for r in rows:
-        assert r["fraction"] >= 0.5, r
+        assert r["bf16_gpu_vs_fp32_cpu"]["fraction_matched"] >= 0.9, r

@@ -1,0 +1,129 @@
+"""Multi-process plate runs (cpx.plate / cpx.launch): well shards,
+per-rank parquet parts, merge into CSVs sorted by (ImageNumber, ObjectNumber) — byte-identical
+to one process.  CPU: world-2 gloo ranks with a stub measurement; GPU: two real pipeline
+processes on the one GPU vs one process."""
+import filecmp
+import os
+import socket
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from cpx import plate
+from cpx.csvout import OBJECT_TABLES, PlateTables
+
+
+def _table(n_wells=7, sites=3):
+    rows = []
+    for w in range(n_wells):
+        for s in range(sites):
+            rows.append({"Metadata_Plate": "P01", "Metadata_Well": f"C{w + 1:02d}", "Metadata_Site": s + 1,
+                         "Metadata_Timepoint": 24, "FileName_DNA": f"w{w}s{s}.tiff"})
+    return pd.DataFrame(rows)
+
+
+def _stub_frames(table, rows, chans=("DNA",)):
+    """Deterministic fake measurements of the given LoadData rows."""
+    out = PlateTables(list(chans))
+    status = []
+    for i in rows:
+        img = i + 1
+        rng = np.random.default_rng(img)
+        k = int(rng.integers(0, 4))
+        out.add_image(img, table.iloc[i].to_dict(), rng.standard_normal(1), rng.random(1),
+                      {t: k for t in OBJECT_TABLES})
+        for t in OBJECT_TABLES:
+            out.add_objects(t, img, np.arange(1, k + 1), rng.standard_normal((k, len(out.cols))))
+        status.append({"ImageNumber": img, "status": "success" if k else "empty", "n_cells": k})
+    f = out.frames()
+    f["site_status"] = pd.DataFrame(status, columns=["ImageNumber", "status", "n_cells"])
+    return f
+
+
+def test_shard_rows_keeps_wells_together():
+    t = _table()
+    parts = [plate.shard_rows(t, r, 3) for r in range(3)]
+    assert sorted(sum(parts, [])) == list(range(len(t)))
+    for r, p in enumerate(parts):
+        assert {w % 3 for w in t.iloc[p]["Metadata_Well"].str[1:].astype(int) - 1} == {r}
+    assert plate.shard_rows(t, 0, 1) == list(range(len(t)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, d):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t = _table()
+        plate.write_part(d, rank, world, _stub_frames(t, plate.shard_rows(t, rank, world)))
+        dist.barrier()
+        if rank == 0:
+            plate.merge_parts(d, world)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_parts_merge_byte_identical(tmp_path):
+    t = _table()
+    one = tmp_path / "one"
+    one.mkdir()
+    for name, df in _stub_frames(t, list(range(len(t)))).items():
+        df.to_csv(one / f"{name}.csv", index=False)
+    two = tmp_path / "two"
+    two.mkdir()
+    ctx = mp.get_context("spawn")
+    port = _port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, str(two))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert not (two / plate.PARTS).exists()
+    for name in ("Image", *OBJECT_TABLES, "site_status"):
+        assert filecmp.cmp(one / f"{name}.csv", two / f"{name}.csv", shallow=False), name
+
+
+@pytest.mark.gpu
+def test_launch_two_processes_one_gpu_byte_identical(tmp_path, dev):
+    """cpx.launch with two ranks on the one GPU == one cpx.plate process, byte for byte; a
+    missing plane gives the reference's 'empty' site in both."""
+    from cpx import launch, tiffio
+    from cpx.synth import synth_fovs
+    n, C, H, W = 6, 2, 384, 416
+    chans = ["DNA", "AGP"]
+    raw = synth_fovs(n, C, H, W, dev.torch_device, seed=9).cpu().numpy().view(np.uint16)
+    imgdir = tmp_path / "images"
+    imgdir.mkdir()
+    rows = []
+    for f in range(n):
+        row = {"Metadata_Plate": "P03", "Metadata_Well": f"D{f // 2 + 1:02d}", "Metadata_Site": f % 2 + 1,
+               "Metadata_Timepoint": 6}
+        for c, ch in enumerate(chans):
+            name = f"f{f}c{c}.tiff"
+            if not (f == 3 and c == 1):  # one missing plane -> empty site
+                tiffio.imwrite(str(imgdir / name), raw[f * C + c])
+            row[f"FileName_{ch}"] = name
+        rows.append(row)
+    ld = tmp_path / "ld.csv"
+    pd.DataFrame(rows).to_csv(ld, index=False)
+    common = ["--load-data", str(ld), "--data-path", str(imgdir), "--channels", *chans,
+              "--batch", "2", "--threads", "2", "--pipes", "1"]
+    d1 = plate.run(common + ["--out", str(tmp_path / "one"), "--world", "1", "--rank", "0"])
+    dirs = launch.main(["--gpus", "2", "--devices", "0,0", "--", *common, "--out", str(tmp_path / "two")])
+    d2 = dirs[0]
+    st = pd.read_csv(os.path.join(d1, "site_status.csv"))
+    assert st.loc[st.ImageNumber == 4, "status"].item() == "empty"
+    for name in ("Image", *OBJECT_TABLES, "site_status"):
+        assert filecmp.cmp(os.path.join(d1, f"{name}.csv"), os.path.join(d2, f"{name}.csv"), shallow=False), name
