@@ -105,6 +105,7 @@ SIGNATURES = {
     "cpx_seg_percentiles": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "cpx_seg_tiles": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P]),
     "cpx_seg_average": (_I, [_P, _P, _I, _I, _I, _P, _P, _P]),
+    "cpx_embed_preprocess": (_I, [_P, _P, _P, _I, _I, _I, ct.c_float, ct.c_float, _P]),
     "cpx_seg_masks": (_I, [_P, _P, _I, _P, _I, _I, _I, ct.c_double, _I, _I, _I, _P, _P]),
     "cpx_cpnet_epilogue": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I]),
     "cpx_cpnet_pool": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),

@@ -1,0 +1,303 @@
+"""Per-cell embeddings — the MI355X counterpart of Cellpose_GPU_s3fs.py.
+
+Same contract as the reference script:
+  * flags (:478-489) --bucket_input --data_base_path --num_consumers --max_workers
+    --load_data_key --csv_image_key --channels --out_data_path --single_cell --save_coords
+    --xgb_model_path --filter_dead_cells (+ --local-root: a directory standing in for S3 — the
+    LoadData CSV is <local-root>/<bucket_input>/<load_data_key>, outputs go under
+    <local-root>/<out_data_path>);
+  * --csv_image_key: LoadData rows with ImageQC_* flags are dropped and the planes divided by
+    <csv_image_key>/<ch>_illum.npy (:252-255, :53-74);
+  * per site: segmentation (Cellpose nuclei, diameter 100), regionprops in label order, integer
+    centroids, cells whose 200 x 200 box leaves the image dropped, masked crops, per crop and
+    channel scale_to_8bit -> RGB -> EfficientNetV2-L pooler_output (1280) under fp16 autocast
+    (:140-206); a site that cannot be read, or has no (kept) cell, is {'status': 'empty',
+    'n_cells': 0} (:123-136, :150-152, :172-174);
+  * outputs (:326-471): <out>_counts.csv (LoadData + Cell_Count [+ Dead_Cells]),
+    <out>_coords.parquet (--save_coords: Cell_ID "{well}_{site}_cell{i}", Y_Center, X_Center,
+    Is_Dead), <out>_well_aggregated.parquet (per Metadata_Well: mean_features = per-channel
+    mean embedding, Cell_Count, first Metadata_Timepoint / Metadata_Plate), and with
+    --single_cell <out>_single_cell.parquet (one row per cell: LoadData columns, Cell_Index,
+    single_cell_features = the C x 1280 vector).
+Design: the GPU path of cpx.pipeline (illumination, segmentation, object table, a7 crops with
+the a9 scale_to_8bit fused) runs on batches of FOVs resident in HBM; libcpx
+cpx_embed_preprocess does the processor's bicubic resize / normalisation (Pillow-exact 8-bit
+arithmetic) straight from the crops; the EfficientNetV2-L forward runs in PyTorch-ROCm under
+fp16 autocast (channels_last), as the reference's.  The result assembly is the reference's own
+pandas / numpy arithmetic (host).  Weights: timm/tf_efficientnetv2_l.in21k is a remote
+download, so --effnet-weights takes a local state_dict, else a seeded initialisation
+(embedding values parity-unpinned).
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+
+import numpy as np
+
+from . import effnet
+
+log = logging.getLogger("cpx.embed")
+BOX_SIZE = 200                 # Cellpose_GPU_s3fs.py:30
+INFERENCE_BATCH_SIZE = 1000    # :31 (images per forward; halved on out-of-memory)
+
+
+class Embedder:
+    """EfficientNetV2-L on one device: crops8 [B][ML][C][S][S] uint8 -> per FOV [n, C, 1280]."""
+
+    def __init__(self, dev, weights: str | None = None, seed: int = 0, batch_images: int = 256,
+                 size: int = effnet.INPUT_SIZE):
+        import torch
+        self.dev, self.torch = dev, torch
+        self.size = size
+        self.batch = batch_images
+        self.model = effnet.build_effnet(seed=seed, state_dict_path=weights).to(dev.torch_device)
+        self.model = self.model.to(memory_format=torch.channels_last)
+
+    def pixel_values(self, crops8, index, S):
+        """Preprocessed fp16 [len(index), 3, D, D] for the crop images at `index` (int64 image
+        offsets into crops8)."""
+        from ._lib import check
+        from .device import _ptr
+        torch = self.torch
+        idx = torch.as_tensor(np.asarray(index, np.int64), device=self.dev.torch_device)
+        out = torch.empty((len(index), 3, self.size, self.size), dtype=torch.float16, device=self.dev.torch_device)
+        self.dev._bind_stream()
+        check(self.dev.lib.cpx_embed_preprocess(self.dev.h, _ptr(crops8), _ptr(idx), len(index), S, self.size,
+                                                float(effnet.MEAN[0]), float(effnet.STD[0]), _ptr(out)),
+              "cpx_embed_preprocess")
+        return out
+
+    def forward(self, x):
+        torch = self.torch
+        with torch.no_grad(), torch.autocast(device_type="cuda", dtype=torch.float16):
+            y = self.model(x.contiguous(memory_format=torch.channels_last))
+        return y.float()
+
+    def embed(self, crops8, n_kept, C: int):
+        """crops8: device uint8 [B][ML][C][S][S] (slot = cell_idx); n_kept: cells per FOV."""
+        torch = self.torch
+        B, ML, _, S, _ = crops8.shape
+        index = [((b * ML + k) * C + c) for b in range(B) for k in range(int(n_kept[b])) for c in range(C)]
+        feats = []
+        i, step = 0, self.batch
+        while i < len(index):
+            j = min(i + step, len(index))
+            try:
+                x = self.pixel_values(crops8, index[i:j], S)
+                feats.append(self.forward(x).cpu().numpy())
+                i = j
+            except torch.cuda.OutOfMemoryError:  # Cellpose_GPU_s3fs.py:196-202
+                torch.cuda.empty_cache()
+                step = max(1, step // 2)
+                if step == 1:
+                    raise
+        allf = np.concatenate(feats) if feats else np.zeros((0, effnet.FEATURE_LENGTH), np.float32)
+        out, o = [], 0
+        for b in range(B):
+            n = int(n_kept[b]) * C
+            out.append(allf[o:o + n].reshape(int(n_kept[b]), C, effnet.FEATURE_LENGTH))
+            o += n
+        return out
+
+
+def assemble(load_data, results, channels, out_data_path, save_coords=False, single_cell=False,
+             xgb=False, filter_dead_cells=False):
+    """Cellpose_GPU_s3fs.py:326-471 on the per-site results
+    {index: {'status', 'features' [n, C, 1280] float32, 'coords' [(y, x)], 'is_dead' [n]}}.
+    Returns the output paths written."""
+    import pandas as pd
+    C = len(channels)
+    L = effnet.FEATURE_LENGTH
+    load_data = load_data.copy()
+    original_indices = list(load_data.index)
+    site_features, site_coords, site_dead_flags = [], [], []
+    for idx in original_indices:
+        res = results[idx]
+        if res["status"] == "empty":
+            site_features.append(np.zeros((0, C, L), dtype=np.float32))
+            site_coords.append([])
+            site_dead_flags.append(np.array([], dtype=bool))
+        else:
+            site_features.append(res["features"])
+            site_coords.append([tuple(c) for c in res["coords"]])
+            site_dead_flags.append(res["is_dead"])
+    aggregated_features, final_site_counts, final_dead_counts = [], [], []
+    for feats, flags in zip(site_features, site_dead_flags):
+        if len(feats) == 0:
+            aggregated_features.append(np.zeros((C, L), dtype=np.float32))
+            final_site_counts.append(0)
+        elif xgb and filter_dead_cells:
+            alive = ~flags
+            n_alive = int(np.sum(alive))
+            aggregated_features.append(np.sum(feats[alive], axis=0) if n_alive > 0 else np.zeros((C, L), np.float32))
+            final_site_counts.append(n_alive)
+            final_dead_counts.append(int(flags.sum()))
+        else:
+            aggregated_features.append(np.sum(feats, axis=0))
+            final_site_counts.append(len(feats))
+    load_data["Cell_Count"] = final_site_counts
+    if xgb:
+        load_data["Dead_Cells"] = final_dead_counts
+    written = []
+    counts_out_path = out_data_path.replace(".parquet", "_counts.csv")
+    os.makedirs(os.path.dirname(os.path.abspath(counts_out_path)), exist_ok=True)
+    load_data.to_csv(counts_out_path, index=False)
+    written.append(counts_out_path)
+    if save_coords:
+        recs = []
+        for idx, coords_list, dead_flags in zip(original_indices, site_coords, site_dead_flags):
+            well = load_data.loc[idx, "Metadata_Well"]
+            site = load_data.loc[idx, "Metadata_Site"] if "Metadata_Site" in load_data.columns else str(idx)
+            for cell_idx, (y, x) in enumerate(coords_list):
+                is_dead = dead_flags[cell_idx] if len(dead_flags) > 0 else False
+                recs.append({"Cell_ID": f"{well}_{site}_cell{cell_idx}", "Y_Center": y, "X_Center": x,
+                             "Is_Dead": is_dead})
+        if recs:
+            p = out_data_path.replace(".parquet", "_coords.parquet")
+            pd.DataFrame(recs).to_parquet(p, engine="pyarrow")
+            written.append(p)
+    agg = load_data.copy()
+    agg["sum_features"] = aggregated_features
+    funcs = {"sum_features": lambda s: np.sum(np.stack(s.values), axis=0), "Cell_Count": "sum"}
+    for col in ["Metadata_Well", "Metadata_Timepoint", "Metadata_Plate"]:
+        if col != "Metadata_Well" and col in agg.columns:
+            funcs[col] = "first"
+    well = agg.groupby("Metadata_Well").agg(funcs).reset_index()
+    # numpy 1.24 (requirements.txt:1-12): float32 sums / int count stay float32
+    well["mean_features"] = well.apply(
+        lambda r: (r["sum_features"] / np.float32(r["Cell_Count"])).tolist() if r["Cell_Count"] > 0
+        else np.zeros((C, L)).tolist(), axis=1)
+    well = well.drop(columns=["sum_features"])
+    p = out_data_path.replace(".parquet", "_filtered_well_aggregated.parquet" if filter_dead_cells
+                              else "_well_aggregated.parquet")
+    well.to_parquet(p, engine="pyarrow")
+    written.append(p)
+    if single_cell:
+        sc = out_data_path.replace(".parquet", "_single_cell.parquet")
+        valid = [i for i, f in enumerate(site_features) if len(f) > 0]
+        if not valid:
+            load_data.to_parquet(sc, engine="pyarrow")
+            return written + [sc]
+        sites = load_data.iloc[valid].copy()
+        vf = [site_features[i] for i in valid]
+        flags = [site_dead_flags[i] for i in valid]
+        ex = sites.loc[sites.index.repeat([len(f) for f in vf])].copy()
+        ex["Cell_Index"] = ex.groupby(level=0).cumcount()
+        st = np.concatenate(vf, axis=0)
+        ex["single_cell_features"] = list(st.reshape(st.shape[0], -1))
+        if xgb:
+            ex["is_dead_cell"] = np.concatenate(flags)
+        if "Cell_Count" in ex.columns:
+            ex = ex.drop(columns=["Cell_Count"])
+        ex.to_parquet(sc, engine="pyarrow", row_group_size=100000)
+        written.append(sc)
+    return written
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description="Cell segmentation, crops and EfficientNetV2-L embeddings on the GPU.")
+    ap.add_argument("--bucket_input", type=str, required=True)
+    ap.add_argument("--data_base_path", type=str, required=True)
+    ap.add_argument("--num_consumers", type=int, default=2, help="pipelines (batches in flight) on the GPU")
+    ap.add_argument("--max_workers", type=int, default=24, help="TIFF decode threads")
+    ap.add_argument("--load_data_key", type=str, required=True)
+    ap.add_argument("--csv_image_key", type=str, required=False)
+    ap.add_argument("--channels", nargs="+", type=str, required=True)
+    ap.add_argument("--out_data_path", type=str, required=True)
+    ap.add_argument("--single_cell", action="store_true")
+    ap.add_argument("--save_coords", action="store_true")
+    ap.add_argument("--xgb_model_path", type=str, default=None)
+    ap.add_argument("--filter_dead_cells", action="store_true")
+    ap.add_argument("--local-root", default="", help="directory standing in for S3 (bucket/key paths)")
+    ap.add_argument("--batch", type=int, default=8, help="FOVs per GPU batch")
+    ap.add_argument("--effnet-weights", default=None, help="local EfficientNetV2-L state_dict")
+    ap.add_argument("--cpnet-weights", default=None)
+    ap.add_argument("--device", type=int, default=0)
+    return ap.parse_args(argv)
+
+
+def run(argv=None):
+    import concurrent.futures
+    import pandas as pd
+    import torch
+    from . import tiffio
+    from .device import Device, as_numpy
+    from .pipeline import FovPipeline, PipelineConfig
+    from .plate import qc_filter
+    a = parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
+    root = a.local_root
+    load_data = pd.read_csv(os.path.join(root, a.bucket_input, a.load_data_key))
+    if a.csv_image_key:
+        load_data = qc_filter(load_data, pd.read_csv(os.path.join(a.csv_image_key, "Image.csv")))
+    else:
+        log.info("No csv_image_key provided — skipping image QC filtering.")
+    bst = None
+    if a.xgb_model_path:
+        import xgboost as xgb  # the reference's optional dead-cell classifier (absent here: fails loudly)
+        bst = xgb.Booster()
+        bst.load_model(a.xgb_model_path)
+    chans = list(a.channels)
+    C = len(chans)
+    tasks = [(idx, [f"{a.data_base_path}/{row[f'FileName_{c}']}" for c in chans]) for idx, row in load_data.iterrows()]
+    illum = None
+    if a.csv_image_key:
+        illum = [np.load(f"{a.csv_image_key}/{c}_illum.npy") for c in chans]
+    first = next(tiffio.imread(p[0]) for _, p in tasks if os.path.exists(p[0]))
+    H, W = first.shape
+    cw = a.cpnet_weights or os.path.join(os.path.dirname(__file__), "weights", "cpnet_nuclei_synth.pt")
+    cfg = PipelineConfig(H=H, W=W, C=C, batch=a.batch, channels=tuple(chans), crops=True, crops_f32=False, box=BOX_SIZE,
+                         weights=cw if os.path.exists(cw) else None)
+    dev = Device(a.device)
+    pipe = FovPipeline(dev, cfg, None if illum is None else np.stack([x.astype(np.float32) for x in illum]))
+    emb = Embedder(dev, a.effnet_weights)
+    results = {}
+
+    def read(paths):
+        try:
+            planes = [tiffio.imread(p) for p in paths]
+            if any(p.shape != (H, W) for p in planes):
+                raise ValueError("plane shape")
+            return np.stack(planes).astype(np.uint16)
+        except Exception as e:  # noqa: BLE001 (producer sends (site_id, None))
+            log.error(f"failed on site: {e}")
+            return None
+
+    B = cfg.batch
+    with concurrent.futures.ThreadPoolExecutor(max(1, a.max_workers)) as ex:
+        for i in range(0, len(tasks), B):
+            chunk = tasks[i:i + B]
+            fovs = list(ex.map(read, [p for _, p in chunk]))
+            host = np.zeros((B * C, H, W), np.uint16)
+            for k, f in enumerate(fovs):
+                if f is not None:
+                    host[k * C:(k + 1) * C] = f
+            slot = pipe.run(torch.from_numpy(host.view(np.int16)).to(dev.torch_device))
+            res = pipe.fetch(slot)
+            kept = [0 if fovs[k] is None else int(res.hdr["Nuclei"][k]["n_kept"]) for k in range(len(chunk))]
+            kept += [0] * (B - len(chunk))
+            feats = emb.embed(pipe.crops8, kept, C)
+            for k, (idx, _) in enumerate(chunk):
+                if fovs[k] is None or kept[k] == 0:
+                    results[idx] = {"status": "empty", "n_cells": 0}
+                    continue
+                o = res.objects["Nuclei"][k]
+                o = o[o["kept"] != 0]
+                o = o[np.argsort(o["cell_idx"])]
+                f = feats[k]
+                is_dead = np.zeros(len(f), dtype=bool)
+                if bst is not None:
+                    import xgboost as xgb
+                    is_dead = bst.predict(xgb.DMatrix(f.reshape(len(f), -1))) > 0.5
+                results[idx] = {"status": "success", "features": f, "n_cells": len(f),
+                                "coords": list(zip(o["yc"].tolist(), o["xc"].tolist())), "is_dead": is_dead}
+            log.info("sites %d-%d of %d embedded", i + 1, i + len(chunk), len(tasks))
+    out_path = os.path.join(root, a.out_data_path) if root else a.out_data_path
+    return assemble(load_data, results, chans, out_path, a.save_coords, a.single_cell,
+                    bst is not None, a.filter_dead_cells)
+
+
+if __name__ == "__main__":
+    run()

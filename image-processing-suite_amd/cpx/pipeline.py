@@ -48,6 +48,7 @@ class PipelineConfig:
     seed: int = 0
     use_graph: bool = True
     crops: bool = False              # a7 crops for the embedding consumer (off in the bench)
+    crops_f32: bool = True           # also keep the float crops (the embedder needs only crops8)
     slots: int = 2                   # result buffer sets (fetch of step i overlaps step i + 1)
 
 
@@ -99,7 +100,8 @@ class FovPipeline:
         self._use_slot(0)
         self.crops = None
         if cfg.crops:
-            self.crops = torch.zeros((B, ML, cfg.box, cfg.box, C), dtype=torch.float32, device=td)
+            self.crops = (torch.zeros((B, ML, cfg.box, cfg.box, C), dtype=torch.float32, device=td)
+                          if cfg.crops_f32 else None)
             self.crops8 = torch.zeros((B, ML, C, cfg.box, cfg.box), dtype=torch.uint8, device=td)
         dev.reserve(B * C, H, W, B, ML)
 
@@ -129,7 +131,7 @@ class FovPipeline:
             self.dev.objects(self.labels[s], cfg.max_objects, cfg.box, self.lstats, self.objects[s], self.hdr[s])
             self.dev.features(self.labels[s], self.corr, cfg.C, cfg.max_objects, self.objects[s],
                               self.hdr[s], self.feats[s])
-        if self.crops is not None:
+        if self.cfg.crops:
             self.dev.objects(self.labels["Nuclei"], cfg.max_objects, cfg.box, self.lstats,
                              self.objects["Nuclei"], self.hdr["Nuclei"])
             self.dev.crops(self.labels["Nuclei"], self.corr, cfg.C, cfg.max_objects, self.objects["Nuclei"],

@@ -28,6 +28,9 @@ struct cpx_ctx {
   cpx_fov_state* fov = nullptr;
   // re-binning coefficient tables currently uploaded (WS_REBIN): W, out_w, H, out_h
   int rebin_key[4] = {0, 0, 0, 0};
+  // embedding preprocessing coefficient table currently uploaded (WS_EMBED): S, D
+  int embed_key[2] = {0, 0};
+  void* embed_tab = nullptr;
 };
 
 void cpx_fov_free(cpx_ctx* ctx);
@@ -47,6 +50,7 @@ enum {
   WS_SEG_FILL = 10,  // fill-hole owner map
   WS_REBIN = 11,     // LANCZOS re-binning bounds + weights (both axes)
   WS_REBIN_TMP = 12, // re-binning horizontal-pass intermediate (16-bit)
+  WS_EMBED = 13,     // embedding preprocessing coefficients + horizontal-pass intermediate
 };
 
 void cpx_set_error(const char* fmt, ...);

@@ -278,7 +278,7 @@ __global__ __launch_bounds__(kThreads) void k_crops(const int* __restrict__ labe
   const int* lab = labels + (long long)fov * N;
   const float* img = corr + (long long)fov * C * N;
   const long long npx = (long long)box * box;
-  float* dst = crops + ((long long)fov * max_crops + slot) * npx * C;
+  float* dst = crops ? crops + ((long long)fov * max_crops + slot) * npx * C : nullptr;
   __shared__ float smin[8][kThreads / 64], smax[8][kThreads / 64];
   float mn[8], mx[8];
   for (int ch = 0; ch < C && ch < 8; ++ch) {
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(kThreads) void k_crops(const int* __restrict__ labe
     const bool in = lab[gi] == o.label;
     for (int ch = 0; ch < C; ++ch) {
       const float v = img[ch * N + gi] * (in ? 1.0f : 0.0f);
-      dst[p * C + ch] = v;
+      if (dst) dst[p * C + ch] = v;
       if (ch < 8) {
         mn[ch] = fminf(mn[ch], v);
         mx[ch] = fmaxf(mx[ch], v);
@@ -319,7 +319,14 @@ __global__ __launch_bounds__(kThreads) void k_crops(const int* __restrict__ labe
     for (long long p = threadIdx.x; p < npx; p += kThreads) {
       unsigned char u = 0;
       if (b != a) {
-        const float v = dst[p * C + ch];
+        float v;
+        if (dst) {
+          v = dst[p * C + ch];
+        } else {  // no float crop kept: the same masked value again from the plane
+          const int yy = (int)(p / box), xx = (int)(p % box);
+          const long long gi = (long long)(y1 + yy) * W + (x1 + xx);
+          v = img[ch * N + gi] * (lab[gi] == o.label ? 1.0f : 0.0f);
+        }
         float t = v - a;
         t = 255.0f * t;
         t = t / rng;
@@ -357,8 +364,8 @@ extern "C" int cpx_crops(cpx_ctx* ctx, const int32_t* labels_dev, const float* c
                          int C, int H, int W, int max_label, const cpx_object* objects_dev,
                          const cpx_fov_objects* hdr_dev, int box, int max_crops, float* crops_dev,
                          uint8_t* crops8_dev) {
-  CPX_REQUIRE(ctx && labels_dev && corr_dev && objects_dev && hdr_dev && crops_dev, CPX_ERR_ARG,
-              "cpx_crops: null argument");
+  CPX_REQUIRE(ctx && labels_dev && corr_dev && objects_dev && hdr_dev && (crops_dev || crops8_dev),
+              CPX_ERR_ARG, "cpx_crops: null argument");
   CPX_REQUIRE(B > 0 && B <= 65535 && C > 0 && C <= 8 && H > 0 && W > 0 && box > 0 &&
                   max_crops > 0 && max_label > 0,
               CPX_ERR_ARG, "cpx_crops: bad sizes (C must be <= 8)");

@@ -284,7 +284,8 @@ __global__ __launch_bounds__(kT) void k_seg_average(const void* __restrict__ net
 // dynamics (dynamics.compute_masks) at the dynamics resolution Dy x Dx: the full H x W with
 // resample=True (CellposeModel.eval's default, the reference call), Ly x Lx with resample=False.
 struct DynBufs {
-  float2* dps;           // [B][n] (dY, dX) * cp_mask / 5: the follow_flows field
+  double2* dps;          // [B][n] (dY, dX) * cp_mask / 5: the follow_flows field (fp32 values
+                         // held as fp64: the step's fp64 expression reads them without converting)
   float2* dpf;           // [B][n] (dY, dX) network flows (flow-error input)
   float2* p;             // [B][n] final positions (written for moving pixels only)
   unsigned char* mov;    // [B][n] pixel follows the flow (|dY * cp / 5| > 1e-3)
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(kT) void k_dyn_prep(const float* __restrict__ yf, i
     }
     const float cp = v[2] > 0.0f ? 1.0f : 0.0f;  // cellprob > cellprob_threshold (0.0)
     const float dy = (v[0] * cp) / 5.0f, dx = (v[1] * cp) / 5.0f;
-    d.dps[(long long)fov * n + q] = make_float2(dy, dx);
+    d.dps[(long long)fov * n + q] = make_double2((double)dy, (double)dx);
     d.dpf[(long long)fov * n + q] = make_float2(v[0], v[1]);
     // np.abs(dP[0]) > 1e-3: numpy compares the float32 array with the scalar cast to float32
     const bool moving = fabsf(dy) > 1e-3f;
@@ -408,7 +409,7 @@ __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, in
   if (n_moving < 5) return;  // follow_flows returns inds=None -> no masks
   const int n_in = from_act ? n_moving : in_cnt[fov];
   const int steps = min(K, niter - step0);
-  const float2* __restrict__ I = d.dps + (long long)fov * n;
+  const double2* __restrict__ I = d.dps + (long long)fov * n;
   float2* __restrict__ P = d.p + (long long)fov * n;
   const FollowItem* src = in + (long long)fov * n;
   FollowItem* dst = out + (long long)fov * n;
@@ -437,15 +438,25 @@ __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, in
     for (int s = 0; s < steps; ++s) {
       if (done) continue;
       const int yi = (int)py, xi = (int)px;
-      const double yy = (double)py - (double)yi, xx = (double)px - (double)xi;
       const int y0 = min(Dy - 1, max(0, yi)), x0 = min(Dx - 1, max(0, xi));
-      const int y1 = min(Dy - 1, y0 + 1), x1 = min(Dx - 1, x0 + 1);
-      const float2 a = I[(long long)y0 * Dx + x0], b = I[(long long)y0 * Dx + x1];
-      const float2 c = I[(long long)y1 * Dx + x0], e = I[(long long)y1 * Dx + x1];
-      const double vy = (double)a.x * (1.0 - yy) * (1.0 - xx) + (double)b.x * (1.0 - yy) * xx +
-                        (double)c.x * yy * (1.0 - xx) + (double)e.x * yy * xx;
-      const double vx = (double)a.y * (1.0 - yy) * (1.0 - xx) + (double)b.y * (1.0 - yy) * xx +
-                        (double)c.y * yy * (1.0 - xx) + (double)e.y * yy * xx;
+      const int i00 = y0 * Dx + x0;
+      const int dxo = x0 + 1 < Dx ? 1 : 0, dyo = y0 + 1 < Dy ? Dx : 0;
+      const double2 a = I[i00], b = I[i00 + dxo], c = I[i00 + dyo], e = I[i00 + dyo + dxo];
+      double vy, vx;
+      if (py >= 1.0f && px >= 1.0f) {
+        // yy = frac(py) and 1 - yy are exact in fp32 (multiples of 2^-23 in [0, 1]), so
+        // I * (1 - yy) is exact in fp64 and (I * (1 - yy)) * (1 - xx) == I * w00 with
+        // w00 = (1 - yy) * (1 - xx) exact: the same single rounding, four fewer multiplies
+        const float yf = py - (float)yi, xf = px - (float)xi;
+        const double y1 = (double)yf, x1 = (double)xf, y0d = (double)(1.0f - yf), x0d = (double)(1.0f - xf);
+        const double w00 = y0d * x0d, w01 = y0d * x1, w10 = y1 * x0d, w11 = y1 * x1;
+        vy = a.x * w00 + b.x * w01 + c.x * w10 + e.x * w11;
+        vx = a.y * w00 + b.y * w01 + c.y * w10 + e.y * w11;
+      } else {  // within one pixel of the top / left edge: the literal expression
+        const double yy = (double)py - (double)yi, xx = (double)px - (double)xi;
+        vy = a.x * (1.0 - yy) * (1.0 - xx) + b.x * (1.0 - yy) * xx + c.x * yy * (1.0 - xx) + e.x * yy * xx;
+        vx = a.y * (1.0 - yy) * (1.0 - xx) + b.y * (1.0 - yy) * xx + c.y * yy * (1.0 - xx) + e.y * yy * xx;
+      }
       const float ny = fminf(fLy, fmaxf(0.0f, py + (float)vy));
       const float nx = fminf(fLx, fmaxf(0.0f, px + (float)vx));
       if (ny == py && nx == px) done = true;  // exact fixed point
@@ -928,40 +939,39 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
     if (tid == 0 && niter > 0) T[ym * lx + xm] = 1.0;  // the first iteration's T[centre] += 1
     __syncthreads();
     double nv[U][kFeKS];
-    double nvc = 0.0;  // the centre cell's new value (owner thread only)
-    int ci = -1;       // its unit
+    const int cidx = ym * lx + xm;
+    bool cown = false;  // this thread owns the centre cell
 #pragma unroll
     for (int i = 0; i < U; ++i)
-      if (ujc[i] >= 0) ci = i;
+      if (ujc[i] >= 0) cown = true;
     for (int it = 0; it < niter; ++it) {
 #pragma unroll
       for (int i = 0; i < U; ++i) {
         if (!um[i]) continue;  // no mask cell in this unit (or no unit)
-        // opaque per-iteration base: stops the compiler from keeping every row address of
-        // every unit live across the iteration loop (it hoisted ~90 of them and spilled)
-        int tb = (uy0[i] - 1) * lx + ux[i];
-        int lim = ly - uy0[i];
-        asm volatile("" : "+v"(tb), "+v"(lim));
-        const double* Tu = T + tb;
-        double ul = Tu[-1], uc = Tu[0], ur = Tu[1];
-        double cl = Tu[lx - 1], cc = Tu[lx], cr = Tu[lx + 1];
-        const double* T2 = Tu + min(2, lim) * lx;
-        double dl = T2[-1], dc = T2[0], dr = T2[1];
+        // element offsets of the unit's rows; the opaque base keeps the compiler from holding
+        // every row address of every unit across the iteration loop (it spilled), and rows
+        // past the object's last row read the zero border row (clamped): their sums are
+        // never written
+        int r = (uy0[i] - 1) * lx + ux[i];
+        int rmax = (ly - 1) * lx + ux[i];
+        asm volatile("" : "+v"(r), "+v"(rmax));
+        double ul = T[r - 1], uc = T[r], ur = T[r + 1];
+        r += lx;
+        double cl = T[r - 1], cc = T[r], cr = T[r + 1];
+        r = min(r + lx, rmax);
+        double dl = T[r - 1], dc = T[r], dr = T[r + 1];
 #pragma unroll
         for (int j = 0; j < kFeKS; ++j) {
-          // the next row's loads are issued before this row's sum, which hides their latency;
-          // the scheduling barrier keeps the compiler from hoisting more rows (register budget)
-          // rows past the last strip's object rows read the zero border row (clamped): their
-          // sums are never written
+          // the next row's loads are issued before this row's sum (latency hidden); the
+          // scheduling barrier keeps the compiler from hoisting more rows (register budget)
           double nl = 0.0, nc = 0.0, nr = 0.0;
           if (j + 1 < kFeKS) {
-            const double* Tn = Tu + min(j + 3, lim) * lx;
-            nl = Tn[-1];
-            nc = Tn[0];
-            nr = Tn[1];
+            r = min(r + lx, rmax);
+            nl = T[r - 1];
+            nc = T[r];
+            nr = T[r + 1];
           }
           nv[i][j] = 1 / 9. * (cc + uc + dc + cl + cr + ul + ur + dl + dr);
-          if (j == ujc[i]) nvc = nv[i][j];
           ul = cl; uc = cc; ur = cr;
           cl = dl; cc = dc; cr = dr;
           dl = nl; dc = nc; dr = nr;
@@ -969,19 +979,17 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
         }
       }
       __syncthreads();
-      const bool last = it + 1 == niter;
 #pragma unroll
       for (int i = 0; i < U; ++i) {
         if (!um[i]) continue;
         int wb = uy0[i] * lx + ux[i];
         asm volatile("" : "+v"(wb));
-        double* Tw = T + wb;
 #pragma unroll
         for (int j = 0; j < kFeKS; ++j)
-          if ((um[i] >> j) & 1u) Tw[j * lx] = nv[i][j];
+          if ((um[i] >> j) & 1u) T[wb + j * lx] = nv[i][j];
       }
       // the next iteration's T[centre] += 1, by the centre's owner after its own store
-      if (ci >= 0 && !last) T[ym * lx + xm] = nvc + 1.0;
+      if (cown && it + 1 < niter) T[cidx] = T[cidx] + 1.0;
       __syncthreads();
     }
     // ---- gradients, normalisation, error vs dP/5
@@ -1546,6 +1554,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
   const int ntile = cpx_div_up(std::max(n, nh), kOcTile);
   const size_t sz_f2 = al(sizeof(float2) * B * n);
+  const size_t sz_d2 = al(sizeof(double2) * B * n);
   const size_t sz_b = al((size_t)B * n);
   const size_t sz_h = al(sizeof(int) * B * nh), sz_hb = al((size_t)B * nh);
   const size_t sz_m0 = resample ? 0 : al(sizeof(int) * B * n);
@@ -1557,12 +1566,12 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   const size_t sz_fcnt = al(sizeof(int) * (size_t)B * (rounds + 1));
   const size_t sz_items = al((size_t)16 * B * n);
   const size_t sz_tiles = al(sizeof(int) * (size_t)B * ntile);
-  const size_t total = 3 * sz_f2 + 2 * sz_b + 2 * sz_h + sz_hb + sz_m0 + 2 * sz_seeds + 3 * sz_cnt +
+  const size_t total = sz_d2 + 2 * sz_f2 + 2 * sz_b + 2 * sz_h + sz_hb + sz_m0 + 2 * sz_seeds + 3 * sz_cnt +
                        sz_act + sz_small + sz_tiles + sz_fcnt + 2 * sz_items;
   unsigned char* w = (unsigned char*)cpx_ws(ctx, WS_SEG_DYN, total);
   if (!w) return CPX_ERR_OOM;
   DynBufs d;
-  d.dps = (float2*)w; w += sz_f2;
+  d.dps = (double2*)w; w += sz_d2;
   d.dpf = (float2*)w; w += sz_f2;
   d.p = (float2*)w; w += sz_f2;
   d.mov = w; w += sz_b;

@@ -258,8 +258,8 @@ int cpx_objects(cpx_ctx* ctx, const int32_t* labels_dev, int B, int H, int W, in
 /* ---- a7 crops + a9 scale_to_8bit ------------------------------------------------------------ *
  * Replaces Cellpose_GPU_s3fs.py:164-170 (img[y1:y2,x1:x2,:] * (mask==label)) and :34-43 /
  * :178-181 (scale_to_8bit per crop-channel).  For every kept object of every FOV, writes
- * crops_dev [B][max_crops][box][box][C] float32 (HWC, as the reference's crop) and, if non-NULL,
- * crops8_dev [B][max_crops][C][box][box] uint8.  Slot = cell_idx; cell_idx >= max_crops is
+ * crops_dev [B][max_crops][box][box][C] float32 (HWC, as the reference's crop) and
+ * crops8_dev [B][max_crops][C][box][box] uint8; either may be NULL (not both).  Slot = cell_idx; cell_idx >= max_crops is
  * skipped.  corr_dev is planar [B][C][H][W].                                                    */
 int cpx_crops(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B, int C,
               int H, int W, int max_label, const cpx_object* objects_dev,
@@ -334,6 +334,15 @@ int cpx_seg_average(cpx_ctx* ctx, const void* net_dev, int layout, int B, int no
 int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx_seg_geom* geom, int H,
                   int W, int niter, double flow_threshold, int min_size, int max_objects,
                   int resample, int32_t* labels_dev, cpx_seg_stats* stats_dev);
+
+/* ---- f3: embedding preprocessing ------------------------------------ *
+ * Replaces Cellpose_GPU_s3fs.py:177-187 between scale_to_8bit and the EfficientNetV2-L forward:
+ * PIL L -> RGB, TimmWrapperImageProcessor (Image.resize(D, BICUBIC) with Pillow's 8-bit fixed
+ * point resampler, CenterCrop, ToTensor /255, Normalize (x - mean) / std), fp16 autocast.
+ * crops8_dev: uint8 S x S images; image i of the batch is crops8_dev + index_dev[i] * S * S
+ * (index_dev int64 [N], device).  out_dev: fp16 [N][3][D][D] (R = G = B).                  */
+int cpx_embed_preprocess(cpx_ctx* ctx, const uint8_t* crops8_dev, const int64_t* index_dev, int N,
+                         int S, int D, float mean, float stdv, void* out_dev);
 
 /* ---- a4 CPnet glue (bf16 NHWC activations around MIOpen convolutions) ----------------------
  * Cellpose resnet_torch.CPnet forward (used at Cellpose_GPU_s3fs.py:108-110 through

@@ -163,7 +163,10 @@ def test_crops_and_scale8_bit_exact(dev, golden_dir):
     crops = torch.zeros((1, nk, box, box, C), dtype=torch.float32, device=dev.torch_device)
     crops8 = torch.zeros((1, nk, C, box, box), dtype=torch.uint8, device=dev.torch_device)
     dev.crops(labt, corr, C, 64, obj, hdr, box, nk, crops, crops8)
+    crops8_only = torch.zeros_like(crops8)  # the embedder's call: no float crops kept
+    dev.crops(labt, corr, C, 64, obj, hdr, box, nk, None, crops8_only)
     dev.sync()
+    assert torch.equal(crops8_only, crops8)
     tab = orc.object_table(lab, box)
     ref = orc.crops(np.moveaxis(planes, 0, -1), lab, tab, box)
     assert len(ref) == nk
