@@ -152,6 +152,16 @@ def test_masks_without_flow_filter_and_min_size(dev):
     np.testing.assert_array_equal(got[0], ref)
 
 
+@pytest.mark.parametrize("niter", [0, 7, 300])
+def test_masks_other_niter(dev, niter):
+    """niter below / above the tile kernel's step cap, and 0 (positions stay the starts)."""
+    H, W = 700, 760
+    g = make_geom(H, W)
+    yf, _ = _synthetic_yf(g.Ly, g.Lx, 8)
+    got, _ = _gpu_masks(dev, yf[None], g, H, W, niter=niter)
+    np.testing.assert_array_equal(got[0], so.compute_masks(yf, H, W, niter=niter))
+
+
 def test_moving_threshold_is_float32(dev):
     """|dY * cp / 5| == float32(1e-3) exactly does not move (numpy compares in float32)."""
     H, W = 700, 760

@@ -23,6 +23,8 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -
   python -u bench.py --pipes 1 --steps 3 --warmup 1 --no-cpu-baseline --stage-steps 1 > $O/bench_fetch.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- \
   python -u bench.py --pipes 1 --steps 3 --warmup 1 --no-cpu-baseline --stage-steps 1 > $O/bench_write.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O/mfma -o run -- \
+  python -u bench.py --pipes 1 --steps 3 --warmup 1 --no-cpu-baseline --stage-steps 1 > $O/bench_mfma.log 2>&1
 
 # summarise on the box (raw per-dispatch CSVs are too large to bring back)
 python tools/prof_summary.py $O/kt/run_kernel_trace.csv --steps 4 --md > $O/kernels_steady.md
@@ -30,5 +32,6 @@ python tools/prof_summary.py $O/kt2/run_kernel_trace.csv --steps 4 --md > $O/ker
 cp $O/kt/run_kernel_stats.csv $O/kernel_stats.csv
 cp $O/kt2/run_kernel_stats.csv $O/kernel_stats_concurrent.csv
 python tools/pmc_traffic.py $O/fetch $O/write --batch $BATCH --out $O/pmc_traffic.json > $O/pmc_traffic.log
-rm -rf $O/kt $O/kt2 $O/fetch $O/write
+python tools/pmc_mfma.py $O/mfma --out $O/pmc_mfma.json > $O/pmc_mfma.log
+rm -rf $O/kt $O/kt2 $O/fetch $O/write $O/mfma
 echo done
