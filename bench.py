@@ -345,7 +345,8 @@ def cpu_baseline(ctx, pool_batch, illum, C, H, W, cfg):
         for i in range(n):
             path = os.path.join(td, f"fov{i}.npy")
             np.save(path, raw[i % B])
-            jobs.append((path, ill_path, cfg.weights, cfg.seed, cfg.model, cfg.diameter, cfg.cell_expand))
+            jobs.append((path, ill_path, cfg.weights, cfg.seed, cfg.model, cfg.diameter, cfg.cell_expand,
+                         cfg.cells, cfg.cell_channel))
         t0 = time.perf_counter()
         with ctx.Pool(cores) as pool:
             out = pool.map(_cpu_worker, jobs, chunksize=1)
@@ -356,7 +357,7 @@ def cpu_baseline(ctx, pool_batch, illum, C, H, W, cfg):
             "sample": f"{n} FOVs of the same synthetic plate ({H}x{W}x{C}), one per worker process "
                       f"(multiprocessing forkserver Pool({cores}), OMP_NUM_THREADS=1), "
                       f"oracle/cpu_pipeline.run_fov = the CPU restatement (QC, fp32 CPnet, "
-                      f"full-resolution dynamics with the C oracle loops, features); value = FOVs / "
+                      f"full-resolution dynamics with the C oracle loops, Cells by the heap watershed in C, features); value = FOVs / "
                       f"slowest worker; wall incl. start-up {wall:.1f} s; mean stage seconds: " +
                       ", ".join(f"{k}={v:.2f}" for k, v in mean.items())}
 
@@ -370,12 +371,13 @@ def _cpu_worker(job):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import cpu_pipeline
     from cpx.cpnet import build_cpnet
-    path, ill_path, weights, seed, model, diameter, expand = job
+    path, ill_path, weights, seed, model, diameter, expand, cells, cell_ch = job
     raw = np.load(path)
     illum = np.load(ill_path, mmap_mode="r")
     net = build_cpnet(seed=seed, model=model, state_dict_path=weights)
     tm = {}
-    cpu_pipeline.run_fov(raw, np.asarray(illum), net, expand, model, diameter, timings=tm)
+    cpu_pipeline.run_fov(raw, np.asarray(illum), net, expand, model, diameter, timings=tm, cells=cells,
+                         cell_channel=cell_ch)
     return tm
 
 

@@ -102,6 +102,7 @@ SIGNATURES = {
     "cpx_crops": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P]),
     "cpx_features": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cpx_expand_labels": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
+    "cpx_watershed_cells": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I]),
     "cpx_seg_percentiles": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "cpx_seg_tiles": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P]),
     "cpx_seg_average": (_I, [_P, _P, _I, _I, _I, _P, _P, _P]),

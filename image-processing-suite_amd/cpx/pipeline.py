@@ -7,7 +7,8 @@ This is the MI355X replacement of the per-FOV work split across the reference's 
 for a batch of B FOVs that are already resident in HBM (uint16 planes [B*C, H, W]):
   A  libcpx cpx_illum_correct (fp32 corrected planes + PercentMaximal) + cpx_qc_rps (slope)
   B  Segmenter (libcpx normalise/tiles -> CPnet bf16 -> libcpx tile average/dynamics/masks)
-  C  libcpx cpx_expand_labels (Cells, Cytoplasm) + cpx_objects for Nuclei / Cells / Cytoplasm
+  C  libcpx cpx_watershed_cells (Cells by marker watershed from the Nuclei, Cytoplasm; or
+     cpx_expand_labels with cells="expand") + cpx_objects for Nuclei / Cells / Cytoplasm
   D  libcpx cpx_features for the three object sets (+ optional a7 crops)
 Everything is enqueued on one HIP stream.  Results (QC, object tables, features) live in
 `slots` alternating buffer sets: `run()` writes slot i % slots and records an event, and
@@ -41,7 +42,13 @@ class PipelineConfig:
     cpnet_precision: str = "bf16"    # "bf16": native MFMA convolutions (headline); "fp32": the
                                      # same network in fp32 (PyTorch eager), masks identical to
                                      # the fp32 CPU network on the e2e plates
-    cell_expand: int = 15            # Cells = expand_labels(Nuclei, cell_expand)
+    cells: str = "watershed"         # "watershed": marker watershed of the inverted cell channel
+                                     # inside the expand_labels(Nuclei, cell_expand) footprint
+                                     # (DESIGN.md §7); "expand": Cells = that footprint's labels
+    cell_expand: int = 15            # footprint distance (px)
+    cell_channel: int = 3            # watershed elevation channel (AGP)
+    ws_rounds: tuple = (24, 48)      # watershed relax / label tile rounds enqueued per batch
+                                     # (bench plates use <= 9 / <= 17; idle rounds cost ~6 us)
     max_objects: int = 2048          # per FOV and object set
     box: int = 200                   # Cellpose_GPU_s3fs.py:30 BOX_SIZE
     weights: str | None = None       # local CPnet state_dict; None = seeded random init
@@ -124,9 +131,19 @@ class FovPipeline:
         from .device import _ptr
         cfg = self.cfg
         B, H, W = cfg.batch, cfg.H, cfg.W
-        check(self.dev.lib.cpx_expand_labels(self.dev.h, _ptr(self.labels["Nuclei"]), B, H, W,
-                                             cfg.cell_expand, _ptr(self.labels["Cells"]),
-                                             _ptr(self.labels["Cytoplasm"])), "cpx_expand_labels")
+        if cfg.cells == "watershed":
+            st = self.seg.stats  # cpx_seg_stats [B] (32 bytes): cells_status is int32 field 6
+            check(self.dev.lib.cpx_watershed_cells(
+                self.dev.h, _ptr(self.labels["Nuclei"]), _ptr(self.corr), B, cfg.C, cfg.cell_channel,
+                H, W, cfg.cell_expand, cfg.ws_rounds[0], cfg.ws_rounds[1], _ptr(self.labels["Cells"]),
+                _ptr(self.labels["Cytoplasm"]), st.data_ptr() + 6 * 4, 8),
+                "cpx_watershed_cells")
+        elif cfg.cells == "expand":
+            check(self.dev.lib.cpx_expand_labels(self.dev.h, _ptr(self.labels["Nuclei"]), B, H, W,
+                                                 cfg.cell_expand, _ptr(self.labels["Cells"]),
+                                                 _ptr(self.labels["Cytoplasm"])), "cpx_expand_labels")
+        else:
+            raise ValueError(f"PipelineConfig.cells: {cfg.cells!r}")
         for s in OBJECT_SETS:
             self.dev.objects(self.labels[s], cfg.max_objects, cfg.box, self.lstats, self.objects[s], self.hdr[s])
             self.dev.features(self.labels[s], self.corr, cfg.C, cfg.max_objects, self.objects[s],
@@ -192,4 +209,7 @@ class FovPipeline:
             feats[s] = [f[b, : n_b[b]].copy() for b in range(B)]
             objs[s] = [o[b, : n_b[b]].copy() for b in range(B)]
         seg_stats = hb["seg_stats"].numpy().view(SEG_STATS_DTYPE).copy()
+        if self.cfg.cells == "watershed" and (seg_stats["cells_status"] < 0).any():
+            raise RuntimeError("cpx_watershed_cells: the flood did not converge within ws_rounds "
+                               f"{self.cfg.ws_rounds} (status {seg_stats['cells_status'].ravel().tolist()})")
         return FovResults(qc=qc, hdr=hdrs, objects=objs, feats=feats, seg_stats=seg_stats)

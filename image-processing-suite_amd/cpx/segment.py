@@ -54,7 +54,7 @@ class SegGeom(ct.Structure):
 
 
 SEG_STATS_DTYPE = np.dtype([("n_moving", "i4"), ("n_seeds", "i4"), ("n_masks", "i4"),
-                            ("n_bad_flow", "i4"), ("n_final", "i4"), ("overflow", "i4"), ("_pad", "i4", (2,))])
+                            ("n_bad_flow", "i4"), ("n_final", "i4"), ("overflow", "i4"), ("cells_status", "i4"), ("_pad", "i4")])
 
 
 def _pad_amounts(L: int, div: int = 16, extra: int = 1):

@@ -51,6 +51,7 @@ enum {
   WS_REBIN = 11,     // LANCZOS re-binning bounds + weights (both axes)
   WS_REBIN_TMP = 12, // re-binning horizontal-pass intermediate (16-bit)
   WS_EMBED = 13,     // embedding preprocessing coefficients + horizontal-pass intermediate
+  WS_WATERSHED = 14, // Cells watershed flood levels + tile flags
 };
 
 void cpx_set_error(const char* fmt, ...);

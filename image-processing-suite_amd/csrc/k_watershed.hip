@@ -1,0 +1,686 @@
+// a8 secondary objects: Cells by marker watershed from the Nuclei (skimage
+// 0.18.3 segmentation.watershed, skimage/segmentation/_watershed.py:94), Cytoplasm = Cells minus
+// Nuclei.  Stated inputs (oracle/ws_oracle.py): markers = Nuclei, mask = the
+// expand_labels(Nuclei, distance) footprint, elevation key(p) = (65535 - q16(corr_cell(p))) << 23
+// | (y*W + x) — all keys distinct, so skimage's heap flood (pop by (value, age), label at push)
+// has one total pop order and its result has a parallel characterisation:
+//
+//   B(p)  = min over 4-paths marker -> p inside the mask of the max key on the path (markers:
+//           B = key): the flood level at which p is popped (the running max of popped keys);
+//   label = a free pixel is labelled by the first of its neighbours to pop = its neighbour with
+//           the smallest B (neighbours tied on B were popped in the same "phase", opened by the
+//           pass pixel whose key is that B, and carry the same label).
+//
+// Both are computed tile by tile (64 x 64 pixels + 1-pixel halo in LDS), in rounds over the
+// whole batch with no host synchronisation, as label-correcting worklists: only pixels whose
+// level (label) just changed are visited again, so the work is ~2 visits per free pixel instead
+// of whole-tile sweeps (15 % of a FOV's pixels are free: the rings around the nuclei):
+//   k_ws_relax  B(n) = max(key(n), B(p)) pushed from every improved pixel p to its free
+//               neighbours with an LDS atomic min; each wave drains its own LDS queue (no block
+//               barrier per hop), the tile is at its fixed point when every queue is empty;
+//   k_ws_label  a free pixel takes, once, the label of a labelled neighbour whose B is the
+//               minimum of its four neighbours' (write-once: every label written is final);
+// a tile whose border changes flags the facing neighbour, which in the next round re-evaluates
+// only its border pixels against the new halo (a queue overflow re-runs the whole tile).  k_ws_status fails the FOV (status -1) when the
+// rounds enqueued did not reach the fixed point (the host raises).  Exactness vs the sequential
+// heap flood: tests/test_watershed.py (oracle) and tests/test_gpu_watershed.py (this kernel),
+// pinned to skimage itself by tests/golden/watershed_cases.npz.
+#include "cpx_internal.h"
+#include <stdio.h>
+#include <stdlib.h>
+
+namespace {
+
+constexpr int kT = 32;                 // tile edge
+constexpr int kThreads = 64;           // one wave per tile: no block barrier on the hop path,
+constexpr int kWaves = kThreads / 64;  // ~9 independent tiles per CU (17-19 KB of LDS each)
+constexpr int kLS = kT + 3;            // LDS row stride (odd)
+constexpr int kLRows = kT + 2;
+constexpr int kPerThread = kT * kT / kThreads;
+constexpr unsigned long long kBlocked = ~0ull;          // outside the mask / the image
+constexpr unsigned long long kUnreached = ~0ull - 1ull; // free pixel the flood has not reached
+constexpr unsigned kMark = 1u << 16, kBlk = 1u << 17;
+constexpr int kKeyShift = 23;
+// tile flag bits (per round)
+constexpr unsigned char kUp = 1, kLeft = 2, kRight = 4, kDown = 8;  // that border changed
+constexpr unsigned char kSelf = 16;   // a wave queue overflowed: re-run the whole tile
+constexpr unsigned char kUnres = 32;  // label: reached pixels still unlabelled
+constexpr int kQCap = 2048;           // per-wave LDS queue (tile-local pixel indices)
+static_assert(kQCap >= kT * kT + 3 * 64, "the seeds of a whole tile plus one drain step fit");
+static_assert(kWaves == 1, "one wave per tile");
+constexpr unsigned long long kMarkBit = 1ull << 40;  // stored level of a marker: key | kMarkBit
+static_assert(kKeyShift + 16 < 40, "keys stay below the marker bit");
+
+struct WsArgs {
+  const int* nuc;      // [B][H][W] markers
+  const int* foot;     // [B][H][W] expand_labels footprint (!= 0 = in mask)
+  const float* corr;   // [B][C][H][W]
+  int C, ch, H, W, ntx, nty, total;
+  unsigned long long* Bg;  // [B][H][W] stored levels: kBlocked | key | kMarkBit (markers) | B
+  unsigned short* inv;     // [B][H][W] 65535 - q16 of free pixels (tiles with free pixels)
+  unsigned char* tfree;    // [B * tiles] tile has free pixels
+  int* last;               // [B][2] last active relax / label round
+  unsigned long long* dbg; // optional counters (CPX_WS_DEBUG): [kernel][round][4]
+};
+
+__device__ __forceinline__ unsigned q16(float v) {
+  if (!(v < 65535.0f)) return 65535u;  // NaN, inf, >= 65535
+  return v > 0.0f ? (unsigned)v : 0u;  // truncation
+}
+
+__device__ __forceinline__ unsigned long long key_of(unsigned inf, long long pix) {
+  return ((unsigned long long)(inf & 0xffffu) << kKeyShift) | (unsigned long long)pix;
+}
+
+__device__ __forceinline__ unsigned long long init_level(unsigned inf, long long pix) {
+  if (inf & kBlk) return kBlocked;
+  if (inf & kMark) return key_of(inf, pix);
+  return kUnreached;
+}
+
+__device__ __forceinline__ unsigned char border_bits(int y, int x) {
+  unsigned char m = 0;
+  if (y == 0) m |= kUp;
+  if (y == kT - 1) m |= kDown;
+  if (x == 0) m |= kLeft;
+  if (x == kT - 1) m |= kRight;
+  return m;
+}
+
+__device__ __forceinline__ bool neighbour_flagged(const unsigned char* Fp, int fov, int ty, int tx,
+                                                  int nty, int ntx, unsigned char self_bits) {
+  const int base = fov * nty * ntx;
+  const int t = base + ty * ntx + tx;
+  if (Fp[t] & self_bits) return true;
+  if (ty > 0 && (Fp[t - ntx] & kDown)) return true;
+  if (ty + 1 < nty && (Fp[t + ntx] & kUp)) return true;
+  if (tx > 0 && (Fp[t - 1] & kRight)) return true;
+  if (tx + 1 < ntx && (Fp[t + 1] & kLeft)) return true;
+  return false;
+}
+
+// halo pixel h of 4*kT (top row, bottom row, left column, right column) -> tile-local (y, x)
+__device__ __forceinline__ void halo_pos(int h, int& y, int& x) {
+  const int side = h / kT, k = h % kT;
+  if (side == 0) { y = -1; x = k; }
+  else if (side == 1) { y = kT; x = k; }
+  else if (side == 2) { y = k; x = -1; }
+  else { y = k; x = kT; }
+}
+
+
+// stored level -> level (markers: their key); kBlocked / kUnreached are stored as themselves
+__device__ __forceinline__ bool stored_marker(unsigned long long v) { return v < kUnreached && (v & kMarkBit); }
+__device__ __forceinline__ unsigned long long level_of(unsigned long long v) {
+  return stored_marker(v) ? (v & ~kMarkBit) : v;
+}
+
+// wave-local queue of tile pixel indices (ring of kQCap): head / tail are wave-uniform
+struct WaveQueue {
+  unsigned short* q;
+  int head, tail;
+  __device__ __forceinline__ void push(bool pred, int item, int lane) {
+    const unsigned long long m = __ballot(pred);
+    if (pred) {
+      const int pos = tail + __popcll(m & ((1ull << lane) - 1ull));
+      q[pos & (kQCap - 1)] = (unsigned short)item;
+    }
+    tail += __popcll(m);
+  }
+};
+
+__device__ __forceinline__ int lds_off(int i) { return (1 + i / kT) * kLS + 1 + i % kT; }
+
+// index of the k-th border pixel (k < 4*kT) of the tile
+__device__ __forceinline__ int border_pixel(int k) {
+  const int side = k / kT, j = k % kT;
+  if (side == 0) return j;
+  if (side == 1) return (kT - 1) * kT + j;
+  if (side == 2) return j * kT;
+  return j * kT + kT - 1;
+}
+
+
+// Tiles of this block for this round: t = blockIdx.x + k * gridDim.x.  Every thread evaluates one
+// tile's activity at once (flags of the previous round), writes the flags of inactive tiles and
+// appends active ones to the LDS list — an idle round costs one pass over the flags, not a
+// serial walk.  mode 0: relax (tile has free pixels and a facing border changed, or kSelf; every
+// tile active in round 0); mode 1: label (additionally needs kUnres unless kSelf).
+__device__ int schedule_tiles(const WsArgs& a, int round, int mode, const unsigned char* Fp,
+                              unsigned char* Fn, int* list, int* s_n) {
+  if (threadIdx.x == 0) *s_n = 0;
+  __syncthreads();
+  const int per = a.nty * a.ntx;
+  for (int k = threadIdx.x;; k += blockDim.x) {
+    const int t = blockIdx.x + k * gridDim.x;
+    if (t >= a.total) break;
+    const int fov = t / per, tt = t - fov * per, ty = tt / a.ntx, tx = tt - ty * a.ntx;
+    // all flags loaded before use (clamped neighbour indices; edges masked after)
+    const int base = fov * per;
+    const unsigned char fs = Fp[t], fr = a.tfree[t];
+    const unsigned char fu = Fp[ty > 0 ? t - a.ntx : t], fd = Fp[ty + 1 < a.nty ? t + a.ntx : t];
+    const unsigned char fl = Fp[tx > 0 ? t - 1 : t], fg = Fp[tx + 1 < a.ntx ? t + 1 : t];
+    const bool nb = (ty > 0 && (fu & kDown)) || (ty + 1 < a.nty && (fd & kUp)) ||
+                    (tx > 0 && (fl & kRight)) || (tx + 1 < a.ntx && (fg & kLeft));
+    (void)base;
+    bool act;
+    unsigned char keep = 0;
+    if (mode == 0) {
+      act = round == 0 || (fr && (nb || (fs & kSelf)));
+    } else if (!fr) {
+      act = false;
+    } else if (round == 0) {
+      act = true;
+    } else {
+      act = (fs & kSelf) || ((fs & kUnres) && nb);
+      keep = fs & kUnres;
+    }
+    if (act) list[atomicAdd(s_n, 1)] = t;
+    else Fn[t] = keep;
+  }
+  __syncthreads();
+  return *s_n;
+}
+
+// info word from the three inputs: (65535 - q) | marker | blocked
+__device__ __forceinline__ unsigned info_of(int n, int f, float v) {
+  if (n != 0) return (65535u - q16(v)) | kMark;
+  if (f == 0) return kBlk;
+  return 65535u - q16(v);
+}
+
+// border bits of a padded LDS offset (tile rows / columns 1..kT)
+__device__ __forceinline__ unsigned char border_bits_off(int o) {
+  return border_bits(o / kLS - 1, o % kLS - 1);
+}
+
+template <bool R0>
+__global__ __launch_bounds__(kThreads, 3) void k_ws_relax(WsArgs a, int round,
+                                                       const unsigned char* __restrict__ Fp,
+                                                       unsigned char* __restrict__ Fn) {
+  // levels of the tile + halo, and the key of every free tile pixel (kBlocked for markers,
+  // blocked pixels and the halo: max(kBlocked, .) never lowers them, so the pushes need no
+  // bounds or type checks); the queue holds padded LDS offsets
+  __shared__ unsigned long long sB[kLRows * kLS];
+  __shared__ unsigned long long sK[kLRows * kLS];
+  __shared__ unsigned short sQ[kQCap];
+  __shared__ unsigned short sS[kT * kT];  // seed candidates
+  __shared__ unsigned s_bits;
+  __shared__ int s_list[kThreads], s_n;
+  const int lane = threadIdx.x;
+  const long long hw = (long long)a.H * a.W;
+  const int nact = schedule_tiles(a, round, 0, Fp, Fn, s_list, &s_n);
+  const long long hwc = hw * a.C;
+  for (int j = 0; j < nact; ++j) {
+    const int t = s_list[j];
+    const int per = a.nty * a.ntx;
+    const int fov = t / per, tt = t - fov * per, ty = tt / a.ntx, tx = tt - ty * a.ntx;
+    const bool full = R0 || (Fp[t] & kSelf) != 0;
+    const int y0 = ty * kT, x0 = tx * kT;
+    if (lane == 0) s_bits = 0;
+    const int* nucf = a.nuc + fov * hw;
+    const int* footf = a.foot + fov * hw;
+    const float* cf = a.corr + fov * hwc + (long long)a.ch * hw;
+    const unsigned long long* Bf = a.Bg + fov * hw;
+    // every load of the tile and of this lane's halo pixels in flight before any is used
+    // (round 0: nuclei, footprint, cell channel; later rounds: stored level, inverted key)
+    unsigned long long w0_[kPerThread];
+    int w1_[kPerThread];
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) {
+      const int i = lane + k * kThreads, y = y0 + i / kT, x = x0 + i % kT;
+      const long long pix = (y < a.H && x < a.W) ? (long long)y * a.W + x : 0;
+      if (R0) {
+        w0_[k] = ((unsigned long long)(unsigned)nucf[pix] << 32) | (unsigned)footf[pix];
+        w1_[k] = __float_as_int(cf[pix]);
+      } else {
+        w0_[k] = Bf[pix];
+        w1_[k] = a.inv[fov * hw + pix];
+      }
+    }
+    // halo: loads from clamped addresses issued unconditionally with the tile's, resolved after
+    constexpr int kHalo = (4 * kT + kThreads - 1) / kThreads;
+    unsigned long long hw0[kHalo];
+    int hw1[kHalo], ho[kHalo];
+    bool hin[kHalo];
+#pragma unroll
+    for (int k = 0; k < kHalo; ++k) {
+      const int h = lane + k * kThreads;
+      int hy = 0, hx = 0;
+      if (h < 4 * kT) halo_pos(h, hy, hx);
+      ho[k] = h < 4 * kT ? (1 + hy) * kLS + 1 + hx : -1;
+      const int y = y0 + hy, x = x0 + hx;
+      hin[k] = h < 4 * kT && y >= 0 && y < a.H && x >= 0 && x < a.W;
+      const long long pix = hin[k] ? (long long)y * a.W + x : 0;
+      if (R0) {
+        hw0[k] = ((unsigned long long)(unsigned)nucf[pix] << 32) | (unsigned)footf[pix];
+        hw1[k] = __float_as_int(cf[pix]);
+      } else {
+        hw0[k] = Bf[pix];
+        hw1[k] = 0;
+      }
+    }
+    int any_free = 0;
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) {
+      const int i = lane + k * kThreads, y = y0 + i / kT, x = x0 + i % kT;
+      unsigned long long b = kBlocked, key = kBlocked;
+      if (y < a.H && x < a.W) {
+        const long long pix = (long long)y * a.W + x;
+        if (R0) {
+          const unsigned inf = info_of((int)(w0_[k] >> 32), (int)(unsigned)w0_[k], __int_as_float(w1_[k]));
+          b = init_level(inf, pix);
+          if (!(inf & (kMark | kBlk))) key = key_of(inf, pix);
+        } else {
+          const unsigned long long v = w0_[k];
+          b = level_of(v);
+          if (v != kBlocked && !stored_marker(v)) key = key_of((unsigned)w1_[k], pix);
+        }
+      }
+      any_free |= key != kBlocked;
+      sB[lds_off(i)] = b;
+      sK[lds_off(i)] = key;
+    }
+#pragma unroll
+    for (int k = 0; k < kHalo; ++k) {
+      if (ho[k] < 0) continue;
+      unsigned long long hb = kBlocked;
+      if (hin[k]) {
+        const int hh = lane + k * kThreads;
+        int hy, hx;
+        halo_pos(hh, hy, hx);
+        const long long pix = (long long)(y0 + hy) * a.W + x0 + hx;
+        hb = R0 ? init_level(info_of((int)(hw0[k] >> 32), (int)(unsigned)hw0[k], __int_as_float(hw1[k])), pix)
+                : level_of(hw0[k]);
+      }
+      sB[ho[k]] = hb;
+      sK[ho[k]] = kBlocked;
+    }
+    any_free = __syncthreads_or(any_free);
+    if (R0) {
+      if (lane == 0) a.tfree[t] = (unsigned char)(any_free != 0);
+      if (!any_free) {  // no free pixel: only the border ring is ever read (as a neighbour's halo)
+        for (int k = lane; k < 4 * kT; k += kThreads) {
+          const int i = border_pixel(k), y = y0 + i / kT, x = x0 + i % kT;
+          if (y < a.H && x < a.W) {
+            const unsigned long long b = sB[lds_off(i)];
+            a.Bg[fov * hw + (long long)y * a.W + x] = b == kBlocked ? b : (b | kMarkBit);
+          }
+        }
+        if (lane == 0) Fn[t] = 0;
+        __syncthreads();
+        continue;
+      }
+    }
+    WaveQueue wq{sQ, 0, 0};
+    unsigned bits = 0;
+    // seeds: every free pixel (full) or the border pixels (new halo), pulled from its neighbours;
+    // the candidates are compacted first (a fifth of a tile's pixels are free)
+    int nseed = 0;
+    if (full) {
+#pragma unroll
+      for (int k = 0; k < kPerThread; ++k) {
+        const int o = lds_off(lane + k * kThreads);
+        const bool c = sK[o] != kBlocked;
+        const unsigned long long m = __ballot(c);
+        if (c) sS[nseed + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)o;
+        nseed += __popcll(m);
+      }
+    } else {
+      for (int k = lane; k < 4 * kT; k += kThreads) sS[k] = (unsigned short)lds_off(border_pixel(k));
+      nseed = 4 * kT;
+    }
+    __syncthreads();
+    for (int base = 0; base < nseed; base += kThreads) {
+      const int o = base + lane < nseed ? (int)sS[base + lane] : kLS + 1;
+      const unsigned long long key = base + lane < nseed ? sK[o] : kBlocked;
+      bool imp = false;
+      if (key != kBlocked) {
+        const unsigned long long u = sB[o - kLS], l = sB[o - 1], r = sB[o + 1], d = sB[o + kLS];
+        unsigned long long m = u < l ? u : l;
+        m = r < m ? r : m;
+        m = d < m ? d : m;
+        const unsigned long long nv = m > key ? m : key;
+        if (nv < sB[o]) imp = nv < atomicMin(&sB[o], nv);
+      }
+      if (imp) bits |= border_bits_off(o);
+      wq.push(imp, o, lane);
+    }
+    // drain: push the improved level to the four neighbours (all reads of a step issued together)
+    bool ovf = false;
+    int dsteps = 0, ditems = 0;
+    while (wq.tail != wq.head) {
+      const int cnt = min(64, wq.tail - wq.head);
+      ++dsteps;
+      ditems += cnt;
+      if (wq.tail - wq.head + 3 * cnt > kQCap) {
+        ovf = true;
+        break;
+      }
+      const bool act = lane < cnt;
+      const int o = act ? (int)wq.q[(wq.head + lane) & (kQCap - 1)] : kLS + 1;
+      wq.head += cnt;
+      const int nb[4] = {o - kLS, o - 1, o + 1, o + kLS};
+      const unsigned long long b = sB[o];
+      unsigned long long kk[4], bb[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        kk[d] = sK[nb[d]];
+        bb[d] = sB[nb[d]];
+      }
+      bool imp[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const unsigned long long nv = b > kk[d] ? b : kk[d];
+        imp[d] = act && nv < bb[d];
+        if (imp[d]) imp[d] = nv < atomicMin(&sB[nb[d]], nv);
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        if (imp[d]) bits |= border_bits_off(nb[d]);
+        wq.push(imp[d], nb[d], lane);
+      }
+    }
+    if (ovf) bits |= kSelf;
+    if (bits) atomicOr(&s_bits, bits);
+    if (a.dbg && lane == 0) {
+      unsigned long long* c = a.dbg + (0 * 64 + round) * 4;
+      atomicAdd(c, 1ull);
+      atomicAdd(c + 1, (unsigned long long)dsteps);
+      atomicAdd(c + 2, (unsigned long long)ditems);
+      atomicAdd(c + 3, (unsigned long long)ovf);
+    }
+    __syncthreads();
+    for (int i = lane; i < kT * kT; i += kThreads) {
+      const int y = y0 + i / kT, x = x0 + i % kT;
+      if (y >= a.H || x >= a.W) continue;
+      const long long pix = fov * hw + (long long)y * a.W + x;
+      const int o = lds_off(i);
+      const unsigned long long b = sB[o], key = sK[o];
+      if (key != kBlocked) {
+        a.Bg[pix] = b;
+        if (R0) a.inv[pix] = (unsigned short)(key >> kKeyShift);
+      } else if (R0) {
+        a.Bg[pix] = b == kBlocked ? b : (b | kMarkBit);
+      }
+    }
+    if (lane == 0) {
+      Fn[t] = (unsigned char)s_bits;
+      a.last[fov * 2] = round;
+    }
+    __syncthreads();
+  }
+}
+
+template <bool R0>
+__global__ __launch_bounds__(kThreads, 3) void k_ws_label(WsArgs a, int round,
+                                                       const unsigned char* __restrict__ Fp,
+                                                       unsigned char* __restrict__ Fn,
+                                                       int* __restrict__ cells, int* __restrict__ cyto) {
+  // levels (tile + halo); per unlabelled reached free tile pixel the minimum level of its four
+  // neighbours (kBlocked elsewhere); labels (tile + halo: 0 = unknown inside the tile, -1 =
+  // unknown in the halo, which is never a source nor a target)
+  __shared__ unsigned long long sB[kLRows * kLS];
+  __shared__ unsigned long long sM[kLRows * kLS];
+  __shared__ int sL[kLRows * kLS];
+  __shared__ unsigned short sQ[kQCap];
+  __shared__ unsigned short sS[kT * kT];  // seed candidates
+  __shared__ unsigned s_bits;
+  __shared__ int s_list[kThreads], s_n;
+  const int lane = threadIdx.x;
+  const long long hw = (long long)a.H * a.W;
+  const int nact = schedule_tiles(a, round, 1, Fp, Fn, s_list, &s_n);
+  for (int j = 0; j < nact; ++j) {
+    const int t = s_list[j];
+    const int per = a.nty * a.ntx;
+    const int fov = t / per, tt = t - fov * per, ty = tt / a.ntx, tx = tt - ty * a.ntx;
+    const bool full = R0 || (Fp[t] & kSelf) != 0;
+    const int y0 = ty * kT, x0 = tx * kT;
+    if (lane == 0) s_bits = 0;
+    constexpr int kLoads = (kT * kT + 4 * kT + kThreads - 1) / kThreads;
+    unsigned long long bv_[kLoads];
+    int nv_[kLoads], cv_[kLoads];
+#pragma unroll
+    for (int k = 0; k < kLoads; ++k) {
+      const int i = lane + k * kThreads;
+      int iy = 0, ix = 0;
+      if (i < kT * kT) {
+        iy = i / kT;
+        ix = i - iy * kT;
+      } else if (i < kT * kT + 4 * kT) {
+        halo_pos(i - kT * kT, iy, ix);
+      }
+      const int y = y0 + iy, x = x0 + ix;
+      const bool in = i < kT * kT + 4 * kT && y >= 0 && y < a.H && x >= 0 && x < a.W;
+      const long long pix = fov * hw + (in ? (long long)y * a.W + x : 0);
+      bv_[k] = in ? a.Bg[pix] : kBlocked;
+      nv_[k] = a.nuc[pix];
+      cv_[k] = R0 ? 0 : cells[pix];
+    }
+#pragma unroll
+    for (int k = 0; k < kLoads; ++k) {
+      const int i = lane + k * kThreads;
+      if (i >= kT * kT + 4 * kT) continue;
+      int iy, ix;
+      if (i < kT * kT) {
+        iy = i / kT;
+        ix = i - iy * kT;
+      } else {
+        halo_pos(i - kT * kT, iy, ix);
+      }
+      const int o = (1 + iy) * kLS + 1 + ix;
+      const unsigned long long v = bv_[k];
+      int l = v == kBlocked ? 0 : (stored_marker(v) ? nv_[k] : cv_[k]);
+      if (i >= kT * kT && l == 0) l = -1;
+      sB[o] = level_of(v);
+      sL[o] = l;
+      sM[o] = kBlocked;
+    }
+    __syncthreads();
+    // minimum neighbour level of every unlabelled reached free pixel
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) {
+      const int o = lds_off(lane + k * kThreads);
+      if (sL[o] == 0 && sB[o] < kUnreached) {
+        const unsigned long long u = sB[o - kLS], l = sB[o - 1], r = sB[o + 1], d = sB[o + kLS];
+        unsigned long long m = u < l ? u : l;
+        m = r < m ? r : m;
+        sM[o] = d < m ? d : m;
+      }
+    }
+    __syncthreads();
+    WaveQueue wq{sQ, 0, 0};
+    unsigned bits = 0;
+    // seeds: unlabelled pixels (all, or the border ones) that already see a labelled neighbour
+    // at their minimum neighbour level; candidates compacted first
+    int nseed = 0;
+    if (full) {
+#pragma unroll
+      for (int k = 0; k < kPerThread; ++k) {
+        const int o = lds_off(lane + k * kThreads);
+        const bool c = sM[o] != kBlocked;
+        const unsigned long long m = __ballot(c);
+        if (c) sS[nseed + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)o;
+        nseed += __popcll(m);
+      }
+    } else {
+      for (int k = lane; k < 4 * kT; k += kThreads) sS[k] = (unsigned short)lds_off(border_pixel(k));
+      nseed = 4 * kT;
+    }
+    __syncthreads();
+    for (int base = 0; base < nseed; base += kThreads) {
+      const int o = base + lane < nseed ? (int)sS[base + lane] : kLS + 1;
+      const unsigned long long m = base + lane < nseed ? sM[o] : kBlocked;
+      bool got = false;
+      if (m != kBlocked && sL[o] == 0) {
+        const int nb[4] = {o - kLS, o - 1, o + 1, o + kLS};
+        int lab = 0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int ld = sL[nb[d]];
+          if (lab <= 0 && ld > 0 && sB[nb[d]] == m) lab = ld;
+        }
+        if (lab > 0) got = atomicCAS(&sL[o], 0, lab) == 0;
+      }
+      if (got) bits |= border_bits_off(o);
+      wq.push(got, o, lane);
+    }
+    bool ovf = false;
+    int dsteps = 0, ditems = 0;
+    while (wq.tail != wq.head) {
+      const int cnt = min(64, wq.tail - wq.head);
+      ++dsteps;
+      ditems += cnt;
+      if (wq.tail - wq.head + 3 * cnt > kQCap) {
+        ovf = true;
+        break;
+      }
+      const bool act = lane < cnt;
+      const int o = act ? (int)wq.q[(wq.head + lane) & (kQCap - 1)] : kLS + 1;
+      wq.head += cnt;
+      const int nb[4] = {o - kLS, o - 1, o + 1, o + kLS};
+      const unsigned long long bp = sB[o];
+      const int lp = sL[o];
+      unsigned long long mm[4];
+      int ll[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        mm[d] = sM[nb[d]];
+        ll[d] = sL[nb[d]];
+      }
+      bool got[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        got[d] = act && ll[d] == 0 && mm[d] == bp;
+        if (got[d]) got[d] = atomicCAS(&sL[nb[d]], 0, lp) == 0;
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        if (got[d]) bits |= border_bits_off(nb[d]);
+        wq.push(got[d], nb[d], lane);
+      }
+    }
+    if (ovf) bits |= kSelf;
+    if (bits) atomicOr(&s_bits, bits);
+    if (a.dbg && lane == 0) {
+      unsigned long long* c = a.dbg + (1 * 64 + round) * 4;
+      atomicAdd(c, 1ull);
+      atomicAdd(c + 1, (unsigned long long)dsteps);
+      atomicAdd(c + 2, (unsigned long long)ditems);
+      atomicAdd(c + 3, (unsigned long long)ovf);
+    }
+    __syncthreads();
+    int unres = 0;
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) {  // own pixels are the first kPerThread loads
+      const int i = lane + k * kThreads;
+      const int y = y0 + i / kT, x = x0 + i % kT;
+      if (y >= a.H || x >= a.W) continue;
+      const unsigned long long v = bv_[k];
+      if (v == kBlocked || stored_marker(v)) continue;
+      const int o = lds_off(i);
+      const long long pix = fov * hw + (long long)y * a.W + x;
+      const int l = sL[o];
+      unres |= l == 0 && v < kUnreached;
+      cells[pix] = l;
+      cyto[pix] = l;
+    }
+    unres = __syncthreads_or(unres);
+    if (lane == 0) {
+      Fn[t] = (unsigned char)(s_bits | (unres ? kUnres : 0));
+      a.last[fov * 2 + 1] = round;
+    }
+    __syncthreads();
+  }
+}
+
+// per FOV: converged when the last relax round left no border change / capped tile and the
+// last label round no unlabelled reached pixel
+__global__ void k_ws_status(const unsigned char* __restrict__ Fr, const unsigned char* __restrict__ Fl,
+                            int per, const int* __restrict__ last, int* __restrict__ status, int stride) {
+  const int fov = blockIdx.x;
+  int bad = 0;
+  for (int i = threadIdx.x; i < per; i += blockDim.x)
+    bad |= (Fr[fov * per + i] & (kUp | kLeft | kRight | kDown | kSelf)) | (Fl[fov * per + i] & kUnres);
+  bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0)
+    status[(long long)fov * stride] = bad ? -1 : (last[fov * 2] + 1) * 100 + last[fov * 2 + 1] + 1;
+}
+
+}  // namespace
+
+extern "C" int cpx_watershed_cells(cpx_ctx* ctx, const int32_t* nuclei_dev, const float* corr_dev,
+                                   int B, int C, int cell_channel, int H, int W, int distance,
+                                   int relax_rounds, int label_rounds, int32_t* cells_dev,
+                                   int32_t* cyto_dev, int32_t* status_dev, int status_stride) {
+  CPX_REQUIRE(ctx && nuclei_dev && corr_dev && cells_dev && cyto_dev && status_dev, CPX_ERR_ARG,
+              "cpx_watershed_cells: null argument");
+  CPX_REQUIRE(relax_rounds <= 64 && label_rounds <= 64 && B > 0 && B <= 65535 && C > 0 && cell_channel >= 0 && cell_channel < C && H > 0 &&
+                  W > 0 && (long long)H * W <= (1ll << kKeyShift) && relax_rounds > 0 &&
+                  label_rounds > 0 && status_stride > 0,
+              CPX_ERR_ARG, "cpx_watershed_cells: bad sizes (H*W must be <= 2^23)");
+  // the footprint (mask) and the Cytoplasm of every pixel the flood does not relabel
+  int rc = cpx_expand_labels(ctx, nuclei_dev, B, H, W, distance, cells_dev, cyto_dev);
+  if (rc != CPX_OK) return rc;
+  const int ntx = cpx_div_up(W, kT), nty = cpx_div_up(H, kT), per = ntx * nty, total = B * per;
+  const size_t nB = sizeof(unsigned long long) * (size_t)B * H * W;
+  const size_t nF = (size_t)total;
+  const size_t nI = (sizeof(unsigned short) * (size_t)B * H * W + 255) / 256 * 256;
+  char* ws = (char*)cpx_ws(ctx, WS_WATERSHED, nB + nI + 5 * nF + sizeof(int) * 2 * B + 1024);
+  if (!ws) return CPX_ERR_OOM;
+  WsArgs a;
+  a.nuc = nuclei_dev;
+  a.foot = cells_dev;
+  a.corr = corr_dev;
+  a.C = C;
+  a.ch = cell_channel;
+  a.H = H;
+  a.W = W;
+  a.ntx = ntx;
+  a.nty = nty;
+  a.total = total;
+  a.Bg = (unsigned long long*)ws;
+  a.inv = (unsigned short*)(ws + nB);
+  unsigned char* F = (unsigned char*)(ws + nB + nI);  // relax ping-pong, label ping-pong, tile-free
+  unsigned char* Fr[2] = {F, F + nF};
+  unsigned char* Fl[2] = {F + 2 * nF, F + 3 * nF};
+  a.tfree = F + 4 * nF;
+  a.last = (int*)(((uintptr_t)(F + 5 * nF) + 255) & ~(uintptr_t)255);
+  const bool debug = getenv("CPX_WS_DEBUG") != nullptr;
+  a.dbg = nullptr;
+  if (debug) {
+    CPX_CHECK_HIP(hipMallocAsync((void**)&a.dbg, sizeof(unsigned long long) * 2 * 64 * 4, ctx->stream));
+    CPX_CHECK_HIP(hipMemsetAsync(a.dbg, 0, sizeof(unsigned long long) * 2 * 64 * 4, ctx->stream));
+  }
+  CPX_CHECK_HIP(hipMemsetAsync(a.last, 0xff, sizeof(int) * 2 * B, ctx->stream));
+  // ~9 one-wave blocks per CU fit the LDS; each block schedules its tiles t = block + k * grid
+  // (at most kThreads of them: the LDS list)
+  const int grid = std::max(std::min(total, ctx->n_cu * 9), cpx_div_up(total, kThreads));
+  // The expand footprint is read in every relax round; the label rounds then overwrite the
+  // free pixels of cells / cyto (the footprint is no longer needed: blocked <=> B == kBlocked).
+  for (int r = 0; r < relax_rounds; ++r)
+    hipLaunchKernelGGL(r == 0 ? k_ws_relax<true> : k_ws_relax<false>, dim3(grid), dim3(kThreads), 0,
+                       ctx->stream, a, r, (const unsigned char*)Fr[(r + 1) & 1], Fr[r & 1]);
+  for (int r = 0; r < label_rounds; ++r)
+    hipLaunchKernelGGL(r == 0 ? k_ws_label<true> : k_ws_label<false>, dim3(grid), dim3(kThreads), 0,
+                       ctx->stream, a, r, (const unsigned char*)Fl[(r + 1) & 1], Fl[r & 1], cells_dev,
+                       cyto_dev);
+  hipLaunchKernelGGL(k_ws_status, dim3(B), dim3(256), 0, ctx->stream,
+                     (const unsigned char*)Fr[(relax_rounds - 1) & 1],
+                     (const unsigned char*)Fl[(label_rounds - 1) & 1], per, (const int*)a.last,
+                     status_dev, status_stride);
+  CPX_CHECK_LAUNCH("cpx_watershed_cells");
+  if (debug) {  // profiling aid: per round tiles / drain steps / items / overflows
+    unsigned long long h[2 * 64 * 4];
+    CPX_CHECK_HIP(hipMemcpyAsync(h, a.dbg, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+    CPX_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    for (int k = 0; k < 2; ++k)
+      for (int r = 0; r < (k ? label_rounds : relax_rounds); ++r) {
+        const unsigned long long* c = h + (k * 64 + r) * 4;
+        if (c[0]) fprintf(stderr, "ws %s round %d: tiles %llu steps %llu items %llu overflow %llu\n",
+                          k ? "label" : "relax", r, c[0], c[1], c[2], c[3]);
+      }
+    CPX_CHECK_HIP(hipFreeAsync(a.dbg, ctx->stream));
+  }
+  return CPX_OK;
+}

@@ -283,6 +283,21 @@ int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev,
 int cpx_expand_labels(cpx_ctx* ctx, const int32_t* nuclei_dev, int B, int H, int W, int distance,
                       int32_t* cells_dev, int32_t* cyto_dev);
 
+/* Cells by marker watershed (skimage 0.18.3 segmentation.watershed,
+ * skimage/segmentation/_watershed.py:94, connectivity 1) from the Nuclei, bit-identical to
+ *   watershed(key, markers=nuclei, mask=expand_labels(nuclei, distance) > 0)
+ * with the stated elevation key(p) = (65535 - q16(corr[cell_channel](p))) * 2^23 + (y*W + x),
+ * q16(v) = 65535 if !(v < 65535) else max(0, trunc(v))  (inverted 16-bit cell channel, raster
+ * index tie-break).  cyto = cells where nuclei == 0.  corr_dev: fp32 [B][C][H][W].
+ * The flood runs in `relax_rounds` + `label_rounds` tile rounds without host synchronisation;
+ * status_dev[b * status_stride] (int32) receives 100 * (relax rounds used) + (label rounds used),
+ * or -1 when the rounds enqueued did not reach the fixed point (labels then invalid).
+ * H * W <= 2^23.                                                                               */
+int cpx_watershed_cells(cpx_ctx* ctx, const int32_t* nuclei_dev, const float* corr_dev, int B, int C,
+                        int cell_channel, int H, int W, int distance, int relax_rounds,
+                        int label_rounds, int32_t* cells_dev, int32_t* cyto_dev, int32_t* status_dev,
+                        int status_stride);
+
 /* ---- a6: segmentation (Cellpose <= v3 evaluation, restated) -- *
  * Replaces the work inside cell_model.eval(image_4ch, diameter=100) (Cellpose_GPU_s3fs.py:143)
  * except the CPnet U-Net forward itself, which runs in PyTorch-ROCm between cpx_seg_tiles and
@@ -304,7 +319,8 @@ typedef struct cpx_seg_stats {
   int32_t n_bad_flow; /* masks removed by the flow-error test                                 */
   int32_t n_final;    /* labels after fill_holes_and_remove_small_masks                       */
   int32_t overflow;   /* capacity exceeded (seeds or labels truncated)                        */
-  int32_t _pad[2];
+  int32_t cells_status; /* written by cpx_watershed_cells when pointed here (else untouched)     */
+  int32_t _pad;
 } cpx_seg_stats;      /* 32 bytes */
 
 #define CPX_TILE_F32_NCHW 0  /* tiles/net output as float32 [n][c][by][bx]                   */

@@ -4,7 +4,8 @@ Used by tests and by bench.py's cpu_baseline leg (never by the product).  One FO
   flat-field + QC (cpx_oracle: the reference's Illumination_QC_mult arithmetic)
   -> segmentation (CPnet forward in PyTorch on the CPU, fp32, same seeded weights as the GPU run,
      then seg_oracle: tile average, dynamics, masks)
-  -> Cells / Cytoplasm (cpx_oracle.secondary_objects)
+  -> Cells / Cytoplasm (ws_oracle.cells_watershed: the stated marker watershed, heap flood in C;
+     cells="expand": cpx_oracle.secondary_objects)
   -> features for Nuclei / Cells / Cytoplasm (cpx_oracle.features, skimage 0.18.3 definitions).
 """
 from __future__ import annotations
@@ -18,7 +19,8 @@ import seg_oracle as so
 
 
 def run_fov(raw: np.ndarray, illum: np.ndarray, net, cell_expand: int = 15, model: str = "nuclei",
-            diameter: float = 100.0, timings: dict | None = None):
+            diameter: float = 100.0, timings: dict | None = None, cells: str = "watershed",
+            cell_channel: int = 3):
     """raw uint16 [C,H,W], illum fp32 [C,H,W]; net = CPU CPnet (torch).  Returns dict of outputs."""
     import torch
     t = time.perf_counter()
@@ -37,7 +39,11 @@ def run_fov(raw: np.ndarray, illum: np.ndarray, net, cell_expand: int = 15, mode
     yf = so.average_tiles(y, g)
     nuclei = so.compute_masks(yf, H, W)
     t2 = time.perf_counter()
-    cells, cyto = orc.secondary_objects(nuclei, cell_expand)
+    if cells == "watershed":
+        import ws_oracle
+        cells, cyto = ws_oracle.cells_watershed(nuclei, corr[cell_channel], cell_expand)
+    else:
+        cells, cyto = orc.secondary_objects(nuclei, cell_expand)
     feats = {"Nuclei": orc.features(nuclei, corr), "Cells": orc.features(cells, corr),
              "Cytoplasm": orc.features(cyto, corr)}
     t3 = time.perf_counter()

@@ -5,7 +5,8 @@ on the same inputs.
   * QC: PercentMaximal exact, PowerLogLogSlope rel 1e-9 (oracle = the reference's arithmetic);
   * segmentation post-processing: seg_oracle.compute_masks (resample=True, niter 1176) fed the
     GPU's own tile-averaged flows gives bit-identical Nuclei labels at 2080^2;
-  * Cells / Cytoplasm bit-identical to cpx_oracle.secondary_objects of those Nuclei;
+  * Cells / Cytoplasm (marker watershed) bit-identical to ws_oracle.cells_watershed of those
+    Nuclei (the sequential heap flood, pinned to skimage 0.18.3);
   * object tables bit-exact and all three feature tables within rtol 1e-5 of cpx_oracle.features;
   * the bf16 CPnet's (and an fp32 GPU CPnet's) masks vs the same network in fp32 on the CPU,
     then the oracle's dynamics: identical-mask and IoU-matched fractions (north_star asks for
@@ -20,6 +21,7 @@ import torch
 
 import cpx_oracle as orc
 import seg_oracle as so
+import ws_oracle as wo
 
 pytestmark = pytest.mark.gpu
 
@@ -70,11 +72,15 @@ def test_e2e_nuclei_bit_exact_on_gpu_flows(e2e):
         np.testing.assert_array_equal(got, ref, err_msg=f"fov {b}")
         assert ref.max() >= 150  # a realistic FOV: hundreds of nuclei
         assert e2e["res"].seg_stats[b]["n_final"] == ref.max()
+        assert e2e["res"].seg_stats[b]["cells_status"] > 0
 
 
 def test_e2e_cells_cytoplasm_bit_exact(e2e):
     for b in range(e2e["yf"].shape[0]):
-        cells, cyto = orc.secondary_objects(e2e["labels"]["Nuclei"][b], e2e["cfg"].cell_expand)
+        cfg = e2e["cfg"]
+        assert cfg.cells == "watershed"
+        cells, cyto = wo.cells_watershed(e2e["labels"]["Nuclei"][b], e2e["corr"][b, cfg.cell_channel],
+                                         cfg.cell_expand)
         np.testing.assert_array_equal(e2e["labels"]["Cells"][b], cells)
         np.testing.assert_array_equal(e2e["labels"]["Cytoplasm"][b], cyto)
 
