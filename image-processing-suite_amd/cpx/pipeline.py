@@ -47,8 +47,8 @@ class PipelineConfig:
                                      # (DESIGN.md §7); "expand": Cells = that footprint's labels
     cell_expand: int = 15            # footprint distance (px)
     cell_channel: int = 3            # watershed elevation channel (AGP)
-    ws_rounds: tuple = (24, 48)      # watershed relax / label tile rounds enqueued per batch
-                                     # (bench plates use <= 9 / <= 17; idle rounds cost ~6 us)
+    ws_rounds: tuple = (24, 16)      # watershed relax tile rounds / label pointer-jump rounds
+                                     # enqueued per batch (bench plates: <= 9 / ~8; idle ~6 us)
     max_objects: int = 2048          # per FOV and object set
     box: int = 200                   # Cellpose_GPU_s3fs.py:30 BOX_SIZE
     weights: str | None = None       # local CPnet state_dict; None = seeded random init

@@ -11,20 +11,21 @@
 //           the smallest B (neighbours tied on B were popped in the same "phase", opened by the
 //           pass pixel whose key is that B, and carry the same label).
 //
-// Both are computed tile by tile (64 x 64 pixels + 1-pixel halo in LDS), in rounds over the
-// whole batch with no host synchronisation, as label-correcting worklists: only pixels whose
-// level (label) just changed are visited again, so the work is ~2 visits per free pixel instead
-// of whole-tile sweeps (15 % of a FOV's pixels are free: the rings around the nuclei):
-//   k_ws_relax  B(n) = max(key(n), B(p)) pushed from every improved pixel p to its free
-//               neighbours with an LDS atomic min; each wave drains its own LDS queue (no block
-//               barrier per hop), the tile is at its fixed point when every queue is empty;
-//   k_ws_label  a free pixel takes, once, the label of a labelled neighbour whose B is the
-//               minimum of its four neighbours' (write-once: every label written is final);
-// a tile whose border changes flags the facing neighbour, which in the next round re-evaluates
-// only its border pixels against the new halo (a queue overflow re-runs the whole tile).  k_ws_status fails the FOV (status -1) when the
-// rounds enqueued did not reach the fixed point (the host raises).  Exactness vs the sequential
-// heap flood: tests/test_watershed.py (oracle) and tests/test_gpu_watershed.py (this kernel),
-// pinned to skimage itself by tests/golden/watershed_cases.npz.
+// Computed in two phases over the whole batch, with no host synchronisation:
+//   k_ws_relax  (rounds) B by a label-correcting worklist per 32 x 32 tile held in LDS (one wave
+//               per tile, its own LDS queue, no barrier on the hop path): every improved pixel
+//               p pushes max(key(n), B(p)) to its neighbours with an LDS atomic min, so the work
+//               is ~2 visits per free pixel (15 % of a FOV's pixels are free: the rings around
+//               the nuclei); a tile whose border changes flags the facing neighbour, which in
+//               the next round re-evaluates only its border pixels against the new halo (a
+//               queue overflow re-runs the whole tile);
+//   k_ws_ptr_init + k_ws_jump (rounds)  labels by pointer jumping over the converged B: a member
+//               of a phase points at its pass pixel, a phase start at the pass of its minimum
+//               neighbour, every chain ends at a marker (see the comment above k_ws_ptr_init).
+// k_ws_status / k_ws_jump_fail fail a FOV (status -1) when the rounds enqueued did not reach the
+// fixed point (the host raises).  Exactness vs the sequential heap flood: tests/test_watershed.py
+// (oracle) and tests/test_gpu_watershed.py (this kernel), pinned to skimage itself by
+// tests/golden/watershed_cases.npz.
 #include "cpx_internal.h"
 #include <stdio.h>
 #include <stdlib.h>
@@ -44,7 +45,6 @@ constexpr int kKeyShift = 23;
 // tile flag bits (per round)
 constexpr unsigned char kUp = 1, kLeft = 2, kRight = 4, kDown = 8;  // that border changed
 constexpr unsigned char kSelf = 16;   // a wave queue overflowed: re-run the whole tile
-constexpr unsigned char kUnres = 32;  // label: reached pixels still unlabelled
 constexpr int kQCap = 2048;           // per-wave LDS queue (tile-local pixel indices)
 static_assert(kQCap >= kT * kT + 3 * 64, "the seeds of a whole tile plus one drain step fit");
 static_assert(kWaves == 1, "one wave per tile");
@@ -144,9 +144,9 @@ __device__ __forceinline__ int border_pixel(int k) {
 // Tiles of this block for this round: t = blockIdx.x + k * gridDim.x.  Every thread evaluates one
 // tile's activity at once (flags of the previous round), writes the flags of inactive tiles and
 // appends active ones to the LDS list — an idle round costs one pass over the flags, not a
-// serial walk.  mode 0: relax (tile has free pixels and a facing border changed, or kSelf; every
-// tile active in round 0); mode 1: label (additionally needs kUnres unless kSelf).
-__device__ int schedule_tiles(const WsArgs& a, int round, int mode, const unsigned char* Fp,
+// serial walk.  Active: every tile in round 0, later a tile with free pixels whose facing
+// neighbour's border changed (or whose own queue overflowed: kSelf).
+__device__ int schedule_tiles(const WsArgs& a, int round, const unsigned char* Fp,
                               unsigned char* Fn, int* list, int* s_n) {
   if (threadIdx.x == 0) *s_n = 0;
   __syncthreads();
@@ -163,18 +163,8 @@ __device__ int schedule_tiles(const WsArgs& a, int round, int mode, const unsign
     const bool nb = (ty > 0 && (fu & kDown)) || (ty + 1 < a.nty && (fd & kUp)) ||
                     (tx > 0 && (fl & kRight)) || (tx + 1 < a.ntx && (fg & kLeft));
     (void)base;
-    bool act;
-    unsigned char keep = 0;
-    if (mode == 0) {
-      act = round == 0 || (fr && (nb || (fs & kSelf)));
-    } else if (!fr) {
-      act = false;
-    } else if (round == 0) {
-      act = true;
-    } else {
-      act = (fs & kSelf) || ((fs & kUnres) && nb);
-      keep = fs & kUnres;
-    }
+    const bool act = round == 0 || (fr && (nb || (fs & kSelf)));
+    const unsigned char keep = 0;
     if (act) list[atomicAdd(s_n, 1)] = t;
     else Fn[t] = keep;
   }
@@ -209,7 +199,7 @@ __global__ __launch_bounds__(kThreads, 3) void k_ws_relax(WsArgs a, int round,
   __shared__ int s_list[kThreads], s_n;
   const int lane = threadIdx.x;
   const long long hw = (long long)a.H * a.W;
-  const int nact = schedule_tiles(a, round, 0, Fp, Fn, s_list, &s_n);
+  const int nact = schedule_tiles(a, round, Fp, Fn, s_list, &s_n);
   const long long hwc = hw * a.C;
   for (int j = 0; j < nact; ++j) {
     const int t = s_list[j];
@@ -412,199 +402,155 @@ __global__ __launch_bounds__(kThreads, 3) void k_ws_relax(WsArgs a, int round,
   }
 }
 
-template <bool R0>
-__global__ __launch_bounds__(kThreads, 3) void k_ws_label(WsArgs a, int round,
-                                                       const unsigned char* __restrict__ Fp,
-                                                       unsigned char* __restrict__ Fn,
-                                                       int* __restrict__ cells, int* __restrict__ cyto) {
-  // levels (tile + halo); per unlabelled reached free tile pixel the minimum level of its four
-  // neighbours (kBlocked elsewhere); labels (tile + halo: 0 = unknown inside the tile, -1 =
-  // unknown in the halo, which is never a source nor a target)
-  __shared__ unsigned long long sB[kLRows * kLS];
-  __shared__ unsigned long long sM[kLRows * kLS];
-  __shared__ int sL[kLRows * kLS];
-  __shared__ unsigned short sQ[kQCap];
-  __shared__ unsigned short sS[kT * kT];  // seed candidates
-  __shared__ unsigned s_bits;
-  __shared__ int s_list[kThreads], s_n;
-  const int lane = threadIdx.x;
+// Labels from the converged levels, by pointer jumping.  A free reached pixel p belongs to the
+// flood phase opened by its pass pixel: pass(p) = the pixel whose key is B(p) (the low 23 bits of
+// B).  A member (B(p) > key(p)) has the label of its pass; a phase start (B(p) == key(p)) has the
+// label of its first-popped neighbour, i.e. of the pass of its neighbours' minimum level S(p)
+// (neighbours tied at S share that pass).  So ptr(p) = pass of (member ? B(p) : S(p)) — always an
+// earlier-popped pass or a marker — and following ptr ends at the marker whose label p takes.
+// k_ws_ptr_init resolves the pixels whose target is a marker and lists the rest; each k_ws_jump
+// round resolves the listed pixels whose target is labelled and halves the others' chains.
+constexpr int kJumpThreads = 256;
+constexpr long long kIdxMask = (1ll << kKeyShift) - 1;
+
+// Survivors of a block are gathered in LDS and appended to the global list with one atomic per
+// block (a per-wave atomic on one counter serialises ~10^6 times per batch).
+constexpr int kJumpPer = 8;                       // list items / pixels per thread
+constexpr int kJumpChunk = kJumpThreads * kJumpPer;
+
+__device__ __forceinline__ void block_append(bool pred, int item, int* s_buf, int* s_cnt) {
+  const unsigned long long m = __ballot(pred);
+  if (!m) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(s_cnt, __popcll(m));
+  base = __shfl(base, leader, 64);
+  if (pred) s_buf[base + __popcll(m & ((1ull << lane) - 1ull))] = item;
+}
+
+__device__ __forceinline__ void block_flush(const int* s_buf, int* s_cnt, int* s_base, int* list, int* cnt) {
+  __syncthreads();
+  if (threadIdx.x == 0) *s_base = *s_cnt ? atomicAdd(cnt, *s_cnt) : 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < *s_cnt; i += kJumpThreads) list[*s_base + i] = s_buf[i];
+  __syncthreads();
+  if (threadIdx.x == 0) *s_cnt = 0;
+  __syncthreads();
+}
+
+// one block per 32 x 32 tile (tiles without free pixels stored only their border ring: nothing
+// to label there)
+__global__ __launch_bounds__(kJumpThreads) void k_ws_ptr_init(WsArgs a, int* __restrict__ cells,
+                                                              int* __restrict__ cyto, int* __restrict__ ptr,
+                                                              int* __restrict__ list, int* __restrict__ cnt) {
+  __shared__ int s_buf[kT * kT];
+  __shared__ int s_cnt, s_base;
+  const int t = blockIdx.x;
+  if (!a.tfree[t]) return;
+  const int per = a.nty * a.ntx;
+  const int fov = t / per, tt = t - fov * per, ty = tt / a.ntx, tx = tt - ty * a.ntx;
   const long long hw = (long long)a.H * a.W;
-  const int nact = schedule_tiles(a, round, 1, Fp, Fn, s_list, &s_n);
-  for (int j = 0; j < nact; ++j) {
-    const int t = s_list[j];
-    const int per = a.nty * a.ntx;
-    const int fov = t / per, tt = t - fov * per, ty = tt / a.ntx, tx = tt - ty * a.ntx;
-    const bool full = R0 || (Fp[t] & kSelf) != 0;
-    const int y0 = ty * kT, x0 = tx * kT;
-    if (lane == 0) s_bits = 0;
-    constexpr int kLoads = (kT * kT + 4 * kT + kThreads - 1) / kThreads;
-    unsigned long long bv_[kLoads];
-    int nv_[kLoads], cv_[kLoads];
-#pragma unroll
-    for (int k = 0; k < kLoads; ++k) {
-      const int i = lane + k * kThreads;
-      int iy = 0, ix = 0;
-      if (i < kT * kT) {
-        iy = i / kT;
-        ix = i - iy * kT;
-      } else if (i < kT * kT + 4 * kT) {
-        halo_pos(i - kT * kT, iy, ix);
-      }
-      const int y = y0 + iy, x = x0 + ix;
-      const bool in = i < kT * kT + 4 * kT && y >= 0 && y < a.H && x >= 0 && x < a.W;
-      const long long pix = fov * hw + (in ? (long long)y * a.W + x : 0);
-      bv_[k] = in ? a.Bg[pix] : kBlocked;
-      nv_[k] = a.nuc[pix];
-      cv_[k] = R0 ? 0 : cells[pix];
-    }
-#pragma unroll
-    for (int k = 0; k < kLoads; ++k) {
-      const int i = lane + k * kThreads;
-      if (i >= kT * kT + 4 * kT) continue;
-      int iy, ix;
-      if (i < kT * kT) {
-        iy = i / kT;
-        ix = i - iy * kT;
-      } else {
-        halo_pos(i - kT * kT, iy, ix);
-      }
-      const int o = (1 + iy) * kLS + 1 + ix;
-      const unsigned long long v = bv_[k];
-      int l = v == kBlocked ? 0 : (stored_marker(v) ? nv_[k] : cv_[k]);
-      if (i >= kT * kT && l == 0) l = -1;
-      sB[o] = level_of(v);
-      sL[o] = l;
-      sM[o] = kBlocked;
-    }
-    __syncthreads();
-    // minimum neighbour level of every unlabelled reached free pixel
-#pragma unroll
-    for (int k = 0; k < kPerThread; ++k) {
-      const int o = lds_off(lane + k * kThreads);
-      if (sL[o] == 0 && sB[o] < kUnreached) {
-        const unsigned long long u = sB[o - kLS], l = sB[o - 1], r = sB[o + 1], d = sB[o + kLS];
-        unsigned long long m = u < l ? u : l;
-        m = r < m ? r : m;
-        sM[o] = d < m ? d : m;
-      }
-    }
-    __syncthreads();
-    WaveQueue wq{sQ, 0, 0};
-    unsigned bits = 0;
-    // seeds: unlabelled pixels (all, or the border ones) that already see a labelled neighbour
-    // at their minimum neighbour level; candidates compacted first
-    int nseed = 0;
-    if (full) {
-#pragma unroll
-      for (int k = 0; k < kPerThread; ++k) {
-        const int o = lds_off(lane + k * kThreads);
-        const bool c = sM[o] != kBlocked;
-        const unsigned long long m = __ballot(c);
-        if (c) sS[nseed + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)o;
-        nseed += __popcll(m);
-      }
-    } else {
-      for (int k = lane; k < 4 * kT; k += kThreads) sS[k] = (unsigned short)lds_off(border_pixel(k));
-      nseed = 4 * kT;
-    }
-    __syncthreads();
-    for (int base = 0; base < nseed; base += kThreads) {
-      const int o = base + lane < nseed ? (int)sS[base + lane] : kLS + 1;
-      const unsigned long long m = base + lane < nseed ? sM[o] : kBlocked;
-      bool got = false;
-      if (m != kBlocked && sL[o] == 0) {
-        const int nb[4] = {o - kLS, o - 1, o + 1, o + kLS};
-        int lab = 0;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const int ld = sL[nb[d]];
-          if (lab <= 0 && ld > 0 && sB[nb[d]] == m) lab = ld;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  for (int k = 0; k < kT * kT / kJumpThreads; ++k) {
+    const int i = threadIdx.x + k * kJumpThreads, y = ty * kT + i / kT, x = tx * kT + i % kT;
+    bool app = false;
+    long long g = 0;
+    if (y < a.H && x < a.W) {
+      const long long idx = (long long)y * a.W + x;
+      g = fov * hw + idx;
+      const unsigned long long v = a.Bg[g];
+      if (v != kBlocked && !stored_marker(v)) {
+        if (v >= kUnreached) {  // never flooded: left unlabelled, as skimage leaves it
+          cells[g] = 0;
+          cyto[g] = 0;
+        } else {
+          const unsigned long long key = ((unsigned long long)a.inv[g] << kKeyShift) | (unsigned long long)idx;
+          unsigned long long S = kBlocked;
+          if (y > 0) S = min(S, level_of(a.Bg[g - a.W]));
+          if (x > 0) S = min(S, level_of(a.Bg[g - 1]));
+          if (x + 1 < a.W) S = min(S, level_of(a.Bg[g + 1]));
+          if (y + 1 < a.H) S = min(S, level_of(a.Bg[g + a.W]));
+          const long long tg = fov * hw + (long long)((v == key ? S : v) & (unsigned long long)kIdxMask);
+          const int l = stored_marker(a.Bg[tg]) ? a.nuc[tg] : 0;
+          cells[g] = l;
+          cyto[g] = l;
+          ptr[g] = (int)tg;
+          app = l == 0;
         }
-        if (lab > 0) got = atomicCAS(&sL[o], 0, lab) == 0;
       }
-      if (got) bits |= border_bits_off(o);
-      wq.push(got, o, lane);
     }
-    bool ovf = false;
-    int dsteps = 0, ditems = 0;
-    while (wq.tail != wq.head) {
-      const int cnt = min(64, wq.tail - wq.head);
-      ++dsteps;
-      ditems += cnt;
-      if (wq.tail - wq.head + 3 * cnt > kQCap) {
-        ovf = true;
-        break;
-      }
-      const bool act = lane < cnt;
-      const int o = act ? (int)wq.q[(wq.head + lane) & (kQCap - 1)] : kLS + 1;
-      wq.head += cnt;
-      const int nb[4] = {o - kLS, o - 1, o + 1, o + kLS};
-      const unsigned long long bp = sB[o];
-      const int lp = sL[o];
-      unsigned long long mm[4];
-      int ll[4];
+    block_append(app, (int)g, s_buf, &s_cnt);
+  }
+  block_flush(s_buf, &s_cnt, &s_base, list, cnt);
+}
+
+__global__ __launch_bounds__(kJumpThreads) void k_ws_jump(int r, int* __restrict__ cells, int* __restrict__ cyto,
+                                                          int* __restrict__ ptr, const int* __restrict__ in,
+                                                          int* __restrict__ out, int* __restrict__ cnt) {
+  __shared__ int s_buf[kJumpChunk];
+  __shared__ int s_cnt, s_base;
+  const int n = cnt[r];
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  for (int c0 = blockIdx.x * kJumpChunk; c0 < n; c0 += gridDim.x * kJumpChunk) {
+    int g_[kJumpPer], q_[kJumpPer];
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        mm[d] = sM[nb[d]];
-        ll[d] = sL[nb[d]];
-      }
-      bool got[4];
+    for (int k = 0; k < kJumpPer; ++k) {
+      const int i = c0 + threadIdx.x + k * kJumpThreads;
+      g_[k] = i < n ? in[i] : -1;
+    }
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        got[d] = act && ll[d] == 0 && mm[d] == bp;
-        if (got[d]) got[d] = atomicCAS(&sL[nb[d]], 0, lp) == 0;
-      }
+    for (int k = 0; k < kJumpPer; ++k) q_[k] = g_[k] >= 0 ? ptr[g_[k]] : 0;
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        if (got[d]) bits |= border_bits_off(nb[d]);
-        wq.push(got[d], nb[d], lane);
+    for (int k = 0; k < kJumpPer; ++k) {
+      bool app = false;
+      if (g_[k] >= 0) {
+        const int l = cells[q_[k]];
+        if (l > 0) {
+          cells[g_[k]] = l;
+          cyto[g_[k]] = l;
+        } else {
+          ptr[g_[k]] = ptr[q_[k]];
+          app = true;
+        }
       }
+      block_append(app, g_[k], s_buf, &s_cnt);
     }
-    if (ovf) bits |= kSelf;
-    if (bits) atomicOr(&s_bits, bits);
-    if (a.dbg && lane == 0) {
-      unsigned long long* c = a.dbg + (1 * 64 + round) * 4;
-      atomicAdd(c, 1ull);
-      atomicAdd(c + 1, (unsigned long long)dsteps);
-      atomicAdd(c + 2, (unsigned long long)ditems);
-      atomicAdd(c + 3, (unsigned long long)ovf);
-    }
-    __syncthreads();
-    int unres = 0;
-#pragma unroll
-    for (int k = 0; k < kPerThread; ++k) {  // own pixels are the first kPerThread loads
-      const int i = lane + k * kThreads;
-      const int y = y0 + i / kT, x = x0 + i % kT;
-      if (y >= a.H || x >= a.W) continue;
-      const unsigned long long v = bv_[k];
-      if (v == kBlocked || stored_marker(v)) continue;
-      const int o = lds_off(i);
-      const long long pix = fov * hw + (long long)y * a.W + x;
-      const int l = sL[o];
-      unres |= l == 0 && v < kUnreached;
-      cells[pix] = l;
-      cyto[pix] = l;
-    }
-    unres = __syncthreads_or(unres);
-    if (lane == 0) {
-      Fn[t] = (unsigned char)(s_bits | (unres ? kUnres : 0));
-      a.last[fov * 2 + 1] = round;
-    }
-    __syncthreads();
+    block_flush(s_buf, &s_cnt, &s_base, out, cnt + r + 1);
   }
 }
 
-// per FOV: converged when the last relax round left no border change / capped tile and the
-// last label round no unlabelled reached pixel
-__global__ void k_ws_status(const unsigned char* __restrict__ Fr, const unsigned char* __restrict__ Fl,
-                            int per, const int* __restrict__ last, int* __restrict__ status, int stride) {
+// a FOV whose pixels are still listed after the last jump round failed
+__global__ __launch_bounds__(kJumpThreads) void k_ws_jump_fail(int r, const int* __restrict__ in,
+                                                               const int* __restrict__ cnt, long long hw,
+                                                               int* __restrict__ status, int stride) {
+  const int n = cnt[r];
+  for (int i = blockIdx.x * kJumpThreads + threadIdx.x; i < n; i += gridDim.x * kJumpThreads)
+    status[(in[i] / hw) * stride] = -1;
+}
+
+// per FOV: the relax rounds converged when the last one left no border change / capped tile;
+// status = 100 * (relax rounds used) + (jump rounds the batch needed); k_ws_jump_fail then
+// overrides FOVs whose labels are still unresolved
+__global__ void k_ws_status(const unsigned char* __restrict__ Fr, int per, const int* __restrict__ last,
+                            const int* __restrict__ cnt, int jump_rounds, int* __restrict__ status,
+                            int stride) {
   const int fov = blockIdx.x;
   int bad = 0;
   for (int i = threadIdx.x; i < per; i += blockDim.x)
-    bad |= (Fr[fov * per + i] & (kUp | kLeft | kRight | kDown | kSelf)) | (Fl[fov * per + i] & kUnres);
+    bad |= Fr[fov * per + i] & (kUp | kLeft | kRight | kDown | kSelf);
   bad = __syncthreads_or(bad);
-  if (threadIdx.x == 0)
-    status[(long long)fov * stride] = bad ? -1 : (last[fov * 2] + 1) * 100 + last[fov * 2 + 1] + 1;
+  if (threadIdx.x == 0) {
+    int used = jump_rounds;
+    for (int r = 0; r <= jump_rounds; ++r)
+      if (cnt[r] == 0) {
+        used = r;
+        break;
+      }
+    status[(long long)fov * stride] = bad ? -1 : (last[fov * 2] + 1) * 100 + used;
+  }
 }
 
 }  // namespace
@@ -626,7 +572,9 @@ extern "C" int cpx_watershed_cells(cpx_ctx* ctx, const int32_t* nuclei_dev, cons
   const size_t nB = sizeof(unsigned long long) * (size_t)B * H * W;
   const size_t nF = (size_t)total;
   const size_t nI = (sizeof(unsigned short) * (size_t)B * H * W + 255) / 256 * 256;
-  char* ws = (char*)cpx_ws(ctx, WS_WATERSHED, nB + nI + 5 * nF + sizeof(int) * 2 * B + 1024);
+  const size_t nP = (sizeof(int) * (size_t)B * H * W + 255) / 256 * 256;  // ptr, two lists
+  CPX_REQUIRE((long long)B * H * W < (1ll << 31), CPX_ERR_ARG, "cpx_watershed_cells: batch too large");
+  char* ws = (char*)cpx_ws(ctx, WS_WATERSHED, nB + nI + 3 * nP + 5 * nF + sizeof(int) * (2 * B + 80) + 2048);
   if (!ws) return CPX_ERR_OOM;
   WsArgs a;
   a.nuc = nuclei_dev;
@@ -641,11 +589,13 @@ extern "C" int cpx_watershed_cells(cpx_ctx* ctx, const int32_t* nuclei_dev, cons
   a.total = total;
   a.Bg = (unsigned long long*)ws;
   a.inv = (unsigned short*)(ws + nB);
-  unsigned char* F = (unsigned char*)(ws + nB + nI);  // relax ping-pong, label ping-pong, tile-free
+  int* ptr = (int*)(ws + nB + nI);
+  int* lists[2] = {(int*)(ws + nB + nI + nP), (int*)(ws + nB + nI + 2 * nP)};
+  unsigned char* F = (unsigned char*)(ws + nB + nI + 3 * nP);  // relax ping-pong, tile-free
   unsigned char* Fr[2] = {F, F + nF};
-  unsigned char* Fl[2] = {F + 2 * nF, F + 3 * nF};
   a.tfree = F + 4 * nF;
   a.last = (int*)(((uintptr_t)(F + 5 * nF) + 255) & ~(uintptr_t)255);
+  int* cnt = a.last + 2 * B;  // jump list counts, one per round
   const bool debug = getenv("CPX_WS_DEBUG") != nullptr;
   a.dbg = nullptr;
   if (debug) {
@@ -653,6 +603,7 @@ extern "C" int cpx_watershed_cells(cpx_ctx* ctx, const int32_t* nuclei_dev, cons
     CPX_CHECK_HIP(hipMemsetAsync(a.dbg, 0, sizeof(unsigned long long) * 2 * 64 * 4, ctx->stream));
   }
   CPX_CHECK_HIP(hipMemsetAsync(a.last, 0xff, sizeof(int) * 2 * B, ctx->stream));
+  CPX_CHECK_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (label_rounds + 1), ctx->stream));
   // ~9 one-wave blocks per CU fit the LDS; each block schedules its tiles t = block + k * grid
   // (at most kThreads of them: the LDS list)
   const int grid = std::max(std::min(total, ctx->n_cu * 9), cpx_div_up(total, kThreads));
@@ -661,26 +612,35 @@ extern "C" int cpx_watershed_cells(cpx_ctx* ctx, const int32_t* nuclei_dev, cons
   for (int r = 0; r < relax_rounds; ++r)
     hipLaunchKernelGGL(r == 0 ? k_ws_relax<true> : k_ws_relax<false>, dim3(grid), dim3(kThreads), 0,
                        ctx->stream, a, r, (const unsigned char*)Fr[(r + 1) & 1], Fr[r & 1]);
+  const int jgrid = ctx->n_cu * 8;
+  hipLaunchKernelGGL(k_ws_ptr_init, dim3(total), dim3(kJumpThreads), 0, ctx->stream, a, cells_dev, cyto_dev,
+                     ptr, lists[0], cnt);
   for (int r = 0; r < label_rounds; ++r)
-    hipLaunchKernelGGL(r == 0 ? k_ws_label<true> : k_ws_label<false>, dim3(grid), dim3(kThreads), 0,
-                       ctx->stream, a, r, (const unsigned char*)Fl[(r + 1) & 1], Fl[r & 1], cells_dev,
-                       cyto_dev);
+    hipLaunchKernelGGL(k_ws_jump, dim3(jgrid), dim3(kJumpThreads), 0, ctx->stream, r, cells_dev, cyto_dev,
+                       ptr, (const int*)lists[r & 1], lists[(r + 1) & 1], cnt);
   hipLaunchKernelGGL(k_ws_status, dim3(B), dim3(256), 0, ctx->stream,
-                     (const unsigned char*)Fr[(relax_rounds - 1) & 1],
-                     (const unsigned char*)Fl[(label_rounds - 1) & 1], per, (const int*)a.last,
-                     status_dev, status_stride);
+                     (const unsigned char*)Fr[(relax_rounds - 1) & 1], per, (const int*)a.last,
+                     (const int*)cnt, label_rounds, status_dev, status_stride);
+  hipLaunchKernelGGL(k_ws_jump_fail, dim3(64), dim3(kJumpThreads), 0, ctx->stream, label_rounds,
+                     (const int*)lists[label_rounds & 1], (const int*)cnt, (long long)H * W, status_dev,
+                     status_stride);
   CPX_CHECK_LAUNCH("cpx_watershed_cells");
   if (debug) {  // profiling aid: per round tiles / drain steps / items / overflows
     unsigned long long h[2 * 64 * 4];
     CPX_CHECK_HIP(hipMemcpyAsync(h, a.dbg, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
     CPX_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-    for (int k = 0; k < 2; ++k)
-      for (int r = 0; r < (k ? label_rounds : relax_rounds); ++r) {
+    for (int k = 0; k < 1; ++k)
+      for (int r = 0; r < relax_rounds; ++r) {
         const unsigned long long* c = h + (k * 64 + r) * 4;
         if (c[0]) fprintf(stderr, "ws %s round %d: tiles %llu steps %llu items %llu overflow %llu\n",
                           k ? "label" : "relax", r, c[0], c[1], c[2], c[3]);
       }
     CPX_CHECK_HIP(hipFreeAsync(a.dbg, ctx->stream));
+    int hc[65];
+    CPX_CHECK_HIP(hipMemcpy(hc, cnt, sizeof(int) * (label_rounds + 1), hipMemcpyDeviceToHost));
+    fprintf(stderr, "ws jump list sizes:");
+    for (int r = 0; r <= label_rounds; ++r) fprintf(stderr, " %d", hc[r]);
+    fprintf(stderr, "\n");
   }
   return CPX_OK;
 }

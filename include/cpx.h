@@ -289,9 +289,10 @@ int cpx_expand_labels(cpx_ctx* ctx, const int32_t* nuclei_dev, int B, int H, int
  * with the stated elevation key(p) = (65535 - q16(corr[cell_channel](p))) * 2^23 + (y*W + x),
  * q16(v) = 65535 if !(v < 65535) else max(0, trunc(v))  (inverted 16-bit cell channel, raster
  * index tie-break).  cyto = cells where nuclei == 0.  corr_dev: fp32 [B][C][H][W].
- * The flood runs in `relax_rounds` + `label_rounds` tile rounds without host synchronisation;
- * status_dev[b * status_stride] (int32) receives 100 * (relax rounds used) + (label rounds used),
- * or -1 when the rounds enqueued did not reach the fixed point (labels then invalid).
+ * The flood levels converge in up to `relax_rounds` tile rounds and the labels in up to
+ * `label_rounds` pointer-jumping rounds, without host synchronisation; status_dev[b *
+ * status_stride] (int32) receives 100 * (relax rounds used) + (jump rounds used), or -1 when the
+ * rounds enqueued did not reach the fixed point (labels then invalid; the host must raise).
  * H * W <= 2^23.                                                                               */
 int cpx_watershed_cells(cpx_ctx* ctx, const int32_t* nuclei_dev, const float* corr_dev, int B, int C,
                         int cell_channel, int H, int W, int distance, int relax_rounds,

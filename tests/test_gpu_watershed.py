@@ -97,7 +97,7 @@ def full_size():
 def test_full_size_2080(dev, full_size):
     nuc, corr, ref = full_size
     cells, cyto, st = _ws_gpu(dev, nuc, corr, 0, 15)
-    print("status (100 x relax rounds + label rounds):", st.tolist())
+    print("status (100 x relax rounds + jump rounds):", st.tolist())
     for b in range(2):
         assert st[b] > 0, st
         np.testing.assert_array_equal(cells[b], ref[b][0], err_msg=f"fov {b}")
@@ -108,4 +108,10 @@ def test_full_size_2080(dev, full_size):
 def test_status_reports_unconverged(dev, full_size):
     nuc, corr, _ = full_size
     _, _, st = _ws_gpu(dev, nuc, corr, 0, 15, rounds=(1, 1))
+    assert (st == -1).all(), st
+
+
+def test_status_reports_unresolved_labels(dev, full_size):
+    nuc, corr, _ = full_size
+    _, _, st = _ws_gpu(dev, nuc, corr, 0, 15, rounds=(24, 1))  # levels converge, chains do not
     assert (st == -1).all(), st
