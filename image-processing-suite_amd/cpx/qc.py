@@ -8,12 +8,16 @@ Contract kept from the reference (Illumination_QC_mult.py):
   * flat-field per channel from <ch>_illum.npy, else Illum<ch>.npy, else none; an illum of
     another shape than the plane is ignored (:148-153, :180-199);
   * stale ImageQuality_* / QC_Error columns dropped, new ones appended per row (:171-225).
-Design: host threads only decode TIFFs.  Each site's planes go to the GPU together
-(cpx_fov_submit: H2D, flat-field, PercentMaximal statistics; cpx_fov_qc: fp64 pruned-FFT ring
-spectrum + slope), one libcpx context per process, calls serialised by the session lock.
+Design: host threads only decode TIFFs.  The CLI (`main`) batches sites: `--batch` decoded
+sites whose planes are all present, 2-D uint16 of one shape go to the GPU in ONE call
+(cpx_illum_correct + cpx_qc_rps over batch x C planes: flat-field, PercentMaximal, fp64
+pruned-FFT ring spectrum + slope); sites that are not (a missing or unreadable plane, another
+dtype or shape, a flat-field of another shape) take the per-site path `process_site`, which is
+also the drop-in worker for callers that drive their own pool.  One libcpx context per process;
+GPU calls are serialised by the session lock.
 
     python -m cpx.qc --load-data LoadData.csv --data-path IMAGES --illum-path ILLUM \
-                     --channels DNA AGP Mito --output QC_Results.csv --threads 24
+                     --channels DNA AGP Mito --output QC_Results.csv --threads 24 [--batch 16]
 """
 from __future__ import annotations
 
@@ -51,6 +55,7 @@ def parse_args(argv=None):
     ap.add_argument("--channels", nargs="+", required=True, help="channel names, in column order")
     ap.add_argument("--output", default="QC_Results.csv", help="CSV written with the QC columns appended")
     ap.add_argument("--threads", type=int, default=24, help="host threads decoding TIFF planes")
+    ap.add_argument("--batch", type=int, default=16, help="sites per GPU call (1 = one call per site)")
     return ap.parse_args(argv)
 
 
@@ -142,6 +147,108 @@ def process_site(site_data):
     return index, site_results
 
 
+def _decode_site(site_data):
+    """Reader-thread half of a site: (index, planes or None).  None = the site needs the
+    per-site path (a plane missing / unreadable / not 2-D uint16 / shapes differ)."""
+    index, paths, channels, illum_cache = site_data
+    planes = []
+    try:
+        for path in paths:
+            if not os.path.exists(path):
+                return index, None
+            img = _read(path)
+            if img.ndim != 2 or img.dtype != np.uint16 or (planes and img.shape != planes[0].shape):
+                return index, None
+            planes.append(img)
+    except Exception:  # noqa: BLE001 (the per-site path reports the error per channel)
+        return index, None
+    return index, planes
+
+
+class _BatchQC:
+    """One GPU call for a batch of clean sites: raw planes [n*C][H][W] (plane p = channel
+    p % C), the flat-fields [C][H][W] when every channel has one of the plane shape."""
+
+    def __init__(self, channels, illum):
+        self.channels, self.illum = channels, illum
+        self.s = session()
+        self._ill_dev = {}
+
+    def _illum_dev(self, H, W):
+        if (H, W) not in self._ill_dev:
+            t = None
+            ill = self.illum
+            if ill and all(a is not None and a.shape == (H, W) for a in ill):
+                a = np.stack([np.asarray(x) for x in ill])
+                if a.dtype not in (np.float32, np.float64):
+                    a = a.astype(np.float64)
+                t = self.s.torch.from_numpy(np.ascontiguousarray(a)).to(self.s.td)
+            self._ill_dev[(H, W)] = t
+        return self._ill_dev[(H, W)]
+
+    def usable(self, H, W):
+        """Batched path only when the flat-fields apply uniformly (all of this shape, or none)."""
+        ill = self.illum
+        return (not ill or all(a is None for a in ill) or self._illum_dev(H, W) is not None)
+
+    def run(self, sites):
+        """sites: [(index, planes)] of one shape -> {index: result dict}."""
+        from .device import _illum_dtype, _ptr
+        torch, s = self.s.torch, self.s
+        C = len(self.channels)
+        H, W = sites[0][1][0].shape
+        n = len(sites) * C
+        host = np.stack([p for _, planes in sites for p in planes]).view(np.int16)
+        ill = self._illum_dev(H, W)
+        with s.lock:
+            raw = torch.from_numpy(host).to(s.td)
+            stats = torch.empty(64 * n, dtype=torch.uint8, device=s.td)
+            qc = torch.empty(24 * n, dtype=torch.uint8, device=s.td)
+            _lib.check(s.lib.cpx_illum_correct(s.h, _ptr(raw), _ptr(ill), _illum_dtype(ill), C, n, H, W, None,
+                                               _ptr(stats)), "cpx_illum_correct")
+            _lib.check(s.lib.cpx_qc_rps(s.h, _ptr(raw), _ptr(ill), _illum_dtype(ill), C, n, H, W, _ptr(stats),
+                                        None, _ptr(qc)), "cpx_qc_rps")
+            q = np.frombuffer(qc.cpu().numpy().tobytes(), dtype=[("slope", "f8"), ("pct_max", "f8"),
+                                                                 ("n_valid", "i4"), ("n_rings", "i4")])
+        out = {}
+        for k, (index, _) in enumerate(sites):
+            res = {}
+            for c, ch in enumerate(self.channels):
+                r = q[k * C + c]
+                st = _lib.CPX_QC_NAN if r["slope"] != r["slope"] else (
+                    _lib.CPX_QC_FLAT if r["n_valid"] <= 2 else _lib.CPX_QC_OK)
+                res.update(_metrics(ch, r["slope"], r["pct_max"], st))
+            out[index] = res
+        return out
+
+
+def run_sites(jobs, channels, illum, threads, batch):
+    """All sites of a LoadData table -> {index: result dict}: reader threads decode, the GPU
+    takes `batch` clean sites of one shape per call, the rest go through process_site."""
+    per_site = {}
+    bq = _BatchQC(channels, illum)
+    pending = {}  # shape -> [(index, planes)]
+
+    def flush(shape):
+        group = pending.pop(shape, [])
+        if group:
+            per_site.update(bq.run(group))
+
+    by_index = {j[0]: j for j in jobs}
+    with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, threads)) as pool:
+        for index, planes in pool.map(_decode_site, jobs):
+            if planes is None or batch <= 1 or not bq.usable(*planes[0].shape):
+                per_site[index] = process_site(by_index[index])[1]
+                continue
+            shape = planes[0].shape
+            pending.setdefault(shape, []).append((index, planes))
+            if len(pending[shape]) >= batch:
+                flush(shape)
+        for shape in list(pending):
+            flush(shape)
+    return per_site
+
+
 def load_illum(illum_path, channels):
     """Flat-field per channel: <ch>_illum.npy, else Illum<ch>.npy, else None (raw planes)."""
     if not illum_path:
@@ -172,10 +279,10 @@ def main(argv=None):
     cols = [f"FileName_{ch}" for ch in args.channels]
     jobs = [(i, [os.path.join(args.data_path, r[c]) for c in cols], args.channels, illum)
             for i, r in table.iterrows()]
-    log.info("%d sites, %d channels, %d reader threads", len(jobs), len(args.channels), args.threads)
+    log.info("%d sites, %d channels, %d reader threads, %d sites per GPU call", len(jobs),
+             len(args.channels), args.threads, args.batch)
     session()
-    with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, args.threads)) as pool:
-        per_site = dict(pool.map(process_site, jobs))
+    per_site = run_sites(jobs, args.channels, illum, args.threads, args.batch)
     # rows in table order; columns in order of first appearance (channel order within a row)
     qc = pd.DataFrame.from_dict({i: per_site[i] for i in sorted(per_site)}, orient="index")
     out = pd.concat([table, qc.sort_index()], axis=1)

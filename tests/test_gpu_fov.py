@@ -21,15 +21,17 @@ def sess():
     return qc.session()  # the CLI's process-wide session
 
 
-def test_qc_cli_matches_reference_csv(sess, golden_dir, tmp_path):
+@pytest.mark.parametrize("batch", [1, 2, 16])
+def test_qc_cli_matches_reference_csv(sess, golden_dir, tmp_path, batch):
     """cpx.qc.main on the LoadData fixture == the reference CLI's CSV (same rows, columns,
-    error strings; slopes to 1e-9 relative, PercentMaximal exactly)."""
+    error strings; slopes to 1e-9 relative, PercentMaximal exactly), whether the sites go to the
+    GPU one per call or batched (the fixture mixes clean sites with missing planes)."""
     from cpx import qc
     d = os.path.join(golden_dir, "qc_cli")
     out = tmp_path / "qc.csv"
     qc.main(["--load-data", os.path.join(d, "load_data.csv"), "--data-path", os.path.join(d, "images"),
              "--illum-path", os.path.join(d, "illum"), "--channels", "DNA", "AGP", "Mito",
-             "--output", str(out), "--threads", "3"])
+             "--output", str(out), "--threads", "3", "--batch", str(batch)])
     got = pd.read_csv(out, float_precision="round_trip")
     exp = pd.read_csv(os.path.join(d, "expected_qc.csv"), float_precision="round_trip")
     assert list(got.columns) == list(exp.columns)
