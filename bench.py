@@ -32,7 +32,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=32, help="FOVs per step per GPU (384-well plate = 12 steps)")
-    ap.add_argument("--pool", type=int, default=2, help="distinct synthetic batches cycled per GPU")
+    ap.add_argument("--pool", type=int, default=12,
+                    help="distinct synthetic batches cycled per GPU (12 x 32 = the 384 wells of configs[1])")
     ap.add_argument("--size", type=int, default=2080)
     ap.add_argument("--channels", type=int, default=5)
     ap.add_argument("--weights", default=None, help="CPnet state_dict (default: seeded random init)")
@@ -254,7 +255,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": f"fp32 planes / fp64 QC+features / {a.cpnet_precision} CPnet",
-        "data": "synthetic (HBM-resident uint16 plates, Poisson background, Gaussian nuclei + halos)",
+        "data": f"synthetic (HBM-resident uint16 plates, Poisson background, Gaussian nuclei + halos; "
+                f"{a.pool} distinct batches = {a.pool * B} distinct FOVs per GPU, cycled)",
         "config": {"workload": ("configs[1]: 384-well plate, 1 FOV/well, 2080x2080x5ch, illum->seg->feat"
                                 if Z <= 1 else
                                 f"configs[4] variant: {H}x{W}x{C}ch x {Z} z-planes, z-max->illum->seg->feat"),

@@ -111,13 +111,22 @@ __device__ __forceinline__ T wave_max(T v) {
 // fallback kernels (the two predicates must agree between the translation units).
 constexpr int kFastCropPx = 24576;
 constexpr int kFastMaskWords = 1024;
-constexpr int kFastShapeWords = 2048;  // 16 KiB of LDS for both masks: 8 blocks per CU
+constexpr int kFastShapeWords = 4096;  // 32 KiB of LDS for both masks: 5 blocks per CU (watershed
+                                       // Cells reach ~320 x 320 bboxes)
 __host__ __device__ inline bool cpx_tex_fits(int bh, int bw) {
   return bh * bw <= kFastCropPx && bh * ((bw + 31) >> 5) <= kFastMaskWords;
 }
 __host__ __device__ inline bool cpx_shape_fits(int bh, int bw) {
   return (bh + 4) * ((bw + 4 + 31) >> 5) <= kFastShapeWords;
 }
+// Objects the fast paths skip, listed per FOV by k_crop_offsets so the fallback kernels visit
+// only them: shape[fov * max_label + i] (i < n_shape[fov]) and tex[...] (i < n_tex[fov]).
+struct cpx_fallback_lists {
+  int* shape;
+  int* tex;
+  int* n_shape;
+  int* n_tex;
+};
 int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B, int C,
                       int H, int W, int max_label, int F, const cpx_object* objects_dev,
-                      const cpx_fov_objects* hdr_dev, double* feats_dev, long long** crop_off_out);
+                      const cpx_fov_objects* hdr_dev, double* feats_dev, cpx_fallback_lists* fb);

@@ -71,16 +71,17 @@ __device__ __forceinline__ bool is_border(const int* lab, int H, int W, int r, i
 }
 
 // ---------------------------------------------------------------------------------------------
-// Shape: one block per (object, fov).
+// Shape: one block per listed object (those the LDS fast path skips, k_crop_offsets' list).
 __global__ __launch_bounds__(kShapeThreads) void k_shape(const int* __restrict__ labels, int H,
                                                          int W, int max_label, int F,
                                                          const cpx_object* __restrict__ objects,
-                                                         const cpx_fov_objects* __restrict__ hdr,
+                                                         const int* __restrict__ list,
+                                                         const int* __restrict__ n_list,
                                                          double* __restrict__ feats) {
-  const int k = blockIdx.x, fov = blockIdx.y;
-  if (k >= hdr[fov].n_objects) return;
+  const int fov = blockIdx.y;
+  for (int i = blockIdx.x; i < n_list[fov]; i += gridDim.x) {
+  const int k = list[(long long)fov * max_label + i];
   const cpx_object o = objects[(long long)fov * max_label + k];
-  if (cpx_shape_fits(o.bbox[2] - o.bbox[0], o.bbox[3] - o.bbox[1])) return;  // fast path did it
   const int* lab = labels + (long long)fov * H * W;
   const int L = o.label;
   const int r0 = o.bbox[0], c0 = o.bbox[1], r1 = o.bbox[2], c1 = o.bbox[3];
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(kShapeThreads) void k_shape(const int* __restrict__
   n1 = block_sum<int, kShapeThreads>(n1, s32);
   n2 = block_sum<int, kShapeThreads>(n2, s32);
   n3 = block_sum<int, kShapeThreads>(n3, s32);
-  if (threadIdx.x != 0) return;
+  if (threadIdx.x == 0) {
   double* f = feats + ((long long)fov * max_label + k) * F;
   const double SQ2 = 1.4142135623730951;
   const double area = (double)n;
@@ -162,6 +163,9 @@ __global__ __launch_bounds__(kShapeThreads) void k_shape(const int* __restrict__
   f[CPX_SHAPE_BBOX_MIN_X] = c0;
   f[CPX_SHAPE_BBOX_MAX_Y] = r1;
   f[CPX_SHAPE_BBOX_MAX_X] = c1;
+  }
+  __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -361,8 +365,7 @@ __device__ void glcm_angle(const TexCtx& t, const unsigned char* crop, int r0, i
 __global__ __launch_bounds__(kTexThreads) void k_intensity_texture(
     const int* __restrict__ labels, const float* __restrict__ corr, int C, int H, int W,
     int max_label, int F, const cpx_object* __restrict__ objects,
-    const cpx_fov_objects* __restrict__ hdr, double* __restrict__ feats,
-    const long long* __restrict__ crop_off) {
+    const int* __restrict__ list, const int* __restrict__ n_list, double* __restrict__ feats) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned int* tab = reinterpret_cast<unsigned int*>(smem);
   unsigned int* dh = tab + kTabWords;
@@ -371,16 +374,18 @@ __global__ __launch_bounds__(kTexThreads) void k_intensity_texture(
   double* redd = reinterpret_cast<double*>(red);
   float* redf = reinterpret_cast<float*>(red);
   const int fov = blockIdx.y;
-  const int n_items = hdr[fov].n_objects * C;
+  // items (object, channel, angle): the few objects the fast path did not stage are the largest,
+  // so their four angles run on four blocks (the intensity pass is repeated, written once)
+  const int n_items = n_list[fov] * C * CPX_N_ANGLES;
   if ((int)blockIdx.x >= n_items) return;
   for (int x = threadIdx.x; x < kTabWords; x += kTexThreads) tab[x] = 0u;
   for (int x = threadIdx.x; x < 256; x += kTexThreads) dh[x] = 0u;
   __syncthreads();
   const long long N = (long long)H * W;
   for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
-    const int k = item / C, ch = item % C;
+    const int ang = item % CPX_N_ANGLES, kc = item / CPX_N_ANGLES;
+    const int k = list[(long long)fov * max_label + kc / C], ch = kc % C;
     const cpx_object o = objects[(long long)fov * max_label + k];
-    if (crop_off[(long long)fov * max_label + k] >= 0) continue;  // fast path did it
     TexCtx t;
     t.lab = labels + (long long)fov * N;
     t.img = corr + ((long long)fov * C + ch) * N;
@@ -432,7 +437,7 @@ __global__ __launch_bounds__(kTexThreads) void k_intensity_texture(
     __syncthreads();
     double* f = feats + ((long long)fov * max_label + k) * F + CPX_N_SHAPE +
                 (long long)ch * CPX_FEATURES_PER_CHANNEL;
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && ang == 0) {
       const double mean = n ? s / (double)n : 0.0;
       double var = n ? (ss - s * mean) / (double)n : 0.0;
       if (var < 0.0) var = 0.0;
@@ -469,7 +474,7 @@ __global__ __launch_bounds__(kTexThreads) void k_intensity_texture(
     }
     // offsets (dr, dc) = (round(sin a * 3), round(cos a * 3)) for a = 0, 45, 90, 135 deg
     const int DR[4] = {0, 2, 3, 2}, DC[4] = {3, 2, 0, -2};
-    for (int a = 0; a < CPX_N_ANGLES; ++a) {
+    for (int a = ang; a <= ang; ++a) {
       double* out = f + CPX_N_INT + a * CPX_N_TEX_PROPS;
       if (staged) glcm_angle<true, true>(t, crop, r0, c0, r1, c1, DR[a], DC[a], tab, dh, red, out);
       else if (nb <= 65535) glcm_angle<false, true>(t, crop, r0, c0, r1, c1, DR[a], DC[a], tab, dh, red, out);
@@ -488,13 +493,14 @@ extern "C" int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float
   CPX_REQUIRE(B > 0 && B <= 65535 && C > 0 && C <= 65535 && H > 0 && W > 0 && max_label > 0,
               CPX_ERR_ARG, "cpx_features: bad sizes");
   const int F = CPX_N_SHAPE + C * CPX_FEATURES_PER_CHANNEL;
-  long long* crop_off = nullptr;
+  cpx_fallback_lists fb;
   const int rc = cpx_features_fast(ctx, labels_dev, corr_dev, B, C, H, W, max_label, F, objects_dev,
-                                   hdr_dev, feats_dev, &crop_off);
+                                   hdr_dev, feats_dev, &fb);
   if (rc) return rc;
-  // fallback kernels for objects too large for the LDS fast paths (skip the others)
-  hipLaunchKernelGGL(k_shape, dim3(max_label, B), dim3(kShapeThreads), 0, ctx->stream,
-                     (const int*)labels_dev, H, W, max_label, F, objects_dev, hdr_dev, feats_dev);
+  // fallback kernels for the objects too large for the LDS fast paths (listed per FOV)
+  hipLaunchKernelGGL(k_shape, dim3(std::max(1, std::min(max_label, (4 * ctx->n_cu + B - 1) / B)), B),
+                     dim3(kShapeThreads), 0, ctx->stream, (const int*)labels_dev, H, W, max_label, F,
+                     objects_dev, (const int*)fb.shape, (const int*)fb.n_shape, feats_dev);
   CPX_CHECK_LAUNCH("k_shape");
   static bool attr = false;
   const size_t lds = sizeof(unsigned int) * (kTabWords + 256) +
@@ -504,10 +510,10 @@ extern "C" int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  const int per_fov = std::max(1, std::min(max_label * C, (ctx->n_cu + B - 1) / B));
+  const int per_fov = std::max(1, std::min(max_label * C * CPX_N_ANGLES, (ctx->n_cu + B - 1) / B));
   hipLaunchKernelGGL(k_intensity_texture, dim3(per_fov, B), dim3(kTexThreads), lds,
                      ctx->stream, (const int*)labels_dev, corr_dev, C, H, W, max_label, F,
-                     objects_dev, hdr_dev, feats_dev, (const long long*)crop_off);
+                     objects_dev, (const int*)fb.tex, (const int*)fb.n_tex, feats_dev);
   CPX_CHECK_LAUNCH("k_intensity_texture");
   return CPX_OK;
 }

@@ -8,10 +8,8 @@
 //    for the intensity statistics and the scale_to_8bit range, then writes the 8-bit masked
 //    crop to a global scratch slot (offsets from a per-FOV scan); phase B (one 1024-thread
 //    block per CU with a 128 KiB LDS pair table) copies the crop to LDS and runs the four GLCM
-//    angles from LDS: exact u32 pair sums in registers, |i-j| < 8 counted in packed
-//    registers, ASM from the returned counts of a 64K-entry packed u16 LDS table, background
-//    (0,0) pairs by branch; DPP wave sums, greycoprops on one wave while the others clear the
-//    table with 16-byte stores.
+//    angles from LDS: exact u32 pair sums in registers per run of equal keys, ASM from the
+//    counts the table's atomics return, background (0,0) pairs by branch; DPP wave sums.
 //  * AreaShape: bbox + 2-pixel margin bitmask in LDS; the 4-neighbour border and the
 //    Benkrid-Crookes perimeter code are evaluated bit-parallel, moments are exact int64 sums.
 #include "cpx_internal.h"
@@ -44,7 +42,6 @@ constexpr int kTabW = 32768;         // packed u16 pair counters (128 KiB)
 constexpr int kCrop = kFastCropPx;   // u8 crop capacity (pixels)
 constexpr int kMaskW = kFastMaskWords;  // membership bitmask words (bh * ceil(bw/32))
 constexpr int kNW = kTT / 64;
-constexpr int kList = 3680;          // distinct-key list capacity (u16 keys)
 
 __device__ __forceinline__ int quantize(float v, bool in, float mn, float rng, bool flat) {
   const float m = v * (in ? 1.0f : 0.0f);
@@ -97,18 +94,17 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 
 // GLCM of one (object, channel) item: skimage graycomatrix offsets (dr, dc) for angles
 // 0, pi/4, pi/2, 3pi/4 at distance 3, symmetric=False, normed, then greycoprops.
-//  1. count (per angle): every pixel pair adds 1 to its packed-u16 counter in a 64K-key LDS
-//     table (background pairs (0, 0) are only counted in a register); a pair that finds its
-//     counter at 0 appends the key to a distinct-key list (wave-aggregated slot reservation);
-//  2. walk (per angle): per distinct key (i, j) with count c, exact u32 sums of c*i, c*j, c*i^2,
-//     c*j^2, c*i*j, c^2 (ASM), c*d^2 and c*d (d = |i-j|), and a u64 fixed-point sum of
-//     c * round(2^48 / (1 + d^2)) for homogeneity (per-term relative error <= 1.2e-10); the
-//     counter half is cleared by an LDS atomic AND as it is read.  With at most 65535 pairs per
-//     item every total fits (sum c*d^2 <= 65535 * 255^2 < 2^32, sum c^2 <= 65535^2 < 2^32).  A
-//     crop with more distinct keys than the list holds scans (and clears) the whole table;
+//  1. count (per angle): runs of equal keys along a thread's segment are added at once to their
+//     packed-u16 counter in a 64K-key LDS table (background pairs (0, 0) only counted in a
+//     register); each run also adds its exact u32 sums of c*i, c*j, c*i^2, c*j^2, c*i*j, c*d^2,
+//     c*d (d = |i-j|) and a u64 fixed-point c * round(2^48 / (1 + d^2)) for homogeneity (per-term
+//     relative error <= 1.2e-10), and ASM = sum c^2 grows by cnt * (2 old + cnt) from the counter
+//     value its atomic returns — so counts are never read back.  With at most 65535 pairs per
+//     item every total fits (sum c*d^2 <= 65535 * 255^2 < 2^32, sum c^2 <= 65535^2 < 2^32);
+//  2. clear the table with 16-byte stores;
 //  3. finish (once per item, all four angles): DPP wave sums, one cross-wave pass through the
 //     (by then all-zero) table, greycoprops on four lanes.  All sums are integer, so the result
-//     never depends on the order in which pairs or keys were visited.
+//     never depends on the order in which pairs or runs were visited.
 struct HomTable {
   unsigned long long m[256];
   constexpr HomTable() : m() {
@@ -138,29 +134,34 @@ __device__ __forceinline__ void glcm_key(unsigned int c, unsigned int i, unsigne
   A.hom += (unsigned long long)c * kHom.m[d];
 }
 
-// Add a run of cnt pairs of one key; the lane that finds the counter at 0 appends the key to
-// the distinct-key list (slots reserved once per wave among the flushing lanes).
-__device__ __forceinline__ void glcm_flush(unsigned int* tab, unsigned short* list, int* nlist,
-                                           unsigned int key, unsigned int cnt, int lane) {
+// Add a run of cnt pairs of one key: the pair sums of the run go straight into the registers
+// (c*i, c*j, ..., c * hom(d) from the LDS copy of the homogeneity table), and ASM = sum c_k^2
+// grows by (old + cnt)^2 - old^2 = cnt * (2*old + cnt) from the counter value the atomic returns,
+// so the counts never have to be read back: the table is only cleared after the angle.
+__device__ __forceinline__ void glcm_flush(unsigned int* tab, const unsigned long long* hom,
+                                           unsigned int key, unsigned int cnt, GlcmAcc& A) {
   const unsigned int sh = (key & 1u) << 4;
-  const unsigned int old = atomicAdd(&tab[key >> 1], cnt << sh);
-  const bool fresh = ((old >> sh) & 0xffffu) == 0u;
-  const unsigned long long m = __ballot(fresh);
-  if (m) {
-    const int leader = __builtin_ffsll((long long)m) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(nlist, __popcll(m));
-    base = __shfl(base, leader);
-    const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
-    if (fresh && pos < kList) list[pos] = (unsigned short)key;
-  }
+  const unsigned int old = (atomicAdd(&tab[key >> 1], cnt << sh) >> sh) & 0xffffu;
+  const unsigned int i = key >> 8, j = key & 255u;
+  const unsigned int ci = cnt * i, cj = cnt * j;
+  const unsigned int d = i > j ? i - j : j - i;
+  A.si += ci;
+  A.sj += cj;
+  A.sii += ci * i;
+  A.sjj += cj * j;
+  A.sij += ci * j;
+  A.asq += cnt * (2u * old + cnt);
+  A.con += cnt * d * d;
+  A.dis += cnt * d;
+  A.hom += (unsigned long long)cnt * hom[d];
 }
 
 // Phase 1 of one angle over an 8-bit crop in LDS (or the global scratch slot); returns this
 // thread's background-pair count.
 template <bool LDS_CROP>
 __device__ unsigned int glcm_count(const unsigned char* __restrict__ crop, unsigned int* tab,
-                                   unsigned short* list, int* nlist, int bh, int bw, int dr, int dc) {
+                                   const unsigned long long* hom, GlcmAcc& A, int bh, int bw, int dr,
+                                   int dc) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int rend = bh - dr;  // dr >= 0
   const int cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
@@ -195,7 +196,7 @@ __device__ unsigned int glcm_count(const unsigned char* __restrict__ crop, unsig
       for (int u = 0; u < 4; ++u) {
         if (p + u >= pend) break;
         if (key[u] != cur) {
-          if (cur) glcm_flush(tab, list, nlist, cur, cnt, lane);
+          if (cur) glcm_flush(tab, hom, cur, cnt, A);
           else bg += cnt;
           cur = key[u];
           cnt = 0;
@@ -204,42 +205,16 @@ __device__ unsigned int glcm_count(const unsigned char* __restrict__ crop, unsig
       }
     }
   }
-  if (cur) glcm_flush(tab, list, nlist, cur, cnt, lane);
+  if (cur) glcm_flush(tab, hom, cur, cnt, A);
   else bg += cnt;
   return bg;
 }
 
-// Phase 2 of one angle: the n listed keys (or the whole table if the list overflowed) into A,
-// leaving every counter at zero.
-__device__ void glcm_walk(unsigned int* tab, const unsigned short* list, int n, GlcmAcc& A) {
-  if (n <= kList) {
-    for (int x = threadIdx.x; x < n; x += kTT) {
-      const unsigned int key = list[x];
-      const unsigned int sh = (key & 1u) << 4;
-      const unsigned int c = (tab[key >> 1] >> sh) & 0xffffu;
-      // the partner key of the same word may be read by another thread: clear only this half
-      __hip_atomic_fetch_and(&tab[key >> 1], ~(0xffffu << sh), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-      glcm_key(c, key >> 8, key & 255u, A);
-    }
-  } else {  // dense fallback: scan and clear the whole table
-    uint4* t4 = reinterpret_cast<uint4*>(tab);
-    for (int x = threadIdx.x; x < kTabW / 4; x += kTT) {
-      const uint4 v = t4[x];
-      if ((v.x | v.y | v.z | v.w) == 0u) continue;
-      t4[x] = uint4{0u, 0u, 0u, 0u};
-      const unsigned int i = (unsigned int)x >> 5;  // the 8 keys 8x .. 8x+7 share i
-      const unsigned int w4[4] = {v.x, v.y, v.z, v.w};
+// Phase 2 of one angle: clear the table for the next angle with 16-byte stores.
+__device__ __forceinline__ void glcm_clear(unsigned int* tab) {
+  uint4* t4 = reinterpret_cast<uint4*>(tab);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const unsigned int c = (w4[e] >> (16 * hh)) & 0xffffu;
-          if (c) glcm_key(c, i, ((unsigned int)(8 * x) & 255u) + 2u * e + hh, A);
-        }
-      }
-    }
-  }
+  for (int x = threadIdx.x; x < kTabW / 4; x += kTT) t4[x] = uint4{0u, 0u, 0u, 0u};
 }
 
 // Phase 3: reduce the four angles' sums over the block and write greycoprops.  `red` is
@@ -529,13 +504,12 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_code[2];  // queue codes (see glcm_grab), double-buffered by iteration parity
   unsigned int* tab = reinterpret_cast<unsigned int*>(smem);
-  int* nlist = reinterpret_cast<int*>(tab + kTabW);  // two counters: angle a uses a & 1
-  unsigned char* crop = reinterpret_cast<unsigned char*>(nlist + 4);
-  unsigned short* list = reinterpret_cast<unsigned short*>(crop + kCrop);
+  unsigned long long* hom = reinterpret_cast<unsigned long long*>(tab + kTabW);  // 2 KiB
+  unsigned char* crop = reinterpret_cast<unsigned char*>(hom + 256);
   const int B = gridDim.y;
   int q_fov = blockIdx.y, q_visited = 0;  // thread 0's queue position
   for (int x = threadIdx.x; x < kTabW; x += kTT) tab[x] = 0u;
-  if (threadIdx.x < 4) nlist[threadIdx.x] = 0;
+  if (threadIdx.x < 256) hom[threadIdx.x] = kHom.m[threadIdx.x];
   if (threadIdx.x == 0) {
     s_code[0] = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next);
     s_code[1] = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next);
@@ -582,19 +556,12 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
     for (int a = 0; a < CPX_N_ANGLES; ++a) {
       const int dr = a == 0 ? 0 : a == 2 ? 3 : 2;
       const int dc = a == 0 ? 3 : a == 1 ? 2 : a == 2 ? 0 : -2;
-      int* nl = nlist + (a & 1);
       acc[a].bg = it.nb <= kCrop
-                      ? glcm_count<true>(crop, tab, list, nl, it.bh, it.bw, dr, dc)
-                      : glcm_count<false>(it.src, tab, list, nl, it.bh, it.bw, dr, dc);
+                      ? glcm_count<true>(crop, tab, hom, acc[a], it.bh, it.bw, dr, dc)
+                      : glcm_count<false>(it.src, tab, hom, acc[a], it.bh, it.bw, dr, dc);
       __syncthreads();
       GLCM_MARK(2, &pt);
-      const int n = *nl;
-#ifdef CPX_GLCM_PROF
-      if (threadIdx.x == 0 && n > kList) atomicAdd(&g_glcm_prof[0], 1ull);  // dense walks
-#endif
-      // the other counter was last read before the previous barrier; the next angle uses it
-      if (threadIdx.x == 0) nlist[(a + 1) & 1] = 0;
-      glcm_walk(tab, list, n, acc[a]);
+      glcm_clear(tab);
       __syncthreads();
       GLCM_MARK(3, &pt);
     }
@@ -609,13 +576,17 @@ __global__ __launch_bounds__(1024) void k_crop_offsets(int C, int max_label,
                                                       const cpx_object* __restrict__ objects,
                                                       const cpx_fov_objects* __restrict__ hdr,
                                                       long long cap, long long* __restrict__ crop_off,
-                                                      int* __restrict__ glcm_next) {
+                                                      int* __restrict__ glcm_next, cpx_fallback_lists fb) {
   const int fov = blockIdx.x;
   const int n = hdr[fov].n_objects;
   if (threadIdx.x == 0) glcm_next[fov] = 0;  // k_tex_glcm's work queue of this FOV
   __shared__ long long wsum[16];
   __shared__ long long base;
-  if (threadIdx.x == 0) base = 0;
+  __shared__ int ns, nt;
+  if (threadIdx.x == 0) {
+    base = 0;
+    ns = nt = 0;
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int k0 = 0; k0 < n; k0 += blockDim.x) {
@@ -637,7 +608,14 @@ __global__ __launch_bounds__(1024) void k_crop_offsets(int C, int max_label,
     long long off = base;
     for (int w = 0; w < wid; ++w) off += wsum[w];
     off += x - sz;
-    if (k < n) crop_off[(long long)fov * max_label + k] = (sz > 0 && off + sz <= cap) ? off : -1;
+    if (k < n) {
+      const bool staged = sz > 0 && off + sz <= cap;
+      crop_off[(long long)fov * max_label + k] = staged ? off : -1;
+      const cpx_object o = objects[(long long)fov * max_label + k];
+      if (!staged) fb.tex[(long long)fov * max_label + atomicAdd(&nt, 1)] = k;
+      if (!cpx_shape_fits(o.bbox[2] - o.bbox[0], o.bbox[3] - o.bbox[1]))
+        fb.shape[(long long)fov * max_label + atomicAdd(&ns, 1)] = k;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       long long t = 0;
@@ -645,6 +623,10 @@ __global__ __launch_bounds__(1024) void k_crop_offsets(int C, int max_label,
       base += t;
     }
     __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    fb.n_shape[fov] = ns;
+    fb.n_tex[fov] = nt;
   }
 }
 
@@ -810,10 +792,10 @@ __global__ __launch_bounds__(kST) void k_shape_fast(const int* __restrict__ labe
 // internal launchers used by cpx_features (k_features.hip)
 int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B, int C,
                       int H, int W, int max_label, int F, const cpx_object* objects_dev,
-                      const cpx_fov_objects* hdr_dev, double* feats_dev, long long** crop_off_out) {
+                      const cpx_fov_objects* hdr_dev, double* feats_dev, cpx_fallback_lists* fb) {
   static bool attr = false;
-  const size_t lds_t = sizeof(unsigned int) * (kTabW + 4) + kCrop + 2 * kList;
-  static_assert(sizeof(unsigned int) * (kTabW + 4) + kCrop + 2 * kList <= 160 * 1024,
+  const size_t lds_t = sizeof(unsigned int) * kTabW + sizeof(unsigned long long) * 256 + kCrop;
+  static_assert(sizeof(unsigned int) * kTabW + sizeof(unsigned long long) * 256 + kCrop <= 160 * 1024,
                 "GLCM LDS budget");
   static_assert(kNW * 4 * kAccW <= kTabW, "reduction scratch inside the table");
   const size_t lds_s = sizeof(unsigned int) * 2 * kShapeW;
@@ -826,18 +808,22 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   }
   // workspace: crop offsets [B][max_label] + scratch (2 bytes per pixel-channel per FOV)
   const long long per_fov = ((2LL * H * W * C + 255) / 256) * 256;
-  // + one GLCM work-queue counter per FOV (zeroed by k_crop_offsets)
-  const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + sizeof(int) * (size_t)B + 255) / 256) * 256;
+  // + one GLCM work-queue counter per FOV (zeroed by k_crop_offsets) + the fallback lists
+  const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + sizeof(int) * (size_t)B * 3 +
+                             sizeof(int) * 2 * (size_t)B * max_label + 255) / 256) * 256;
   unsigned char* ws = (unsigned char*)cpx_ws(ctx, WS_MISC, off_bytes + (size_t)B * per_fov + 256);  // +256: GLCM key read-ahead
   if (!ws) return CPX_ERR_OOM;
   CPX_REQUIRE(B < 2048 && (long long)max_label * C < (1 << 20), CPX_ERR_SHAPE,
               "GLCM queue codes hold fov < 2048 and items < 2^20");
   long long* crop_off = (long long*)ws;
   int* glcm_next = (int*)(crop_off + (size_t)B * max_label);
+  fb->n_shape = glcm_next + B;
+  fb->n_tex = fb->n_shape + B;
+  fb->shape = fb->n_tex + B;
+  fb->tex = fb->shape + (size_t)B * max_label;
   unsigned char* scratch = ws + off_bytes;
-  *crop_off_out = crop_off;
   hipLaunchKernelGGL(k_crop_offsets, dim3(B), dim3(1024), 0, ctx->stream, C, max_label,
-                     objects_dev, hdr_dev, per_fov, crop_off, glcm_next);
+                     objects_dev, hdr_dev, per_fov, crop_off, glcm_next, *fb);
   CPX_CHECK_LAUNCH("k_crop_offsets");
   const int per_fov_s = std::max(1, std::min(max_label, (8 * ctx->n_cu + B - 1) / B));
   hipLaunchKernelGGL(k_shape_fast, dim3(per_fov_s, B), dim3(kST), lds_s, ctx->stream,

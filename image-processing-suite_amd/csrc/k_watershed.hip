@@ -185,7 +185,7 @@ __device__ __forceinline__ unsigned char border_bits_off(int o) {
 }
 
 template <bool R0>
-__global__ __launch_bounds__(kThreads, 3) void k_ws_relax(WsArgs a, int round,
+__global__ __launch_bounds__(kThreads, 2) void k_ws_relax(WsArgs a, int round,
                                                        const unsigned char* __restrict__ Fp,
                                                        unsigned char* __restrict__ Fn) {
   // levels of the tile + halo, and the key of every free tile pixel (kBlocked for markers,
