@@ -348,7 +348,7 @@ def cpu_baseline(ctx, pool_batch, illum, C, H, W, cfg):
             path = os.path.join(td, f"fov{i}.npy")
             np.save(path, raw[i % B])
             jobs.append((path, ill_path, cfg.weights, cfg.seed, cfg.model, cfg.diameter, cfg.cell_expand,
-                         cfg.cells, cfg.cell_channel))
+                         cfg.cells, cfg.ws_channel()))
         t0 = time.perf_counter()
         with ctx.Pool(cores) as pool:
             out = pool.map(_cpu_worker, jobs, chunksize=1)

@@ -46,7 +46,8 @@ class PipelineConfig:
                                      # inside the expand_labels(Nuclei, cell_expand) footprint
                                      # (DESIGN.md §7); "expand": Cells = that footprint's labels
     cell_expand: int = 15            # footprint distance (px)
-    cell_channel: int = 3            # watershed elevation channel (AGP)
+    cell_channel: int | None = None  # watershed elevation channel; None: "AGP" when present
+                                     # among the first C channel names, else the last channel
     ws_rounds: tuple = (24, 16)      # watershed relax tile rounds / label pointer-jump rounds
                                      # enqueued per batch (bench plates: <= 9 / ~8; idle ~6 us)
     max_objects: int = 2048          # per FOV and object set
@@ -57,6 +58,13 @@ class PipelineConfig:
     crops: bool = False              # a7 crops for the embedding consumer (off in the bench)
     crops_f32: bool = True           # also keep the float crops (the embedder needs only crops8)
     slots: int = 2                   # result buffer sets (fetch of step i overlaps step i + 1)
+
+    def ws_channel(self) -> int:
+        """The watershed elevation channel (cell_channel, or "AGP" / the last channel)."""
+        if self.cell_channel is not None:
+            return self.cell_channel
+        names = list(self.channels)[: self.C]
+        return names.index("AGP") if "AGP" in names else self.C - 1
 
 
 @dataclasses.dataclass
@@ -132,9 +140,10 @@ class FovPipeline:
         cfg = self.cfg
         B, H, W = cfg.batch, cfg.H, cfg.W
         if cfg.cells == "watershed":
+            ch = cfg.ws_channel()
             st = self.seg.stats  # cpx_seg_stats [B] (32 bytes): cells_status is int32 field 6
             check(self.dev.lib.cpx_watershed_cells(
-                self.dev.h, _ptr(self.labels["Nuclei"]), _ptr(self.corr), B, cfg.C, cfg.cell_channel,
+                self.dev.h, _ptr(self.labels["Nuclei"]), _ptr(self.corr), B, cfg.C, ch,
                 H, W, cfg.cell_expand, cfg.ws_rounds[0], cfg.ws_rounds[1], _ptr(self.labels["Cells"]),
                 _ptr(self.labels["Cytoplasm"]), st.data_ptr() + 6 * 4, 8),
                 "cpx_watershed_cells")

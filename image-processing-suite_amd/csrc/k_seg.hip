@@ -1223,7 +1223,6 @@ __global__ __launch_bounds__(kFillThreads) void k_fill_holes(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned int* own = reinterpret_cast<unsigned int*>(smem);
   unsigned int* reach = own + kFillMaxWords;
-  __shared__ int changed;
   const int fov = blockIdx.y;
   const int nobj = hdr[fov].n_objects;
   for (int k = blockIdx.x; k < nobj; k += gridDim.x) {
@@ -1255,8 +1254,6 @@ __global__ __launch_bounds__(kFillThreads) void k_fill_holes(
   __syncthreads();
   // flood the non-object cells from the bbox border (4-connectivity), in place until stable
   for (int iter = 0; iter < bh * bw + 1; ++iter) {
-    if (threadIdx.x == 0) changed = 0;
-    __syncthreads();
     int ch = 0;
     for (int w = threadIdx.x; w < nw; w += kFillThreads) {
       const int r = w / wpr, cw = w - r * wpr;
@@ -1274,9 +1271,10 @@ __global__ __launch_bounds__(kFillThreads) void k_fill_holes(
         ch = 1;
       }
     }
-    if (ch) changed = 1;
-    __syncthreads();
-    if (!changed) break;
+    // one barrier that also returns the block-wide decision: a flag reset by thread 0 at the
+    // top of the next iteration could be read as 0 by a wave still leaving this one (which then
+    // broke out early: an incomplete flood, barriers out of step)
+    if (!__syncthreads_or(ch)) break;
   }
   // holes: free and unreached; mark fill owner and absorbed objects
   for (int w = threadIdx.x; w < nw; w += kFillThreads) {

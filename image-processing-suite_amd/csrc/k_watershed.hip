@@ -564,7 +564,7 @@ extern "C" int cpx_watershed_cells(cpx_ctx* ctx, const int32_t* nuclei_dev, cons
   CPX_REQUIRE(relax_rounds <= 64 && label_rounds <= 64 && B > 0 && B <= 65535 && C > 0 && cell_channel >= 0 && cell_channel < C && H > 0 &&
                   W > 0 && (long long)H * W <= (1ll << kKeyShift) && relax_rounds > 0 &&
                   label_rounds > 0 && status_stride > 0,
-              CPX_ERR_ARG, "cpx_watershed_cells: bad sizes (H*W must be <= 2^23)");
+              CPX_ERR_ARG, "cpx_watershed_cells: bad sizes (H*W <= 2^23, 0 <= cell_channel < C, rounds 1..64)");
   // the footprint (mask) and the Cytoplasm of every pixel the flood does not relabel
   int rc = cpx_expand_labels(ctx, nuclei_dev, B, H, W, distance, cells_dev, cyto_dev);
   if (rc != CPX_OK) return rc;

@@ -79,7 +79,7 @@ def test_e2e_cells_cytoplasm_bit_exact(e2e):
     for b in range(e2e["yf"].shape[0]):
         cfg = e2e["cfg"]
         assert cfg.cells == "watershed"
-        cells, cyto = wo.cells_watershed(e2e["labels"]["Nuclei"][b], e2e["corr"][b, cfg.cell_channel],
+        cells, cyto = wo.cells_watershed(e2e["labels"]["Nuclei"][b], e2e["corr"][b, cfg.ws_channel()],
                                          cfg.cell_expand)
         np.testing.assert_array_equal(e2e["labels"]["Cells"][b], cells)
         np.testing.assert_array_equal(e2e["labels"]["Cytoplasm"][b], cyto)
