@@ -20,8 +20,10 @@ import seg_oracle as so
 
 def run_fov(raw: np.ndarray, illum: np.ndarray, net, cell_expand: int = 15, model: str = "nuclei",
             diameter: float = 100.0, timings: dict | None = None, cells: str = "watershed",
-            cell_channel: int = 3):
-    """raw uint16 [C,H,W], illum fp32 [C,H,W]; net = CPU CPnet (torch).  Returns dict of outputs."""
+            cell_channel: int = 3, flows: np.ndarray | None = None):
+    """raw uint16 [C,H,W], illum fp32 [C,H,W]; net = CPU CPnet (torch).  Returns dict of outputs.
+    flows: tile-averaged network output [3,H',W'] to use instead of running `net` (the CSV parity
+    test feeds the GPU's own flows, so everything after the network is compared bit for bit)."""
     import torch
     t = time.perf_counter()
     C, H, W = raw.shape
@@ -32,11 +34,14 @@ def run_fov(raw: np.ndarray, illum: np.ndarray, net, cell_expand: int = 15, mode
         qc.append(orc.calculate_qc_metrics(img, str(c)))
         corr[c] = orc.illum_correct_producer(raw[c], illum[c])
     t1 = time.perf_counter()
-    Ly, Lx = so.net_size(H, W, model, diameter)
-    tiles, g = so.make_net_input(corr, Ly, Lx)
-    with torch.no_grad():
-        y = net(torch.from_numpy(tiles)).numpy()
-    yf = so.average_tiles(y, g)
+    if flows is None:
+        Ly, Lx = so.net_size(H, W, model, diameter)
+        tiles, g = so.make_net_input(corr, Ly, Lx)
+        with torch.no_grad():
+            y = net(torch.from_numpy(tiles)).numpy()
+        yf = so.average_tiles(y, g)
+    else:
+        yf = flows
     nuclei = so.compute_masks(yf, H, W)
     t2 = time.perf_counter()
     if cells == "watershed":
@@ -49,4 +54,4 @@ def run_fov(raw: np.ndarray, illum: np.ndarray, net, cell_expand: int = 15, mode
     t3 = time.perf_counter()
     if timings is not None:
         timings.update(illum_qc=t1 - t, segment=t2 - t1, objects_features=t3 - t2, total=t3 - t)
-    return dict(qc=qc, nuclei=nuclei, cells=cells, cyto=cyto, feats=feats)
+    return dict(qc=qc, nuclei=nuclei, cells=cells, cyto=cyto, feats=feats, corr=corr, flows=yf)

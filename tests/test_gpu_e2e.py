@@ -160,3 +160,34 @@ def test_e2e_network_precision_agreement(e2e, dev):
     print(json.dumps(rows))
     for r in rows:
         assert r["bf16_gpu_vs_fp32_cpu"]["fraction_matched"] >= 0.9, r
+
+
+def test_e2e_csv_tables(e2e, tmp_path):
+    """north_star's CSV parity: the four result tables (Image / Nuclei / Cells / Cytoplasm, as
+    Pycyto_pertime.py reads them) written from the GPU results vs written from the CPU pipeline
+    (oracle/cpu_pipeline.run_fov) on the same raw FOV and the GPU's own flows.  ObjectNumber /
+    ImageNumber columns and counts identical, PercentMaximal exact, PowerLogLogSlope rel 1e-9,
+    every feature column within rtol 1e-5."""
+    import pandas as pd
+    import cpu_pipeline
+    from csv_tables import cpu_tables, gpu_tables
+    cfg, res = e2e["cfg"], e2e["res"]
+    for b in range(e2e["yf"].shape[0]):
+        ref = cpu_pipeline.run_fov(e2e["raw"][b], e2e["illum"], None, cell_expand=cfg.cell_expand,
+                                   cell_channel=cfg.ws_channel(), flows=e2e["yf"][b])
+        dirs = {}
+        for side, t in (("cpu", cpu_tables(ref, image_number=b + 1)), ("gpu", gpu_tables(res, b, image_number=b + 1))):
+            dirs[side] = t.write(str(tmp_path / side), "P01", 24)
+        for name in ("Image", "Nuclei", "Cells", "Cytoplasm"):
+            c = pd.read_csv(os.path.join(dirs["cpu"], f"{name}.csv"))
+            g = pd.read_csv(os.path.join(dirs["gpu"], f"{name}.csv"))
+            assert list(c.columns) == list(g.columns), name
+            assert len(c) == len(g) and len(c) > 0, (name, len(c), len(g))
+            exact = [k for k in c.columns if k in ("ImageNumber", "ObjectNumber", "Number_Object_Number")
+                     or k.startswith(("Count_", "ImageQuality_PercentMaximal", "Metadata_"))]
+            for k in exact:
+                assert (c[k].to_numpy() == g[k].to_numpy()).all(), (name, k)
+            rest = [k for k in c.columns if k not in exact]
+            rtol = 1e-9 if name == "Image" else 1e-5
+            np.testing.assert_allclose(g[rest].to_numpy(np.float64), c[rest].to_numpy(np.float64),
+                                       rtol=rtol, atol=1e-9, err_msg=name)
