@@ -109,13 +109,8 @@ __device__ __forceinline__ T wave_max(T v) {
 
 // Objects handled by the LDS fast paths in k_texture.hip; the rest go to the k_features.hip
 // fallback kernels (the two predicates must agree between the translation units).
-constexpr int kFastCropPx = 24576;
-constexpr int kFastMaskWords = 1024;
 constexpr int kFastShapeWords = 4096;  // 32 KiB of LDS for both masks: 5 blocks per CU (watershed
                                        // Cells reach ~320 x 320 bboxes)
-__host__ __device__ inline bool cpx_tex_fits(int bh, int bw) {
-  return bh * bw <= kFastCropPx && bh * ((bw + 31) >> 5) <= kFastMaskWords;
-}
 __host__ __device__ inline bool cpx_shape_fits(int bh, int bw) {
   return (bh + 4) * ((bw + 4 + 31) >> 5) <= kFastShapeWords;
 }

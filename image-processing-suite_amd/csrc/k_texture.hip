@@ -36,12 +36,12 @@ __device__ unsigned long long g_glcm_prof[8];
   } while (0)
 #endif
 
-constexpr int kTT = 1024;            // GLCM block: 32 rows x 32 columns (16 waves)
-constexpr int kRows = kTT / 32;
-constexpr int kTabW = 32768;         // packed u16 pair counters (128 KiB)
-constexpr int kCrop = kFastCropPx;   // u8 crop capacity (pixels)
-constexpr int kMaskW = kFastMaskWords;  // membership bitmask words (bh * ceil(bw/32))
+constexpr int kTT = 1024;            // GLCM block (16 waves, one block per CU)
 constexpr int kNW = kTT / 64;
+constexpr int kTabW = 32768;         // 64K packed u16 pair counters (128 KiB), diagonal-major
+constexpr int kSmall = 256 + 320 + 16;  // LDS after the table: atomic sinks, reduction totals, queue codes
+constexpr int kCrop = 160 * 1024 - 4 * kTabW - kSmall;  // u8 crop bytes held in LDS
+constexpr int kSlack = 16;           // bytes the GLCM may read past a crop's last row (masked)
 
 __device__ __forceinline__ int quantize(float v, bool in, float mn, float rng, bool flat) {
   const float m = v * (in ? 1.0f : 0.0f);
@@ -52,59 +52,32 @@ __device__ __forceinline__ int quantize(float v, bool in, float mn, float rng, b
   return (int)(unsigned char)(int)x;
 }
 
-__device__ __forceinline__ bool mask_bit(const unsigned int* m, int wpr, int r, int c) {
-  return (m[r * wpr + (c >> 5)] >> (c & 31)) & 1u;
-}
-
-// Wave-wide sum of a u32 on the VALU/DPP path (no LDS traffic); the result is wave-uniform.
-// row_shr 1,2,4,8 = inclusive scan within each row of 16 lanes; row_bcast:15 / row_bcast:31
-// carry the row totals upward, so lane 63 holds the wave total.
-__device__ __forceinline__ unsigned int wave_sum_u32(unsigned int v) {
-  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
-  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
-  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
-  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
-  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
-  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
-  return (unsigned int)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-// The same scan for a u64 (both halves moved by DPP, 64-bit adds): no LDS round trips, where
-// the generic __shfl_xor sum costs twelve ds_bpermute.
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
-#define CPX_U64_DPP_STEP(CTRL, ROWMASK)                                                         \
-  {                                                                                            \
-    const unsigned int lo_ = (unsigned int)__builtin_amdgcn_update_dpp(0, (int)(unsigned int)v, \
-                                                                       CTRL, ROWMASK, 0xf, false); \
-    const unsigned int hi_ = (unsigned int)__builtin_amdgcn_update_dpp(                        \
-        0, (int)(unsigned int)(v >> 32), CTRL, ROWMASK, 0xf, false);                           \
-    v += ((unsigned long long)hi_ << 32) | lo_;                                                \
-  }
-  CPX_U64_DPP_STEP(0x111, 0xf)
-  CPX_U64_DPP_STEP(0x112, 0xf)
-  CPX_U64_DPP_STEP(0x114, 0xf)
-  CPX_U64_DPP_STEP(0x118, 0xf)
-  CPX_U64_DPP_STEP(0x142, 0xa)
-  CPX_U64_DPP_STEP(0x143, 0xc)
-#undef CPX_U64_DPP_STEP
-  const unsigned int lo = (unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)v, 63);
-  const unsigned int hi = (unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)(v >> 32), 63);
-  return ((unsigned long long)hi << 32) | lo;
+// Staged 8-bit crops: rows padded to a multiple of 8 bytes (the GLCM reads eight pixels per
+// load), kSlack bytes after the last row, slot size a multiple of 16 (uint4 copies).
+__host__ __device__ __forceinline__ int crop_stride(int bw) { return (bw + 7) & ~7; }
+__host__ __device__ __forceinline__ long long crop_bytes(int bh, int bw) {
+  return ((long long)bh * crop_stride(bw) + kSlack + 15) / 16 * 16;
 }
 
 // GLCM of one (object, channel) item: skimage graycomatrix offsets (dr, dc) for angles
-// 0, pi/4, pi/2, 3pi/4 at distance 3, symmetric=False, normed, then greycoprops.
-//  1. count (per angle): runs of equal keys along a thread's segment are added at once to their
-//     packed-u16 counter in a 64K-key LDS table (background pairs (0, 0) only counted in a
-//     register); each run also adds its exact u32 sums of c*i, c*j, c*i^2, c*j^2, c*i*j, c*d^2,
-//     c*d (d = |i-j|) and a u64 fixed-point c * round(2^48 / (1 + d^2)) for homogeneity (per-term
-//     relative error <= 1.2e-10), and ASM = sum c^2 grows by cnt * (2 old + cnt) from the counter
-//     value its atomic returns — so counts are never read back.  With at most 65535 pairs per
-//     item every total fits (sum c*d^2 <= 65535 * 255^2 < 2^32, sum c^2 <= 65535^2 < 2^32);
-//  2. clear the table with 16-byte stores;
-//  3. finish (once per item, all four angles): DPP wave sums, one cross-wave pass through the
-//     (by then all-zero) table, greycoprops on four lanes.  All sums are integer, so the result
-//     never depends on the order in which pairs or runs were visited.
+// 0, pi/4, pi/2, 3pi/4 at distance 3, symmetric=False, normed, then greycoprops.  Per angle:
+//  1. count: each thread takes chunks of eight horizontally adjacent reference pixels (one
+//     8-byte load of a, two of b + byte alignment), masks the columns outside the angle's
+//     valid range to 0, and adds
+//       - the pair sums that need no table from byte-SIMD instructions on the four-pixel words:
+//         sum i, sum j and sum |i - j| by v_sad_u8, sum i^2, j^2, ij by v_dot4_u32_u8
+//         (contrast = sum i^2 + j^2 - 2ij);
+//       - each non-background pair (i, j) != (0, 0) to its u16 counter with a no-return LDS
+//         atomic.  The table is diagonal-major: key = (dd << 8) | i with dd = (j - i) mod 256,
+//         so a row dd of 256 counters holds |i - j| = dd for i <= 255 - dd and 256 - dd after;
+//  2. scan (which also clears): one wave per row dd skips all-zero rows by ballot; otherwise
+//     ASM = sum c^2 (v_dot2_u32_u16 on the packed counters), the non-background pair count
+//     sum c, and homogeneity sum c * round(2^48 / (1 + d^2)) with d constant on each half-row
+//     (per-term relative error <= 1.2e-10), then zeroes the row;
+//  3. finish (once per item): background pairs = T - sum c, block reduction through LDS,
+//     greycoprops on four lanes.
+// Every sum is an integer (T <= 65535 pairs per item bounds them all below 2^32, the
+// homogeneity below 2^64), so the result never depends on the order in which pairs are visited.
 struct HomTable {
   unsigned long long m[256];
   constexpr HomTable() : m() {
@@ -114,180 +87,259 @@ struct HomTable {
 __constant__ HomTable kHom = HomTable();
 constexpr double kHomScale = 1.0 / 281474976710656.0;  // 2^-48
 
-struct GlcmAcc {
-  unsigned int si, sj, sii, sjj, sij, asq, con, dis, bg;
-  unsigned long long hom;
+struct GlcmSums {
+  unsigned int sisj;                        // count pass: sum i + (sum j << 16) (< 2^16 each per thread)
+  unsigned int sii, sjj, sij, dis;
+  unsigned int asq, cnt;                    // scan: sum c^2, sum c over non-background keys
+  unsigned long long hom;                   // scan: sum c * hom(d)
 };
-constexpr int kAccW = 11;  // 32-bit words per angle in the cross-wave reduction
+constexpr int kRedW = 10;  // 32-bit words per angle in the block reduction
 
-__device__ __forceinline__ void glcm_key(unsigned int c, unsigned int i, unsigned int j, GlcmAcc& A) {
-  const unsigned int ci = c * i, cj = c * j;
-  const unsigned int d = i > j ? i - j : j - i;
-  A.si += ci;
-  A.sj += cj;
-  A.sii += ci * i;
-  A.sjj += cj * j;
-  A.sij += ci * j;
-  A.asq += c * c;
-  A.con += c * d * d;
-  A.dis += c * d;
-  A.hom += (unsigned long long)c * kHom.m[d];
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned int dot2_u16(unsigned int a, unsigned int b, unsigned int c) {
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b), c, false);
 }
 
-// Add a run of cnt pairs of one key: the pair sums of the run go straight into the registers
-// (c*i, c*j, ..., c * hom(d) from the LDS copy of the homogeneity table), and ASM = sum c_k^2
-// grows by (old + cnt)^2 - old^2 = cnt * (2*old + cnt) from the counter value the atomic returns,
-// so the counts never have to be read back: the table is only cleared after the angle.
-__device__ __forceinline__ void glcm_flush(unsigned int* tab, const unsigned long long* hom,
-                                           unsigned int key, unsigned int cnt, GlcmAcc& A) {
-  const unsigned int sh = (key & 1u) << 4;
-  const unsigned int old = (atomicAdd(&tab[key >> 1], cnt << sh) >> sh) & 0xffffu;
-  const unsigned int i = key >> 8, j = key & 255u;
-  const unsigned int ci = cnt * i, cj = cnt * j;
-  const unsigned int d = i > j ? i - j : j - i;
-  A.si += ci;
-  A.sj += cj;
-  A.sii += ci * i;
-  A.sjj += cj * j;
-  A.sij += ci * j;
-  A.asq += cnt * (2u * old + cnt);
-  A.con += cnt * d * d;
-  A.dis += cnt * d;
-  A.hom += (unsigned long long)cnt * hom[d];
+// per-byte (x - y) mod 256 of four packed bytes (no borrow crosses a byte)
+__device__ __forceinline__ unsigned int bytes_sub(unsigned int x, unsigned int y) {
+  return ((x | 0x80808080u) - (y & 0x7f7f7f7fu)) ^ ((x ^ ~y) & 0x80808080u);
 }
 
-// Phase 1 of one angle over an 8-bit crop in LDS (or the global scratch slot); returns this
-// thread's background-pair count.
-template <bool LDS_CROP>
-__device__ unsigned int glcm_count(const unsigned char* __restrict__ crop, unsigned int* tab,
-                                   const unsigned long long* hom, GlcmAcc& A, int bh, int bw, int dr,
-                                   int dc) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int rend = bh - dr;  // dr >= 0
+// Background and masked pairs (key 0) go to a per-lane sink word instead of a branch.
+__device__ __forceinline__ void glcm_add(unsigned int* tab, unsigned int* sink, unsigned int key) {
+  atomicAdd(key ? &tab[key >> 1] : sink, (key & 1u) * 0xffffu + 1u);  // half = i & 1
+}
+
+template <int ANG, bool LDS_CROP>
+__device__ __forceinline__ void glcm_count(const unsigned char* __restrict__ crop, unsigned int* tab,
+                                           GlcmSums& S, int bh, int bw) {
+  unsigned int* sink = tab + kTabW + (threadIdx.x & 63);
+  constexpr int dr = ANG == 0 ? 0 : ANG == 2 ? 3 : 2;
+  constexpr int dc = ANG == 0 ? 3 : ANG == 1 ? 2 : ANG == 2 ? 0 : -2;
+  constexpr int sh = dc >= 0 ? dc : dc + 8;  // byte offset of b in its aligned 16-byte window
+  const int bwp = crop_stride(bw), nch = bwp >> 3;
+  const int rend = bh - dr;
   const int cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
-  const long long T = (rend > 0 && cend > cbeg) ? (long long)rend * (cend - cbeg) : 0;
-  // Thread = one contiguous run of the angle's T pairs (row-major); the 64 lanes of a wave
-  // take runs T/64 apart (segment lane*16 + wave), so one wave-instruction touches unrelated
-  // keys, and a lane adds a whole run of equal keys at once: LDS atomics to one address are
-  // serialised (~2 cycles per lane), and smooth crops repeat keys along a row.
-  unsigned int bg = 0;
-  const int Wc = cend - cbeg;
-  const int seg = (int)((T + kTT - 1) / kTT);
-  int p = (lane * kNW + wid) * seg;
-  const int pend = (int)min((long long)p + seg, T);
-  unsigned int cur = 0, cnt = 0;
-  if (p < pend) {
-    const int r = p / Wc, c = p - r * Wc;
-    const unsigned char* a = crop + r * bw + cbeg + c;
-    const unsigned char* b = a + dr * bw + dc;
-    int left = Wc - c;  // pairs left in this row
-    for (; p < pend; p += 4) {
-      // four keys loaded ahead (the 8 byte loads issue together), then consumed in order
-      unsigned int key[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        key[u] = ((unsigned int)*a << 8) | (unsigned int)*b;
-        const bool wrap = --left == 0;
-        a += wrap ? (bw - Wc + 1) : 1;
-        b += wrap ? (bw - Wc + 1) : 1;
-        left = wrap ? Wc : left;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (p + u >= pend) break;
-        if (key[u] != cur) {
-          if (cur) glcm_flush(tab, hom, cur, cnt, A);
-          else bg += cnt;
-          cur = key[u];
-          cnt = 0;
-        }
-        ++cnt;
+  if (rend <= 0 || cend <= cbeg) return;
+  const int nc = rend * nch;  // chunk q covers bytes 8q .. 8q + 7 of the crop (rows are whole chunks)
+  // chunk q = t, t + 1024, ... of this thread is visited at crop position p = q * m mod nc (m an
+  // odd prime not dividing nc): the lanes of a wave land on scattered pixels, so one LDS atomic
+  // instruction rarely has two lanes on the same counter (same-address lanes serialise), which
+  // neighbouring pixels of a smooth crop would.  p and its (row, chunk column) advance
+  // incrementally.
+  const int mul = nc % 7919 ? 7919 : 7907;
+  int p = (int)(((long long)threadIdx.x * mul) % nc);
+  const int step = (int)(((long long)kTT * mul) % nc);
+  const int sr = step / nch, sc = step - sr * nch;
+  int r = p / nch, ci = p - r * nch;
+  const int boff = dr * bwp + (dc < 0 ? -8 : 0);
+  for (int q = threadIdx.x; q < nc; q += kTT) {
+    const unsigned char* pa = crop + 8 * p;
+    const uint2 A = *reinterpret_cast<const uint2*>(pa);
+    unsigned int b0, b1;
+    if constexpr (sh == 0) {
+      const uint2 Bw = *reinterpret_cast<const uint2*>(pa + boff);
+      b0 = Bw.x;
+      b1 = Bw.y;
+    } else {
+      const uint2 L = *reinterpret_cast<const uint2*>(pa + boff);
+      const uint2 R = *reinterpret_cast<const uint2*>(pa + boff + 8);
+      if constexpr (sh < 4) {
+        b0 = __builtin_amdgcn_alignbyte(L.y, L.x, sh);
+        b1 = __builtin_amdgcn_alignbyte(R.x, L.y, sh);
+      } else {
+        b0 = __builtin_amdgcn_alignbyte(R.x, L.y, sh - 4);
+        b1 = __builtin_amdgcn_alignbyte(R.y, R.x, sh - 4);
       }
     }
+    const int c0 = 8 * ci;
+    const int hi = min(cend - c0, 8), lo = max(cbeg - c0, 0);
+    unsigned long long m = hi >= 8 ? ~0ull : (hi <= 0 ? 0ull : (1ull << (8 * hi)) - 1ull);
+    m &= ~0ull << (8 * lo);
+    const unsigned int m0 = (unsigned int)m, m1 = (unsigned int)(m >> 32);
+    const unsigned int a0 = A.x & m0, a1 = A.y & m1;
+    b0 &= m0;
+    b1 &= m1;
+    S.sisj = __builtin_amdgcn_sad_u8(a0, 0u, S.sisj);
+    S.sisj = __builtin_amdgcn_sad_u8(a1, 0u, S.sisj);
+    S.sisj += __builtin_amdgcn_sad_u8(b1, 0u, __builtin_amdgcn_sad_u8(b0, 0u, 0u)) << 16;
+    S.dis = __builtin_amdgcn_sad_u8(a0, b0, S.dis);
+    S.dis = __builtin_amdgcn_sad_u8(a1, b1, S.dis);
+    S.sii = __builtin_amdgcn_udot4(a0, a0, S.sii, false);
+    S.sii = __builtin_amdgcn_udot4(a1, a1, S.sii, false);
+    S.sjj = __builtin_amdgcn_udot4(b0, b0, S.sjj, false);
+    S.sjj = __builtin_amdgcn_udot4(b1, b1, S.sjj, false);
+    S.sij = __builtin_amdgcn_udot4(a0, b0, S.sij, false);
+    S.sij = __builtin_amdgcn_udot4(a1, b1, S.sij, false);
+    // keys (dd << 8) | i, two per word: selectors 0-3 pick i (src1), 4-7 pick dd (src0)
+    const unsigned int d0 = bytes_sub(b0, a0), d1 = bytes_sub(b1, a1);
+    const unsigned int k01 = __builtin_amdgcn_perm(d0, a0, 0x05010400u);
+    const unsigned int k23 = __builtin_amdgcn_perm(d0, a0, 0x07030602u);
+    const unsigned int k45 = __builtin_amdgcn_perm(d1, a1, 0x05010400u);
+    const unsigned int k67 = __builtin_amdgcn_perm(d1, a1, 0x07030602u);
+    glcm_add(tab, sink, k01 & 0xffffu);
+    glcm_add(tab, sink, k01 >> 16);
+    glcm_add(tab, sink, k23 & 0xffffu);
+    glcm_add(tab, sink, k23 >> 16);
+    glcm_add(tab, sink, k45 & 0xffffu);
+    glcm_add(tab, sink, k45 >> 16);
+    glcm_add(tab, sink, k67 & 0xffffu);
+    glcm_add(tab, sink, k67 >> 16);
+    p += step;
+    r += sr;
+    ci += sc;
+    if (ci >= nch) {
+      ci -= nch;
+      ++r;
+    }
+    if (p >= nc) {
+      p -= nc;
+      r -= rend;
+    }
   }
-  if (cur) glcm_flush(tab, hom, cur, cnt, A);
-  else bg += cnt;
-  return bg;
 }
 
-// Phase 2 of one angle: clear the table for the next angle with 16-byte stores.
-__device__ __forceinline__ void glcm_clear(unsigned int* tab) {
-  uint4* t4 = reinterpret_cast<uint4*>(tab);
-#pragma unroll
-  for (int x = threadIdx.x; x < kTabW / 4; x += kTT) t4[x] = uint4{0u, 0u, 0u, 0u};
+// Scan + clear of one angle's table (see above).  Row dd = 128 words; lane l holds keys
+// i = 4l .. 4l + 3 (two words), of which min(max(256 - dd - 4l, 0), 4) have |i - j| = dd.  Wave w
+// owns rows w + 16k (k < 16), read four at a time so the LDS latency overlaps; the homogeneity
+// weights of its rows come from registers (hv: lane k holds hom(dd_k), lane 16 + k
+// hom(256 - dd_k)) by v_readlane, never from memory inside the loop.
+__device__ __forceinline__ unsigned long long lane_u64(unsigned long long v, int l) {
+  return ((unsigned long long)(unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)(v >> 32), l) << 32) |
+         (unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)v, l);
 }
 
-// Phase 3: reduce the four angles' sums over the block and write greycoprops.  `red` is
-// kNW * 4 * kAccW words of the all-zero table; wave 0 zeroes them again before returning.
-__device__ void glcm_finish(const GlcmAcc (&A)[4], unsigned int* red, int bh, int bw,
-                            double* __restrict__ out) {
+__device__ __forceinline__ void glcm_scan(unsigned int* tab, GlcmSums& S, unsigned long long hv) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint2* rows = reinterpret_cast<uint2*>(tab) + wid * 64 + lane;
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const unsigned int w[9] = {A[a].si, A[a].sj, A[a].sii, A[a].sjj, A[a].sij,
-                               A[a].asq, A[a].con, A[a].dis, A[a].bg};
+  for (int k0 = 0; k0 < 16; k0 += 4) {
+    uint2 w[4];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      const unsigned int t = wave_sum_u32(w[k]);
-      if (lane == 0) red[(wid * 4 + a) * kAccW + k] = t;
-    }
-    const unsigned long long hs = wave_sum_u64(A[a].hom);
-    if (lane == 0) {
-      red[(wid * 4 + a) * kAccW + 9] = (unsigned int)hs;
-      red[(wid * 4 + a) * kAccW + 10] = (unsigned int)(hs >> 32);
+    for (int k = 0; k < 4; ++k) w[k] = rows[(k0 + k) * kNW * 64];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (!__builtin_amdgcn_ballot_w64((w[k].x | w[k].y) != 0u)) continue;
+      rows[(k0 + k) * kNW * 64] = uint2{0u, 0u};
+      const int dd = wid + kNW * (k0 + k);
+      S.asq = dot2_u16(w[k].x, w[k].x, S.asq);
+      S.asq = dot2_u16(w[k].y, w[k].y, S.asq);
+      const unsigned int sall = dot2_u16(w[k].x, 0x10001u, dot2_u16(w[k].y, 0x10001u, 0u));
+      const int r = 256 - dd - 4 * lane;
+      const unsigned int mx = r >= 2 ? ~0u : (r == 1 ? 0xffffu : 0u);
+      const unsigned int my = r >= 4 ? ~0u : (r == 3 ? 0xffffu : 0u);
+      const unsigned int slo = dot2_u16(w[k].x & mx, 0x10001u, dot2_u16(w[k].y & my, 0x10001u, 0u));
+      S.cnt += sall;
+      S.hom += (unsigned long long)slo * lane_u64(hv, k0 + k) +
+               (unsigned long long)(sall - slo) * lane_u64(hv, 16 + k0 + k);
     }
   }
-  __syncthreads();
-  if (wid == 0) {
-    if (lane < 4) {
-      const int a = lane;
-      const int dr = a == 0 ? 0 : a == 2 ? 3 : 2;
-      const int dc = a == 0 ? 3 : a == 1 ? 2 : a == 2 ? 0 : -2;
-      const int rend = bh - dr;
-      const int cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
-      const long long T = (rend > 0 && cend > cbeg) ? (long long)rend * (cend - cbeg) : 0;
-      unsigned int v[9] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-      unsigned long long hs = 0;
-      for (int x = 0; x < kNW; ++x) {
-        const unsigned int* r = red + (x * 4 + a) * kAccW;
+}
+
+// the scan's homogeneity weights for this thread's wave (see glcm_scan)
+__device__ __forceinline__ unsigned long long glcm_scan_weights() {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane >= 32) return 0;
+  const int dd = wid + kNW * (lane & 15);
+  return kHom.m[lane < 16 ? dd : (256 - dd) & 255];
+}
+
+// Sum of a u64 over each half-wave (lanes 0-31 -> lane 31, 32-63 -> lane 63) on the DPP path.
+__device__ __forceinline__ unsigned long long half_wave_sum_u64(unsigned long long v) {
+#define CPX_U64_DPP_STEP(CTRL, ROWMASK)                                                         \
+  {                                                                                            \
+    const unsigned int lo_ = (unsigned int)__builtin_amdgcn_update_dpp(0, (int)(unsigned int)v, \
+                                                                       CTRL, ROWMASK, 0xf, false); \
+    const unsigned int hi_ = (unsigned int)__builtin_amdgcn_update_dpp(                        \
+        0, (int)(unsigned int)(v >> 32), CTRL, ROWMASK, 0xf, false);                           \
+    v += ((unsigned long long)hi_ << 32) | lo_;                                                \
+  }
+  CPX_U64_DPP_STEP(0x111, 0xf)  // row_shr:1,2,4,8 -> inclusive scan within each row of 16 lanes
+  CPX_U64_DPP_STEP(0x112, 0xf)
+  CPX_U64_DPP_STEP(0x114, 0xf)
+  CPX_U64_DPP_STEP(0x118, 0xf)
+  CPX_U64_DPP_STEP(0x142, 0xa)  // row_bcast:15 -> rows 1 and 3 add the totals of rows 0 and 2
+#undef CPX_U64_DPP_STEP
+  return v;
+}
+
+// Finish: the four angles' per-thread sums are reduced through LDS in two rounds of two angles
+// (`red` = 2 * kRedW * kTT words of the all-zero table, zeroed again before returning; `tot` =
+// 4 * kRedW u64 of static LDS), then lanes 0-3 evaluate greycoprops for angles 0-3.
+__device__ void glcm_finish(const GlcmSums (&S)[4], unsigned int* red, unsigned long long* tot,
+                            int bh, int bw, double* __restrict__ out, long long* pt) {
+  const int t = threadIdx.x, lane = t & 63;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) v[k] += r[k];
-        hs += (unsigned long long)r[9] | ((unsigned long long)r[10] << 32);
-      }
-      const unsigned int tsi = v[0], tsj = v[1], tsii = v[2], tsjj = v[3], tsij = v[4];
-      const unsigned int tas = v[5], ct = v[6], dt = v[7], nbg = v[8];
-      hs += (unsigned long long)nbg * kHom.m[0];  // background pairs: d = 0
-      double con = 0.0, dis = 0.0, hom = 0.0, asmv = 0.0, ene = 0.0, cor = 1.0;
-      if (T > 0) {
-        const double Td = (double)T;
-        con = (double)ct / Td;
-        dis = (double)dt / Td;
-        hom = ((double)hs * kHomScale) / Td;
-        asmv = (double)((unsigned long long)tas + (unsigned long long)nbg * nbg) / (Td * Td);
-        ene = sqrt(asmv);
-        const long long vi = T * (long long)tsii - (long long)tsi * tsi;
-        const long long vj = T * (long long)tsjj - (long long)tsj * tsj;
-        const long long cv = T * (long long)tsij - (long long)tsi * tsj;
-        const double sdi = sqrt((double)vi) / Td, sdj = sqrt((double)vj) / Td;
-        cor = (sdi < 1e-15 || sdj < 1e-15) ? 1.0 : ((double)cv / (Td * Td)) / (sdi * sdj);
-      }
-      double* o = out + a * CPX_N_TEX_PROPS;
-      o[CPX_TEX_CONTRAST] = con;
-      o[CPX_TEX_DISSIMILARITY] = dis;
-      o[CPX_TEX_HOMOGENEITY] = hom;
-      o[CPX_TEX_ASM] = asmv;
-      o[CPX_TEX_ENERGY] = ene;
-      o[CPX_TEX_CORRELATION] = cor;
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int a2 = 0; a2 < 2; ++a2) {
+      const GlcmSums& s = S[2 * h + a2];
+      const unsigned int v[kRedW] = {s.sisj & 0xffffu, s.sisj >> 16, s.sii, s.sjj, s.sij, s.dis, s.asq, s.cnt,
+                                     (unsigned int)s.hom, (unsigned int)(s.hom >> 32)};
+#pragma unroll
+      for (int k = 0; k < kRedW; ++k) red[(a2 * kRedW + k) * kTT + t] = v[k];
     }
-    // re-zero the reduction words (the table must be all-zero for the next item)
-    for (int x = lane; x < kNW * 4 * kAccW; x += 64) red[x] = 0u;
+    __syncthreads();
+    unsigned long long x = 0;
+    if (t < 2 * kRedW * 32) {
+      // lane p sums words 32p .. 32p + 31 of its row in a lane-rotated order (bank spread)
+      const uint4* src = reinterpret_cast<const uint4*>(red + (t >> 5) * kTT + (t & 31) * 32);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint4 q = src[(i + t) & 7];
+        x += (unsigned long long)q.x + q.y + (unsigned long long)q.z + q.w;
+      }
+    }
+    x = half_wave_sum_u64(x);
+    if (t < 2 * kRedW * 32 && (lane & 31) == 31) tot[h * 2 * kRedW + (t >> 5)] = x;
+    __syncthreads();
+    GLCM_MARK(0, pt);
+  }
+#pragma unroll
+  for (int k = 0; k < 2 * kRedW; ++k) red[k * kTT + t] = 0u;
+  GLCM_MARK(1, pt);
+  if (t < 4) {
+    const int a = t;
+    const int dr = a == 0 ? 0 : a == 2 ? 3 : 2;
+    const int dc = a == 0 ? 3 : a == 1 ? 2 : a == 2 ? 0 : -2;
+    const int rend = bh - dr;
+    const int cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
+    const long long T = (rend > 0 && cend > cbeg) ? (long long)rend * (cend - cbeg) : 0;
+    const unsigned long long* v = tot + a * kRedW;
+    const long long tsi = (long long)v[0], tsj = (long long)v[1], tsii = (long long)v[2],
+                    tsjj = (long long)v[3], tsij = (long long)v[4];
+    const unsigned long long dt = v[5], tas = v[6], ncnt = v[7];
+    const unsigned long long nbg = (unsigned long long)T - ncnt;  // background pairs (0, 0)
+    const unsigned long long hs = v[8] + (v[9] << 32) + nbg * kHom.m[0];
+    double con = 0.0, dis = 0.0, hom = 0.0, asmv = 0.0, ene = 0.0, cor = 1.0;
+    if (T > 0) {
+      const double Td = (double)T;
+      con = (double)(tsii + tsjj - 2 * tsij) / Td;
+      dis = (double)dt / Td;
+      hom = ((double)hs * kHomScale) / Td;
+      asmv = (double)(tas + nbg * nbg) / (Td * Td);
+      ene = sqrt(asmv);
+      const long long vi = T * tsii - tsi * tsi;
+      const long long vj = T * tsjj - tsj * tsj;
+      const long long cv = T * tsij - tsi * tsj;
+      const double sdi = sqrt((double)vi) / Td, sdj = sqrt((double)vj) / Td;
+      cor = (sdi < 1e-15 || sdj < 1e-15) ? 1.0 : ((double)cv / (Td * Td)) / (sdi * sdj);
+    }
+    double* o = out + a * CPX_N_TEX_PROPS;
+    o[CPX_TEX_CONTRAST] = con;
+    o[CPX_TEX_DISSIMILARITY] = dis;
+    o[CPX_TEX_HOMOGENEITY] = hom;
+    o[CPX_TEX_ASM] = asmv;
+    o[CPX_TEX_ENERGY] = ene;
+    o[CPX_TEX_CORRELATION] = cor;
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// Phase A (high occupancy, one block per (object, channel) item): intensity features and the
+// Phase A (one block per object, its C channels in turn): intensity features and the
 // scale_to_8bit range from one coalesced pass over the bbox, then the 8-bit masked crop is
-// written to a global scratch slot (L2-resident until phase B reads it).
+// written to a global scratch slot (L2-resident until phase B reads it); membership from the
+// object's LDS bitmask, so the label image is not read again.
 constexpr int kAT = 256;  // 8 rows x 32 columns
 
 __global__ __launch_bounds__(kAT) void k_tex_stage(const int* __restrict__ labels,
@@ -404,33 +456,30 @@ __global__ __launch_bounds__(kAT) void k_tex_stage(const int* __restrict__ label
     }
     const float rng = mmax - mmin;
     const bool flat = !(mmax != mmin);
-    unsigned char* dst = scratch + (long long)fov * scratch_per_fov + off +
-                         (long long)ch * (((long long)bh * bw + 15) / 16 * 16);
-    // the crop is written as a flat row-major byte array, four pixels per thread per step
-    // packed into one 32-bit store (slots are 16-byte aligned): all lanes busy whatever bw is,
-    // and a wave stores 256 contiguous bytes instead of 64 single bytes
-    const int nb = bh * bw;
+    unsigned char* dst = scratch + (long long)fov * scratch_per_fov + off + (long long)ch * crop_bytes(bh, bw);
+    // the crop is written row by row at the padded stride (pad bytes 0), four pixels per thread
+    // per step packed into one 32-bit store: all lanes busy whatever bw is, and a wave stores
+    // 256 contiguous bytes instead of 64 single bytes
+    const int bwp = crop_stride(bw);
+    const int nb = bh * bwp;
     for (int f0 = 4 * threadIdx.x; f0 < nb; f0 += 4 * kAT) {
-      int r = f0 / bw, c = f0 - r * bw;
+      const int r = f0 / bwp, c = f0 - r * bwp;  // bwp % 4 == 0: the four pixels share a row
+      // pad pixels (c + u >= bw) load the row's last pixel (branch-free) and store 0
+      const long long rw = (long long)r * W;
       float vv[4];
       int ll[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        vv[u] = 0.0f;
-        ll[u] = -1;
-        if (f0 + u < nb) {
-          vv[u] = img[(long long)r * W + c];
-          ll[u] = lb[(long long)r * W + c];
-        }
-        if (++c == bw) {
-          c = 0;
-          ++r;
-        }
+        const int cu = min(c + u, bw - 1);
+        vv[u] = img[rw + cu];
+        ll[u] = lb[rw + cu];
       }
       unsigned int word = 0u;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        word |= (unsigned int)quantize(vv[u], ll[u] == L, mmin, rng, flat) << (8 * u);
+      for (int u = 0; u < 4; ++u) {
+        const unsigned int q = (unsigned int)quantize(vv[u], ll[u] == L, mmin, rng, flat);
+        word |= (c + u < bw ? q : 0u) << (8 * u);
+      }
       *reinterpret_cast<unsigned int*>(dst + f0) = word;
     }
   }
@@ -438,6 +487,7 @@ __global__ __launch_bounds__(kAT) void k_tex_stage(const int* __restrict__ label
 
 struct GlcmItem {
   int fov, k, ch, bh, bw, nb;  // nb <= 0: nothing to do (no slot, > 65535 px, or queue drained)
+  int bytes;                   // staged crop slot size (crop_bytes)
   const unsigned char* src;
 };
 
@@ -459,15 +509,14 @@ __device__ __forceinline__ int glcm_grab(int& f, int& visited, int B, int C,
   return -1;
 }
 
-constexpr int kPre = (kCrop / 16 + kTT - 1) / kTT;  // uint4 prefetch registers per thread
-static_assert(kPre == 2, "glcm_prefetch holds two uint4 per thread");
+static_assert(kCrop / 16 <= 2 * kTT, "a crop is copied with two uint4 per thread");
 
 __device__ __forceinline__ GlcmItem glcm_item(int code, int C, int max_label,
                                               const cpx_object* objects,
                                               const long long* crop_off,
                                               const unsigned char* scratch,
                                               long long scratch_per_fov) {
-  GlcmItem g{0, 0, 0, 0, 0, 0, nullptr};
+  GlcmItem g{0, 0, 0, 0, 0, 0, 0, nullptr};
   if (code < 0) return g;
   const int fov = code >> 20, item = code & 0xfffff;
   g.fov = fov;
@@ -478,18 +527,32 @@ __device__ __forceinline__ GlcmItem glcm_item(int code, int C, int max_label,
   g.bh = o.bbox[2] - o.bbox[0];
   g.bw = o.bbox[3] - o.bbox[1];
   const int nb = g.bh * g.bw;
-  if (off < 0 || nb > 65535) return g;  // u32 / packed u16 sums: fallback kernel
+  if (off < 0 || nb > 65535) return g;  // u16 counters / u32 sums: fallback kernel
   g.nb = nb;
-  g.src = scratch + (long long)fov * scratch_per_fov + off + (long long)g.ch * ((nb + 15) / 16 * 16);
+  g.bytes = (int)crop_bytes(g.bh, g.bw);
+  g.src = scratch + (long long)fov * scratch_per_fov + off + (long long)g.ch * g.bytes;
   return g;
 }
 
-__device__ __forceinline__ void glcm_prefetch(const GlcmItem& g, uint4& p0, uint4& p1) {
-  if (g.nb <= 0 || g.nb > kCrop) return;
-  const int n16 = (g.nb + 15) / 16;
-  const uint4* s16 = reinterpret_cast<const uint4*>(g.src);
-  if ((int)threadIdx.x < n16) p0 = s16[threadIdx.x];
-  if ((int)threadIdx.x + kTT < n16) p1 = s16[threadIdx.x + kTT];
+// Touch every 128-byte line of the next item's LDS-sized crop (one dword per line): the lines
+// move to this XCD's L2 while the current item runs, and the loaded word is only consumed at the
+// next item (one VGPR instead of holding the crop in registers).
+__device__ __forceinline__ unsigned int glcm_touch(const GlcmItem& g) {
+  if (g.nb <= 0 || g.bytes > kCrop) return 0u;
+  return (int)threadIdx.x * 128 < g.bytes ? *reinterpret_cast<const unsigned int*>(g.src + threadIdx.x * 128) : 0u;
+}
+
+template <int A>
+__device__ __forceinline__ void glcm_angle(const GlcmItem& it, const unsigned char* crop,
+                                           unsigned int* tab, GlcmSums& S, unsigned long long hv,
+                                           long long* pt) {
+  if (it.bytes <= kCrop) glcm_count<A, true>(crop, tab, S, it.bh, it.bw);
+  else glcm_count<A, false>(it.src, tab, S, it.bh, it.bw);
+  __syncthreads();
+  GLCM_MARK(2, pt);
+  glcm_scan(tab, S, hv);
+  __syncthreads();
+  GLCM_MARK(3, pt);
 }
 
 // Phase B (one 1024-thread block per CU, 128 KiB LDS pair table): GLCM of staged crops.
@@ -501,32 +564,39 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
                                                  long long scratch_per_fov,
                                                  int* __restrict__ glcm_next,
                                                  double* __restrict__ feats) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ int s_code[2];  // queue codes (see glcm_grab), double-buffered by iteration parity
-  unsigned int* tab = reinterpret_cast<unsigned int*>(smem);
-  unsigned long long* hom = reinterpret_cast<unsigned long long*>(tab + kTabW);  // 2 KiB
-  unsigned char* crop = reinterpret_cast<unsigned char*>(hom + 256);
+  // LDS: table at offset 0 (static, so the atomics' addresses need no base), then the
+  // 64 sink words, the reduction totals, the queue codes and the crop
+  __shared__ __attribute__((aligned(16))) unsigned int lds[40 * 1024];  // all 160 KiB, static
+  unsigned char* smem = reinterpret_cast<unsigned char*>(lds);
+  unsigned int* tab = lds;
+  unsigned long long* s_tot = reinterpret_cast<unsigned long long*>(smem + 4 * kTabW + 256);
+  int* s_code = reinterpret_cast<int*>(smem + 4 * kTabW + 256 + 320);  // double-buffered by parity
+  unsigned char* crop = smem + 4 * kTabW + kSmall;
   const int B = gridDim.y;
   int q_fov = blockIdx.y, q_visited = 0;  // thread 0's queue position
+  const unsigned long long hv = glcm_scan_weights();
   for (int x = threadIdx.x; x < kTabW; x += kTT) tab[x] = 0u;
-  if (threadIdx.x < 256) hom[threadIdx.x] = kHom.m[threadIdx.x];
   if (threadIdx.x == 0) {
     s_code[0] = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next);
     s_code[1] = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next);
   }
   __syncthreads();
-  // software pipeline: the next item's metadata and LDS-sized crop are loaded into registers
-  // while the current item runs its four angles (the crop was written by k_tex_stage, possibly
-  // on another XCD, so the loads are HBM/MALL latency); thread 0 grabs the item after that one
+  // software pipeline: the next item's metadata is loaded and its crop's lines are touched into
+  // L2 while the current item runs its four angles (the crop was written by k_tex_stage, possibly
+  // on another XCD, so a cold load is HBM/MALL latency); thread 0 grabs the item after that one
   // from the queue during the current item, so the atomic's latency is hidden too.
   GlcmItem cur = glcm_item(s_code[0], C, max_label, objects, crop_off, scratch, scratch_per_fov);
-  uint4 p0 = {0u, 0u, 0u, 0u}, p1 = {0u, 0u, 0u, 0u};
-  glcm_prefetch(cur, p0, p1);
+  unsigned int touched = glcm_touch(cur), sink_word = 0u;
   int ahead = -2;  // -2: nothing grabbed yet
   for (int par = 1; s_code[par ^ 1] >= 0; par ^= 1) {
     // s_code[par ^ 1] holds the current item (cur), s_code[par] receives the next one
-    if (cur.nb > 0 && cur.nb <= kCrop) {
-      const int n16 = (cur.nb + 15) / 16;
+    sink_word += touched;
+    if (cur.nb > 0 && cur.bytes <= kCrop) {
+      const int n16 = cur.bytes / 16;
+      const uint4* s16 = reinterpret_cast<const uint4*>(cur.src);
+      uint4 p0 = {0u, 0u, 0u, 0u}, p1 = {0u, 0u, 0u, 0u};
+      if ((int)threadIdx.x < n16) p0 = s16[threadIdx.x];
+      if ((int)threadIdx.x + kTT < n16) p1 = s16[threadIdx.x + kTT];
       if ((int)threadIdx.x < n16) reinterpret_cast<uint4*>(crop)[threadIdx.x] = p0;
       if ((int)threadIdx.x + kTT < n16) reinterpret_cast<uint4*>(crop)[threadIdx.x + kTT] = p1;
     }
@@ -536,7 +606,7 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
     __syncthreads();
     const GlcmItem it = cur;
     cur = glcm_item(s_code[par], C, max_label, objects, crop_off, scratch, scratch_per_fov);
-    glcm_prefetch(cur, p0, p1);
+    touched = glcm_touch(cur);
     if (threadIdx.x == 0) ahead = s_code[par] >= 0 ? glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next) : -1;
     if (it.nb <= 0) continue;
     double* f = feats + ((long long)it.fov * max_label + it.k) * F + CPX_N_SHAPE +
@@ -547,27 +617,19 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
       pt = clock64();
       atomicAdd(&g_glcm_prof[5], 1ull);
       atomicAdd(&g_glcm_prof[6], (unsigned long long)it.nb);
-      if (it.nb > kCrop) atomicAdd(&g_glcm_prof[7], 1ull);
+      if (it.bytes > kCrop) atomicAdd(&g_glcm_prof[7], 1ull);
     }
 #endif
-    // skimage offsets (dr, dc) for angles 0, pi/4, pi/2, 3pi/4 at distance 3
-    GlcmAcc acc[4] = {};
-#pragma unroll
-    for (int a = 0; a < CPX_N_ANGLES; ++a) {
-      const int dr = a == 0 ? 0 : a == 2 ? 3 : 2;
-      const int dc = a == 0 ? 3 : a == 1 ? 2 : a == 2 ? 0 : -2;
-      acc[a].bg = it.nb <= kCrop
-                      ? glcm_count<true>(crop, tab, hom, acc[a], it.bh, it.bw, dr, dc)
-                      : glcm_count<false>(it.src, tab, hom, acc[a], it.bh, it.bw, dr, dc);
-      __syncthreads();
-      GLCM_MARK(2, &pt);
-      glcm_clear(tab);
-      __syncthreads();
-      GLCM_MARK(3, &pt);
-    }
-    glcm_finish(acc, tab, it.bh, it.bw, f);
+    GlcmSums S[4] = {};
+    glcm_angle<0>(it, crop, tab, S[0], hv, &pt);
+    glcm_angle<1>(it, crop, tab, S[1], hv, &pt);
+    glcm_angle<2>(it, crop, tab, S[2], hv, &pt);
+    glcm_angle<3>(it, crop, tab, S[3], hv, &pt);
+    glcm_finish(S, tab, s_tot, it.bh, it.bw, f, &pt);
     GLCM_MARK(4, &pt);
   }
+  // keeps the touch loads alive: never true (C > 0), but the compiler cannot know that
+  if (C < 0 && sink_word + touched == 0x9e3779b9u) feats[0] = 0.0;
 }
 
 // crop slots: per FOV exclusive scan of C * bbox area; objects beyond the scratch capacity or
@@ -594,8 +656,8 @@ __global__ __launch_bounds__(1024) void k_crop_offsets(int C, int max_label,
     long long sz = 0;
     if (k < n) {
       const cpx_object o = objects[(long long)fov * max_label + k];
-      const long long nb = (long long)(o.bbox[2] - o.bbox[0]) * (o.bbox[3] - o.bbox[1]);
-      sz = nb <= 65535 ? ((nb + 15) / 16) * 16 * C : 0;
+      const int bh = o.bbox[2] - o.bbox[0], bw = o.bbox[3] - o.bbox[1];
+      sz = (long long)bh * bw <= 65535 ? crop_bytes(bh, bw) * C : 0;
     }
     // inclusive wave scan
     long long x = sz;
@@ -643,11 +705,165 @@ __device__ __forceinline__ bool shape_fits(const cpx_object& o) {
   return cpx_shape_fits(o.bbox[2] - o.bbox[0], o.bbox[3] - o.bbox[1]);
 }
 
+// Membership bitmask of object o over its bbox + 2-px margin (rows x wpr words in M): each
+// 32-lane half-wave builds one 32-bit word (r, cw); four words per half-wave are loaded before
+// the first ballot so the label loads overlap.
+template <int NT>
+__device__ __forceinline__ void shape_mask(const int* __restrict__ lab, int H, int W, const cpx_object& o,
+                                           unsigned int* M) {
+  const int lane = threadIdx.x & 63;
+  const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31;
+  const int L = o.label;
+  const int R0 = o.bbox[0] - 2, C0 = o.bbox[1] - 2;  // region origin (2-px margin)
+  const int rows = o.bbox[2] - o.bbox[0] + 4, cols = o.bbox[3] - o.bbox[1] + 4;
+  const int wpr = (cols + 31) >> 5;
+  const int nw = rows * wpr;
+  for (int w0 = 0; w0 < nw; w0 += 4 * (NT / 32)) {
+    int lv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int w = w0 + u * (NT / 32) + ty;
+      const int r = w / wpr, cw = w - r * wpr;
+      const int c = cw * 32 + tx;
+      const int gr = R0 + r, gc = C0 + c;
+      const bool ok = w < nw && c < cols && gr >= 0 && gr < H && gc >= 0 && gc < W;
+      lv[u] = ok ? lab[(long long)gr * W + gc] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int w = w0 + u * (NT / 32) + ty;
+      const unsigned long long b = __ballot(lv[u] == L);
+      if (w < nw) {
+        if (lane == 0) M[w] = (unsigned int)b;
+        if (lane == 32) M[w] = (unsigned int)(b >> 32);
+      }
+    }
+  }
+}
+
+// AreaShape sums of object o from its membership mask M (shape_mask; all threads, M complete and
+// visible): border mask in Bd, Benkrid-Crookes perimeter codes, exact int64 moments -> raw[0..8]
+// (n, sum r, sum c, sum r^2, sum c^2, sum rc, n1, n2, n3); k_shape_props turns them into the
+// AreaShape columns (the fp64 tail runs once per object there instead of in every stage kernel,
+// whose registers it would otherwise inflate).
+constexpr int kShapeRaw = 9;
+template <int NT>
+__device__ void shape_sums(const cpx_object& o, const unsigned int* M, unsigned int* Bd,
+                           long long (*red)[NT / 64], int (*redi)[NT / 64], long long* __restrict__ raw) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int rows = o.bbox[2] - o.bbox[0] + 4, cols = o.bbox[3] - o.bbox[1] + 4;
+  const int wpr = (cols + 31) >> 5;
+  // border = in & !(up & down & left & right)
+  for (int w = threadIdx.x; w < rows * wpr; w += NT) {
+    const int r = w / wpr, cw = w - r * wpr;
+    const unsigned int x = M[w];
+    const unsigned int up = getw(M, wpr, rows, r - 1, cw), dn = getw(M, wpr, rows, r + 1, cw);
+    const unsigned int lf = (x << 1) | (getw(M, wpr, rows, r, cw - 1) >> 31);
+    const unsigned int rt = (x >> 1) | (getw(M, wpr, rows, r, cw + 1) << 31);
+    Bd[w] = x & ~(up & dn & lf & rt);
+  }
+  __syncthreads();
+  long long n = 0, sr = 0, sc = 0, srr = 0, scc = 0, src = 0;
+  int n1 = 0, n2 = 0, n3 = 0;
+  for (int w = threadIdx.x; w < rows * wpr; w += NT) {
+    const int r = w / wpr, cw = w - r * wpr;
+    unsigned int x = M[w];
+    const unsigned int bx = Bd[w];
+    while (x) {
+      const int b = __ffs(x) - 1;
+      x &= x - 1;
+      const int c = cw * 32 + b;
+      const long long rr = r - 2, cc = c - 2;  // bbox-local coordinates
+      n += 1;
+      sr += rr;
+      sc += cc;
+      srr += rr * rr;
+      scc += cc * cc;
+      src += rr * cc;
+      if (!((bx >> b) & 1u)) continue;
+      auto bit = [&](int rr2, int cc2) -> int {
+        return (int)((getw(Bd, wpr, rows, rr2, cc2 >> 5) >> (cc2 & 31)) & 1u);
+      };
+      const int code = 1 + 2 * (bit(r - 1, c) + bit(r + 1, c) + bit(r, c - 1) + bit(r, c + 1)) +
+                       10 * (bit(r - 1, c - 1) + bit(r - 1, c + 1) + bit(r + 1, c - 1) + bit(r + 1, c + 1));
+      if (code == 5 || code == 7 || code == 15 || code == 17 || code == 25 || code == 27) n1 += 1;
+      else if (code == 21 || code == 33) n2 += 1;
+      else if (code == 13 || code == 23) n3 += 1;
+    }
+  }
+  n = wave_sum(n); sr = wave_sum(sr); sc = wave_sum(sc);
+  srr = wave_sum(srr); scc = wave_sum(scc); src = wave_sum(src);
+  n1 = wave_sum(n1); n2 = wave_sum(n2); n3 = wave_sum(n3);
+  if (lane == 0) {
+    red[0][wid] = n; red[1][wid] = sr; red[2][wid] = sc;
+    red[3][wid] = srr; red[4][wid] = scc; red[5][wid] = src;
+    redi[0][wid] = n1; redi[1][wid] = n2; redi[2][wid] = n3;
+  }
+  __syncthreads();
+  if (threadIdx.x < kShapeRaw) {
+    long long t = 0;
+    for (int w = 0; w < NT / 64; ++w) t += threadIdx.x < 6 ? red[threadIdx.x][w] : (long long)redi[threadIdx.x - 6][w];
+    raw[threadIdx.x] = t;
+  }
+}
+
+// AreaShape columns from shape_sums' raw sums, one thread per object (objects the LDS fast
+// paths handled: shape_fits).
+__global__ __launch_bounds__(256) void k_shape_props(int max_label, int F,
+                                                    const cpx_object* __restrict__ objects,
+                                                    const cpx_fov_objects* __restrict__ hdr,
+                                                    const long long* __restrict__ raws,
+                                                    double* __restrict__ feats) {
+  const int fov = blockIdx.y, k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= hdr[fov].n_objects) return;
+  const cpx_object o = objects[(long long)fov * max_label + k];
+  if (!shape_fits(o)) return;
+  const long long* raw = raws + ((long long)fov * max_label + k) * kShapeRaw;
+  const long long n = raw[0], sr = raw[1], sc = raw[2], srr = raw[3], scc = raw[4], src = raw[5];
+  const long long n1 = raw[6], n2 = raw[7], n3 = raw[8];
+  double* f = feats + ((long long)fov * max_label + k) * F;
+  const double SQ2 = 1.4142135623730951;
+  const double area = (double)n;
+  const int r0 = o.bbox[0], c0 = o.bbox[1], r1 = o.bbox[2], c1 = o.bbox[3];
+  const double bba = (double)(r1 - r0) * (double)(c1 - c0);
+  f[CPX_SHAPE_AREA] = area;
+  f[CPX_SHAPE_PERIMETER] = (double)n1 + (double)n2 * SQ2 + (double)n3 * ((1.0 + SQ2) / 2.0);
+  f[CPX_SHAPE_CENTER_Y] = o.centroid_r;
+  f[CPX_SHAPE_CENTER_X] = o.centroid_c;
+  f[CPX_SHAPE_BBOX_AREA] = bba;
+  f[CPX_SHAPE_EXTENT] = area / bba;
+  f[CPX_SHAPE_EQUIV_DIAMETER] = sqrt(4.0 * area / 3.14159265358979323846);
+  const i128 NN = n;
+  const i128 m20n = NN * srr - (i128)sr * sr;
+  const i128 m02n = NN * scc - (i128)sc * sc;
+  const i128 m11n = NN * src - (i128)sr * sc;
+  const double n2d = area * area;
+  const double a = (double)m02n / n2d, b = -(double)m11n / n2d, c = (double)m20n / n2d;
+  const double hm = 0.5 * (a + c), hd = 0.5 * (a - c);
+  const double rt = sqrt(hd * hd + b * b);
+  double l1 = hm + rt;
+  const i128 detn4 = m02n * m20n - m11n * m11n;
+  double l2 = (l1 > 0.0) ? ((double)detn4 / (n2d * n2d)) / l1 : 0.0;
+  if (l1 < 0.0) l1 = 0.0;
+  if (l2 < 0.0) l2 = 0.0;
+  if (l2 > l1) l2 = l1;
+  f[CPX_SHAPE_MAJOR_AXIS] = 4.0 * sqrt(l1);
+  f[CPX_SHAPE_MINOR_AXIS] = 4.0 * sqrt(l2);
+  f[CPX_SHAPE_ECCENTRICITY] = (l1 == 0.0) ? 0.0 : sqrt(1.0 - l2 / l1);
+  f[CPX_SHAPE_ORIENTATION] = (a - c == 0.0) ? ((b < 0.0) ? -3.14159265358979323846 / 4.0
+                                                          : 3.14159265358979323846 / 4.0)
+                                            : 0.5 * atan2(-2.0 * b, c - a);
+  f[CPX_SHAPE_BBOX_MIN_Y] = r0;
+  f[CPX_SHAPE_BBOX_MIN_X] = c0;
+  f[CPX_SHAPE_BBOX_MAX_Y] = r1;
+  f[CPX_SHAPE_BBOX_MAX_X] = c1;
+}
+
 __global__ __launch_bounds__(kST) void k_shape_fast(const int* __restrict__ labels, int H, int W,
-                                                   int max_label, int F,
+                                                   int max_label,
                                                    const cpx_object* __restrict__ objects,
                                                    const cpx_fov_objects* __restrict__ hdr,
-                                                   double* __restrict__ feats) {
+                                                   long long* __restrict__ raws) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned int* M = reinterpret_cast<unsigned int*>(smem);
   unsigned int* Bd = M + kShapeW;
@@ -655,134 +871,14 @@ __global__ __launch_bounds__(kST) void k_shape_fast(const int* __restrict__ labe
   __shared__ int redi[3][kST / 64];
   const int fov = blockIdx.y;
   const int nobj = hdr[fov].n_objects;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31;  // 8 x 32
   const int* lab = labels + (long long)fov * H * W;
   for (int k = blockIdx.x; k < nobj; k += gridDim.x) {
     const cpx_object o = objects[(long long)fov * max_label + k];
     if (!shape_fits(o)) continue;
-    const int L = o.label;
-    const int R0 = o.bbox[0] - 2, C0 = o.bbox[1] - 2;  // region origin (2-px margin)
-    const int rows = o.bbox[2] - o.bbox[0] + 4, cols = o.bbox[3] - o.bbox[1] + 4;
-    const int wpr = (cols + 31) >> 5;
     __syncthreads();
-    // membership bitmask: each 32-lane half-wave builds one 32-bit word (r, cw); four words per
-    // half-wave are loaded before the first ballot so the label loads overlap
-    const int nw = rows * wpr;
-    for (int w0 = 0; w0 < nw; w0 += 4 * (kST / 32)) {
-      int lv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int w = w0 + u * (kST / 32) + ty;
-        const int r = w / wpr, cw = w - r * wpr;
-        const int c = cw * 32 + tx;
-        const int gr = R0 + r, gc = C0 + c;
-        const bool ok = w < nw && c < cols && gr >= 0 && gr < H && gc >= 0 && gc < W;
-        lv[u] = ok ? lab[(long long)gr * W + gc] : -1;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int w = w0 + u * (kST / 32) + ty;
-        const unsigned long long b = __ballot(lv[u] == L);
-        if (w < nw) {
-          if (lane == 0) M[w] = (unsigned int)b;
-          if (lane == 32) M[w] = (unsigned int)(b >> 32);
-        }
-      }
-    }
+    shape_mask<kST>(lab, H, W, o, M);
     __syncthreads();
-    // border = in & !(up & down & left & right)
-    for (int w = threadIdx.x; w < rows * wpr; w += kST) {
-      const int r = w / wpr, cw = w - r * wpr;
-      const unsigned int x = M[w];
-      const unsigned int up = getw(M, wpr, rows, r - 1, cw), dn = getw(M, wpr, rows, r + 1, cw);
-      const unsigned int lf = (x << 1) | (getw(M, wpr, rows, r, cw - 1) >> 31);
-      const unsigned int rt = (x >> 1) | (getw(M, wpr, rows, r, cw + 1) << 31);
-      Bd[w] = x & ~(up & dn & lf & rt);
-    }
-    __syncthreads();
-    long long n = 0, sr = 0, sc = 0, srr = 0, scc = 0, src = 0;
-    int n1 = 0, n2 = 0, n3 = 0;
-    for (int w = threadIdx.x; w < rows * wpr; w += kST) {
-      const int r = w / wpr, cw = w - r * wpr;
-      unsigned int x = M[w];
-      const unsigned int bx = Bd[w];
-      while (x) {
-        const int b = __ffs(x) - 1;
-        x &= x - 1;
-        const int c = cw * 32 + b;
-        const long long rr = r - 2, cc = c - 2;  // bbox-local coordinates
-        n += 1;
-        sr += rr;
-        sc += cc;
-        srr += rr * rr;
-        scc += cc * cc;
-        src += rr * cc;
-        if (!((bx >> b) & 1u)) continue;
-        auto bit = [&](int rr2, int cc2) -> int {
-          return (int)((getw(Bd, wpr, rows, rr2, cc2 >> 5) >> (cc2 & 31)) & 1u);
-        };
-        const int code = 1 + 2 * (bit(r - 1, c) + bit(r + 1, c) + bit(r, c - 1) + bit(r, c + 1)) +
-                         10 * (bit(r - 1, c - 1) + bit(r - 1, c + 1) + bit(r + 1, c - 1) + bit(r + 1, c + 1));
-        if (code == 5 || code == 7 || code == 15 || code == 17 || code == 25 || code == 27) n1 += 1;
-        else if (code == 21 || code == 33) n2 += 1;
-        else if (code == 13 || code == 23) n3 += 1;
-      }
-    }
-    n = wave_sum(n); sr = wave_sum(sr); sc = wave_sum(sc);
-    srr = wave_sum(srr); scc = wave_sum(scc); src = wave_sum(src);
-    n1 = wave_sum(n1); n2 = wave_sum(n2); n3 = wave_sum(n3);
-    if (lane == 0) {
-      red[0][wid] = n; red[1][wid] = sr; red[2][wid] = sc;
-      red[3][wid] = srr; red[4][wid] = scc; red[5][wid] = src;
-      redi[0][wid] = n1; redi[1][wid] = n2; redi[2][wid] = n3;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      n = sr = sc = srr = scc = src = 0;
-      n1 = n2 = n3 = 0;
-      for (int w = 0; w < kST / 64; ++w) {
-        n += red[0][w]; sr += red[1][w]; sc += red[2][w];
-        srr += red[3][w]; scc += red[4][w]; src += red[5][w];
-        n1 += redi[0][w]; n2 += redi[1][w]; n3 += redi[2][w];
-      }
-      double* f = feats + ((long long)fov * max_label + k) * F;
-      const double SQ2 = 1.4142135623730951;
-      const double area = (double)n;
-      const int r0 = o.bbox[0], c0 = o.bbox[1], r1 = o.bbox[2], c1 = o.bbox[3];
-      const double bba = (double)(r1 - r0) * (double)(c1 - c0);
-      f[CPX_SHAPE_AREA] = area;
-      f[CPX_SHAPE_PERIMETER] = (double)n1 + (double)n2 * SQ2 + (double)n3 * ((1.0 + SQ2) / 2.0);
-      f[CPX_SHAPE_CENTER_Y] = o.centroid_r;
-      f[CPX_SHAPE_CENTER_X] = o.centroid_c;
-      f[CPX_SHAPE_BBOX_AREA] = bba;
-      f[CPX_SHAPE_EXTENT] = area / bba;
-      f[CPX_SHAPE_EQUIV_DIAMETER] = sqrt(4.0 * area / 3.14159265358979323846);
-      const i128 NN = n;
-      const i128 m20n = NN * srr - (i128)sr * sr;
-      const i128 m02n = NN * scc - (i128)sc * sc;
-      const i128 m11n = NN * src - (i128)sr * sc;
-      const double n2d = area * area;
-      const double a = (double)m02n / n2d, b = -(double)m11n / n2d, c = (double)m20n / n2d;
-      const double hm = 0.5 * (a + c), hd = 0.5 * (a - c);
-      const double rt = sqrt(hd * hd + b * b);
-      double l1 = hm + rt;
-      const i128 detn4 = m02n * m20n - m11n * m11n;
-      double l2 = (l1 > 0.0) ? ((double)detn4 / (n2d * n2d)) / l1 : 0.0;
-      if (l1 < 0.0) l1 = 0.0;
-      if (l2 < 0.0) l2 = 0.0;
-      if (l2 > l1) l2 = l1;
-      f[CPX_SHAPE_MAJOR_AXIS] = 4.0 * sqrt(l1);
-      f[CPX_SHAPE_MINOR_AXIS] = 4.0 * sqrt(l2);
-      f[CPX_SHAPE_ECCENTRICITY] = (l1 == 0.0) ? 0.0 : sqrt(1.0 - l2 / l1);
-      f[CPX_SHAPE_ORIENTATION] = (a - c == 0.0) ? ((b < 0.0) ? -3.14159265358979323846 / 4.0
-                                                              : 3.14159265358979323846 / 4.0)
-                                                : 0.5 * atan2(-2.0 * b, c - a);
-      f[CPX_SHAPE_BBOX_MIN_Y] = r0;
-      f[CPX_SHAPE_BBOX_MIN_X] = c0;
-      f[CPX_SHAPE_BBOX_MAX_Y] = r1;
-      f[CPX_SHAPE_BBOX_MAX_X] = c1;
-    }
+    shape_sums<kST>(o, M, Bd, red, redi, raws + ((long long)fov * max_label + k) * kShapeRaw);
   }
 }
 
@@ -794,14 +890,11 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
                       int H, int W, int max_label, int F, const cpx_object* objects_dev,
                       const cpx_fov_objects* hdr_dev, double* feats_dev, cpx_fallback_lists* fb) {
   static bool attr = false;
-  const size_t lds_t = sizeof(unsigned int) * kTabW + sizeof(unsigned long long) * 256 + kCrop;
-  static_assert(sizeof(unsigned int) * kTabW + sizeof(unsigned long long) * 256 + kCrop <= 160 * 1024,
-                "GLCM LDS budget");
-  static_assert(kNW * 4 * kAccW <= kTabW, "reduction scratch inside the table");
+  static_assert(sizeof(unsigned int) * kTabW + kSmall + kCrop == 160 * 1024, "GLCM LDS budget");
+  static_assert(sizeof(unsigned long long) * 4 * kRedW == 320 && kCrop % 16 == 0, "GLCM LDS layout");
+  static_assert(2 * kRedW * kTT <= kTabW, "reduction scratch inside the table");
   const size_t lds_s = sizeof(unsigned int) * 2 * kShapeW;
   if (!attr) {
-    CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_tex_glcm,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_t));
     CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_shape_fast,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_s));
     attr = true;
@@ -809,9 +902,11 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   // workspace: crop offsets [B][max_label] + scratch (2 bytes per pixel-channel per FOV)
   const long long per_fov = ((2LL * H * W * C + 255) / 256) * 256;
   // + one GLCM work-queue counter per FOV (zeroed by k_crop_offsets) + the fallback lists
+  // + the AreaShape raw sums [B][max_label][kShapeRaw]
   const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + sizeof(int) * (size_t)B * 3 +
                              sizeof(int) * 2 * (size_t)B * max_label + 255) / 256) * 256;
-  unsigned char* ws = (unsigned char*)cpx_ws(ctx, WS_MISC, off_bytes + (size_t)B * per_fov + 256);  // +256: GLCM key read-ahead
+  const size_t raw_bytes = ((sizeof(long long) * kShapeRaw * (size_t)B * max_label + 255) / 256) * 256;
+  unsigned char* ws = (unsigned char*)cpx_ws(ctx, WS_MISC, off_bytes + raw_bytes + (size_t)B * per_fov + 256);  // +256: crop read slack
   if (!ws) return CPX_ERR_OOM;
   CPX_REQUIRE(B < 2048 && (long long)max_label * C < (1 << 20), CPX_ERR_SHAPE,
               "GLCM queue codes hold fov < 2048 and items < 2^20");
@@ -821,21 +916,25 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   fb->n_tex = fb->n_shape + B;
   fb->shape = fb->n_tex + B;
   fb->tex = fb->shape + (size_t)B * max_label;
-  unsigned char* scratch = ws + off_bytes;
+  long long* raws = (long long*)(ws + off_bytes);
+  unsigned char* scratch = ws + off_bytes + raw_bytes;
   hipLaunchKernelGGL(k_crop_offsets, dim3(B), dim3(1024), 0, ctx->stream, C, max_label,
                      objects_dev, hdr_dev, per_fov, crop_off, glcm_next, *fb);
   CPX_CHECK_LAUNCH("k_crop_offsets");
   const int per_fov_s = std::max(1, std::min(max_label, (8 * ctx->n_cu + B - 1) / B));
   hipLaunchKernelGGL(k_shape_fast, dim3(per_fov_s, B), dim3(kST), lds_s, ctx->stream,
-                     (const int*)labels_dev, H, W, max_label, F, objects_dev, hdr_dev, feats_dev);
+                     (const int*)labels_dev, H, W, max_label, objects_dev, hdr_dev, raws);
   CPX_CHECK_LAUNCH("k_shape_fast");
+  hipLaunchKernelGGL(k_shape_props, dim3(cpx_div_up(max_label, 256), B), dim3(256), 0, ctx->stream,
+                     max_label, F, objects_dev, hdr_dev, (const long long*)raws, feats_dev);
+  CPX_CHECK_LAUNCH("k_shape_props");
   const int per_fov_a = std::max(1, std::min(max_label * C, (16 * ctx->n_cu + B - 1) / B));
   hipLaunchKernelGGL(k_tex_stage, dim3(per_fov_a, B), dim3(kAT), 0, ctx->stream,
                      (const int*)labels_dev, corr_dev, C, H, W, max_label, F, objects_dev, hdr_dev,
                      (const long long*)crop_off, scratch, per_fov, feats_dev);
   CPX_CHECK_LAUNCH("k_tex_stage");
   const int per_fov_t = std::max(1, std::min(max_label * C, (ctx->n_cu + B - 1) / B));
-  hipLaunchKernelGGL(k_tex_glcm, dim3(per_fov_t, B), dim3(kTT), lds_t, ctx->stream, C, max_label,
+  hipLaunchKernelGGL(k_tex_glcm, dim3(per_fov_t, B), dim3(kTT), 0, ctx->stream, C, max_label,
                      F, objects_dev, hdr_dev, (const long long*)crop_off,
                      (const unsigned char*)scratch, per_fov, glcm_next, feats_dev);
   CPX_CHECK_LAUNCH("k_tex_glcm");

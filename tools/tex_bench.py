@@ -67,7 +67,7 @@ def main():
         if prof:
             prof(buf, 1)
             items = max(buf[5], 1)
-            names = ["overflow_angles", "-", "count", "walk", "finish"]
+            names = ["reduce", "zero", "count", "scan", "props"]
             line += " | cycles/item " + " ".join(f"{nm}={buf[k] / items:.0f}" for k, nm in enumerate(names))
             line += f" | items {buf[5] // a.reps} px/item {buf[6] / items:.0f} global {buf[7] / items:.2f}"
         print(line)
