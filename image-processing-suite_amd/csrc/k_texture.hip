@@ -39,7 +39,8 @@ __device__ unsigned long long g_glcm_prof[8];
 constexpr int kTT = 1024;            // GLCM block (16 waves, one block per CU)
 constexpr int kNW = kTT / 64;
 constexpr int kTabW = 32768;         // 64K packed u16 pair counters (128 KiB), diagonal-major
-constexpr int kSmall = 256 + 320 + 16;  // LDS after the table: atomic sinks, reduction totals, queue codes
+constexpr int kSmall = 256 + 320 + 16 + 2048;  // LDS after the table: atomic sinks, reduction totals,
+                                               // queue codes, homogeneity table
 constexpr int kCrop = 160 * 1024 - 4 * kTabW - kSmall;  // u8 crop bytes held in LDS
 constexpr int kSlack = 16;           // bytes the GLCM may read past a crop's last row (masked)
 
@@ -91,7 +92,7 @@ struct GlcmSums {
   unsigned int sisj;                        // count pass: sum i + (sum j << 16) (< 2^16 each per thread)
   unsigned int sii, sjj, sij, dis;
   unsigned int asq, cnt;                    // scan: sum c^2, sum c over non-background keys
-  unsigned long long hom;                   // scan: sum c * hom(d)
+  unsigned long long hom;                   // count: sum over pair slots of hom(|i - j|)
 };
 constexpr int kRedW = 10;  // 32-bit words per angle in the block reduction
 
@@ -112,7 +113,7 @@ __device__ __forceinline__ void glcm_add(unsigned int* tab, unsigned int* sink, 
 
 template <int ANG, bool LDS_CROP>
 __device__ __forceinline__ void glcm_count(const unsigned char* __restrict__ crop, unsigned int* tab,
-                                           GlcmSums& S, int bh, int bw) {
+                                           const unsigned long long* hom, GlcmSums& S, int bh, int bw) {
   unsigned int* sink = tab + kTabW + (threadIdx.x & 63);
   constexpr int dr = ANG == 0 ? 0 : ANG == 2 ? 3 : 2;
   constexpr int dc = ANG == 0 ? 3 : ANG == 1 ? 2 : ANG == 2 ? 0 : -2;
@@ -172,6 +173,15 @@ __device__ __forceinline__ void glcm_count(const unsigned char* __restrict__ cro
     S.sij = __builtin_amdgcn_udot4(a0, b0, S.sij, false);
     S.sij = __builtin_amdgcn_udot4(a1, b1, S.sij, false);
     // keys (dd << 8) | i, two per word: selectors 0-3 pick i (src1), 4-7 pick dd (src0)
+    // homogeneity per pair slot from the LDS table (masked slots are (0, 0) -> hom(0); finish
+    // subtracts them, background pairs stay)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned int ia = (a0 >> (8 * u)) & 255u, ib = (b0 >> (8 * u)) & 255u;
+      const unsigned int ja = (a1 >> (8 * u)) & 255u, jb = (b1 >> (8 * u)) & 255u;
+      S.hom += hom[ia > ib ? ia - ib : ib - ia];
+      S.hom += hom[ja > jb ? ja - jb : jb - ja];
+    }
     const unsigned int d0 = bytes_sub(b0, a0), d1 = bytes_sub(b1, a1);
     const unsigned int k01 = __builtin_amdgcn_perm(d0, a0, 0x05010400u);
     const unsigned int k23 = __builtin_amdgcn_perm(d0, a0, 0x07030602u);
@@ -199,17 +209,10 @@ __device__ __forceinline__ void glcm_count(const unsigned char* __restrict__ cro
   }
 }
 
-// Scan + clear of one angle's table (see above).  Row dd = 128 words; lane l holds keys
-// i = 4l .. 4l + 3 (two words), of which min(max(256 - dd - 4l, 0), 4) have |i - j| = dd.  Wave w
-// owns rows w + 16k (k < 16), read four at a time so the LDS latency overlaps; the homogeneity
-// weights of its rows come from registers (hv: lane k holds hom(dd_k), lane 16 + k
-// hom(256 - dd_k)) by v_readlane, never from memory inside the loop.
-__device__ __forceinline__ unsigned long long lane_u64(unsigned long long v, int l) {
-  return ((unsigned long long)(unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)(v >> 32), l) << 32) |
-         (unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)v, l);
-}
-
-__device__ __forceinline__ void glcm_scan(unsigned int* tab, GlcmSums& S, unsigned long long hv) {
+// Scan + clear of one angle's table: ASM = sum c^2 (v_dot2_u32_u16 on the packed counters) and
+// the non-background pair count sum c; wave w owns rows w + 16k (k < 16), read four at a time so
+// the LDS latency overlaps, all-zero rows skipped by ballot.
+__device__ __forceinline__ void glcm_scan(unsigned int* tab, GlcmSums& S) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint2* rows = reinterpret_cast<uint2*>(tab) + wid * 64 + lane;
 #pragma unroll
@@ -221,27 +224,12 @@ __device__ __forceinline__ void glcm_scan(unsigned int* tab, GlcmSums& S, unsign
     for (int k = 0; k < 4; ++k) {
       if (!__builtin_amdgcn_ballot_w64((w[k].x | w[k].y) != 0u)) continue;
       rows[(k0 + k) * kNW * 64] = uint2{0u, 0u};
-      const int dd = wid + kNW * (k0 + k);
       S.asq = dot2_u16(w[k].x, w[k].x, S.asq);
       S.asq = dot2_u16(w[k].y, w[k].y, S.asq);
-      const unsigned int sall = dot2_u16(w[k].x, 0x10001u, dot2_u16(w[k].y, 0x10001u, 0u));
-      const int r = 256 - dd - 4 * lane;
-      const unsigned int mx = r >= 2 ? ~0u : (r == 1 ? 0xffffu : 0u);
-      const unsigned int my = r >= 4 ? ~0u : (r == 3 ? 0xffffu : 0u);
-      const unsigned int slo = dot2_u16(w[k].x & mx, 0x10001u, dot2_u16(w[k].y & my, 0x10001u, 0u));
-      S.cnt += sall;
-      S.hom += (unsigned long long)slo * lane_u64(hv, k0 + k) +
-               (unsigned long long)(sall - slo) * lane_u64(hv, 16 + k0 + k);
+      S.cnt = dot2_u16(w[k].x, 0x10001u, S.cnt);
+      S.cnt = dot2_u16(w[k].y, 0x10001u, S.cnt);
     }
   }
-}
-
-// the scan's homogeneity weights for this thread's wave (see glcm_scan)
-__device__ __forceinline__ unsigned long long glcm_scan_weights() {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane >= 32) return 0;
-  const int dd = wid + kNW * (lane & 15);
-  return kHom.m[lane < 16 ? dd : (256 - dd) & 255];
 }
 
 // Sum of a u64 over each half-wave (lanes 0-31 -> lane 31, 32-63 -> lane 63) on the DPP path.
@@ -310,7 +298,9 @@ __device__ void glcm_finish(const GlcmSums (&S)[4], unsigned int* red, unsigned 
                     tsjj = (long long)v[3], tsij = (long long)v[4];
     const unsigned long long dt = v[5], tas = v[6], ncnt = v[7];
     const unsigned long long nbg = (unsigned long long)T - ncnt;  // background pairs (0, 0)
-    const unsigned long long hs = v[8] + (v[9] << 32) + nbg * kHom.m[0];
+    // the count visited rend * crop_stride(bw) pair slots; the masked ones added hom(0) each
+    const unsigned long long slots = rend > 0 ? (unsigned long long)rend * crop_stride(bw) : 0ull;
+    const unsigned long long hs = v[8] + (v[9] << 32) - (slots - (unsigned long long)T) * kHom.m[0];
     double con = 0.0, dis = 0.0, hom = 0.0, asmv = 0.0, ene = 0.0, cor = 1.0;
     if (T > 0) {
       const double Td = (double)T;
@@ -544,13 +534,13 @@ __device__ __forceinline__ unsigned int glcm_touch(const GlcmItem& g) {
 
 template <int A>
 __device__ __forceinline__ void glcm_angle(const GlcmItem& it, const unsigned char* crop,
-                                           unsigned int* tab, GlcmSums& S, unsigned long long hv,
+                                           unsigned int* tab, const unsigned long long* hom, GlcmSums& S,
                                            long long* pt) {
-  if (it.bytes <= kCrop) glcm_count<A, true>(crop, tab, S, it.bh, it.bw);
-  else glcm_count<A, false>(it.src, tab, S, it.bh, it.bw);
+  if (it.bytes <= kCrop) glcm_count<A, true>(crop, tab, hom, S, it.bh, it.bw);
+  else glcm_count<A, false>(it.src, tab, hom, S, it.bh, it.bw);
   __syncthreads();
   GLCM_MARK(2, pt);
-  glcm_scan(tab, S, hv);
+  glcm_scan(tab, S);
   __syncthreads();
   GLCM_MARK(3, pt);
 }
@@ -571,11 +561,12 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
   unsigned int* tab = lds;
   unsigned long long* s_tot = reinterpret_cast<unsigned long long*>(smem + 4 * kTabW + 256);
   int* s_code = reinterpret_cast<int*>(smem + 4 * kTabW + 256 + 320);  // double-buffered by parity
+  unsigned long long* s_hom = reinterpret_cast<unsigned long long*>(smem + 4 * kTabW + 256 + 320 + 16);
   unsigned char* crop = smem + 4 * kTabW + kSmall;
   const int B = gridDim.y;
   int q_fov = blockIdx.y, q_visited = 0;  // thread 0's queue position
-  const unsigned long long hv = glcm_scan_weights();
   for (int x = threadIdx.x; x < kTabW; x += kTT) tab[x] = 0u;
+  if (threadIdx.x < 256) s_hom[threadIdx.x] = kHom.m[threadIdx.x];
   if (threadIdx.x == 0) {
     s_code[0] = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next);
     s_code[1] = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next);
@@ -621,10 +612,10 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
     }
 #endif
     GlcmSums S[4] = {};
-    glcm_angle<0>(it, crop, tab, S[0], hv, &pt);
-    glcm_angle<1>(it, crop, tab, S[1], hv, &pt);
-    glcm_angle<2>(it, crop, tab, S[2], hv, &pt);
-    glcm_angle<3>(it, crop, tab, S[3], hv, &pt);
+    glcm_angle<0>(it, crop, tab, s_hom, S[0], &pt);
+    glcm_angle<1>(it, crop, tab, s_hom, S[1], &pt);
+    glcm_angle<2>(it, crop, tab, s_hom, S[2], &pt);
+    glcm_angle<3>(it, crop, tab, s_hom, S[3], &pt);
     glcm_finish(S, tab, s_tot, it.bh, it.bw, f, &pt);
     GLCM_MARK(4, &pt);
   }
