@@ -485,22 +485,23 @@ __global__ __launch_bounds__(kTexThreads) void k_intensity_texture(
 
 }  // namespace
 
-extern "C" int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B,
-                            int C, int H, int W, int max_label, const cpx_object* objects_dev,
-                            const cpx_fov_objects* hdr_dev, double* feats_dev) {
-  CPX_REQUIRE(ctx && labels_dev && corr_dev && objects_dev && hdr_dev && feats_dev, CPX_ERR_ARG,
-              "cpx_features: null argument");
-  CPX_REQUIRE(B > 0 && B <= 65535 && C > 0 && C <= 65535 && H > 0 && W > 0 && max_label > 0,
-              CPX_ERR_ARG, "cpx_features: bad sizes");
-  const int F = CPX_N_SHAPE + C * CPX_FEATURES_PER_CHANNEL;
-  cpx_fallback_lists fb;
-  const int rc = cpx_features_fast(ctx, labels_dev, corr_dev, B, C, H, W, max_label, F, objects_dev,
-                                   hdr_dev, feats_dev, &fb);
-  if (rc) return rc;
-  // fallback kernels for the objects too large for the LDS fast paths (listed per FOV)
+namespace {
+struct FallbackArgs {
+  const int32_t* labels_dev;
+  const float* corr_dev;
+  int B, C, H, W, max_label, F;
+  const cpx_object* objects_dev;
+  double* feats_dev;
+};
+
+// fallback kernels for the objects too large for the LDS fast paths (listed per FOV), launched by
+// cpx_features_fast on its side stream
+int launch_fallbacks(cpx_ctx* ctx, hipStream_t stream, const cpx_fallback_lists& fb, void* arg) {
+  const FallbackArgs& a = *static_cast<const FallbackArgs*>(arg);
+  const int B = a.B, C = a.C, H = a.H, W = a.W, max_label = a.max_label, F = a.F;
   hipLaunchKernelGGL(k_shape, dim3(std::max(1, std::min(max_label, (4 * ctx->n_cu + B - 1) / B)), B),
-                     dim3(kShapeThreads), 0, ctx->stream, (const int*)labels_dev, H, W, max_label, F,
-                     objects_dev, (const int*)fb.shape, (const int*)fb.n_shape, feats_dev);
+                     dim3(kShapeThreads), 0, stream, (const int*)a.labels_dev, H, W, max_label, F,
+                     a.objects_dev, (const int*)fb.shape, (const int*)fb.n_shape, a.feats_dev);
   CPX_CHECK_LAUNCH("k_shape");
   static bool attr = false;
   const size_t lds = sizeof(unsigned int) * (kTabWords + 256) +
@@ -511,9 +512,24 @@ extern "C" int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float
     attr = true;
   }
   const int per_fov = std::max(1, std::min(max_label * C * CPX_N_ANGLES, (ctx->n_cu + B - 1) / B));
-  hipLaunchKernelGGL(k_intensity_texture, dim3(per_fov, B), dim3(kTexThreads), lds,
-                     ctx->stream, (const int*)labels_dev, corr_dev, C, H, W, max_label, F,
-                     objects_dev, (const int*)fb.tex, (const int*)fb.n_tex, feats_dev);
+  hipLaunchKernelGGL(k_intensity_texture, dim3(per_fov, B), dim3(kTexThreads), lds, stream,
+                     (const int*)a.labels_dev, a.corr_dev, C, H, W, max_label, F, a.objects_dev,
+                     (const int*)fb.tex, (const int*)fb.n_tex, a.feats_dev);
   CPX_CHECK_LAUNCH("k_intensity_texture");
   return CPX_OK;
+}
+}  // namespace
+
+extern "C" int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B,
+                            int C, int H, int W, int max_label, const cpx_object* objects_dev,
+                            const cpx_fov_objects* hdr_dev, double* feats_dev) {
+  CPX_REQUIRE(ctx && labels_dev && corr_dev && objects_dev && hdr_dev && feats_dev, CPX_ERR_ARG,
+              "cpx_features: null argument");
+  CPX_REQUIRE(B > 0 && B <= 65535 && C > 0 && C <= 65535 && H > 0 && W > 0 && max_label > 0,
+              CPX_ERR_ARG, "cpx_features: bad sizes");
+  const int F = CPX_N_SHAPE + C * CPX_FEATURES_PER_CHANNEL;
+  FallbackArgs fa{labels_dev, corr_dev, B, C, H, W, max_label, F, objects_dev, feats_dev};
+  cpx_fallback_lists fb;
+  return cpx_features_fast(ctx, labels_dev, corr_dev, B, C, H, W, max_label, F, objects_dev, hdr_dev,
+                           feats_dev, &fb, launch_fallbacks, &fa);
 }

@@ -879,7 +879,8 @@ __global__ __launch_bounds__(kST) void k_shape_fast(const int* __restrict__ labe
 // internal launchers used by cpx_features (k_features.hip)
 int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B, int C,
                       int H, int W, int max_label, int F, const cpx_object* objects_dev,
-                      const cpx_fov_objects* hdr_dev, double* feats_dev, cpx_fallback_lists* fb) {
+                      const cpx_fov_objects* hdr_dev, double* feats_dev, cpx_fallback_lists* fb,
+                      cpx_fallback_fn fallback, void* fallback_arg) {
   static bool attr = false;
   static_assert(sizeof(unsigned int) * kTabW + kSmall + kCrop == 160 * 1024, "GLCM LDS budget");
   static_assert(sizeof(unsigned long long) * 4 * kRedW == 320 && kCrop % 16 == 0, "GLCM LDS layout");
@@ -912,6 +913,15 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   hipLaunchKernelGGL(k_crop_offsets, dim3(B), dim3(1024), 0, ctx->stream, C, max_label,
                      objects_dev, hdr_dev, per_fov, crop_off, glcm_next, *fb);
   CPX_CHECK_LAUNCH("k_crop_offsets");
+  // fork: the fallback kernels (a few, the largest objects, each one long block) run on the side
+  // stream beside the fast path instead of as a serial tail after it
+  if (fallback) {
+    CPX_CHECK_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
+    CPX_CHECK_HIP(hipStreamWaitEvent(ctx->side_stream, ctx->ev_fork, 0));
+    const int rc = fallback(ctx, ctx->side_stream, *fb, fallback_arg);
+    if (rc) return rc;
+    CPX_CHECK_HIP(hipEventRecord(ctx->ev_join, ctx->side_stream));
+  }
   const int per_fov_s = std::max(1, std::min(max_label, (8 * ctx->n_cu + B - 1) / B));
   hipLaunchKernelGGL(k_shape_fast, dim3(per_fov_s, B), dim3(kST), lds_s, ctx->stream,
                      (const int*)labels_dev, H, W, max_label, objects_dev, hdr_dev, raws);
@@ -929,6 +939,7 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
                      F, objects_dev, hdr_dev, (const long long*)crop_off,
                      (const unsigned char*)scratch, per_fov, glcm_next, feats_dev);
   CPX_CHECK_LAUNCH("k_tex_glcm");
+  if (fallback) CPX_CHECK_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // join
   return CPX_OK;
 }
 
