@@ -157,11 +157,12 @@ def main():
     # the stream every stage is launched on (torch's current stream; libcpx is bound to it)
     stages = ["illum_qc", "segment", "objects_features"]
     acc = {s: 0.0 for s in stages}
-    sub = {"illum": 0.0, "qc_rps": 0.0, "seg_prep": 0.0, "cpnet": 0.0, "seg_post": 0.0}
+    sub = {"illum": 0.0, "qc_rps": 0.0, "seg_prep": 0.0, "cpnet": 0.0, "seg_post": 0.0, "cells": 0.0,
+           "features": 0.0}
     if Z > 1:
         sub["zmax"] = 0.0
     for i in range(a.stage_steps):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(9)]
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(10)]
         if Z > 1:
             ez = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             ez[0].record()
@@ -179,8 +180,10 @@ def main():
         ev[4].record()
         pipe.seg.postprocess(pipe.labels["Nuclei"])
         ev[5].record()
-        pipe.stage_objects()
+        pipe.stage_cells()
         ev[6].record()
+        pipe.stage_features()
+        ev[7].record()
         torch.cuda.synchronize()
         sub["illum"] += ev[0].elapsed_time(ev[1])
         sub["qc_rps"] += ev[1].elapsed_time(ev[2])
@@ -189,7 +192,9 @@ def main():
         sub["seg_post"] += ev[4].elapsed_time(ev[5])
         acc["illum_qc"] += ev[0].elapsed_time(ev[2])
         acc["segment"] += ev[2].elapsed_time(ev[5])
-        acc["objects_features"] += ev[5].elapsed_time(ev[6])
+        acc["objects_features"] += ev[5].elapsed_time(ev[7])
+        sub["cells"] += ev[5].elapsed_time(ev[6])
+        sub["features"] += ev[6].elapsed_time(ev[7])
         if Z > 1:
             sub["zmax"] += ez[0].elapsed_time(ez[1])
     per_step_ms = {k: v / a.stage_steps for k, v in acc.items()}
@@ -200,11 +205,14 @@ def main():
     illum_bytes = B * C * N * (2 + 4 + 4)                # raw u16 + illum f32 in, fp32 plane out
     # the C fp32 planes once per step plus one int32 label image per object set
     feat_bytes = B * (C * 4 * N + 3 * 4 * N)
+    # Cells watershed: Nuclei labels + the fp32 cell channel in, Cells + Cytoplasm labels out
+    cells_bytes = B * (4 * N + 4 * N + 2 * 4 * N)
     cpnet_flops = B * n_tiles * count_flops(pipe.seg.geom.by)
     kernels = {
         "illum": dict(bound="hbm", work=illum_bytes, ms=sub_ms["illum"]),
         "cpnet": dict(bound="mfma", work=cpnet_flops, ms=sub_ms["cpnet"]),
-        "objects_features": dict(bound="hbm", work=feat_bytes, ms=per_step_ms["objects_features"]),
+        "cells": dict(bound="hbm", work=cells_bytes, ms=sub_ms["cells"]),
+        "features": dict(bound="hbm", work=feat_bytes, ms=sub_ms["features"]),
     }
     if Z > 1:  # Z u16 planes in, one u16 plane out per channel group
         kernels["zmax"] = dict(bound="hbm", work=B * C * N * (2 * Z + 2), ms=sub_ms["zmax"])

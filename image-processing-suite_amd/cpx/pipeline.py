@@ -135,6 +135,11 @@ class FovPipeline:
         self.seg.segment(self.corr, self.labels["Nuclei"])
 
     def stage_objects(self):
+        self.stage_cells()
+        self.stage_features()
+
+    def stage_cells(self):
+        """Cells (marker watershed or expand_labels) and Cytoplasm from the Nuclei labels."""
         from ._lib import check
         from .device import _ptr
         cfg = self.cfg
@@ -153,6 +158,10 @@ class FovPipeline:
                                                  _ptr(self.labels["Cytoplasm"])), "cpx_expand_labels")
         else:
             raise ValueError(f"PipelineConfig.cells: {cfg.cells!r}")
+
+    def stage_features(self):
+        """Object tables and shape / intensity / texture features of the three object sets."""
+        cfg = self.cfg
         for s in OBJECT_SETS:
             self.dev.objects(self.labels[s], cfg.max_objects, cfg.box, self.lstats, self.objects[s], self.hdr[s])
             self.dev.features(self.labels[s], self.corr, cfg.C, cfg.max_objects, self.objects[s],

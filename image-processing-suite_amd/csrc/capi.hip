@@ -64,12 +64,6 @@ int cpx_init(int device, cpx_ctx** out) {
     return cpx_hip_fail(e, "hipStreamCreate");
   }
   c->stream = c->own_stream;
-  if ((e = hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess) {
-    cpx_destroy(c);
-    return cpx_hip_fail(e, "hipStreamCreate / hipEventCreate");
-  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
   *out = c;
@@ -80,13 +74,9 @@ void cpx_destroy(cpx_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->side_stream) (void)hipStreamSynchronize(ctx->side_stream);
   cpx_fov_free(ctx);
   for (int i = 0; i < kWsSlots; ++i)
     if (ctx->ws[i]) (void)hipFree(ctx->ws[i]);
-  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
-  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-  if (ctx->side_stream) (void)hipStreamDestroy(ctx->side_stream);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }

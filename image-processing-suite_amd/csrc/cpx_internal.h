@@ -15,9 +15,9 @@ struct cpx_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
-  // side stream for work that runs beside the main stream inside one call (fork/join by events)
-  hipStream_t side_stream = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // no side streams: every extra stream of a process competes for the GPU_MAX_HW_QUEUES (4)
+  // hardware queues, and two pipelines' streams sharing one queue serialise (measured: a
+  // per-context fork/join side stream cost 14 % of the two-pipeline bench)
   // generic growable device workspaces (never shrunk; see cpx_reserve)
   void* ws[kWsSlots] = {nullptr};
   size_t ws_bytes[kWsSlots] = {0};
@@ -125,7 +125,7 @@ struct cpx_fallback_lists {
   int* n_shape;
   int* n_tex;
 };
-// Fallback launcher cpx_features_fast calls on the side stream once the lists exist.
+// Fallback launcher cpx_features_fast calls on its stream once the lists exist.
 typedef int (*cpx_fallback_fn)(cpx_ctx* ctx, hipStream_t stream, const cpx_fallback_lists& fb,
                                void* arg);
 int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B, int C,

@@ -495,7 +495,7 @@ struct FallbackArgs {
 };
 
 // fallback kernels for the objects too large for the LDS fast paths (listed per FOV), launched by
-// cpx_features_fast on its side stream
+// cpx_features_fast after the fast path
 int launch_fallbacks(cpx_ctx* ctx, hipStream_t stream, const cpx_fallback_lists& fb, void* arg) {
   const FallbackArgs& a = *static_cast<const FallbackArgs*>(arg);
   const int B = a.B, C = a.C, H = a.H, W = a.W, max_label = a.max_label, F = a.F;

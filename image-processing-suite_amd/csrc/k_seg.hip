@@ -284,8 +284,9 @@ __global__ __launch_bounds__(kT) void k_seg_average(const void* __restrict__ net
 // dynamics (dynamics.compute_masks) at the dynamics resolution Dy x Dx: the full H x W with
 // resample=True (CellposeModel.eval's default, the reference call), Ly x Lx with resample=False.
 struct DynBufs {
-  double2* dps;          // [B][n] (dY, dX) * cp_mask / 5: the follow_flows field (fp32 values
-                         // held as fp64: the step's fp64 expression reads them without converting)
+  float2* dps;           // [B][n] (dY, dX) * cp_mask / 5: the follow_flows field (fp32; the step
+                         // converts the four gathered values to fp64 exactly: half the gather
+                         // bytes of an fp64 copy, and the early rounds are L2-bandwidth bound)
   float2* dpf;           // [B][n] (dY, dX) network flows (flow-error input)
   float2* p;             // [B][n] final positions (written for moving pixels only)
   unsigned char* mov;    // [B][n] pixel follows the flow (|dY * cp / 5| > 1e-3)
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(kT) void k_dyn_prep(const float* __restrict__ yf, i
     }
     const float cp = v[2] > 0.0f ? 1.0f : 0.0f;  // cellprob > cellprob_threshold (0.0)
     const float dy = (v[0] * cp) / 5.0f, dx = (v[1] * cp) / 5.0f;
-    d.dps[(long long)fov * n + q] = make_double2((double)dy, (double)dx);
+    d.dps[(long long)fov * n + q] = make_float2(dy, dx);
     d.dpf[(long long)fov * n + q] = make_float2(v[0], v[1]);
     // np.abs(dP[0]) > 1e-3: numpy compares the float32 array with the scalar cast to float32
     const bool moving = fabsf(dy) > 1e-3f;
@@ -409,7 +410,7 @@ __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, in
   if (n_moving < 5) return;  // follow_flows returns inds=None -> no masks
   const int n_in = from_act ? n_moving : in_cnt[fov];
   const int steps = min(K, niter - step0);
-  const double2* __restrict__ I = d.dps + (long long)fov * n;
+  const float2* __restrict__ I = d.dps + (long long)fov * n;
   float2* __restrict__ P = d.p + (long long)fov * n;
   const FollowItem* src = in + (long long)fov * n;
   FollowItem* dst = out + (long long)fov * n;
@@ -441,7 +442,9 @@ __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, in
       const int y0 = min(Dy - 1, max(0, yi)), x0 = min(Dx - 1, max(0, xi));
       const int i00 = y0 * Dx + x0;
       const int dxo = x0 + 1 < Dx ? 1 : 0, dyo = y0 + 1 < Dy ? Dx : 0;
-      const double2 a = I[i00], b = I[i00 + dxo], c = I[i00 + dyo], e = I[i00 + dyo + dxo];
+      const float2 af = I[i00], bf = I[i00 + dxo], cf = I[i00 + dyo], ef = I[i00 + dyo + dxo];
+      const double2 a = {(double)af.x, (double)af.y}, b = {(double)bf.x, (double)bf.y},
+                    c = {(double)cf.x, (double)cf.y}, e = {(double)ef.x, (double)ef.y};
       double vy, vx;
       if (py >= 1.0f && px >= 1.0f) {
         // yy = frac(py) and 1 - yy are exact in fp32 (multiples of 2^-23 in [0, 1]), so
@@ -1552,7 +1555,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
   const int ntile = cpx_div_up(std::max(n, nh), kOcTile);
   const size_t sz_f2 = al(sizeof(float2) * B * n);
-  const size_t sz_d2 = al(sizeof(double2) * B * n);
+  const size_t sz_d2 = al(sizeof(float2) * B * n);
   const size_t sz_b = al((size_t)B * n);
   const size_t sz_h = al(sizeof(int) * B * nh), sz_hb = al((size_t)B * nh);
   const size_t sz_m0 = resample ? 0 : al(sizeof(int) * B * n);
@@ -1569,7 +1572,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   unsigned char* w = (unsigned char*)cpx_ws(ctx, WS_SEG_DYN, total);
   if (!w) return CPX_ERR_OOM;
   DynBufs d;
-  d.dps = (double2*)w; w += sz_d2;
+  d.dps = (float2*)w; w += sz_d2;
   d.dpf = (float2*)w; w += sz_f2;
   d.p = (float2*)w; w += sz_f2;
   d.mov = w; w += sz_b;

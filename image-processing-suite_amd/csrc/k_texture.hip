@@ -1,17 +1,17 @@
 // a8 fast path: AreaShape + Intensity + Texture for objects whose bbox fits in LDS (the common
 // case; larger objects fall back to k_shape / k_intensity_texture in k_features.hip with the same
-// arithmetic).  Same definitions and bit-identical results as the fallback; see k_features.hip.
+// arithmetic).  Same definitions as the fallback (k_features.hip); integer sums are identical,
+// fp64 intensity sums may differ in the last bits (summation order).
 //
 // Design:
-//  * texture in two phases: phase A (high occupancy, one block per object-channel) makes one
-//    coalesced pass over the bbox (2-D thread layout, 4 rows of loads in flight per thread)
-//    for the intensity statistics and the scale_to_8bit range, then writes the 8-bit masked
-//    crop to a global scratch slot (offsets from a per-FOV scan); phase B (one 1024-thread
-//    block per CU with a 128 KiB LDS pair table) copies the crop to LDS and runs the four GLCM
-//    angles from LDS: exact u32 pair sums in registers per run of equal keys, ASM from the
-//    counts the table's atomics return, background (0,0) pairs by branch; DPP wave sums.
-//  * AreaShape: bbox + 2-pixel margin bitmask in LDS; the 4-neighbour border and the
-//    Benkrid-Crookes perimeter code are evaluated bit-parallel, moments are exact int64 sums.
+//  * k_obj_stage (one 512-thread block per object, two per CU): the object's bbox + margin
+//    membership bitmask from one read of the label image (AreaShape sums: bit-parallel border,
+//    Benkrid-Crookes perimeter, exact int64 moments), then per channel one coalesced pass over the
+//    bbox (values held in registers) for the Intensity columns and the scale_to_8bit range, and
+//    the 8-bit masked crop written to a global scratch slot (offsets from a per-FOV scan);
+//  * k_tex_glcm (one 1024-thread block per CU with a 128 KiB LDS pair table) copies a crop to LDS
+//    and runs the four GLCM angles from LDS: byte-SIMD pair sums, no-return LDS atomics on a
+//    diagonal-major u16 table, one scan per angle for ASM / the pair count.
 #include "cpx_internal.h"
 #include <math.h>
 
@@ -325,156 +325,6 @@ __device__ void glcm_finish(const GlcmSums (&S)[4], unsigned int* red, unsigned 
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Phase A (one block per object, its C channels in turn): intensity features and the
-// scale_to_8bit range from one coalesced pass over the bbox, then the 8-bit masked crop is
-// written to a global scratch slot (L2-resident until phase B reads it); membership from the
-// object's LDS bitmask, so the label image is not read again.
-constexpr int kAT = 256;  // 8 rows x 32 columns
-
-__global__ __launch_bounds__(kAT) void k_tex_stage(const int* __restrict__ labels,
-                                                  const float* __restrict__ corr, int C, int H,
-                                                  int W, int max_label, int F,
-                                                  const cpx_object* __restrict__ objects,
-                                                  const cpx_fov_objects* __restrict__ hdr,
-                                                  const long long* __restrict__ crop_off,
-                                                  unsigned char* __restrict__ scratch,
-                                                  long long scratch_per_fov,
-                                                  double* __restrict__ feats) {
-  __shared__ double sd[2][kAT / 64];
-  __shared__ long long sn[kAT / 64];
-  __shared__ float sf[4][kAT / 64];
-  const int fov = blockIdx.y;
-  const int n_items = hdr[fov].n_objects * C;
-  const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31, lane = threadIdx.x & 63,
-            wid = threadIdx.x >> 6;
-  const long long N = (long long)H * W;
-  const int* lab = labels + (long long)fov * N;
-  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
-    const int k = item / C, ch = item - k * C;
-    const long long off = crop_off[(long long)fov * max_label + k];
-    if (off < 0) continue;  // not staged: fallback kernel
-    const cpx_object o = objects[(long long)fov * max_label + k];
-    const int r0 = o.bbox[0], c0 = o.bbox[1];
-    const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
-    const int L = o.label;
-    const float* img = corr + ((long long)fov * C + ch) * N + (long long)r0 * W + c0;
-    const int* lb = lab + (long long)r0 * W + c0;
-    long long n = 0;
-    double sm = 0.0, ss = 0.0;
-    float omin = INFINITY, omax = -INFINITY, mmin = INFINITY, mmax = -INFINITY;
-    for (int rb = 0; rb < bh; rb += 32) {  // 4 rows in flight per thread
-      float vv[4];
-      int ll[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int r = rb + ty + 8 * u;
-        vv[u] = 0.0f;
-        ll[u] = -1;
-        (void)r;
-      }
-      for (int c = tx; c < bw; c += 32) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int r = rb + ty + 8 * u;
-          if (r < bh) {
-            vv[u] = img[(long long)r * W + c];
-            ll[u] = lb[(long long)r * W + c];
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int r = rb + ty + 8 * u;
-          if (r >= bh) continue;
-          const float v = vv[u];
-          const bool in = ll[u] == L;
-          const float m = v * (in ? 1.0f : 0.0f);
-          mmin = fminf(mmin, m);
-          mmax = fmaxf(mmax, m);
-          if (in) {
-            n += 1;
-            sm += (double)v;
-            ss += (double)v * (double)v;
-            omin = fminf(omin, v);
-            omax = fmaxf(omax, v);
-          }
-        }
-      }
-    }
-    n = wave_sum(n);
-    sm = wave_sum(sm);
-    ss = wave_sum(ss);
-    omin = wave_min(omin);
-    omax = wave_max(omax);
-    mmin = wave_min(mmin);
-    mmax = wave_max(mmax);
-    if (lane == 0) {
-      sn[wid] = n;
-      sd[0][wid] = sm;
-      sd[1][wid] = ss;
-      sf[0][wid] = omin;
-      sf[1][wid] = omax;
-      sf[2][wid] = mmin;
-      sf[3][wid] = mmax;
-    }
-    __syncthreads();
-    n = 0;
-    sm = ss = 0.0;
-    omin = mmin = INFINITY;
-    omax = mmax = -INFINITY;
-    for (int w = 0; w < kAT / 64; ++w) {
-      n += sn[w];
-      sm += sd[0][w];
-      ss += sd[1][w];
-      omin = fminf(omin, sf[0][w]);
-      omax = fmaxf(omax, sf[1][w]);
-      mmin = fminf(mmin, sf[2][w]);
-      mmax = fmaxf(mmax, sf[3][w]);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double* f = feats + ((long long)fov * max_label + k) * F + CPX_N_SHAPE +
-                  (long long)ch * CPX_FEATURES_PER_CHANNEL;
-      const double mean = n ? sm / (double)n : 0.0;
-      double var = n ? (ss - sm * mean) / (double)n : 0.0;
-      if (var < 0.0) var = 0.0;
-      f[CPX_INT_INTEGRATED] = sm;
-      f[CPX_INT_MEAN] = mean;
-      f[CPX_INT_STD] = sqrt(var);
-      f[CPX_INT_MIN] = (double)omin;
-      f[CPX_INT_MAX] = (double)omax;
-    }
-    const float rng = mmax - mmin;
-    const bool flat = !(mmax != mmin);
-    unsigned char* dst = scratch + (long long)fov * scratch_per_fov + off + (long long)ch * crop_bytes(bh, bw);
-    // the crop is written row by row at the padded stride (pad bytes 0), four pixels per thread
-    // per step packed into one 32-bit store: all lanes busy whatever bw is, and a wave stores
-    // 256 contiguous bytes instead of 64 single bytes
-    const int bwp = crop_stride(bw);
-    const int nb = bh * bwp;
-    for (int f0 = 4 * threadIdx.x; f0 < nb; f0 += 4 * kAT) {
-      const int r = f0 / bwp, c = f0 - r * bwp;  // bwp % 4 == 0: the four pixels share a row
-      // pad pixels (c + u >= bw) load the row's last pixel (branch-free) and store 0
-      const long long rw = (long long)r * W;
-      float vv[4];
-      int ll[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int cu = min(c + u, bw - 1);
-        vv[u] = img[rw + cu];
-        ll[u] = lb[rw + cu];
-      }
-      unsigned int word = 0u;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const unsigned int q = (unsigned int)quantize(vv[u], ll[u] == L, mmin, rng, flat);
-        word |= (c + u < bw ? q : 0u) << (8 * u);
-      }
-      *reinterpret_cast<unsigned int*>(dst + f0) = word;
-    }
-  }
-}
-
 struct GlcmItem {
   int fov, k, ch, bh, bw, nb;  // nb <= 0: nothing to do (no slot, > 65535 px, or queue drained)
   int bytes;                   // staged crop slot size (crop_bytes)
@@ -632,7 +482,10 @@ __global__ __launch_bounds__(1024) void k_crop_offsets(int C, int max_label,
                                                       int* __restrict__ glcm_next, cpx_fallback_lists fb) {
   const int fov = blockIdx.x;
   const int n = hdr[fov].n_objects;
-  if (threadIdx.x == 0) glcm_next[fov] = 0;  // k_tex_glcm's work queue of this FOV
+  if (threadIdx.x == 0) {  // this FOV's work queues: k_tex_glcm [0, B), k_obj_stage [B, 2B)
+    glcm_next[fov] = 0;
+    glcm_next[gridDim.x + fov] = 0;
+  }
   __shared__ long long wsum[16];
   __shared__ long long base;
   __shared__ int ns, nt;
@@ -648,7 +501,8 @@ __global__ __launch_bounds__(1024) void k_crop_offsets(int C, int max_label,
     if (k < n) {
       const cpx_object o = objects[(long long)fov * max_label + k];
       const int bh = o.bbox[2] - o.bbox[0], bw = o.bbox[3] - o.bbox[1];
-      sz = (long long)bh * bw <= 65535 ? crop_bytes(bh, bw) * C : 0;
+      // staged texture needs the fast path's membership bitmask (k_obj_stage)
+      sz = ((long long)bh * bw <= 65535 && cpx_shape_fits(bh, bw)) ? crop_bytes(bh, bw) * C : 0;
     }
     // inclusive wave scan
     long long x = sz;
@@ -685,7 +539,6 @@ __global__ __launch_bounds__(1024) void k_crop_offsets(int C, int max_label,
 
 // ---------------------------------------------------------------------------------------------
 // AreaShape fast path: bbox + 2-px margin membership bitmask in LDS
-constexpr int kST = 256;
 constexpr int kShapeW = kFastShapeWords;  // 8 KiB per bitmask (x2: membership + border)
 
 __device__ __forceinline__ unsigned int getw(const unsigned int* m, int wpr, int rows, int r, int cw) {
@@ -850,26 +703,222 @@ __global__ __launch_bounds__(256) void k_shape_props(int max_label, int F,
   f[CPX_SHAPE_BBOX_MAX_X] = c1;
 }
 
-__global__ __launch_bounds__(kST) void k_shape_fast(const int* __restrict__ labels, int H, int W,
-                                                   int max_label,
-                                                   const cpx_object* __restrict__ objects,
-                                                   const cpx_fov_objects* __restrict__ hdr,
-                                                   long long* __restrict__ raws) {
+// Per-object staging (one block per object, objects strided over the FOV's blocks): the label
+// image is read once per object into the bbox membership bitmask (AreaShape sums from it), then
+// each channel's bbox is read for the Intensity columns and the scale_to_8bit range and
+// quantised into the object's 8-bit crop slot for k_tex_glcm.  The first kOT * kOG 4-pixel
+// groups stay in registers between the two passes; the rest of a large bbox is read twice, with
+// the block's working set (one channel of one bbox, two blocks per CU) L2-resident in between.
+constexpr int kOT = 512;
+constexpr int kOG = 1;
+
+// in-bbox membership of the 4 pixels (r, c .. c + 3) from the bbox + 2-px margin bitmask
+__device__ __forceinline__ unsigned int member4(const unsigned int* M, int wpr, int r, int c) {
+  const int cb = c + 2, w = cb >> 5, sh = cb & 31;
+  const unsigned int* row = M + (r + 2) * wpr;
+  const unsigned long long two = (unsigned long long)row[w] |
+                                 ((unsigned long long)(w + 1 < wpr ? row[w + 1] : 0u) << 32);
+  return (unsigned int)(two >> sh) & 15u;
+}
+
+__device__ __forceinline__ unsigned int group_desc(const unsigned int* M, int wpr, int bw, int bwp, int W,
+                                                   int g) {
+  const int f0 = 4 * g, r = f0 / bwp, c = f0 - r * bwp;
+  return (unsigned int)(r * W + c) | (member4(M, wpr, r, c) << 24) | ((unsigned int)min(4, bw - c) << 28);
+}
+
+// Intensity columns from the member count and sums (regionprops intensity_* in fp64)
+__device__ __noinline__ void int_finish(double* f, long long n, double sm, double ss, float omin, float omax) {
+  const double mean = n ? sm / (double)n : 0.0;
+  double var = n ? (ss - sm * mean) / (double)n : 0.0;
+  if (var < 0.0) var = 0.0;
+  f[CPX_INT_INTEGRATED] = sm;
+  f[CPX_INT_MEAN] = mean;
+  f[CPX_INT_STD] = sqrt(var);
+  f[CPX_INT_MIN] = (double)omin;
+  f[CPX_INT_MAX] = (double)omax;
+}
+
+// load at a 32-bit byte offset from a block-uniform base (SGPR base + VGPR offset addressing)
+__device__ __forceinline__ float ldg_b(const float* base, unsigned int byte_off) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(base) + byte_off);
+}
+
+struct IntAcc {
+  long long n;
+  double sm, ss;
+  float omin, omax, mmin, mmax;
+};
+
+__device__ __forceinline__ void int_acc(IntAcc& a, float v, bool in) {
+  const float m = v * (in ? 1.0f : 0.0f);
+  a.mmin = fminf(a.mmin, m);
+  a.mmax = fmaxf(a.mmax, m);
+  if (in) {
+    a.n += 1;
+    a.sm += (double)v;
+    a.ss += (double)v * (double)v;
+    a.omin = fminf(a.omin, v);
+    a.omax = fmaxf(a.omax, v);
+  }
+}
+
+__global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ labels,
+                                                  const float* __restrict__ corr, int C, int H,
+                                                  int W, int max_label, int F,
+                                                  const cpx_object* __restrict__ objects,
+                                                  const cpx_fov_objects* __restrict__ hdr,
+                                                  const long long* __restrict__ crop_off,
+                                                  unsigned char* __restrict__ scratch,
+                                                  long long scratch_per_fov,
+                                                  long long* __restrict__ raws,
+                                                  int* __restrict__ obj_next,
+                                                  double* __restrict__ feats) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned int* M = reinterpret_cast<unsigned int*>(smem);
   unsigned int* Bd = M + kShapeW;
-  __shared__ long long red[6][kST / 64];
-  __shared__ int redi[3][kST / 64];
-  const int fov = blockIdx.y;
-  const int nobj = hdr[fov].n_objects;
-  const int* lab = labels + (long long)fov * H * W;
-  for (int k = blockIdx.x; k < nobj; k += gridDim.x) {
+  __shared__ long long red[6][kOT / 64];
+  __shared__ int redi[3][kOT / 64];
+  __shared__ double sd_[2][2][kOT / 64];  // [channel parity]: no barrier before the next channel's
+  __shared__ long long sn_[2][kOT / 64];   // partials overwrite them
+  __shared__ float sf_[2][4][kOT / 64];
+  __shared__ int s_code;
+  const int fov = blockIdx.y, B = gridDim.y;
+  const long long N = (long long)H * W;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int q_fov = fov, q_visited = 0;  // thread 0's queue position (glcm_grab: own FOV first, then
+  while (true) {                    // the next ones, each FOV at most once)
+    __syncthreads();  // the previous object's LDS reads are done before s_code / M change
+    if (threadIdx.x == 0) s_code = glcm_grab(q_fov, q_visited, B, 1, hdr, obj_next);
+    __syncthreads();
+    const int code = __builtin_amdgcn_readfirstlane(s_code);  // block-uniform: scalar registers
+    if (code < 0) break;
+    const int fov = code >> 20, k = code & 0xfffff;
+    const int* lab = labels + (long long)fov * N;
     const cpx_object o = objects[(long long)fov * max_label + k];
-    if (!shape_fits(o)) continue;
+    if (!shape_fits(o)) continue;  // shape and texture both in the fallback kernels
+    shape_mask<kOT>(lab, H, W, o, M);
     __syncthreads();
-    shape_mask<kST>(lab, H, W, o, M);
-    __syncthreads();
-    shape_sums<kST>(o, M, Bd, red, redi, raws + ((long long)fov * max_label + k) * kShapeRaw);
+    shape_sums<kOT>(o, M, Bd, red, redi, raws + ((long long)fov * max_label + k) * kShapeRaw);
+    const long long off = crop_off[(long long)fov * max_label + k];
+    if (off < 0) continue;  // texture not staged: fallback kernel (block-uniform)
+    const int r0 = o.bbox[0], c0 = o.bbox[1];
+    const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
+    const int wpr = (bw + 4 + 31) >> 5;
+    const int bwp = crop_stride(bw);
+    const int ng = bh * bwp / 4;  // 4-pixel groups (bwp % 4 == 0: a group never spans rows)
+    const long long cbytes = crop_bytes(bh, bw);
+    // group descriptors of the register-held groups, the same for every channel: bbox offset of
+    // the group's first pixel (< 2^24: shape_fits bounds bh by 4092 and the launcher W by 4096)
+    // | member bits << 24 | valid pixels (1..4) << 28
+    unsigned int gd[kOG];
+#pragma unroll
+    for (int i = 0; i < kOG; ++i) gd[i] = group_desc(M, wpr, bw, bwp, W, min(threadIdx.x + i * kOT, ng - 1));
+    for (int ch = 0; ch < C; ++ch) {
+      const float* img = corr + ((long long)fov * C + ch) * N + (long long)r0 * W + c0;
+      IntAcc a{0, 0.0, 0.0, INFINITY, -INFINITY, INFINITY, -INFINITY};
+      float v[kOG][4];
+      // opaque per channel: keeps the compiler from hoisting every load's offset out of the
+      // channel loop (4 * kOG more VGPRs live across it)
+#pragma unroll
+      for (int i = 0; i < kOG; ++i) asm volatile("" : "+v"(gd[i]));
+#pragma unroll
+      for (int i = 0; i < kOG; ++i) {
+        const unsigned int o0 = gd[i] & 0xffffffu, nv = gd[i] >> 28;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[i][u] = ldg_b(img, 4u * (o0 + min((unsigned int)u, nv - 1u)));
+      }
+#pragma unroll
+      for (int i = 0; i < kOG; ++i) {
+        if ((int)threadIdx.x + i * kOT >= ng) continue;
+        const unsigned int mb = (gd[i] >> 24) & 15u, nv = gd[i] >> 28;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if ((unsigned int)u < nv) int_acc(a, v[i][u], (mb >> u) & 1u);
+      }
+      // groups past the register-held ones (large bboxes) are read twice; the block's working
+      // set (one channel of one bbox) stays in L2 between the two passes
+      for (int g = threadIdx.x + kOG * kOT; g < ng; g += kOT) {
+        const unsigned int d = group_desc(M, wpr, bw, bwp, W, g);
+        const unsigned int o0 = d & 0xffffffu, mb = (d >> 24) & 15u, nv = d >> 28;
+        float w4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) w4[u] = ldg_b(img, 4u * (o0 + min((unsigned int)u, nv - 1u)));
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if ((unsigned int)u < nv) int_acc(a, w4[u], (mb >> u) & 1u);
+      }
+      a.n = wave_sum(a.n);
+      a.sm = wave_sum(a.sm);
+      a.ss = wave_sum(a.ss);
+      a.omin = wave_min(a.omin);
+      a.omax = wave_max(a.omax);
+      a.mmin = wave_min(a.mmin);
+      a.mmax = wave_max(a.mmax);
+      long long* sn = sn_[ch & 1];
+      double(*sd)[kOT / 64] = sd_[ch & 1];
+      float(*sf)[kOT / 64] = sf_[ch & 1];
+      if (lane == 0) {
+        sn[wid] = a.n;
+        sd[0][wid] = a.sm;
+        sd[1][wid] = a.ss;
+        sf[0][wid] = a.omin;
+        sf[1][wid] = a.omax;
+        sf[2][wid] = a.mmin;
+        sf[3][wid] = a.mmax;
+      }
+      __syncthreads();
+      // every thread needs only the crop range; thread 0 finishes the Intensity columns
+      float mmin = sf[2][0], mmax = sf[3][0];
+#pragma unroll
+      for (int w = 1; w < kOT / 64; ++w) {
+        mmin = fminf(mmin, sf[2][w]);
+        mmax = fmaxf(mmax, sf[3][w]);
+      }
+      if (threadIdx.x == 0) {
+        long long n = 0;
+        double sm = 0.0, ss = 0.0;
+        float omin = INFINITY, omax = -INFINITY;
+        for (int w = 0; w < kOT / 64; ++w) {
+          n += sn[w];
+          sm += sd[0][w];
+          ss += sd[1][w];
+          omin = fminf(omin, sf[0][w]);
+          omax = fmaxf(omax, sf[1][w]);
+        }
+        int_finish(feats + ((long long)fov * max_label + k) * F + CPX_N_SHAPE +
+                       (long long)ch * CPX_FEATURES_PER_CHANNEL, n, sm, ss, omin, omax);
+      }
+      const float rng = mmax - mmin;
+      const bool flat = !(mmax != mmin);
+      unsigned char* dst = scratch + (long long)fov * scratch_per_fov + off + (long long)ch * cbytes;
+      // the crop at the padded row stride (pad bytes 0), one 32-bit store per 4-pixel group
+#pragma unroll
+      for (int i = 0; i < kOG; ++i) {
+        const int g = threadIdx.x + i * kOT;
+        if (g >= ng) continue;
+        const unsigned int mb = (gd[i] >> 24) & 15u, nv = gd[i] >> 28;
+        unsigned int word = 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const unsigned int q = (unsigned int)quantize(v[i][u], (mb >> u) & 1u, mmin, rng, flat);
+          word |= ((unsigned int)u < nv ? q : 0u) << (8 * u);
+        }
+        *reinterpret_cast<unsigned int*>(dst + 4 * g) = word;
+      }
+      for (int g = threadIdx.x + kOG * kOT; g < ng; g += kOT) {
+        const unsigned int d = group_desc(M, wpr, bw, bwp, W, g);
+        const unsigned int o0 = d & 0xffffffu, mb = (d >> 24) & 15u, nv = d >> 28;
+        unsigned int word = 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float x = ldg_b(img, 4u * (o0 + min((unsigned int)u, nv - 1u)));
+          const unsigned int q = (unsigned int)quantize(x, (mb >> u) & 1u, mmin, rng, flat);
+          word |= ((unsigned int)u < nv ? q : 0u) << (8 * u);
+        }
+        *reinterpret_cast<unsigned int*>(dst + 4 * g) = word;
+      }
+    }
   }
 }
 
@@ -887,24 +936,26 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   static_assert(2 * kRedW * kTT <= kTabW, "reduction scratch inside the table");
   const size_t lds_s = sizeof(unsigned int) * 2 * kShapeW;
   if (!attr) {
-    CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_shape_fast,
+    CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_obj_stage,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_s));
     attr = true;
   }
   // workspace: crop offsets [B][max_label] + scratch (2 bytes per pixel-channel per FOV)
   const long long per_fov = ((2LL * H * W * C + 255) / 256) * 256;
-  // + one GLCM work-queue counter per FOV (zeroed by k_crop_offsets) + the fallback lists
+  // + one GLCM and one k_obj_stage work-queue counter per FOV (zeroed by k_crop_offsets) + the
+  // fallback lists
   // + the AreaShape raw sums [B][max_label][kShapeRaw]
-  const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + sizeof(int) * (size_t)B * 3 +
+  const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + sizeof(int) * (size_t)B * 4 +
                              sizeof(int) * 2 * (size_t)B * max_label + 255) / 256) * 256;
   const size_t raw_bytes = ((sizeof(long long) * kShapeRaw * (size_t)B * max_label + 255) / 256) * 256;
   unsigned char* ws = (unsigned char*)cpx_ws(ctx, WS_MISC, off_bytes + raw_bytes + (size_t)B * per_fov + 256);  // +256: crop read slack
   if (!ws) return CPX_ERR_OOM;
   CPX_REQUIRE(B < 2048 && (long long)max_label * C < (1 << 20), CPX_ERR_SHAPE,
               "GLCM queue codes hold fov < 2048 and items < 2^20");
+  CPX_REQUIRE(W <= 4096, CPX_ERR_SHAPE, "k_obj_stage packs bbox offsets (bh <= 4092) x W in 24 bits");
   long long* crop_off = (long long*)ws;
-  int* glcm_next = (int*)(crop_off + (size_t)B * max_label);
-  fb->n_shape = glcm_next + B;
+  int* glcm_next = (int*)(crop_off + (size_t)B * max_label);  // + k_obj_stage's queues at B
+  fb->n_shape = glcm_next + 2 * B;
   fb->n_tex = fb->n_shape + B;
   fb->shape = fb->n_tex + B;
   fb->tex = fb->shape + (size_t)B * max_label;
@@ -913,33 +964,21 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   hipLaunchKernelGGL(k_crop_offsets, dim3(B), dim3(1024), 0, ctx->stream, C, max_label,
                      objects_dev, hdr_dev, per_fov, crop_off, glcm_next, *fb);
   CPX_CHECK_LAUNCH("k_crop_offsets");
-  // fork: the fallback kernels (a few, the largest objects, each one long block) run on the side
-  // stream beside the fast path instead of as a serial tail after it
-  if (fallback) {
-    CPX_CHECK_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
-    CPX_CHECK_HIP(hipStreamWaitEvent(ctx->side_stream, ctx->ev_fork, 0));
-    const int rc = fallback(ctx, ctx->side_stream, *fb, fallback_arg);
-    if (rc) return rc;
-    CPX_CHECK_HIP(hipEventRecord(ctx->ev_join, ctx->side_stream));
-  }
-  const int per_fov_s = std::max(1, std::min(max_label, (8 * ctx->n_cu + B - 1) / B));
-  hipLaunchKernelGGL(k_shape_fast, dim3(per_fov_s, B), dim3(kST), lds_s, ctx->stream,
-                     (const int*)labels_dev, H, W, max_label, objects_dev, hdr_dev, raws);
-  CPX_CHECK_LAUNCH("k_shape_fast");
+  const int per_fov_o = std::max(1, std::min(max_label, (2 * ctx->n_cu + B - 1) / B));  // resident
+  hipLaunchKernelGGL(k_obj_stage, dim3(per_fov_o, B), dim3(kOT), lds_s, ctx->stream,
+                     (const int*)labels_dev, corr_dev, C, H, W, max_label, F, objects_dev, hdr_dev,
+                     (const long long*)crop_off, scratch, per_fov, raws, glcm_next + B, feats_dev);
+  CPX_CHECK_LAUNCH("k_obj_stage");
   hipLaunchKernelGGL(k_shape_props, dim3(cpx_div_up(max_label, 256), B), dim3(256), 0, ctx->stream,
                      max_label, F, objects_dev, hdr_dev, (const long long*)raws, feats_dev);
   CPX_CHECK_LAUNCH("k_shape_props");
-  const int per_fov_a = std::max(1, std::min(max_label * C, (16 * ctx->n_cu + B - 1) / B));
-  hipLaunchKernelGGL(k_tex_stage, dim3(per_fov_a, B), dim3(kAT), 0, ctx->stream,
-                     (const int*)labels_dev, corr_dev, C, H, W, max_label, F, objects_dev, hdr_dev,
-                     (const long long*)crop_off, scratch, per_fov, feats_dev);
-  CPX_CHECK_LAUNCH("k_tex_stage");
   const int per_fov_t = std::max(1, std::min(max_label * C, (ctx->n_cu + B - 1) / B));
   hipLaunchKernelGGL(k_tex_glcm, dim3(per_fov_t, B), dim3(kTT), 0, ctx->stream, C, max_label,
                      F, objects_dev, hdr_dev, (const long long*)crop_off,
                      (const unsigned char*)scratch, per_fov, glcm_next, feats_dev);
   CPX_CHECK_LAUNCH("k_tex_glcm");
-  if (fallback) CPX_CHECK_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // join
+  // the fallback kernels (the few largest objects, one long block each) as the tail
+  if (fallback) return fallback(ctx, ctx->stream, *fb, fallback_arg);
   return CPX_OK;
 }
 

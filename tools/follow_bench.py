@@ -1,6 +1,6 @@
 """Same-box timing of the segmentation post-processing (cpx_seg_masks) on the bench's own
 network outputs: 32 FOVs of the synthetic plate through CPnet once, then the masks call timed
-with HIP events.  Tuning knobs are read by libcpx from the environment (CPX_FOLLOW_CAP)."""
+with HIP events; every repetition's labels are compared with the first (determinism)."""
 import json
 import os
 import sys
@@ -28,16 +28,21 @@ def main():
     torch.cuda.synchronize()
     seg = pipe.seg
     lab = pipe.labels["Nuclei"]
-    ts = []
-    for i in range(4):
+    ts, n_final, same = [], [], []
+    ref = None
+    for i in range(int(os.environ.get("REPS", "4"))):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         seg.postprocess(lab)
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
-    st = seg.seg_stats()
-    print(json.dumps({"cap": os.environ.get("CPX_FOLLOW_CAP"), "seg_post_ms": ts, "n_final": int(st["n_final"].sum())}))
+        n_final.append(int(seg.seg_stats()["n_final"].sum()))
+        if ref is None:
+            ref = lab.clone()
+        else:  # labels of every repetition vs the first: pixels that differ
+            same.append(int((lab != ref).sum().item()))
+    print(json.dumps({"seg_post_ms": ts, "n_final": n_final, "label_px_diff_vs_first": same}))
 
 
 if __name__ == "__main__":

@@ -26,8 +26,9 @@ FAMILIES = [
                "elementwise", "reduce_kernel", "naive_conv")),
     ("seg_post", ("k_seg_average", "k_dyn_", "k_seed_", "k_assign", "k_relabel", "k_flow_error",
                   "k_apply_bad", "k_count_bad", "k_upsample", "k_lab2idx", "k_fill_")),
-    ("objects_features", ("k_edt_", "k_ws_", "k_stats_init", "k_label_stats", "k_objects_finalize",
-                          "k_crop_offsets", "k_shape", "k_tex_", "k_intensity_texture", "k_crops")),
+    ("cells", ("k_edt_", "k_ws_")),
+    ("features", ("k_stats_init", "k_label_stats", "k_objects_finalize",
+                  "k_crop_offsets", "k_obj_stage", "k_shape", "k_tex_", "k_intensity_texture", "k_crops")),
 ]
 
 

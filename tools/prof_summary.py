@@ -20,6 +20,8 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--md", action="store_true")
+    ap.add_argument("--series", default=None,
+                    help="also list the per-dispatch durations (us) of this kernel in the last step")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -47,6 +49,11 @@ def main():
         else:
             print(f"{k:70s} calls/step={c / n_steps:6.1f} avg_us={t / c:9.1f} us/step={t / n_steps:9.1f} {100 * t / tot:5.1f}%")
     print(f"total kernel time per step: {tot / n_steps / 1e3:.3f} ms over {len(sel)} dispatches")
+    if a.series and len(starts) >= 2:
+        last = rows[starts[-2]: starts[-1]]
+        ds = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+              for r in last if a.series in r["Kernel_Name"]]
+        print(f"\n`{a.series}` dispatches of one step (us): " + " ".join(f"{d:.0f}" for d in ds))
 
 
 if __name__ == "__main__":
