@@ -77,6 +77,8 @@ class FovResults:
 
 
 class FovPipeline:
+    _copy_streams: dict = {}
+
     def __init__(self, dev: Device, cfg: PipelineConfig, illum: np.ndarray | None):
         self.dev, self.cfg = dev, cfg
         B, C, H, W = cfg.batch, cfg.C, cfg.H, cfg.W
@@ -110,7 +112,13 @@ class FovPipeline:
             "objects": {s: torch.empty(56 * B * ML, dtype=torch.uint8, pin_memory=True) for s in OBJECT_SETS},
             "feats": {s: torch.empty(B * ML * self.F, dtype=torch.float64, pin_memory=True) for s in OBJECT_SETS},
             "seg_stats": torch.empty(self.seg.stats.shape, dtype=self.seg.stats.dtype, pin_memory=True)}
-        self._copy_stream = torch.cuda.Stream(device=td)
+        # one result-copy stream per device, shared by its pipelines: a process has only
+        # GPU_MAX_HW_QUEUES (4) hardware queues, and streams beyond that share one, which
+        # serialises two pipelines' kernels behind each other
+        key = torch.device(td).index
+        if key not in FovPipeline._copy_streams:
+            FovPipeline._copy_streams[key] = torch.cuda.Stream(device=td)
+        self._copy_stream = FovPipeline._copy_streams[key]
         self._step = 0
         self._use_slot(0)
         self.crops = None

@@ -23,6 +23,8 @@ from .cpnet_fused import FusedCPnet
 from .device import Device, _ptr
 
 DIAM_MEAN = {"nuclei": 17.0, "cyto": 30.0, "cyto2": 30.0, "cyto3": 30.0}
+_capture_streams: dict = {}  # device index -> CPnet warm-up / graph-capture stream
+
 CELLPOSE_MODEL = "nuclei"  # Cellpose_GPU_s3fs.py:28
 DIAMETER = 100.0           # Cellpose_GPU_s3fs.py:143
 BSIZE = 224
@@ -159,14 +161,19 @@ class Segmenter:
                 if self.layout == 1 else self._forward().contiguous()
             return
         if self.graph is None:
-            s = torch.cuda.Stream(self.dev.torch_device)
-            s.wait_stream(torch.cuda.current_stream(self.dev.torch_device))
+            # one warm-up / capture stream per device for every Segmenter (each extra stream
+            # holds one of the process's few hardware queues; see FovPipeline._copy_streams)
+            td = self.dev.torch_device
+            if td.index not in _capture_streams:
+                _capture_streams[td.index] = torch.cuda.Stream(td)
+            s = _capture_streams[td.index]
+            s.wait_stream(torch.cuda.current_stream(td))
             with torch.cuda.stream(s):
                 for _ in range(2):
                     self._forward()
-            torch.cuda.current_stream(self.dev.torch_device).wait_stream(s)
+            torch.cuda.current_stream(td).wait_stream(s)
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, stream=s):
                 out = self._forward()
                 out = out.contiguous(memory_format=torch.channels_last) if self.layout == 1 else out.contiguous()
             self.net_out = out

@@ -85,6 +85,14 @@ int cpx_set_stream(cpx_ctx* ctx, void* hip_stream) {
   CPX_REQUIRE(ctx != nullptr, CPX_ERR_ARG, "cpx_set_stream: ctx is NULL");
   // NULL selects the legacy default stream (torch's default stream handle is 0)
   ctx->stream = (hipStream_t)hip_stream;
+  // the context's own stream is released once the caller supplies one: idle streams still hold
+  // one of the process's GPU_MAX_HW_QUEUES hardware-queue slots, and streams beyond that share
+  // queues (and serialise)
+  if (ctx->own_stream && ctx->stream != ctx->own_stream) {
+    (void)hipStreamSynchronize(ctx->own_stream);
+    (void)hipStreamDestroy(ctx->own_stream);
+    ctx->own_stream = nullptr;
+  }
   return CPX_OK;
 }
 

@@ -141,8 +141,9 @@ void cpx_destroy(cpx_ctx* ctx);
 /* Message of the last error on this thread ("" if none). */
 const char* cpx_last_error(void);
 /* Enqueue all further work on `hip_stream` (a hipStream_t; NULL = the legacy default stream).
- * Until the first call the context uses a private non-blocking stream.  The Python host passes
- * torch's current stream so allocations and kernels stay ordered.                          */
+ * Until the first call the context uses a private non-blocking stream, which the first call
+ * releases.  The Python host passes torch's current stream so allocations and kernels stay
+ * ordered.                                                                                  */
 int cpx_set_stream(cpx_ctx* ctx, void* hip_stream);
 int cpx_sync(cpx_ctx* ctx);
 /* Pre-size internal workspaces (so a later hipGraph capture performs no allocation). */
