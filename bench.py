@@ -31,9 +31,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=32, help="FOVs per step per GPU (384-well plate = 12 steps)")
-    ap.add_argument("--pool", type=int, default=12,
-                    help="distinct synthetic batches cycled per GPU (12 x 32 = the 384 wells of configs[1])")
+    ap.add_argument("--batch", type=int, default=48, help="FOVs per step per GPU (384-well plate = 8 steps)")
+    ap.add_argument("--pool", type=int, default=8,
+                    help="distinct synthetic batches cycled per GPU (8 x 48 = the 384 wells of configs[1])")
     ap.add_argument("--size", type=int, default=2080)
     ap.add_argument("--channels", type=int, default=5)
     ap.add_argument("--weights", default=None, help="CPnet state_dict (default: seeded random init)")
@@ -101,10 +101,10 @@ def main():
     # by the rank's own FOV keys, so ranks never share inputs and exchange nothing
     mine = shard.shard(shard.plate_fovs(n_wells=384), rank, world)
     if Z > 1:
-        pool = [synth_zstack(B, C, Z, H, W, td, seed=shard.fov_seed(mine[(i * B) % len(mine)]))
+        pool = [synth_zstack(B, C, Z, H, W, td, seed=shard.fov_seed(mine[(i * B) % len(mine)]) + 7919 * i)
                 for i in range(a.pool)]
-    else:
-        pool = [synth_fovs(B, C, H, W, td, seed=shard.fov_seed(mine[(i * B) % len(mine)]))
+    else:  # (+ 7919 i: distinct batches even when a rank's wells wrap around)
+        pool = [synth_fovs(B, C, H, W, td, seed=shard.fov_seed(mine[(i * B) % len(mine)]) + 7919 * i)
                 for i in range(a.pool)]
 
     def run_step(i):

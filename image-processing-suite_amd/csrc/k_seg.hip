@@ -806,19 +806,24 @@ __global__ __launch_bounds__(kT) void k_apply_newlab(int Dy, int Dx, DynBufs d) 
 // iterations in fp64, normalised central differences, mean squared difference to dP / 5.
 //
 // k_flow_error_lds: one block per mask (dynamic queue over all masks of the batch).  The
-// diffusion grid T ((bh+2) x (bw+2) fp64, zero outside the mask, padded below to whole strips)
-// lives in LDS as ONE buffer: a work unit is 8 consecutive rows of one column; the thread that
-// owns it slides a 3 x 3 window down the unit (3 LDS reads per row instead of 9 per pixel),
-// keeps the 8 new values in registers and writes them back after a barrier.  Every thread owns
-// up to U units (consecutive threads: consecutive columns, so LDS accesses are conflict-free).
+// diffusion grid T ((bh+2) x (bw+2) fp64 at an even row stride, zero outside the mask) lives in
+// LDS as ONE buffer: a work unit is kFeKS consecutive rows of two adjacent columns (X, X + 1),
+// X odd; the thread that owns it slides a 3 x 4 window down the unit (two 16-byte LDS reads per
+// row for two cells, instead of three 8-byte reads per cell), keeps the new values in registers
+// and writes them back after a barrier.  Every thread owns up to U units (consecutive threads:
+// consecutive column pairs).
 // Sums keep the reference's term order; rows are computed unconditionally (compile-time loop)
 // and only mask cells are written.
 constexpr int kFeKS = 12;
 static_assert(kFeKS <= 32, "unit mask bits");
 
+// the grid's row stride: bw + 2 columns (zero border) rounded up to even, so a column pair
+// (2m, 2m + 1) is one 16-byte LDS word
+__host__ __device__ inline int fe_stride(int bw) { return (bw + 3) & ~1; }
 __host__ __device__ inline bool fe_fits(int bh, int bw, int threads, int units, int cells) {
   const int nsr = (bh + kFeKS - 1) / kFeKS;
-  return (long long)(bh + 2) * (bw + 2) <= cells && (long long)bw * nsr <= (long long)threads * units;
+  return (long long)(bh + 2) * fe_stride(bw) <= cells &&
+         (long long)((bw + 1) / 2) * nsr <= (long long)threads * units;
 }
 
 // exclusive prefix of the per-FOV object counts (queue item -> (fov, object))
@@ -838,7 +843,7 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
     const int* __restrict__ m0, const float2* __restrict__ dpf, int Dy, int Dx, int B, int max_label,
     const cpx_object* __restrict__ objects, const int* __restrict__ off, int* __restrict__ ctr,
     int lo_threads, int lo_units, int lo_cells, double thr, unsigned char* __restrict__ bad) {
-  __shared__ double T[CELLS];
+  __shared__ __attribute__((aligned(16))) double T[CELLS];
   __shared__ double sred[THREADS / 64][2];
   __shared__ unsigned long long sbest[THREADS / 64];
   __shared__ double smed[2];
@@ -863,8 +868,7 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
     if (!fe_fits(bh, bw, THREADS, U, CELLS)) continue;
     if (lo_threads > 0 && fe_fits(bh, bw, lo_threads, lo_units, lo_cells)) continue;
     const int nsr = (bh + kFeKS - 1) / kFeKS;
-    const int ly = bh + 2, lx = bw + 2;
-    const int nunits = bw * nsr;
+    const int ly = bh + 2;
     const int* lab = m0 + (long long)fov * n;
     // ---- medians of the pixel coordinates (row / column counts in the T area, as ints)
     int* rowc = reinterpret_cast<int*>(T);
@@ -915,81 +919,92 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
     const int pbest = (int)(bsel & 0xffffffffu);
     const int ym = pbest / bw + 1, xm = pbest % bw + 1;
     const int niter = 2 * ((bw - 1) + (bh - 1));  // 2 * (ptp(x) + ptp(y))
-    // ---- this thread's units: column X, rows Y0 .. Y0 + 7
+    const int lxp = fe_stride(bw);  // row stride of T (lx = bw + 2 columns used)
+    const int ncp = (bw + 1) / 2;   // column pairs (interior columns 2m + 1, 2m + 2)
+    // ---- this thread's units: columns X, X + 1 (X = 2m + 1), rows Y0 .. Y0 + kFeKS - 1
     int ux[U], uy0[U], ujc[U];
-    unsigned int um[U];
+    unsigned int um[U][2];
 #pragma unroll
     for (int i = 0; i < U; ++i) {
       const int u = tid + i * THREADS;
-      um[i] = 0u;
+      um[i][0] = um[i][1] = 0u;
       ux[i] = 1;
       uy0[i] = 1;
       ujc[i] = -1;
-      if (u < nunits) {
-        const int X = u % bw + 1, Y0 = 1 + (u / bw) * kFeKS;
+      if (u < ncp * nsr) {
+        const int X = 2 * (u % ncp) + 1, Y0 = 1 + (u / ncp) * kFeKS;
         ux[i] = X;
         uy0[i] = Y0;
-        unsigned int m = 0u;
-        for (int j = 0; j < kFeKS && Y0 + j <= bh; ++j)
-          if (lab[(long long)(r0 + Y0 - 1 + j) * Dx + c0 + X - 1] == L) m |= 1u << j;
-        um[i] = m;
-        if (X == xm && ym >= Y0 && ym < Y0 + kFeKS) ujc[i] = ym - Y0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (X + h > bw) continue;  // bw odd: the last pair's second column is the border
+          unsigned int m = 0u;
+          for (int j = 0; j < kFeKS && Y0 + j <= bh; ++j)
+            if (lab[(long long)(r0 + Y0 - 1 + j) * Dx + c0 + X + h - 1] == L) m |= 1u << j;
+          um[i][h] = m;
+          if (X + h == xm && ym >= Y0 && ym < Y0 + kFeKS) ujc[i] = 2 * (ym - Y0) + h;
+        }
       }
     }
     __syncthreads();  // rowc / colc / sbest reads done before T is cleared
-    for (int i = tid; i < ly * lx; i += THREADS) T[i] = 0.0;
+    for (int i = tid; i < ly * lxp; i += THREADS) T[i] = 0.0;
     __syncthreads();
-    if (tid == 0 && niter > 0) T[ym * lx + xm] = 1.0;  // the first iteration's T[centre] += 1
+    if (tid == 0 && niter > 0) T[ym * lxp + xm] = 1.0;  // the first iteration's T[centre] += 1
     __syncthreads();
-    double nv[U][kFeKS];
-    const int cidx = ym * lx + xm;
+    double nv[U][2][kFeKS];
+    const int cidx = ym * lxp + xm;
     bool cown = false;  // this thread owns the centre cell
 #pragma unroll
     for (int i = 0; i < U; ++i)
       if (ujc[i] >= 0) cown = true;
+    const double2* T2 = reinterpret_cast<const double2*>(T);
     for (int it = 0; it < niter; ++it) {
 #pragma unroll
       for (int i = 0; i < U; ++i) {
-        if (!um[i]) continue;  // no mask cell in this unit (or no unit)
-        // element offsets of the unit's rows; the opaque base keeps the compiler from holding
-        // every row address of every unit across the iteration loop (it spilled), and rows
-        // past the object's last row read the zero border row (clamped): their sums are
+        if (!(um[i][0] | um[i][1])) continue;  // no mask cell in this unit (or no unit)
+        // double2 offsets of the unit's rows (columns X - 1 .. X + 2 = two 16-byte words); the
+        // opaque base keeps the compiler from holding every row address across the loop, and
+        // rows past the object's last row read the zero border row (clamped): their sums are
         // never written
-        int r = (uy0[i] - 1) * lx + ux[i];
-        int rmax = (ly - 1) * lx + ux[i];
+        int r = ((uy0[i] - 1) * lxp + ux[i] - 1) >> 1;
+        int rmax = ((ly - 1) * lxp + ux[i] - 1) >> 1;
+        const int rs = lxp >> 1;
         asm volatile("" : "+v"(r), "+v"(rmax));
-        double ul = T[r - 1], uc = T[r], ur = T[r + 1];
-        r += lx;
-        double cl = T[r - 1], cc = T[r], cr = T[r + 1];
-        r = min(r + lx, rmax);
-        double dl = T[r - 1], dc = T[r], dr = T[r + 1];
+        double2 ua = T2[r], ub = T2[r + 1];
+        r += rs;
+        double2 ca = T2[r], cb = T2[r + 1];
+        r = min(r + rs, rmax);
+        double2 da = T2[r], db = T2[r + 1];
 #pragma unroll
         for (int j = 0; j < kFeKS; ++j) {
-          // the next row's loads are issued before this row's sum (latency hidden); the
+          // the next row's loads are issued before this row's sums (latency hidden); the
           // scheduling barrier keeps the compiler from hoisting more rows (register budget)
-          double nl = 0.0, nc = 0.0, nr = 0.0;
+          double2 na = {0.0, 0.0}, nb = {0.0, 0.0};
           if (j + 1 < kFeKS) {
-            r = min(r + lx, rmax);
-            nl = T[r - 1];
-            nc = T[r];
-            nr = T[r + 1];
+            r = min(r + rs, rmax);
+            na = T2[r];
+            nb = T2[r + 1];
           }
-          nv[i][j] = 1 / 9. * (cc + uc + dc + cl + cr + ul + ur + dl + dr);
-          ul = cl; uc = cc; ur = cr;
-          cl = dl; cc = dc; cr = dr;
-          dl = nl; dc = nc; dr = nr;
+          // column X: l = .x of a, c = .y of a, r = .x of b;  column X + 1: l = a.y, c = b.x, r = b.y
+          nv[i][0][j] = 1 / 9. * (ca.y + ua.y + da.y + ca.x + cb.x + ua.x + ub.x + da.x + db.x);
+          nv[i][1][j] = 1 / 9. * (cb.x + ub.x + db.x + ca.y + cb.y + ua.y + ub.y + da.y + db.y);
+          ua = ca; ub = cb;
+          ca = da; cb = db;
+          da = na; db = nb;
           __builtin_amdgcn_sched_barrier(0);
         }
       }
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < U; ++i) {
-        if (!um[i]) continue;
-        int wb = uy0[i] * lx + ux[i];
+        if (!(um[i][0] | um[i][1])) continue;
+        int wb = uy0[i] * lxp + ux[i];
         asm volatile("" : "+v"(wb));
 #pragma unroll
-        for (int j = 0; j < kFeKS; ++j)
-          if ((um[i] >> j) & 1u) T[wb + j * lx] = nv[i][j];
+        for (int j = 0; j < kFeKS; ++j) {
+          if ((um[i][0] >> j) & 1u) T[wb + j * lxp] = nv[i][0][j];
+          if ((um[i][1] >> j) & 1u) T[wb + j * lxp + 1] = nv[i][1][j];
+        }
       }
       // the next iteration's T[centre] += 1, by the centre's owner after its own store
       if (cown && it + 1 < niter) T[cidx] = T[cidx] + 1.0;
@@ -1000,18 +1015,21 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
     double e0 = 0.0, e1 = 0.0;
 #pragma unroll
     for (int i = 0; i < U; ++i) {
-      for (int j = 0; j < kFeKS; ++j) {
-        if (!((um[i] >> j) & 1u)) continue;
-        const int Y = uy0[i] + j, X = ux[i];
-        const double dy = T[(Y + 1) * lx + X] - T[(Y - 1) * lx + X];
-        const double dx = T[Y * lx + X + 1] - T[Y * lx + X - 1];
-        const double nrm = 1e-20 + sqrt(dy * dy + dx * dx);
-        const double my = dy / nrm, mx = dx / nrm;
-        const float2 f = F[(long long)(r0 + Y - 1) * Dx + c0 + X - 1];
-        const double ty = my - (double)(f.x / 5.0f);
-        const double tx = mx - (double)(f.y / 5.0f);
-        e0 += ty * ty;
-        e1 += tx * tx;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        for (int j = 0; j < kFeKS; ++j) {
+          if (!((um[i][h] >> j) & 1u)) continue;
+          const int Y = uy0[i] + j, X = ux[i] + h;
+          const double dy = T[(Y + 1) * lxp + X] - T[(Y - 1) * lxp + X];
+          const double dx = T[Y * lxp + X + 1] - T[Y * lxp + X - 1];
+          const double nrm = 1e-20 + sqrt(dy * dy + dx * dx);
+          const double my = dy / nrm, mx = dx / nrm;
+          const float2 f = F[(long long)(r0 + Y - 1) * Dx + c0 + X - 1];
+          const double ty = my - (double)(f.x / 5.0f);
+          const double tx = mx - (double)(f.y / 5.0f);
+          e0 += ty * ty;
+          e1 += tx * tx;
+        }
       }
     }
     e0 = wave_sum(e0);
@@ -1533,7 +1551,7 @@ __global__ void k_seed_count(int B, const int* __restrict__ totals, cpx_seg_stat
 constexpr int kFeSmallThreads = 256, kFeSmallCells = 5000;    // 40 KiB: 4 blocks per CU
 constexpr int kFeMidThreads = 512, kFeMidCells = 10176;       // 80 KiB: 2 blocks per CU
 constexpr int kFeLargeThreads = 1024, kFeLargeCells = 20224;  // 158 KiB: 1 block per CU
-constexpr int kFeU = 2;                                        // 12-row units per thread
+constexpr int kFeU = 1;                                        // 2-column x 12-row units per thread
 
 extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx_seg_geom* geom,
                              int H, int W, int niter, double flow_threshold, int min_size,

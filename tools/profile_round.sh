@@ -6,7 +6,7 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/round
-BATCH=${BATCH:-32}  # bench.py's default --batch
+BATCH=${BATCH:-48}  # bench.py's default --batch
 mkdir -p $O
 cd $R
 timeout -k 10 420 python -u bench.py > $O/bench_default.log 2>&1
