@@ -249,12 +249,18 @@ def double_sigmoid_host(x):
 
 
 def read_table(path: str):
-    """Pycyto_pertime.py:19-27: the delimiter (';' or ',') is sniffed from the first 1 KiB."""
+    """Pycyto_pertime.py:19-27: the delimiter (';' or ',') is sniffed from the first 1 KiB.
+    Divergence: where the sniffer cannot decide (narrow tables, whose first 1 KiB holds several
+    lines and a cut one — CellProfiler's wide tables never hit this, the reference would raise
+    csv.Error) the table is read with ','."""
     import pandas as pd
     with open(path, "r", encoding="utf-8") as f:
         text = f.read()
-    dialect = csv.Sniffer().sniff(text[:1024], delimiters=";,")
-    return pd.read_csv(io.StringIO(text), sep=dialect.delimiter)
+    try:
+        sep = csv.Sniffer().sniff(text[:1024], delimiters=";,").delimiter
+    except csv.Error:
+        sep = ","
+    return pd.read_csv(io.StringIO(text), sep=sep)
 
 
 def well_profiles(eng: ProfileEngine, image, nuclei, cells, cytoplasm):
