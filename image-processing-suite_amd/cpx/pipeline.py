@@ -202,7 +202,7 @@ class FovPipeline:
 
     def fetch(self, slot: int | None = None) -> FovResults:
         """Copy one slot's results to the host (default: the last run) and return them.  Waits
-        only for that slot's step (its recorded event), with the copies on a side stream, so a
+        only for that slot's step (its recorded event), with the copies on the device's copy stream, so a
         step enqueued after it keeps the GPU busy meanwhile."""
         from .segment import SEG_STATS_DTYPE
         k = self.cur if slot is None else slot

@@ -253,9 +253,11 @@ __device__ __forceinline__ unsigned long long half_wave_sum_u64(unsigned long lo
 
 // Finish: the four angles' per-thread sums are reduced through LDS in two rounds of two angles
 // (`red` = 2 * kRedW * kTT words of the all-zero table, zeroed again before returning; `tot` =
-// 4 * kRedW u64 of static LDS), then lanes 0-3 evaluate greycoprops for angles 0-3.
+// 4 * kRedW u64 of static LDS), then 4 * kRedW lanes store the item's totals to `raw` for
+// k_glcm_props (greycoprops in fp64 on four lanes here held the block's other 1020 threads at
+// the next barrier).
 __device__ void glcm_finish(const GlcmSums (&S)[4], unsigned int* red, unsigned long long* tot,
-                            int bh, int bw, double* __restrict__ out, long long* pt) {
+                            unsigned long long* __restrict__ raw, long long* pt) {
   const int t = threadIdx.x, lane = t & 63;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -286,43 +288,60 @@ __device__ void glcm_finish(const GlcmSums (&S)[4], unsigned int* red, unsigned 
 #pragma unroll
   for (int k = 0; k < 2 * kRedW; ++k) red[k * kTT + t] = 0u;
   GLCM_MARK(1, pt);
-  if (t < 4) {
-    const int a = t;
-    const int dr = a == 0 ? 0 : a == 2 ? 3 : 2;
-    const int dc = a == 0 ? 3 : a == 1 ? 2 : a == 2 ? 0 : -2;
-    const int rend = bh - dr;
-    const int cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
-    const long long T = (rend > 0 && cend > cbeg) ? (long long)rend * (cend - cbeg) : 0;
-    const unsigned long long* v = tot + a * kRedW;
-    const long long tsi = (long long)v[0], tsj = (long long)v[1], tsii = (long long)v[2],
-                    tsjj = (long long)v[3], tsij = (long long)v[4];
-    const unsigned long long dt = v[5], tas = v[6], ncnt = v[7];
-    const unsigned long long nbg = (unsigned long long)T - ncnt;  // background pairs (0, 0)
-    // the count visited rend * crop_stride(bw) pair slots; the masked ones added hom(0) each
-    const unsigned long long slots = rend > 0 ? (unsigned long long)rend * crop_stride(bw) : 0ull;
-    const unsigned long long hs = v[8] + (v[9] << 32) - (slots - (unsigned long long)T) * kHom.m[0];
-    double con = 0.0, dis = 0.0, hom = 0.0, asmv = 0.0, ene = 0.0, cor = 1.0;
-    if (T > 0) {
-      const double Td = (double)T;
-      con = (double)(tsii + tsjj - 2 * tsij) / Td;
-      dis = (double)dt / Td;
-      hom = ((double)hs * kHomScale) / Td;
-      asmv = (double)(tas + nbg * nbg) / (Td * Td);
-      ene = sqrt(asmv);
-      const long long vi = T * tsii - tsi * tsi;
-      const long long vj = T * tsjj - tsj * tsj;
-      const long long cv = T * tsij - tsi * tsj;
-      const double sdi = sqrt((double)vi) / Td, sdj = sqrt((double)vj) / Td;
-      cor = (sdi < 1e-15 || sdj < 1e-15) ? 1.0 : ((double)cv / (Td * Td)) / (sdi * sdj);
-    }
-    double* o = out + a * CPX_N_TEX_PROPS;
-    o[CPX_TEX_CONTRAST] = con;
-    o[CPX_TEX_DISSIMILARITY] = dis;
-    o[CPX_TEX_HOMOGENEITY] = hom;
-    o[CPX_TEX_ASM] = asmv;
-    o[CPX_TEX_ENERGY] = ene;
-    o[CPX_TEX_CORRELATION] = cor;
+  if (t < 4 * kRedW) raw[t] = tot[t];
+}
+
+// greycoprops from k_tex_glcm's integer totals, one thread per (object, channel, angle) of the
+// items the LDS path measured (staged, <= 65535 px).
+__global__ __launch_bounds__(256) void k_glcm_props(int C, int max_label, int F,
+                                                   const cpx_object* __restrict__ objects,
+                                                   const cpx_fov_objects* __restrict__ hdr,
+                                                   const long long* __restrict__ crop_off,
+                                                   const unsigned long long* __restrict__ raws,
+                                                   double* __restrict__ feats) {
+  const int fov = blockIdx.y;
+  const int id = blockIdx.x * 256 + threadIdx.x;  // (k, ch, angle)
+  const int a = id & 3, item = id >> 2, k = item / C, ch = item - k * C;
+  if (k >= hdr[fov].n_objects) return;
+  const long long ok = (long long)fov * max_label + k;
+  const cpx_object o = objects[ok];
+  const int bh = o.bbox[2] - o.bbox[0], bw = o.bbox[3] - o.bbox[1];
+  if (crop_off[ok] < 0 || bh * bw > 65535) return;  // the fallback kernel measures it
+  const unsigned long long* v = raws + (ok * C + ch) * (4 * kRedW) + a * kRedW;
+  const int dr = a == 0 ? 0 : a == 2 ? 3 : 2;
+  const int dc = a == 0 ? 3 : a == 1 ? 2 : a == 2 ? 0 : -2;
+  const int rend = bh - dr;
+  const int cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
+  const long long T = (rend > 0 && cend > cbeg) ? (long long)rend * (cend - cbeg) : 0;
+  const long long tsi = (long long)v[0], tsj = (long long)v[1], tsii = (long long)v[2],
+                  tsjj = (long long)v[3], tsij = (long long)v[4];
+  const unsigned long long dt = v[5], tas = v[6], ncnt = v[7];
+  const unsigned long long nbg = (unsigned long long)T - ncnt;  // background pairs (0, 0)
+  // the count visited rend * crop_stride(bw) pair slots; the masked ones added hom(0) each
+  const unsigned long long slots = rend > 0 ? (unsigned long long)rend * crop_stride(bw) : 0ull;
+  const unsigned long long hs = v[8] + (v[9] << 32) - (slots - (unsigned long long)T) * kHom.m[0];
+  double con = 0.0, dis = 0.0, hom = 0.0, asmv = 0.0, ene = 0.0, cor = 1.0;
+  if (T > 0) {
+    const double Td = (double)T;
+    con = (double)(tsii + tsjj - 2 * tsij) / Td;
+    dis = (double)dt / Td;
+    hom = ((double)hs * kHomScale) / Td;
+    asmv = (double)(tas + nbg * nbg) / (Td * Td);
+    ene = sqrt(asmv);
+    const long long vi = T * tsii - tsi * tsi;
+    const long long vj = T * tsjj - tsj * tsj;
+    const long long cv = T * tsij - tsi * tsj;
+    const double sdi = sqrt((double)vi) / Td, sdj = sqrt((double)vj) / Td;
+    cor = (sdi < 1e-15 || sdj < 1e-15) ? 1.0 : ((double)cv / (Td * Td)) / (sdi * sdj);
   }
+  double* out = feats + ok * F + CPX_N_SHAPE + (long long)ch * CPX_FEATURES_PER_CHANNEL + CPX_N_INT +
+                a * CPX_N_TEX_PROPS;
+  out[CPX_TEX_CONTRAST] = con;
+  out[CPX_TEX_DISSIMILARITY] = dis;
+  out[CPX_TEX_HOMOGENEITY] = hom;
+  out[CPX_TEX_ASM] = asmv;
+  out[CPX_TEX_ENERGY] = ene;
+  out[CPX_TEX_CORRELATION] = cor;
 }
 
 struct GlcmItem {
@@ -403,7 +422,7 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
                                                  const unsigned char* __restrict__ scratch,
                                                  long long scratch_per_fov,
                                                  int* __restrict__ glcm_next,
-                                                 double* __restrict__ feats) {
+                                                 unsigned long long* __restrict__ glcm_raw) {
   // LDS: table at offset 0 (static, so the atomics' addresses need no base), then the
   // 64 sink words, the reduction totals, the queue codes and the crop
   __shared__ __attribute__((aligned(16))) unsigned int lds[40 * 1024];  // all 160 KiB, static
@@ -423,7 +442,7 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
   }
   __syncthreads();
   // software pipeline: the next item's metadata is loaded and its crop's lines are touched into
-  // L2 while the current item runs its four angles (the crop was written by k_tex_stage, possibly
+  // L2 while the current item runs its four angles (the crop was written by k_obj_stage, possibly
   // on another XCD, so a cold load is HBM/MALL latency); thread 0 grabs the item after that one
   // from the queue during the current item, so the atomic's latency is hidden too.
   GlcmItem cur = glcm_item(s_code[0], C, max_label, objects, crop_off, scratch, scratch_per_fov);
@@ -450,8 +469,7 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
     touched = glcm_touch(cur);
     if (threadIdx.x == 0) ahead = s_code[par] >= 0 ? glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next) : -1;
     if (it.nb <= 0) continue;
-    double* f = feats + ((long long)it.fov * max_label + it.k) * F + CPX_N_SHAPE +
-                (long long)it.ch * CPX_FEATURES_PER_CHANNEL + CPX_N_INT;
+    unsigned long long* f = glcm_raw + (((long long)it.fov * max_label + it.k) * C + it.ch) * (4 * kRedW);
     long long pt = 0;
 #ifdef CPX_GLCM_PROF
     if (threadIdx.x == 0) {
@@ -466,11 +484,11 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
     glcm_angle<1>(it, crop, tab, s_hom, S[1], &pt);
     glcm_angle<2>(it, crop, tab, s_hom, S[2], &pt);
     glcm_angle<3>(it, crop, tab, s_hom, S[3], &pt);
-    glcm_finish(S, tab, s_tot, it.bh, it.bw, f, &pt);
+    glcm_finish(S, tab, s_tot, f, &pt);
     GLCM_MARK(4, &pt);
   }
   // keeps the touch loads alive: never true (C > 0), but the compiler cannot know that
-  if (C < 0 && sink_word + touched == 0x9e3779b9u) feats[0] = 0.0;
+  if (C < 0 && sink_word + touched == 0x9e3779b9u) glcm_raw[0] = 0ull;
 }
 
 // crop slots: per FOV exclusive scan of C * bbox area; objects beyond the scratch capacity or
@@ -948,7 +966,10 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + sizeof(int) * (size_t)B * 4 +
                              sizeof(int) * 2 * (size_t)B * max_label + 255) / 256) * 256;
   const size_t raw_bytes = ((sizeof(long long) * kShapeRaw * (size_t)B * max_label + 255) / 256) * 256;
-  unsigned char* ws = (unsigned char*)cpx_ws(ctx, WS_MISC, off_bytes + raw_bytes + (size_t)B * per_fov + 256);  // +256: crop read slack
+  // + the GLCM integer totals [B][max_label][C][4 angles][kRedW] for k_glcm_props
+  const size_t glcm_bytes = ((sizeof(unsigned long long) * 4 * kRedW * (size_t)B * max_label * C + 255) / 256) * 256;
+  unsigned char* ws = (unsigned char*)cpx_ws(ctx, WS_MISC, off_bytes + raw_bytes + glcm_bytes +
+                                             (size_t)B * per_fov + 256);  // +256: crop read slack
   if (!ws) return CPX_ERR_OOM;
   CPX_REQUIRE(B < 2048 && (long long)max_label * C < (1 << 20), CPX_ERR_SHAPE,
               "GLCM queue codes hold fov < 2048 and items < 2^20");
@@ -960,7 +981,8 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   fb->shape = fb->n_tex + B;
   fb->tex = fb->shape + (size_t)B * max_label;
   long long* raws = (long long*)(ws + off_bytes);
-  unsigned char* scratch = ws + off_bytes + raw_bytes;
+  unsigned long long* glcm_raw = (unsigned long long*)(ws + off_bytes + raw_bytes);
+  unsigned char* scratch = ws + off_bytes + raw_bytes + glcm_bytes;
   hipLaunchKernelGGL(k_crop_offsets, dim3(B), dim3(1024), 0, ctx->stream, C, max_label,
                      objects_dev, hdr_dev, per_fov, crop_off, glcm_next, *fb);
   CPX_CHECK_LAUNCH("k_crop_offsets");
@@ -975,8 +997,12 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   const int per_fov_t = std::max(1, std::min(max_label * C, (ctx->n_cu + B - 1) / B));
   hipLaunchKernelGGL(k_tex_glcm, dim3(per_fov_t, B), dim3(kTT), 0, ctx->stream, C, max_label,
                      F, objects_dev, hdr_dev, (const long long*)crop_off,
-                     (const unsigned char*)scratch, per_fov, glcm_next, feats_dev);
+                     (const unsigned char*)scratch, per_fov, glcm_next, glcm_raw);
   CPX_CHECK_LAUNCH("k_tex_glcm");
+  hipLaunchKernelGGL(k_glcm_props, dim3(cpx_div_up(max_label * C * 4, 256), B), dim3(256), 0, ctx->stream,
+                     C, max_label, F, objects_dev, hdr_dev, (const long long*)crop_off,
+                     (const unsigned long long*)glcm_raw, feats_dev);
+  CPX_CHECK_LAUNCH("k_glcm_props");
   // the fallback kernels (the few largest objects, one long block each) as the tail
   if (fallback) return fallback(ctx, ctx->stream, *fb, fallback_arg);
   return CPX_OK;
