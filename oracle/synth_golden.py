@@ -97,6 +97,37 @@ def labels(seed: int, H: int, W: int, n: int = 30, skip_every: int = 7,
     return lab
 
 
+def boundary_objects(H: int = 2200, W: int = 720) -> np.ndarray:
+    """int32 labels whose objects straddle the feature kernels' fast-path limits (integer test,
+    sheared shapes): a texture bbox just under and just over 65535 px, a 2100 x 30 slanted strip
+    (bbox <= 65535 px but > 4096 membership-mask words: shape and texture fallbacks), a 400 x 400
+    blob (both fallbacks), and small / mid objects around them."""
+    lab = np.zeros((H, W), dtype=np.int32)
+    yy = np.arange(H, dtype=np.int64)[:, None]
+    xx = np.arange(W, dtype=np.int64)[None, :]
+
+    def ellipse(value, cy, cx, ry, rx, shear):
+        dy = yy - cy
+        dx = xx - cx + (shear * dy) // 8
+        inside = dy * dy * (rx * rx) + dx * dx * (ry * ry) <= (rx * rx) * (ry * ry)
+        lab[inside] = value
+
+    ellipse(1, 140, 150, 127, 120, 1)     # bbox 255 x 256 = 65280 px: LDS texture path
+    ellipse(2, 450, 160, 129, 128, 1)     # bbox 259 x 274 > 65535 px: texture fallback
+    ellipse(3, 900, 560, 200, 150, 2)     # bbox 401 x 351: shape + texture fallbacks
+    # slanted strip, rows 60 .. 2159, 6 px of slant, 24-25 px wide
+    y0, y1 = 60, 2160
+    dy = yy - y0
+    left = 640 + (dy * 6) // (y1 - y0)
+    strip = (yy >= y0) & (yy < y1) & (xx >= left) & (xx < left + 24 + (dy % 7 == 0))
+    lab[strip] = 4                        # bbox 2100 x 31: (2104) x 2 words > 4096: fallbacks
+    small = labels(12345, H, W - 120, n=30, rmin=4, rmax=40, skip_every=0)
+    small_vals = np.where(small > 0, small + 10, 0)
+    sub = lab[:, : W - 120]
+    sub[(sub == 0) & (small_vals > 0)] = small_vals[(sub == 0) & (small_vals > 0)]
+    return lab
+
+
 def full_case(seed: int, H: int = 2080, W: int = 2080, C: int = 5, n_blobs: int = 300):
     """The full-size FOV used by the golden QC fixture: C planes + C flat-fields."""
     raw = np.stack([plane(seed * 10 + c, H, W, n_blobs=n_blobs, halo=(c > 0)) for c in range(C)])

@@ -200,6 +200,16 @@ def test_features_match_skimage_golden(dev, golden_dir):
     _feat_close(got, d["feat_expected"])
 
 
+def test_features_boundary_objects_golden(dev, golden_dir):
+    """skimage 0.18.3 golden for objects straddling the LDS fast-path limits: texture bbox just
+    under / over 65535 px, a strip beyond the 4096-word membership mask (both fallbacks although
+    its bbox fits the texture limit), a 401 x 317 blob (tools/make_golden_bigobj.py)."""
+    import test_oracle_golden as tog
+    lab, planes, exp = tog._boundary_case(golden_dir)
+    got = _features(dev, lab, planes)
+    _feat_close(got, exp)
+
+
 def test_features_match_oracle_larger(dev):
     H, W, C = 700, 760, 2
     lab = sg.labels(41, H, W, n=40, rmin=5, rmax=150, skip_every=0)

@@ -105,6 +105,24 @@ def test_features_match_skimage(golden_dir):
     np.testing.assert_allclose(got, exp, rtol=1e-9, atol=1e-12)
 
 
+def _boundary_case(golden_dir):
+    d = np.load(os.path.join(golden_dir, "features_boundary.npz"))
+    H, W, C = int(d["H"]), int(d["W"]), int(d["C"])
+    lab = sg.boundary_objects(H, W)
+    assert int(lab.astype(np.int64).sum()) == int(d["labels_sum"])  # same labels as the generator
+    planes = np.stack([sg.plane(700 + c, H, W, n_blobs=40).astype(np.float32) /
+                       sg.illum(750 + c, H, W, np.float32) for c in range(C)]).astype(np.float32)
+    return lab, planes, d["expected"]
+
+
+def test_features_boundary_objects_match_skimage(golden_dir):
+    """Objects at the feature kernels' fast-path limits (tools/make_golden_bigobj.py)."""
+    lab, planes, exp = _boundary_case(golden_dir)
+    got = orc.features(lab, planes)
+    assert got.shape == exp.shape
+    np.testing.assert_allclose(got, exp, rtol=1e-9, atol=1e-12)
+
+
 def test_synthetic_generator_is_deterministic():
     a = sg.plane(5, 33, 47)
     b = sg.plane(5, 33, 47)
