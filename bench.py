@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--cpnet-precision", choices=("bf16", "fp32"), default="bf16",
                     help="CPnet arithmetic: bf16 native MFMA (default) or fp32 (identical masks to the "
                          "fp32 CPU network on the e2e plates; DESIGN §6)")
+    ap.add_argument("--host-inputs", action="store_true",
+                    help="PCIe-inclusive variant (not the headline): the synthetic batches live in "
+                         "pinned host memory and every step copies its planes to the GPU inside the "
+                         "timed region (on the pipeline's stream, so the other pipeline overlaps it)")
     ap.add_argument("--zstack", type=int, default=0,
                     help="configs[4] variant: Z planes per channel, z-max projected on the GPU "
                          "inside every step (default size 2048); not the headline workload")
@@ -107,12 +111,23 @@ def main():
         pool = [synth_fovs(B, C, H, W, td, seed=shard.fov_seed(mine[(i * B) % len(mine)]) + 7919 * i)
                 for i in range(a.pool)]
 
+    if a.host_inputs:  # pinned host copies of the batches; each pipeline gets its own device planes
+        pool = [x.cpu().pin_memory() for x in pool]
+        for q in pipes:
+            q.raw = torch.empty_like(pool[0], device=td)
+
     def run_step(i):
         """Enqueue step i on pipeline i % P (its stream); returns (pipeline, result slot)."""
         q = pipes[i % len(pipes)]
         with torch.cuda.stream(streams[i % len(pipes)]):
             if Z > 1:  # a5: z-max projection into the pipeline's raw planes, then the hot path
-                q.dev.zmax(pool[i % a.pool], q.raw)
+                src = pool[i % a.pool]
+                if a.host_inputs:
+                    src = src.to(td, non_blocking=True)
+                q.dev.zmax(src, q.raw)
+                slot = q.run()
+            elif a.host_inputs:  # H2D of the step's planes, then the hot path on the same stream
+                q.raw.copy_(pool[i % a.pool], non_blocking=True)
                 slot = q.run()
             else:
                 slot = q.run(pool[i % a.pool])
@@ -166,9 +181,9 @@ def main():
         if Z > 1:
             ez = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             ez[0].record()
-            dev.zmax(pool[i % a.pool], pipe.raw)
+            dev.zmax(pool[i % a.pool].to(td) if a.host_inputs else pool[i % a.pool], pipe.raw)
             ez[1].record()
-        src = pipe.raw if Z > 1 else pool[i % a.pool]
+        src = pipe.raw if (Z > 1 or a.host_inputs) else pool[i % a.pool]
         ev[0].record()
         dev.illum_correct(src, pipe.illum, C, pipe.corr, pipe.stats)
         ev[1].record()
@@ -218,7 +233,7 @@ def main():
         kernels["zmax"] = dict(bound="hbm", work=B * C * N * (2 * Z + 2), ms=sub_ms["zmax"])
 
     # the committed PMC traffic was measured on the headline workload; not valid for variants
-    pmc, pmc_src = pmc_traffic(B) if (Z <= 1 and H == 2080) else ({}, None)
+    pmc, pmc_src = pmc_traffic(B) if (Z <= 1 and H == 2080 and not a.host_inputs) else ({}, None)
 
     def roof(k):
         d = kernels[k]
@@ -263,8 +278,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": f"fp32 planes / fp64 QC+features / {a.cpnet_precision} CPnet",
-        "data": f"synthetic (HBM-resident uint16 plates, Poisson background, Gaussian nuclei + halos; "
-                f"{a.pool} distinct batches = {a.pool * B} distinct FOVs per GPU, cycled)",
+        "data": (f"synthetic ({'pinned-host uint16 plates copied to the GPU inside every step (PCIe-inclusive)' if a.host_inputs else 'HBM-resident uint16 plates'}, "
+                 f"Poisson background, Gaussian nuclei + halos; "
+                 f"{a.pool} distinct batches = {a.pool * B} distinct FOVs per GPU, cycled)"),
         "config": {"workload": ("configs[1]: 384-well plate, 1 FOV/well, 2080x2080x5ch, illum->seg->feat"
                                 if Z <= 1 else
                                 f"configs[4] variant: {H}x{W}x{C}ch x {Z} z-planes, z-max->illum->seg->feat"),
@@ -281,7 +297,8 @@ def main():
         "hbm_copy_measured_GBs": round(copy_gbs, 1),
     }
     if cpu_ctx is not None:
-        line["cpu_baseline"] = cpu_baseline(cpu_ctx, pipe.raw if Z > 1 else pool[0], illum, C, H, W, cfg)
+        line["cpu_baseline"] = cpu_baseline(cpu_ctx, pipe.raw if (Z > 1 or a.host_inputs) else pool[0], illum,
+                                            C, H, W, cfg)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
