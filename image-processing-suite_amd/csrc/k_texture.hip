@@ -827,7 +827,8 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
     const int ng = bh * bwp / 4;  // 4-pixel groups (bwp % 4 == 0: a group never spans rows)
     const long long cbytes = crop_bytes(bh, bw);
     // group descriptors of the register-held groups, the same for every channel: bbox offset of
-    // the group's first pixel (< 2^24: shape_fits bounds bh by 4092 and the launcher W by 4096)
+    // the group's first pixel (< 2^24: shape_fits bounds bh by 4092, and only images with
+    // W <= 4096 stage crops)
     // | member bits << 24 | valid pixels (1..4) << 28
     unsigned int gd[kOG];
 #pragma unroll
@@ -973,7 +974,6 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   if (!ws) return CPX_ERR_OOM;
   CPX_REQUIRE(B < 2048 && (long long)max_label * C < (1 << 20), CPX_ERR_SHAPE,
               "GLCM queue codes hold fov < 2048 and items < 2^20");
-  CPX_REQUIRE(W <= 4096, CPX_ERR_SHAPE, "k_obj_stage packs bbox offsets (bh <= 4092) x W in 24 bits");
   long long* crop_off = (long long*)ws;
   int* glcm_next = (int*)(crop_off + (size_t)B * max_label);  // + k_obj_stage's queues at B
   fb->n_shape = glcm_next + 2 * B;
@@ -983,8 +983,10 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   long long* raws = (long long*)(ws + off_bytes);
   unsigned long long* glcm_raw = (unsigned long long*)(ws + off_bytes + raw_bytes);
   unsigned char* scratch = ws + off_bytes + raw_bytes + glcm_bytes;
+  // k_obj_stage packs a staged crop's bbox offsets (bh <= 4092) x W in 24 bits: wider images
+  // measure texture in the fallback kernel (cap 0: nothing staged)
   hipLaunchKernelGGL(k_crop_offsets, dim3(B), dim3(1024), 0, ctx->stream, C, max_label,
-                     objects_dev, hdr_dev, per_fov, crop_off, glcm_next, *fb);
+                     objects_dev, hdr_dev, W <= 4096 ? per_fov : 0LL, crop_off, glcm_next, *fb);
   CPX_CHECK_LAUNCH("k_crop_offsets");
   const int per_fov_o = std::max(1, std::min(max_label, (2 * ctx->n_cu + B - 1) / B));  // resident
   hipLaunchKernelGGL(k_obj_stage, dim3(per_fov_o, B), dim3(kOT), lds_s, ctx->stream,

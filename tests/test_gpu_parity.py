@@ -210,6 +210,17 @@ def test_features_boundary_objects_golden(dev, golden_dir):
     _feat_close(got, exp)
 
 
+def test_features_wide_image(dev):
+    """W > 4096: crops are not staged (k_obj_stage's 24-bit offsets), texture comes from the
+    fallback kernel, AreaShape still from the LDS path; results as the oracle."""
+    H, W, C = 96, 4160, 2
+    lab = sg.labels(61, H, W, n=12, rmin=5, rmax=40, skip_every=0)
+    planes = np.stack([sg.plane(960 + c, H, W, n_blobs=12).astype(np.float32) /
+                       sg.illum(970 + c, H, W) for c in range(C)]).astype(np.float32)
+    got = _features(dev, lab, planes)
+    _feat_close(got, orc.features(lab, planes))
+
+
 def test_features_match_oracle_larger(dev):
     H, W, C = 700, 760, 2
     lab = sg.labels(41, H, W, n=40, rmin=5, rmax=150, skip_every=0)
