@@ -440,9 +440,15 @@ __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, in
       if (done) continue;
       const int yi = (int)py, xi = (int)px;
       const int y0 = min(Dy - 1, max(0, yi)), x0 = min(Dx - 1, max(0, xi));
-      const int i00 = y0 * Dx + x0;
-      const int dxo = x0 + 1 < Dx ? 1 : 0, dyo = y0 + 1 < Dy ? Dx : 0;
-      const float2 af = I[i00], bf = I[i00 + dxo], cf = I[i00 + dyo], ef = I[i00 + dyo + dxo];
+      // 32-bit byte offsets from the FOV's (block-uniform) field base: SGPR-base + VGPR-offset
+      // loads, no 64-bit address arithmetic per step (the field is < 4 GiB per FOV)
+      const unsigned int b00 = 8u * (unsigned int)(y0 * Dx + x0);
+      const unsigned int bdx = x0 + 1 < Dx ? 8u : 0u, bdy = y0 + 1 < Dy ? 8u * (unsigned int)Dx : 0u;
+      const unsigned char* Ib = reinterpret_cast<const unsigned char*>(I);
+      const float2 af = *reinterpret_cast<const float2*>(Ib + b00);
+      const float2 bf = *reinterpret_cast<const float2*>(Ib + (b00 + bdx));
+      const float2 cf = *reinterpret_cast<const float2*>(Ib + (b00 + bdy));
+      const float2 ef = *reinterpret_cast<const float2*>(Ib + (b00 + bdy + bdx));
       const double2 a = {(double)af.x, (double)af.y}, b = {(double)bf.x, (double)bf.y},
                     c = {(double)cf.x, (double)cf.y}, e = {(double)ef.x, (double)ef.y};
       double vy, vx;
@@ -460,8 +466,9 @@ __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, in
         vy = a.x * (1.0 - yy) * (1.0 - xx) + b.x * (1.0 - yy) * xx + c.x * yy * (1.0 - xx) + e.x * yy * xx;
         vx = a.y * (1.0 - yy) * (1.0 - xx) + b.y * (1.0 - yy) * xx + c.y * yy * (1.0 - xx) + e.y * yy * xx;
       }
-      const float ny = fminf(fLy, fmaxf(0.0f, py + (float)vy));
-      const float nx = fminf(fLx, fmaxf(0.0f, px + (float)vx));
+      // clamp to [0, L - 1] in one v_med3_f32 (= fminf(L, fmaxf(0, .)) for the finite values here)
+      const float ny = __builtin_amdgcn_fmed3f(py + (float)vy, 0.0f, fLy);
+      const float nx = __builtin_amdgcn_fmed3f(px + (float)vx, 0.0f, fLx);
       if (ny == py && nx == px) done = true;  // exact fixed point
       py = ny;
       px = nx;
