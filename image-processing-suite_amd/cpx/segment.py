@@ -161,12 +161,15 @@ class Segmenter:
                 if self.layout == 1 else self._forward().contiguous()
             return
         if self.graph is None:
-            # one warm-up / capture stream per device for every Segmenter (each extra stream
-            # holds one of the process's few hardware queues; see FovPipeline._copy_streams)
+            # warm-up / capture on the caller's stream when it is a side stream (a pipeline's
+            # own), else on one shared stream per device: each extra stream holds one of the
+            # process's few hardware queues (see FovPipeline._copy_streams)
             td = self.dev.torch_device
-            if td.index not in _capture_streams:
-                _capture_streams[td.index] = torch.cuda.Stream(td)
-            s = _capture_streams[td.index]
+            s = torch.cuda.current_stream(td)
+            if s == torch.cuda.default_stream(td):
+                if td.index not in _capture_streams:
+                    _capture_streams[td.index] = torch.cuda.Stream(td)
+                s = _capture_streams[td.index]
             s.wait_stream(torch.cuda.current_stream(td))
             with torch.cuda.stream(s):
                 for _ in range(2):
