@@ -39,9 +39,11 @@ class PipelineConfig:
     model: str = CELLPOSE_MODEL
     diameter: float = DIAMETER
     resample: bool = True            # CellposeModel.eval default: dynamics at full resolution
-    cpnet_precision: str = "bf16"    # "bf16": native MFMA convolutions (headline); "fp32": the
-                                     # same network in fp32 (PyTorch eager), masks identical to
-                                     # the fp32 CPU network on the e2e plates
+    cpnet_precision: str = "f16x3"   # "f16x3": native split-fp16 MFMA kernels at the fp32
+                                     # network's accuracy (the reference's precision: masks and
+                                     # IDs identical to the fp32 CPU network);
+                                     # "bf16": native bf16 MFMA kernels (faster, boundary pixels
+                                     # and IDs differ); "fp32": the eager PyTorch module
     cells: str = "watershed"         # "watershed": marker watershed of the inverted cell channel
                                      # inside the expand_labels(Nuclei, cell_expand) footprint
                                      # (DESIGN.md §7); "expand": Cells = that footprint's labels
@@ -92,10 +94,8 @@ class FovPipeline:
         self.lstats = dev.empty_bytes(64 * B * (ML + 1))
         self.F = n_features(C)
         self.seg = Segmenter(dev, H, W, B, model=cfg.model, diameter=cfg.diameter, weights=cfg.weights,
-                             seed=cfg.seed, use_graph=cfg.use_graph and cfg.cpnet_precision == "bf16",
-                             max_objects=ML, resample=cfg.resample,
-                             net_dtype=torch.bfloat16 if cfg.cpnet_precision == "bf16" else torch.float32,
-                             fused=cfg.cpnet_precision == "bf16")
+                             seed=cfg.seed, use_graph=cfg.use_graph and cfg.cpnet_precision != "fp32",
+                             max_objects=ML, resample=cfg.resample, precision=cfg.cpnet_precision)
         # result slots (device) and their pinned host mirrors
         self._slots = []
         for _ in range(max(1, cfg.slots)):
@@ -105,13 +105,15 @@ class FovPipeline:
                 "objects": {s: dev.empty_bytes(56 * B * ML) for s in OBJECT_SETS},
                 "feats": {s: torch.zeros((B, ML, self.F), dtype=torch.float64, device=td) for s in OBJECT_SETS},
                 "seg_stats": torch.empty_like(self.seg.stats),
+                "cpnet_ovf": torch.zeros(1, dtype=torch.int32, device=td),
                 "event": None})
         self._host = {
             "qc": torch.empty(24 * B * C, dtype=torch.uint8, pin_memory=True),
             "hdr": {s: torch.empty(16 * B, dtype=torch.uint8, pin_memory=True) for s in OBJECT_SETS},
             "objects": {s: torch.empty(56 * B * ML, dtype=torch.uint8, pin_memory=True) for s in OBJECT_SETS},
             "feats": {s: torch.empty(B * ML * self.F, dtype=torch.float64, pin_memory=True) for s in OBJECT_SETS},
-            "seg_stats": torch.empty(self.seg.stats.shape, dtype=self.seg.stats.dtype, pin_memory=True)}
+            "seg_stats": torch.empty(self.seg.stats.shape, dtype=self.seg.stats.dtype, pin_memory=True),
+            "cpnet_ovf": torch.zeros(1, dtype=torch.int32, pin_memory=True)}
         # one result-copy stream per device, shared by its pipelines: a process has only
         # GPU_MAX_HW_QUEUES (4) hardware queues, and streams beyond that share one, which
         # serialises two pipelines' kernels behind each other
@@ -196,6 +198,9 @@ class FovPipeline:
         self.stage_segment()
         self.stage_objects()
         sl["seg_stats"].copy_(self.seg.stats)
+        ovf = self.seg.cpnet_overflow()
+        if ovf is not None:
+            sl["cpnet_ovf"].copy_(ovf)
         sl["event"] = torch.cuda.Event()
         sl["event"].record(stream)
         return k
@@ -213,6 +218,7 @@ class FovPipeline:
         with torch.cuda.stream(cs):
             hb["qc"].copy_(sl["qc"], non_blocking=True)
             hb["seg_stats"].copy_(sl["seg_stats"], non_blocking=True)
+            hb["cpnet_ovf"].copy_(sl["cpnet_ovf"], non_blocking=True)
             for s in OBJECT_SETS:
                 hb["hdr"][s].copy_(sl["hdr"][s], non_blocking=True)
         cs.synchronize()
@@ -235,6 +241,9 @@ class FovPipeline:
             feats[s] = [f[b, : n_b[b]].copy() for b in range(B)]
             objs[s] = [o[b, : n_b[b]].copy() for b in range(B)]
         seg_stats = hb["seg_stats"].numpy().view(SEG_STATS_DTYPE).copy()
+        if int(hb["cpnet_ovf"][0]) != 0:
+            raise RuntimeError("CPnet (f16x3): an activation left the fp16 range (|a| >= 65504); "
+                               "run this plate with cpnet_precision='fp32'")
         if self.cfg.cells == "watershed" and (seg_stats["cells_status"] < 0).any():
             raise RuntimeError("cpx_watershed_cells: the flood did not converge within ws_rounds "
                                f"{self.cfg.ws_rounds} (status {seg_stats['cells_status'].ravel().tolist()})")

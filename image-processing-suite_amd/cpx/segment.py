@@ -20,6 +20,7 @@ from . import _lib
 from ._lib import check
 from .cpnet import build_cpnet
 from .cpnet_fused import FusedCPnet
+from .cpnet_x3 import FusedCPnetX3
 from .device import Device, _ptr
 
 DIAM_MEAN = {"nuclei": 17.0, "cyto": 30.0, "cyto2": 30.0, "cyto3": 30.0}
@@ -115,7 +116,8 @@ class Segmenter:
                  diameter: float = DIAMETER, weights: str | None = None, seed: int = 0,
                  use_graph: bool = True, max_objects: int = 4096, net_dtype=torch.bfloat16,
                  fused: bool = True, resample: bool = RESAMPLE,
-                 niter: int | None = None, flow_threshold: float = FLOW_THRESHOLD, min_size: int = MIN_SIZE):
+                 niter: int | None = None, flow_threshold: float = FLOW_THRESHOLD, min_size: int = MIN_SIZE,
+                 precision: str | None = None):
         self.dev = dev
         self.H, self.W, self.B = H, W, batch
         self.geom = make_geom(H, W, model, diameter)
@@ -125,14 +127,30 @@ class Segmenter:
         self.resample = bool(resample)
         self.niter = default_niter(model, diameter, self.resample) if niter is None else int(niter)
         self.flow_threshold, self.min_size = flow_threshold, min_size
+        # precision: "f16x3" (default: native split-fp16 MFMA kernels at the fp32 network's
+        # accuracy, cpx.cpnet_x3), "bf16" (native bf16 MFMA kernels, cpx.cpnet_fused) or "fp32"
+        # (the eager PyTorch module); net_dtype / fused select the latter two for older callers
+        if precision is None:
+            precision = "bf16" if net_dtype == torch.bfloat16 and fused else ("fp32" if net_dtype == torch.float32 else "bf16")
+        if precision not in ("f16x3", "bf16", "fp32"):
+            raise ValueError(f"Segmenter precision {precision!r}")
+        self.precision = precision
+        net_dtype = torch.bfloat16 if precision == "bf16" else torch.float32
         self.net_dtype = net_dtype
-        self.net = build_cpnet(seed=seed, model=model, state_dict_path=weights).to(td)
-        self.layout = 1 if net_dtype == torch.bfloat16 else 0
-        # bf16: MIOpen convs + libcpx fused epilogues (cpnet_fused); fp32: the eager module
-        self.fnet = FusedCPnet(self.net, dev) if (fused and self.layout == 1) else None
+        self.net = build_cpnet(seed=seed, model=model, state_dict_path=weights)
+        self.layout = {"bf16": 1, "fp32": 0, "f16x3": 2}[precision]
+        self.fnet = None
+        if precision == "f16x3":
+            self.fnet = FusedCPnetX3(self.net, dev)
+        self.net = self.net.to(td)
+        if precision == "bf16" and fused:
+            self.fnet = FusedCPnet(self.net, dev)
         self.net = self.net.to(memory_format=torch.channels_last, dtype=net_dtype)
         nt = batch * g.n_tiles
-        if self.layout == 1:
+        if self.layout == 2:
+            self.tiles = torch.empty((nt, g.by, g.bx, NET_CHANNELS), dtype=torch.float32, device=td)
+            self.tiles_nchw = self.tiles
+        elif self.layout == 1:
             self.tiles = torch.empty((nt, g.by, g.bx, NET_CHANNELS), dtype=torch.bfloat16, device=td)
             self.tiles_nchw = self.tiles.permute(0, 3, 1, 2)  # channels_last view
         else:
@@ -149,6 +167,8 @@ class Segmenter:
 
     # -- network -----------------------------------------------------------------------------
     def _forward(self):
+        if self.layout == 2:
+            return self.fnet(self.tiles)
         if self.fnet is not None:
             return self.fnet(self.tiles_nchw)
         with torch.no_grad():
@@ -159,6 +179,9 @@ class Segmenter:
         if not self.use_graph:
             self.net_out = self._forward().contiguous(memory_format=torch.channels_last) \
                 if self.layout == 1 else self._forward().contiguous()
+            return
+        if self.graph is not None:
+            self.graph.replay()
             return
         if self.graph is None:
             # warm-up / capture on the caller's stream when it is a side stream (a pipeline's
@@ -181,6 +204,10 @@ class Segmenter:
                 out = out.contiguous(memory_format=torch.channels_last) if self.layout == 1 else out.contiguous()
             self.net_out = out
         self.graph.replay()
+
+    def cpnet_overflow(self) -> torch.Tensor | None:
+        """Device int32 [1], non-zero once a split-fp16 activation left the fp16 range (f16x3)."""
+        return self.fnet.ovf if self.layout == 2 else None
 
     # -- pipeline ----------------------------------------------------------------------------
     def prepare(self, corr: torch.Tensor):

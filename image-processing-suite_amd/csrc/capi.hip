@@ -39,6 +39,7 @@ void* cpx_ws(cpx_ctx* ctx, int slot, size_t bytes) {
   }
   ctx->ws[slot] = p;
   ctx->ws_bytes[slot] = want;
+  ++ctx->ws_gen[slot];  // never 0 after the first allocation: caches start at generation 0
   return p;
 }
 

@@ -21,19 +21,23 @@ struct cpx_ctx {
   // generic growable device workspaces (never shrunk; see cpx_reserve)
   void* ws[kWsSlots] = {nullptr};
   size_t ws_bytes[kWsSlots] = {0};
+  // allocation generation per slot: a cache of uploaded tables is valid only for the generation
+  // it was uploaded into (a regrown slot can come back at the same address, with fresh contents)
+  unsigned int ws_gen[kWsSlots] = {0};
   int n_cu = 256;
   // QC FFT twiddle tables currently uploaded (WS_QC_MISC)
   int qc_H = 0, qc_W = 0;
-  void* qc_tw = nullptr;
+  unsigned int qc_gen = 0;
   // segmentation coefficient tables currently uploaded (WS_SEG_TAB)
   int seg_key[6] = {0, 0, 0, 0, 0, 0};
-  void* seg_tab = nullptr;
+  unsigned int seg_gen = 0;
   cpx_fov_state* fov = nullptr;
   // re-binning coefficient tables currently uploaded (WS_REBIN): W, out_w, H, out_h
   int rebin_key[4] = {0, 0, 0, 0};
+  unsigned int rebin_gen = 0;
   // embedding preprocessing coefficient table currently uploaded (WS_EMBED): S, D
   int embed_key[2] = {0, 0};
-  void* embed_tab = nullptr;
+  unsigned int embed_gen = 0;
 };
 
 void cpx_fov_free(cpx_ctx* ctx);

@@ -1,0 +1,771 @@
+// a6 CPnet at the reference's precision: 3x3 / 1x1 convolutions on split-fp16 activations
+// (f16x3), the stem, the max-pool and the style vector — the fp32 U-Net of
+// Cellpose_GPU_s3fs.py:108,143 (CellposeModel(gpu, model_type='nuclei'), no half precision)
+// on the gfx950 fp16 matrix cores.
+//
+// Split format.  A value a (fp32) is stored as two fp16 halves, hi = f16(a) (round to nearest)
+// and lo = f16((a - hi) * 2^11); a is read back as hi + lo * 2^-11 (one rounding), within
+// 2^-22 |a| (below f16's normal range: 2^-35 absolute).  Activation tensors are NHWC with the
+// channels in slabs of 16: per pixel and slab, 16 hi halves then 16 lo halves (64 bytes), i.e.
+// 4 bytes per channel like fp32.  |a| >= 65504 does not fit: producers raise *ovf.
+// Products.  With weights split the same way (host, once), a product w x = wh xh + wh xl' 2^-11
+// + wl' xh 2^-11 + O(2^-22 w x): per 16 input channels three v_mfma_f32_32x32x16_f16,
+//   acc0 += Wh Xh,   acc1 += Wh Xl' + Wl' Xh,   result = acc0 + acc1 * 2^-11,
+// fp32 accumulation as the fp32 network (products of two fp16 are exact in fp32).  Measured
+// against the fp32 CPU network this reproduces its masks and object IDs, which
+// the bf16 kernels of k_conv.hip do not.
+//
+// k_conv_x3<KS, CIN, COUT, BM, TY, TX, WM, WN>: implicit GEMM D[cout][pixel] = sum over (tap,
+// cin) W[cout][cin][tap] X[pixel + tap][cin] for a TY x TX tile of one image and BM output
+// channels; 512 threads = 8 waves = (BM / 32 / WM channel groups) x (pixel groups of WN 32-pixel
+// subtiles); a wave owns WM 32-channel slices x WN subtiles (2 accumulator sets).  Input
+// channels go in slabs of 16: the slab's halo tile (64 B per pixel) and its [tap][BM][hi|lo][16]
+// weights are double-buffered in LDS and filled by LDS-DMA (global_load_lds_dwordx4), the
+// 16-byte chunks XOR-swizzled on the source address (chunk c of row r at slot c ^ ((r >> 2) & 3))
+// so the fragment reads are bank-conflict free.  Epilogue (same semantics as k_conv.hip): bias,
+// residual (split, optionally read nearest-upsampled), residual-stream store, style bias, eval
+// BatchNorm, ReLU, next-input store (optionally 2x nearest-upsampled) or the CPnet output head
+// (fp32), all on the fp32 values; output tiles go through LDS as whole 16-byte chunks.
+#include "cpx_internal.h"
+#include <type_traits>
+
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr float kLoScale = 2048.0f;
+constexpr float kLoInv = 1.0f / 2048.0f;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+__device__ uint4 g_x3_zero16 = {0u, 0u, 0u, 0u};
+
+__device__ __forceinline__ int swz4(int row) { return (row >> 2) & 3; }
+
+// output-tile chunk swizzle (Q chunks per pixel row)
+template <int Q>
+__device__ __forceinline__ int swzq(int row) {
+  if constexpr (Q >= 16) return row & 15;
+  else if constexpr (Q == 8) return (row >> 1) & 7;
+  else if constexpr (Q == 4) return (row >> 2) & 3;
+  else return 0;
+}
+
+// 4 fp32 -> (hi, lo) 8-byte pieces; *bad |= not representable
+__device__ __forceinline__ void split4(float a, float b, float c, float d, uint2& hi, uint2& lo, bool& bad) {
+  const float v[4] = {a, b, c, d};
+  f16x4 h, l;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const _Float16 t = (_Float16)v[k];
+    h[k] = t;
+    l[k] = (_Float16)((v[k] - (float)t) * kLoScale);
+    bad |= !(fabsf(v[k]) < 65504.0f);
+  }
+  hi = __builtin_bit_cast(uint2, h);
+  lo = __builtin_bit_cast(uint2, l);
+}
+
+__device__ __forceinline__ void join4(const uint2& hi, const uint2& lo, float* out) {
+  const f16x4 h = __builtin_bit_cast(f16x4, hi), l = __builtin_bit_cast(f16x4, lo);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) out[k] = (float)h[k] + (float)l[k] * kLoInv;
+}
+
+// 8 channels: hi chunk + lo chunk -> fp32
+__device__ __forceinline__ void join8(const uint4& hi, const uint4& lo, float* out) {
+  join4(make_uint2(hi.x, hi.y), make_uint2(lo.x, lo.y), out);
+  join4(make_uint2(hi.z, hi.w), make_uint2(lo.z, lo.w), out + 4);
+}
+
+__device__ __forceinline__ void split8(const float* v, uint4& hi, uint4& lo, bool& bad) {
+  uint2 h0, l0, h1, l1;
+  split4(v[0], v[1], v[2], v[3], h0, l0, bad);
+  split4(v[4], v[5], v[6], v[7], h1, l1, bad);
+  hi = make_uint4(h0.x, h0.y, h1.x, h1.y);
+  lo = make_uint4(l0.x, l0.y, l1.x, l1.y);
+}
+
+struct X3Epi {
+  const float* bias;
+  const uint4* res;    // split [N][h][w][COUT] (res_up: [N][h/2][w/2][COUT])
+  const float* style;  // [N][style_stride] (+ channel)
+  const float* scale;
+  const float* shift;
+  uint4* y;            // residual stream (split)
+  uint4* z;            // next convolution's input (split; z_up: 2x nearest-upsampled)
+  int res_up, relu, z_up, style_stride;
+  const float* head_w;  // [n_head][32]
+  const float* head_b;
+  float* head;          // fp32 [N][h][w][n_head]
+  int n_head;
+  int* ovf;
+};
+
+template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, int N, int H,
+               int W, int tiles_x, int tiles_y) {
+  constexpr int NT = 512, NWV = NT / 64;
+  constexpr int T = KS * KS, HALO = KS / 2;
+  constexpr int MWV = BM / (32 * WM), PW = NWV / MWV;
+  constexpr int HY = TY + KS - 1, HX = TX + KS - 1, NPIX = HY * HX;
+  constexpr int NCH = CIN / 16;
+  constexpr int P = TY * TX, NS = (P + 31) / 32;
+  constexpr int SW = T * BM * 4;                      // 16-byte slots [tap][BM][4 chunks]
+  constexpr int SI = (NPIX * 4 + 63) / 64 * 64;       // [halo pixel][4 chunks]
+  constexpr int SB = SW + SI;
+  constexpr int NWW = SW / 64, NWIN = SI / 64;
+  constexpr int JW = (NWW + NWV - 1) / NWV, JI = (NWIN + NWV - 1) / NWV;
+  constexpr int QB = BM / 4;                          // output chunks per pixel (hi + lo)
+  constexpr int QC = COUT / 4;                        // chunks per pixel of a COUT tensor
+  constexpr int QI = CIN / 4;
+  constexpr int OUT_R = (P * QB + NT - 1) / NT;
+  static_assert(CIN % 16 == 0 && COUT % BM == 0 && BM % (32 * WM) == 0 && NWV % MWV == 0, "shape");
+  static_assert(PW * WN >= NS, "every subtile needs a wave");
+  static_assert(SW % 64 == 0, "weight DMA rows");
+  static_assert(P * QB <= 2 * SB, "output tile must fit the staging LDS");
+  static_assert(2 * SB * 16 <= 163840, "LDS");
+  __shared__ uint4 smem[2 * SB];
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int mw = wid % MWV, pg = wid / MWV;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int tiles = tiles_x * tiles_y;
+  const int n = blockIdx.x / tiles;
+  const int t = blockIdx.x - n * tiles;
+  const int ty0 = (t / tiles_x) * TY, tx0 = (t % tiles_x) * TX;
+  const int nb = blockIdx.y;
+  const uint4* inb = in + (long long)n * H * W * QI;
+
+  // DMA sources: weights (lane-constant swizzle), halo chunk offsets (slab-independent)
+  const int fW = (lane & ~3) | ((lane & 3) ^ ((lane >> 4) & 3));
+  int inOff[JI];
+#pragma unroll
+  for (int jj = 0; jj < JI; ++jj) {
+    const int si = (wid + NWV * jj) * 64 + lane;
+    const int hp = si >> 2, cq = si & 3;
+    const int hy = hp / HX, hx = hp - (hp / HX) * HX;
+    const int gy = ty0 + hy - HALO, gx = tx0 + hx - HALO;
+    inOff[jj] = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+                    ? (gy * W + gx) * QI + (cq ^ swz4(hp)) : -1;
+  }
+  auto issue = [&](int ch, int buf) {
+    const uint4* wsl = wpk + (long long)(nb * NCH + ch) * SW;
+    uint4* dst = smem + buf * SB;
+#pragma unroll
+    for (int jj = 0; jj < JW; ++jj) {
+      const int j = wid + NWV * jj;
+      if (j < NWW)
+        __builtin_amdgcn_global_load_lds((glb_void_t*)(wsl + j * 64 + fW), (lds_void_t*)(dst + j * 64), 16, 0, 0);
+    }
+#pragma unroll
+    for (int jj = 0; jj < JI; ++jj) {
+      const int j = wid + NWV * jj;
+      if (j < NWIN) {
+        const uint4* src = inOff[jj] >= 0 ? inb + inOff[jj] + ch * 4 : &g_x3_zero16;
+        __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(dst + SW + j * 64), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x16 acc0[WM][WN], acc1[WM][WN];
+#pragma unroll
+  for (int m = 0; m < WM; ++m)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc0[m][j][r] = 0.0f;
+        acc1[m][j][r] = 0.0f;
+      }
+
+  const int nsub = max(0, min(WN, NS - pg * WN));
+  int aS[WM];
+#pragma unroll
+  for (int m = 0; m < WM; ++m) {
+    const int r = (mw * WM + m) * 32 + l32;
+    aS[m] = r * 4 + (h ^ swz4(r));
+  }
+  int hp0[WN];
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int px = min((pg * WN + j) * 32 + l32, P - 1);
+    hp0[j] = (px / TX) * HX + (px % TX);
+  }
+
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int ch = 0; ch < NCH; ++ch) {
+    if (ch + 1 < NCH) issue(ch + 1, (ch + 1) & 1);
+    const uint4* sb = smem + (ch & 1) * SB;
+    auto mma = [&](auto cnt) {
+      constexpr int C = decltype(cnt)::value;
+      if constexpr (C > 0) {
+#pragma unroll 1
+        for (int tap = 0; tap < T; ++tap) {
+          const int ky = tap / KS, kx = tap - KS * (tap / KS);
+          f16x8 ah[WM], al[WM];
+#pragma unroll
+          for (int m = 0; m < WM; ++m) {
+            ah[m] = __builtin_bit_cast(f16x8, sb[aS[m] + tap * BM * 4]);
+            al[m] = __builtin_bit_cast(f16x8, sb[(aS[m] ^ 2) + tap * BM * 4]);
+          }
+#pragma unroll
+          for (int j = 0; j < C; ++j) {
+            const int hp = hp0[j] + ky * HX + kx;
+            const int bs = SW + hp * 4 + (h ^ swz4(hp));
+            const f16x8 bh = __builtin_bit_cast(f16x8, sb[bs]);
+            const f16x8 bl = __builtin_bit_cast(f16x8, sb[bs ^ 2]);
+#pragma unroll
+            for (int m = 0; m < WM; ++m) {
+              acc0[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh, acc0[m][j], 0, 0, 0);
+              acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bl, acc1[m][j], 0, 0, 0);
+              acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bh, acc1[m][j], 0, 0, 0);
+            }
+          }
+        }
+      }
+    };
+    if constexpr (WN == 1) {
+      if (nsub == 1) mma(std::integral_constant<int, 1>{});
+    } else if constexpr (WN == 2) {
+      if (nsub == 2) mma(std::integral_constant<int, 2>{});
+      else if (nsub == 1) mma(std::integral_constant<int, 1>{});
+    } else {
+      static_assert(WN <= 2, "WN");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue on the fp32 values ----
+#pragma unroll
+  for (int m = 0; m < WM; ++m)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc0[m][j][r] += acc1[m][j][r] * kLoInv;  // exact product, one rounding
+
+  bool bad = false;
+  auto gpix = [&](int px) -> long long {
+    const int gy = ty0 + px / TX, gx = tx0 + px % TX;
+    if (px >= P || gy >= H || gx >= W) return -1;
+    return ((long long)n * H + gy) * W + gx;
+  };
+  // lane's channel group (m, g): channels cb(m) + 8 g + {0..3} of the block, slab (m', g >> 1)
+  auto slice = [&](int m) { return mw * WM + m; };
+  auto piece = [&](int px, int m, int g, int lo) -> uint2* {
+    const int q = (slice(m) * 2 + (g >> 1)) * 4 + 2 * lo + (g & 1);
+    return reinterpret_cast<uint2*>(smem + px * QB + (q ^ swzq<QB>(px))) + h;
+  };
+  auto chan = [&](int m, int g) { return nb * BM + slice(m) * 32 + 8 * g + 4 * h; };
+  if (ep.bias) {
+#pragma unroll
+    for (int m = 0; m < WM; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 bv = *reinterpret_cast<const float4*>(ep.bias + chan(m, g));
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          acc0[m][j][4 * g + 0] += bv.x;
+          acc0[m][j][4 * g + 1] += bv.y;
+          acc0[m][j][4 * g + 2] += bv.z;
+          acc0[m][j][4 * g + 3] += bv.w;
+        }
+      }
+  }
+  if (ep.res) {
+#pragma unroll
+    for (int r = 0; r < OUT_R; ++r) {
+      const int i = threadIdx.x + r * NT;
+      if (i < P * QB) {
+        const int px = i / QB, k = i - px * QB;
+        const int gy = ty0 + px / TX, gx = tx0 + px % TX;
+        uint4 v = {0u, 0u, 0u, 0u};
+        if (gy < H && gx < W) {
+          const long long rp = ep.res_up ? ((long long)n * (H >> 1) + (gy >> 1)) * (W >> 1) + (gx >> 1)
+                                         : ((long long)n * H + gy) * W + gx;
+          v = ep.res[rp * QC + nb * QB + k];
+        }
+        smem[px * QB + (k ^ swzq<QB>(px))] = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int px = min((pg * WN + j) * 32 + l32, P - 1);
+#pragma unroll
+      for (int m = 0; m < WM; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float rv[4];
+          join4(*piece(px, m, g, 0), *piece(px, m, g, 1), rv);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc0[m][j][4 * g + k] += rv[k];
+        }
+    }
+    __syncthreads();
+  }
+  auto stage = [&]() {
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int px = (pg * WN + j) * 32 + l32;
+      if (j < nsub && px < P) {
+#pragma unroll
+        for (int m = 0; m < WM; ++m)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            uint2 hi, lo;
+            split4(acc0[m][j][4 * g], acc0[m][j][4 * g + 1], acc0[m][j][4 * g + 2], acc0[m][j][4 * g + 3],
+                   hi, lo, bad);
+            *piece(px, m, g, 0) = hi;
+            *piece(px, m, g, 1) = lo;
+          }
+      }
+    }
+  };
+  auto drain = [&](uint4* dst) {
+#pragma unroll
+    for (int r = 0; r < OUT_R; ++r) {
+      const int i = threadIdx.x + r * NT;
+      const int px = i / QB, k = i - px * QB;
+      const long long gp = gpix(px);
+      if (i < P * QB && gp >= 0) dst[gp * QC + nb * QB + k] = smem[px * QB + (k ^ swzq<QB>(px))];
+    }
+  };
+  auto flag = [&]() {
+    if (ep.ovf && __ballot(bad)) {
+      if (lane == 0) atomicOr(ep.ovf, 1);
+    }
+  };
+  if (ep.y) {
+    stage();
+    __syncthreads();
+    drain(ep.y);
+    __syncthreads();
+  }
+  if (!ep.z && !ep.head) {
+    flag();
+    return;
+  }
+  if (ep.style) {
+#pragma unroll
+    for (int m = 0; m < WM; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 sv = *reinterpret_cast<const float4*>(ep.style + (long long)n * ep.style_stride + chan(m, g));
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          acc0[m][j][4 * g + 0] += sv.x;
+          acc0[m][j][4 * g + 1] += sv.y;
+          acc0[m][j][4 * g + 2] += sv.z;
+          acc0[m][j][4 * g + 3] += sv.w;
+        }
+      }
+  }
+  if (ep.scale) {
+#pragma unroll
+    for (int m = 0; m < WM; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 sc = *reinterpret_cast<const float4*>(ep.scale + chan(m, g));
+        const float4 sh = *reinterpret_cast<const float4*>(ep.shift + chan(m, g));
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          acc0[m][j][4 * g + 0] = sc.x * acc0[m][j][4 * g + 0] + sh.x;
+          acc0[m][j][4 * g + 1] = sc.y * acc0[m][j][4 * g + 1] + sh.y;
+          acc0[m][j][4 * g + 2] = sc.z * acc0[m][j][4 * g + 2] + sh.z;
+          acc0[m][j][4 * g + 3] = sc.w * acc0[m][j][4 * g + 3] + sh.w;
+        }
+      }
+  }
+  if (ep.relu) {
+#pragma unroll
+    for (int m = 0; m < WM; ++m)
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc0[m][j][r] = fmaxf(acc0[m][j][r], 0.0f);
+  }
+  if constexpr (COUT == 32 && BM == 32 && WM == 1) {
+    if (ep.head) {
+      // fp32 output 1x1 convolution: lane l and l ^ 32 hold the two halves of a pixel's channels
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int c = 8 * g + 4 * h + k;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (q < ep.n_head) o[q] = __builtin_fmaf(ep.head_w[q * 32 + c], acc0[0][j][4 * g + k], o[q]);
+          }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] += __shfl_xor(o[q], 32, 64);
+        const int px = (pg * WN + j) * 32 + l32;
+        const long long gp = gpix(px);
+        if (h == 0 && j < nsub && gp >= 0) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (q < ep.n_head) ep.head[gp * ep.n_head + q] = o[q] + ep.head_b[q];
+        }
+      }
+      flag();
+      return;
+    }
+  }
+  stage();
+  __syncthreads();
+  if (!ep.z_up) {
+    drain(ep.z);
+  } else {
+    const long long W2 = 2LL * W;
+#pragma unroll
+    for (int r = 0; r < 4 * OUT_R; ++r) {
+      const int i = threadIdx.x + r * NT;
+      if (i >= 4 * P * QB) continue;
+      const int k = i % QB;
+      const int d = i / QB;
+      const int dy = d / (2 * TX), dx = d - dy * (2 * TX);
+      const int px = (dy >> 1) * TX + (dx >> 1);
+      const int gy = ty0 + (dy >> 1), gx = tx0 + (dx >> 1);
+      if (gy >= H || gx >= W) continue;
+      const long long dp = ((long long)n * 2 * H + 2LL * ty0 + dy) * W2 + 2LL * tx0 + dx;
+      ep.z[dp * QC + nb * QB + k] = smem[px * QB + (k ^ swzq<QB>(px))];
+    }
+  }
+  flag();
+}
+
+struct X3Cfg {
+  int bm, ty, tx;
+};
+
+// tile configuration per (KS, CIN, COUT, variant); must match the instances in x3_launch()
+bool x3_cfg(int ks, int cin, int cout, int variant, X3Cfg* c) {
+  if (!((cin == 32 || cin == 64 || cin == 128 || cin == 256) && (cout == 32 || cout == 64 || cout == 128 || cout == 256)))
+    return false;
+  if (ks == 1) {
+    *c = {32, 16, 16};
+    return true;
+  }
+  if (ks != 3) return false;
+  if (cout == 32) *c = {32, 8, 32};
+  else if (cout == 64) *c = variant == 1 ? X3Cfg{32, 16, 16} : X3Cfg{64, 16, 16};
+  else *c = variant == 1 ? X3Cfg{32, 8, 28} : X3Cfg{64, 14, 28};
+  return true;
+}
+
+template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE>
+int x3_run(cpx_ctx* ctx, const void* in, const void* wpk, const X3Epi& ep, int N, int H, int W) {
+  const int tx = cpx_div_up(W, TX), ty = cpx_div_up(H, TY);
+  const long long blocks = (long long)N * tx * ty;
+  CPX_REQUIRE(blocks < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv: too many tiles");
+  hipLaunchKernelGGL((k_conv_x3<KS, CIN, COUT, BM, TY, TX, WM, WN, WPE>), dim3((unsigned)blocks, COUT / BM),
+                     dim3(512), 0, ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N, H, W, tx, ty);
+  CPX_CHECK_LAUNCH("k_conv_x3");
+  return CPX_OK;
+}
+
+int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* in, const void* wpk,
+              const X3Epi& ep, int N, int H, int W) {
+#define X3_3(CI, CO, V, BM_, TY_, TX_, WM_, WN_, WPE_)                                  \
+  if (ks == 3 && cin == CI && cout == CO && variant == V)                                \
+    return x3_run<3, CI, CO, BM_, TY_, TX_, WM_, WN_, WPE_>(ctx, in, wpk, ep, N, H, W);
+#define X3_1(CI, CO)                                                                     \
+  if (ks == 1 && cin == CI && cout == CO)                                                \
+    return x3_run<1, CI, CO, 32, 16, 16, 1, 1, 4>(ctx, in, wpk, ep, N, H, W);
+  // 224^2 level
+  X3_3(32, 32, 0, 32, 8, 32, 1, 1, 4)
+  X3_3(64, 32, 0, 32, 8, 32, 1, 1, 4)
+  // 112^2 level
+  X3_3(32, 64, 0, 64, 16, 16, 2, 1, 2)
+  X3_3(64, 64, 0, 64, 16, 16, 2, 1, 2)
+  X3_3(128, 64, 0, 64, 16, 16, 2, 1, 2)
+  X3_3(32, 64, 1, 32, 16, 16, 1, 1, 4)
+  X3_3(64, 64, 1, 32, 16, 16, 1, 1, 4)
+  X3_3(128, 64, 1, 32, 16, 16, 1, 1, 4)
+  // 56^2 / 28^2 levels
+  X3_3(64, 128, 0, 64, 14, 28, 2, 2, 2)
+  X3_3(128, 128, 0, 64, 14, 28, 2, 2, 2)
+  X3_3(256, 128, 0, 64, 14, 28, 2, 2, 2)
+  X3_3(128, 256, 0, 64, 14, 28, 2, 2, 2)
+  X3_3(256, 256, 0, 64, 14, 28, 2, 2, 2)
+  X3_3(64, 128, 1, 32, 8, 28, 1, 1, 4)
+  X3_3(128, 128, 1, 32, 8, 28, 1, 1, 4)
+  X3_3(256, 128, 1, 32, 8, 28, 1, 1, 4)
+  X3_3(128, 256, 1, 32, 8, 28, 1, 1, 4)
+  X3_3(256, 256, 1, 32, 8, 28, 1, 1, 4)
+  // 1x1 block projections (BatchNorm folded into the weights)
+  X3_1(32, 64)
+  X3_1(64, 128)
+  X3_1(128, 256)
+  X3_1(256, 256)
+  X3_1(256, 128)
+  X3_1(128, 64)
+  X3_1(64, 32)
+#undef X3_3
+#undef X3_1
+  cpx_set_error("cpx_cpnet_x3_conv: no instance for ks %d, %d -> %d channels (variant %d)", ks, cin, cout, variant);
+  return CPX_ERR_SHAPE;
+}
+
+// ---------------------------------------------------------------------------------------------
+// stem (first down block's entry) on the fp32 network input x [N][H][W][2]:
+//   z0 = relu(scale0 x + shift0) (fp32, zero-padded), z = relu(scale1 (conv3x3(z0, w0) + bias0)
+//   + shift1) and p = conv1x1(x, wp) (BatchNorm folded), both stored split.
+constexpr int kSTY = 16, kSTX = 16;
+
+__global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem_x3(
+    const float* __restrict__ x, int N, int H, int W, const float* __restrict__ scale0,
+    const float* __restrict__ shift0, const float* __restrict__ w0, const float* __restrict__ bias0,
+    const float* __restrict__ scale1, const float* __restrict__ shift1, const float* __restrict__ wp,
+    uint4* __restrict__ p_out, uint4* __restrict__ z_out, int tiles_x, int tiles_y, int* ovf) {
+  __shared__ float sz[2][kSTY + 2][kSTX + 2];
+  const int tiles = tiles_x * tiles_y;
+  const int n = blockIdx.x / tiles, t = blockIdx.x - n * tiles;
+  const int ty0 = (t / tiles_x) * kSTY, tx0 = (t % tiles_x) * kSTX;
+  const float s00 = scale0[0], s01 = scale0[1], h00 = shift0[0], h01 = shift0[1];
+  for (int i = threadIdx.x; i < (kSTY + 2) * (kSTX + 2); i += kSTY * kSTX) {
+    const int hy = i / (kSTX + 2), hx = i - hy * (kSTX + 2);
+    const int gy = ty0 + hy - 1, gx = tx0 + hx - 1;
+    float a = 0.0f, b = 0.0f;
+    if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+      const float2 v = *reinterpret_cast<const float2*>(x + (((long long)n * H + gy) * W + gx) * 2);
+      a = fmaxf(s00 * v.x + h00, 0.0f);
+      b = fmaxf(s01 * v.y + h01, 0.0f);
+    }
+    sz[0][hy][hx] = a;
+    sz[1][hy][hx] = b;
+  }
+  __syncthreads();
+  const int ly = threadIdx.x / kSTX, lx = threadIdx.x - ly * kSTX;
+  const int gy = ty0 + ly, gx = tx0 + lx;
+  bool bad = false;
+  if (gy < H && gx < W) {
+    const long long pix = ((long long)n * H + gy) * W + gx;
+    float in[18];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) in[c * 9 + k] = sz[c][ly + k / 3][lx + k % 3];
+    const float2 xv = *reinterpret_cast<const float2*>(x + pix * 2);
+    uint4* zo = z_out + pix * 8;
+    uint4* po = p_out + pix * 8;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // 8 channels per q: slab q >> 1, chunk q & 1
+      float zf[8], pf[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int co = q * 8 + e;
+        float acc = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 18; ++k) acc = __builtin_fmaf(w0[co * 18 + k], in[k], acc);
+        zf[e] = fmaxf(__builtin_fmaf(scale1[co], acc + bias0[co], shift1[co]), 0.0f);
+        pf[e] = __builtin_fmaf(wp[co * 2], xv.x, wp[co * 2 + 1] * xv.y);
+      }
+      uint4 hi, lo;
+      const int base = (q >> 1) * 4 + (q & 1);
+      split8(zf, hi, lo, bad);
+      zo[base] = hi;
+      zo[base + 2] = lo;
+      split8(pf, hi, lo, bad);
+      po[base] = hi;
+      po[base + 2] = lo;
+    }
+  }
+  if (ovf && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
+}
+
+// 2x2/2 max-pool of split [N][2Hh][2Ww][Cn] -> x_out (the maximum's own hi/lo pair, exact) and
+// z_out = split(relu?(scale x + shift)); one thread per (pixel, 8-channel group)
+__global__ __launch_bounds__(256) void k_cpnet_pool_x3(const uint4* __restrict__ in,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, int relu,
+                                                       int N, int Hh, int Ww, int Cn,
+                                                       uint4* __restrict__ xo, uint4* __restrict__ zo,
+                                                       int* ovf) {
+  const long long P = (long long)Hh * Ww;
+  const int G = Cn / 8;         // 8-channel groups per pixel
+  const int Q = Cn / 4;         // chunks per pixel
+  const long long ng = (long long)N * P * G;
+  const long long W2 = 2LL * Ww;
+  bool bad = false;
+  for (long long v = (long long)blockIdx.x * 256 + threadIdx.x; v < ng; v += (long long)gridDim.x * 256) {
+    const long long pix = v / G;
+    const int gi = (int)(v - pix * G);
+    const int q = (gi >> 1) * 4 + (gi & 1);  // hi chunk; lo chunk = q + 2
+    const long long n = pix / P;
+    const long long rem = pix - n * P;
+    const int hh = (int)(rem / Ww), ww = (int)(rem - (long long)hh * Ww);
+    const long long base = (n * 2LL * Hh + 2LL * hh) * W2 + 2LL * ww;
+    const long long src[4] = {base, base + 1, base + W2, base + W2 + 1};
+    uint4 bh = in[src[0] * Q + q], bl = in[src[0] * Q + q + 2];
+    float best[8];
+    join8(bh, bl, best);
+    f16x8 mh = __builtin_bit_cast(f16x8, bh), ml = __builtin_bit_cast(f16x8, bl);
+#pragma unroll
+    for (int s = 1; s < 4; ++s) {
+      const uint4 ch = in[src[s] * Q + q], cl = in[src[s] * Q + q + 2];
+      float f[8];
+      join8(ch, cl, f);
+      const f16x8 fh = __builtin_bit_cast(f16x8, ch), fl = __builtin_bit_cast(f16x8, cl);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (f[k] > best[k]) {  // max_pool2d: first maximum (NaN-free activations)
+          best[k] = f[k];
+          mh[k] = fh[k];
+          ml[k] = fl[k];
+        }
+    }
+    if (xo) {
+      xo[pix * Q + q] = __builtin_bit_cast(uint4, mh);
+      xo[pix * Q + q + 2] = __builtin_bit_cast(uint4, ml);
+    }
+    if (zo) {
+      const int c0 = gi * 8;
+      float z[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float tv = scale ? scale[c0 + k] * best[k] + shift[c0 + k] : best[k];
+        z[k] = relu ? fmaxf(tv, 0.0f) : tv;
+      }
+      uint4 hi, lo;
+      split8(z, hi, lo, bad);
+      zo[pix * Q + q] = hi;
+      zo[pix * Q + q + 2] = lo;
+    }
+  }
+  if (ovf && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
+}
+
+// style vector (CPnet.forward: avg_pool2d over the deepest feature map, L2-normalised) and the
+// up path's style Linear layers, one block per image:
+//   s[c] = mean over pixels of x[., c] (fp64 sum, fp32 result), s /= ||s||_2,
+//   out[n][j] = lin_b[j] + sum_c lin_w[j][c] s[c]  (fp64 accumulation)
+__global__ __launch_bounds__(256) void k_cpnet_style_x3(const uint4* __restrict__ x, int H, int W,
+                                                        int C, const float* __restrict__ lin_w,
+                                                        const float* __restrict__ lin_b, int J,
+                                                        float* __restrict__ out) {
+  __shared__ float s[256];
+  __shared__ double red[256];
+  const int n = blockIdx.x;
+  const int Q = C / 4;
+  const long long P = (long long)H * W;
+  const uint4* xb = x + (long long)n * P * Q;
+  const int c = threadIdx.x;
+  float mean = 0.0f;
+  if (c < C) {
+    const int q = (c / 16) * 4 + ((c % 16) >> 3), e = c & 7;
+    double acc = 0.0;
+    for (long long p = 0; p < P; ++p) {
+      const f16x8 hi = __builtin_bit_cast(f16x8, xb[p * Q + q]);
+      const f16x8 lo = __builtin_bit_cast(f16x8, xb[p * Q + q + 2]);
+      acc += (double)((float)hi[e] + (float)lo[e] * kLoInv);
+    }
+    mean = (float)(acc / (double)P);
+  }
+  red[c] = c < C ? (double)mean * (double)mean : 0.0;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (c < o) red[c] += red[c + o];
+    __syncthreads();
+  }
+  const float nrm = (float)sqrt(red[0]);
+  if (c < C) s[c] = mean / nrm;
+  __syncthreads();
+  for (int j = c; j < J; j += 256) {
+    double acc = 0.0;
+    for (int k = 0; k < C; ++k) acc += (double)lin_w[(long long)j * C + k] * (double)s[k];
+    out[(long long)n * J + j] = (float)(acc + (double)lin_b[j]);
+  }
+}
+
+}  // namespace
+
+extern "C" int cpx_cpnet_x3_cfg(int ks, int cin, int cout, int variant, int* bm) {
+  X3Cfg c;
+  if (!x3_cfg(ks, cin, cout, variant, &c)) return CPX_ERR_SHAPE;
+  if (bm) *bm = c.bm;
+  return CPX_OK;
+}
+
+extern "C" int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* in, int N, int H,
+                                 int W, int cin, int cout, const void* wpk, const float* bias,
+                                 const void* res, int res_up, const float* style, int style_stride,
+                                 const float* scale, const float* shift, int relu, void* y_out,
+                                 void* z_out, int z_up, const float* head_w, const float* head_b,
+                                 int n_head, float* head_out, int* ovf) {
+  CPX_REQUIRE(ctx && in && wpk && (y_out || z_out || head_out), CPX_ERR_ARG,
+              "cpx_cpnet_x3_conv: null argument");
+  CPX_REQUIRE(N > 0 && H > 0 && W > 0, CPX_ERR_ARG, "cpx_cpnet_x3_conv: bad sizes");
+  CPX_REQUIRE(!(scale == nullptr) == !(shift == nullptr), CPX_ERR_ARG,
+              "cpx_cpnet_x3_conv: scale and shift go together");
+  CPX_REQUIRE(!res_up || ((H % 2) == 0 && (W % 2) == 0), CPX_ERR_ARG,
+              "cpx_cpnet_x3_conv: res_up needs even sizes");
+  CPX_REQUIRE(((uintptr_t)in | (uintptr_t)wpk | (uintptr_t)res | (uintptr_t)y_out | (uintptr_t)z_out) % 16 == 0,
+              CPX_ERR_ARG, "cpx_cpnet_x3_conv: misaligned buffers");
+  CPX_REQUIRE(!style || (style_stride >= cout && style_stride % 4 == 0 && ((uintptr_t)style % 16) == 0),
+              CPX_ERR_ARG, "cpx_cpnet_x3_conv: style needs a 16-byte aligned [N][stride >= cout] table");
+  CPX_REQUIRE(!head_out || (ks == 3 && cout == 32 && !z_out && head_w && head_b && n_head >= 1 && n_head <= 4),
+              CPX_ERR_ARG, "cpx_cpnet_x3_conv: head needs a 3x3 conv with cout 32, no z_out, 1..4 outputs");
+  CPX_REQUIRE(!z_up || z_out, CPX_ERR_ARG, "cpx_cpnet_x3_conv: z_up without z_out");
+  X3Epi ep{bias, (const uint4*)res, style, scale, shift, (uint4*)y_out, (uint4*)z_out, res_up, relu,
+           z_up, style_stride, head_w, head_b, head_out, n_head, ovf};
+  return x3_launch(ctx, ks, cin, cout, variant, in, wpk, ep, N, H, W);
+}
+
+extern "C" int cpx_cpnet_x3_stem(cpx_ctx* ctx, const float* x, int N, int H, int W,
+                                 const float* scale0, const float* shift0, const float* w0,
+                                 const float* bias0, const float* scale1, const float* shift1,
+                                 const float* wp, void* p_out, void* z_out, int* ovf) {
+  CPX_REQUIRE(ctx && x && scale0 && shift0 && w0 && bias0 && scale1 && shift1 && wp && p_out && z_out,
+              CPX_ERR_ARG, "cpx_cpnet_x3_stem: null argument");
+  CPX_REQUIRE(N > 0 && H > 0 && W > 0, CPX_ERR_ARG, "cpx_cpnet_x3_stem: bad sizes");
+  CPX_REQUIRE(((uintptr_t)x % 8) == 0 && ((uintptr_t)p_out | (uintptr_t)z_out) % 16 == 0,
+              CPX_ERR_ARG, "cpx_cpnet_x3_stem: misaligned buffers");
+  const int tx = cpx_div_up(W, kSTX), ty = cpx_div_up(H, kSTY);
+  const long long blocks = (long long)N * tx * ty;
+  CPX_REQUIRE(blocks < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_stem: too many tiles");
+  hipLaunchKernelGGL(k_cpnet_stem_x3, dim3((unsigned)blocks), dim3(kSTY * kSTX), 0, ctx->stream, x, N, H,
+                     W, scale0, shift0, w0, bias0, scale1, shift1, wp, (uint4*)p_out, (uint4*)z_out, tx,
+                     ty, ovf);
+  CPX_CHECK_LAUNCH("k_cpnet_stem_x3");
+  return CPX_OK;
+}
+
+extern "C" int cpx_cpnet_x3_pool(cpx_ctx* ctx, const void* in, const float* scale,
+                                 const float* shift, int relu, int N, int Hh, int Ww, int Cn,
+                                 void* x_out, void* z_out, int* ovf) {
+  CPX_REQUIRE(ctx && in && (x_out || z_out), CPX_ERR_ARG, "cpx_cpnet_x3_pool: null argument");
+  CPX_REQUIRE(N > 0 && Hh > 0 && Ww > 0 && Cn > 0 && Cn % 16 == 0, CPX_ERR_ARG,
+              "cpx_cpnet_x3_pool: bad sizes (channels must be a multiple of 16)");
+  CPX_REQUIRE(!(scale == nullptr) == !(shift == nullptr), CPX_ERR_ARG,
+              "cpx_cpnet_x3_pool: scale and shift go together");
+  CPX_REQUIRE(((uintptr_t)in | (uintptr_t)x_out | (uintptr_t)z_out) % 16 == 0, CPX_ERR_ARG,
+              "cpx_cpnet_x3_pool: buffers must be 16-byte aligned");
+  const long long ng = (long long)N * Hh * Ww * Cn / 8;
+  const long long g = std::max(1LL, std::min((ng + 255) / 256, 32LL * ctx->n_cu));
+  hipLaunchKernelGGL(k_cpnet_pool_x3, dim3((unsigned)g), dim3(256), 0, ctx->stream, (const uint4*)in,
+                     scale, shift, relu, N, Hh, Ww, Cn, (uint4*)x_out, (uint4*)z_out, ovf);
+  CPX_CHECK_LAUNCH("k_cpnet_pool_x3");
+  return CPX_OK;
+}
+
+extern "C" int cpx_cpnet_x3_style(cpx_ctx* ctx, const void* x, int N, int H, int W, int C,
+                                  const float* lin_w, const float* lin_b, int J, float* out) {
+  CPX_REQUIRE(ctx && x && lin_w && lin_b && out, CPX_ERR_ARG, "cpx_cpnet_x3_style: null argument");
+  CPX_REQUIRE(N > 0 && H > 0 && W > 0 && C > 0 && C <= 256 && C % 16 == 0 && J > 0, CPX_ERR_ARG,
+              "cpx_cpnet_x3_style: bad sizes");
+  hipLaunchKernelGGL(k_cpnet_style_x3, dim3(N), dim3(256), 0, ctx->stream, (const uint4*)x, H, W, C,
+                     lin_w, lin_b, J, out);
+  CPX_CHECK_LAUNCH("k_cpnet_style_x3");
+  return CPX_OK;
+}

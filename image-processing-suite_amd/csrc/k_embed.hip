@@ -130,7 +130,7 @@ extern "C" int cpx_embed_preprocess(cpx_ctx* ctx, const uint8_t* crops8_dev, con
   int* tab = (int*)cpx_ws(ctx, WS_EMBED, words * sizeof(int) + (size_t)N * S * D + 256);
   if (!tab) return CPX_ERR_OOM;
   unsigned char* tmp = (unsigned char*)(tab + words) + (256 - (words * sizeof(int)) % 256) % 256;
-  if (ctx->embed_key[0] != S || ctx->embed_key[1] != D || ctx->embed_tab != (void*)tab) {
+  if (ctx->embed_key[0] != S || ctx->embed_key[1] != D || ctx->embed_gen != ctx->ws_gen[WS_EMBED]) {
     std::vector<int> h(words);
     CPX_REQUIRE(coeffs_8bpc(S, D, &h[0], &h[D], &h[2 * D]), CPX_ERR_ARG,
                 "cpx_embed_preprocess: downscale factor too large");
@@ -138,7 +138,7 @@ extern "C" int cpx_embed_preprocess(cpx_ctx* ctx, const uint8_t* crops8_dev, con
     CPX_CHECK_HIP(hipStreamSynchronize(ctx->stream));
     ctx->embed_key[0] = S;
     ctx->embed_key[1] = D;
-    ctx->embed_tab = tab;
+    ctx->embed_gen = ctx->ws_gen[WS_EMBED];
   }
   Coeffs c{tab, tab + D, tab + 2 * D};
   const int th = std::min(1024, (D + 63) / 64 * 64);

@@ -492,7 +492,7 @@ extern "C" int cpx_qc_rps(cpx_ctx* ctx, const uint16_t* raw_dev, const void* ill
   if (!misc) return CPX_ERR_OOM;
   double* twH = (double*)misc;
   double* twW = twH + 2 * (size_t)H;
-  if (ctx->qc_H != H || ctx->qc_W != W || ctx->qc_tw != misc) {
+  if (ctx->qc_H != H || ctx->qc_W != W || ctx->qc_gen != ctx->ws_gen[WS_QC_MISC]) {
     std::vector<double> th, tw;
     fill_twiddles(H, th);
     fill_twiddles(W, tw);
@@ -503,7 +503,7 @@ extern "C" int cpx_qc_rps(cpx_ctx* ctx, const uint16_t* raw_dev, const void* ill
     CPX_CHECK_HIP(hipStreamSynchronize(ctx->stream));  // host vectors go out of scope
     ctx->qc_H = H;
     ctx->qc_W = W;
-    ctx->qc_tw = misc;
+    ctx->qc_gen = ctx->ws_gen[WS_QC_MISC];
   }
   const size_t rows_bytes = sizeof(cplx) * (size_t)n_planes * H * KC;
   const size_t ring_bytes = sizeof(double) * (size_t)n_planes * KC * std::max(n_rings, 1);

@@ -317,13 +317,14 @@ extern "C" int cpx_rebin_u16(cpx_ctx* ctx, const uint16_t* src_dev, int G, int H
   const int key[4] = {W, out_w, H, out_h};
   // the vertical bounds depend on whether a horizontal pass runs; H == out_h only happens
   // together with need_h, so (W, out_w, H, out_h) identifies the tables
-  if (!std::equal(key, key + 4, ctx->rebin_key)) {
+  if (!std::equal(key, key + 4, ctx->rebin_key) || ctx->rebin_gen != ctx->ws_gen[WS_REBIN]) {
     CPX_CHECK_HIP(hipStreamSynchronize(ctx->stream));  // earlier launches may read the old tables
     CPX_CHECK_HIP(hipMemcpy(tab, bh.data(), nbh, hipMemcpyHostToDevice));
     CPX_CHECK_HIP(hipMemcpy(tab + o_bv, bv.data(), nbv, hipMemcpyHostToDevice));
     CPX_CHECK_HIP(hipMemcpy(tab + o_kh, kh.data(), nkh, hipMemcpyHostToDevice));
     CPX_CHECK_HIP(hipMemcpy(tab + o_kv, kv.data(), nkv, hipMemcpyHostToDevice));
     std::copy(key, key + 4, ctx->rebin_key);
+    ctx->rebin_gen = ctx->ws_gen[WS_REBIN];
   }
   const int2* dbh = (const int2*)tab;
   const int2* dbv = (const int2*)(tab + o_bv);

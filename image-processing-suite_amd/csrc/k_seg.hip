@@ -240,6 +240,8 @@ __global__ __launch_bounds__(kT) void k_seg_tiles(const float* __restrict__ corr
     }
     if (layout == CPX_TILE_F32_NCHW)
       static_cast<float*>(tiles)[(ntile * nchan + ch) * npx + q] = out;
+    else if (layout == CPX_TILE_F32_NHWC)
+      static_cast<float*>(tiles)[(ntile * npx + q) * nchan + ch] = out;
     else
       static_cast<unsigned short*>(tiles)[(ntile * npx + q) * nchan + ch] = f2bf16(out);
   }
@@ -270,6 +272,7 @@ __global__ __launch_bounds__(kT) void k_seg_average(const void* __restrict__ net
       for (int c = 0; c < nout && c < 4; ++c) {
         float v;
         if (layout == CPX_TILE_F32_NCHW) v = static_cast<const float*>(net)[(t * nout + c) * npx + o];
+        else if (layout == CPX_TILE_F32_NHWC) v = static_cast<const float*>(net)[(t * npx + o) * nout + c];
         else v = bf162f(static_cast<const unsigned short*>(net)[(t * npx + o) * nout + c]);
         acc[c] = acc[c] + v * m;
       }
@@ -1053,17 +1056,413 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
         s1 += sred[w][1];
       }
       const double err = 0.0 + s0 / (double)o.area + s1 / (double)o.area;
-      bad[(long long)fov * (max_label + 1) + L] = err > thr ? 1 : 0;
+      bad[(long long)fov * (max_label + 1) + L] = err > thr ? 1 : 2;
     }
     __syncthreads();
   }
 }
 
-// masks too large for either LDS kernel: one block per FOV walks them with a two-buffer Jacobi
-// in a per-FOV global scratch (no two blocks share a scratch area)
+// k_flow_error_cmp: the same per-mask diffusion for masks whose full (bh + 2) x stride grid does
+// not fit the large LDS kernel: T holds only each row's span of mask cells (row y keeps the
+// column pairs [pb, pe] covering its mask pixels, at T2[base + p]); every cell outside a row's
+// span is a non-mask cell of the reference's grid, which stays 0.0 for the whole diffusion, so
+// reads there return zero.  Round masks keep ~80 % of their bbox, which takes masks up to about
+// 155 x 155 px in one CU.  One unit (2 columns x kFeKS rows) per thread; masks with more units,
+// more than kCmpRows rows or more cells are left to k_flow_error_big (their flag stays 0).
+constexpr int kCmpRows = 256;
+
+template <int THREADS, int CELLS, int U>
+__global__ __launch_bounds__(THREADS, 1) void k_flow_error_cmp(
+    const int* __restrict__ m0, const float2* __restrict__ dpf, int Dy, int Dx, int B, int max_label,
+    const cpx_object* __restrict__ objects, const int* __restrict__ off, int* __restrict__ ctr,
+    int lo_threads, int lo_units, int lo_cells, double thr, unsigned char* __restrict__ bad) {
+  __shared__ __attribute__((aligned(16))) double T[CELLS];
+  __shared__ int2 rowt[kCmpRows + 2];  // (base, pb | pe << 16) per T row; empty: pb 1, pe 0
+  __shared__ double sred[THREADS / 64][2];
+  __shared__ unsigned long long sbest[THREADS / 64];
+  __shared__ double smed[2];
+  __shared__ int sitem, stot;
+  const long long n = (long long)Dy * Dx;
+  const int total = off[B];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const double2 z2 = {0.0, 0.0};
+  while (true) {
+    if (tid == 0) sitem = atomicAdd(ctr, 1);
+    __syncthreads();
+    const int item = sitem;
+    __syncthreads();
+    if (item >= total) break;
+    int fov = 0;
+    while (fov + 1 < B && off[fov + 1] <= item) ++fov;
+    const int kobj = item - off[fov];
+    const cpx_object o = objects[(long long)fov * max_label + kobj];
+    const int L = o.label;
+    const int r0 = o.bbox[0], c0 = o.bbox[1];
+    const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
+    // block-uniform: the smaller kernels' masks, and masks beyond this kernel's limits
+    if (fe_fits(bh, bw, lo_threads, lo_units, lo_cells)) continue;
+    const int nsr = (bh + kFeKS - 1) / kFeKS;
+    const int ncp = (bw + 1) / 2;
+    if (bh > kCmpRows || (long long)ncp * nsr > (long long)THREADS * U) continue;
+    const int* lab = m0 + (long long)fov * n;
+    // ---- coordinate counts (medians) and per-row column extents, in the T area as ints
+    int* rowc = reinterpret_cast<int*>(T);
+    int* colc = rowc + bh;
+    int* rmn = colc + bw;
+    int* rmx = rmn + bh;
+    for (int i = tid; i < bh + bw; i += THREADS) rowc[i] = 0;
+    for (int i = tid; i < bh; i += THREADS) {
+      rmn[i] = INT_MAX;
+      rmx[i] = -1;
+    }
+    __syncthreads();
+    const int nb = bh * bw;
+    for (int p = tid; p < nb; p += THREADS) {
+      const int rr = p / bw, cc = p - rr * bw;
+      if (lab[(long long)(r0 + rr) * Dx + c0 + cc] == L) {
+        atomicAdd(&rowc[rr], 1);
+        atomicAdd(&colc[cc], 1);
+        atomicMin(&rmn[rr], cc);
+        atomicMax(&rmx[rr], cc);
+      }
+    }
+    __syncthreads();
+    if (tid < 2) {
+      const int* hc = tid == 0 ? rowc : colc;
+      const int len = tid == 0 ? bh : bw;
+      const long long cntn = o.area;
+      const long long ka = (cntn - 1) / 2, kb = cntn / 2;
+      long long cum = 0;
+      int va = -1, vb = -1;
+      for (int i = 0; i < len; ++i) {
+        cum += hc[i];
+        if (va < 0 && cum > ka) va = i;
+        if (vb < 0 && cum > kb) { vb = i; break; }
+      }
+      smed[tid] = ((double)(va + 1) + (double)(vb + 1)) / 2.0;
+    }
+    if (tid == 64) {  // row spans (T coordinates: row rr + 1, column cc + 1)
+      int tot = 0;
+      rowt[0] = make_int2(0, 1);
+      for (int y = 1; y <= bh; ++y) {
+        const int rr = y - 1;
+        if (rmx[rr] < 0) {
+          rowt[y] = make_int2(0, 1);
+        } else {
+          const int pb = (rmn[rr] + 1) >> 1, pe = (rmx[rr] + 1) >> 1;
+          rowt[y] = make_int2(tot - pb, pb | (pe << 16));
+          tot += pe - pb + 1;
+        }
+      }
+      rowt[bh + 1] = make_int2(0, 1);
+      stot = tot;
+    }
+    __syncthreads();
+    const int tot2 = stot;
+    if (2 * tot2 > CELLS) continue;  // block-uniform: left for k_flow_error_big
+    // ---- argmin of (x-xmed)^2 + (y-ymed)^2, first in row-major order on ties
+    const double ymed = smed[0], xmed = smed[1];
+    unsigned long long best = ~0ull;
+    for (int p = tid; p < nb; p += THREADS) {
+      const int rr = p / bw, cc = p - rr * bw;
+      if (lab[(long long)(r0 + rr) * Dx + c0 + cc] != L) continue;
+      const double dy = (double)(rr + 1) - ymed, dx = (double)(cc + 1) - xmed;
+      const double dist = dx * dx + dy * dy;
+      const unsigned long long key = ((unsigned long long)(dist * 4.0) << 32) | (unsigned int)p;
+      best = key < best ? key : best;
+    }
+    best = wave_min(best);
+    if (lane == 0) sbest[wid] = best;
+    __syncthreads();
+    unsigned long long bsel = sbest[0];
+    for (int w = 1; w < THREADS / 64; ++w) bsel = sbest[w] < bsel ? sbest[w] : bsel;
+    const int pbest = (int)(bsel & 0xffffffffu);
+    const int ym = pbest / bw + 1, xm = pbest % bw + 1;
+    const int niter = 2 * ((bw - 1) + (bh - 1));
+    // ---- this thread's units (u = tid + i THREADS): columns X, X + 1 (X = 2m + 1), rows Y0 ..
+    unsigned int um[U][2];
+    int X[U], Y0[U];
+    bool cown = false;
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      const int u = tid + i * THREADS;
+      um[i][0] = um[i][1] = 0u;
+      X[i] = 1;
+      Y0[i] = 1;
+      if (u < ncp * nsr) {
+        X[i] = 2 * (u % ncp) + 1;
+        Y0[i] = 1 + (u / ncp) * kFeKS;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (X[i] + h > bw) continue;
+          unsigned int m = 0u;
+          for (int j = 0; j < kFeKS && Y0[i] + j <= bh; ++j)
+            if (lab[(long long)(r0 + Y0[i] - 1 + j) * Dx + c0 + X[i] + h - 1] == L) m |= 1u << j;
+          um[i][h] = m;
+          if (X[i] + h == xm && ym >= Y0[i] && ym < Y0[i] + kFeKS) cown = true;
+        }
+      }
+    }
+    __syncthreads();  // rowc / colc / extents read: T is cleared next
+    for (int i = tid; i < 2 * tot2; i += THREADS) T[i] = 0.0;
+    __syncthreads();
+    const int cidx = 2 * (rowt[ym].x + (xm >> 1)) + (xm & 1);
+    if (tid == 0 && niter > 0) T[cidx] = 1.0;  // the first iteration's T[centre] += 1
+    __syncthreads();
+    const double2* T2 = reinterpret_cast<const double2*>(T);
+    auto ldrow = [&](int y, int pa, double2& a, double2& b) {
+      // opaque row index: keeps the compiler from hoisting every row's span lookup out of the
+      // iteration loop (14 rows x U units of registers)
+      asm volatile("" : "+v"(y));
+      const int2 rt = rowt[y];
+      const int lo = rt.y & 0xffff, hi = rt.y >> 16;
+      a = (pa >= lo && pa <= hi) ? T2[rt.x + pa] : z2;
+      b = (pa + 1 >= lo && pa + 1 <= hi) ? T2[rt.x + pa + 1] : z2;
+    };
+    double nv[U][2][kFeKS];
+    for (int it = 0; it < niter; ++it) {
+#pragma unroll
+      for (int i = 0; i < U; ++i) {
+        if (!(um[i][0] | um[i][1])) continue;
+        const int pa = (X[i] - 1) >> 1;  // column pairs (X - 1, X) and (X + 1, X + 2)
+        double2 ua, ub, ca, cb, da, db;
+        ldrow(Y0[i] - 1, pa, ua, ub);
+        ldrow(Y0[i], pa, ca, cb);
+        ldrow(min(Y0[i] + 1, bh + 1), pa, da, db);
+#pragma unroll
+        for (int j = 0; j < kFeKS; ++j) {
+          double2 na = z2, nb2 = z2;
+          if (j + 1 < kFeKS) ldrow(min(Y0[i] + j + 2, bh + 1), pa, na, nb2);
+          // column X: l = a.x, c = a.y, r = b.x;  column X + 1: l = a.y, c = b.x, r = b.y
+          nv[i][0][j] = 1 / 9. * (ca.y + ua.y + da.y + ca.x + cb.x + ua.x + ub.x + da.x + db.x);
+          nv[i][1][j] = 1 / 9. * (cb.x + ub.x + db.x + ca.y + cb.y + ua.y + ub.y + da.y + db.y);
+          ua = ca; ub = cb;
+          ca = da; cb = db;
+          da = na; db = nb2;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < U; ++i) {
+        if (!(um[i][0] | um[i][1])) continue;
+        const int pa = (X[i] - 1) >> 1;
+        // opaque copies: the per-row write predicates are not hoisted out of the iteration loop
+        unsigned int m0 = um[i][0], m1 = um[i][1];
+        asm volatile("" : "+v"(m0), "+v"(m1));
+#pragma unroll
+        for (int j = 0; j < kFeKS; ++j) {
+          if (!(((m0 | m1) >> j) & 1u)) continue;
+          int y = Y0[i] + j;
+          asm volatile("" : "+v"(y));
+          const int base = rowt[y].x;
+          if ((m0 >> j) & 1u) T[2 * (base + pa) + 1] = nv[i][0][j];
+          if ((m1 >> j) & 1u) T[2 * (base + pa + 1)] = nv[i][1][j];
+        }
+      }
+      if (cown && it + 1 < niter) T[cidx] = T[cidx] + 1.0;
+      __syncthreads();
+    }
+    // ---- gradients, normalisation, error vs dP/5
+    auto ld1 = [&](int y, int x) -> double {
+      const int2 rt = rowt[y];
+      const int p = x >> 1;
+      return (p >= (rt.y & 0xffff) && p <= (rt.y >> 16)) ? T[2 * (rt.x + p) + (x & 1)] : 0.0;
+    };
+    const float2* F = dpf + (long long)fov * n;
+    double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        for (int j = 0; j < kFeKS; ++j) {
+          if (!((um[i][h] >> j) & 1u)) continue;
+          const int Y = Y0[i] + j, Xc = X[i] + h;
+          const double dy = ld1(Y + 1, Xc) - ld1(Y - 1, Xc);
+          const double dx = ld1(Y, Xc + 1) - ld1(Y, Xc - 1);
+          const double nrm = 1e-20 + sqrt(dy * dy + dx * dx);
+          const double my = dy / nrm, mx = dx / nrm;
+          const float2 f = F[(long long)(r0 + Y - 1) * Dx + c0 + Xc - 1];
+          const double ty = my - (double)(f.x / 5.0f);
+          const double tx = mx - (double)(f.y / 5.0f);
+          e0 += ty * ty;
+          e1 += tx * tx;
+        }
+      }
+    }
+    e0 = wave_sum(e0);
+    e1 = wave_sum(e1);
+    if (lane == 0) {
+      sred[wid][0] = e0;
+      sred[wid][1] = e1;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int w = 0; w < THREADS / 64; ++w) {
+        s0 += sred[w][0];
+        s1 += sred[w][1];
+      }
+      const double err = 0.0 + s0 / (double)o.area + s1 / (double)o.area;
+      bad[(long long)fov * (max_label + 1) + L] = err > thr ? 1 : 2;
+    }
+    __syncthreads();
+  }
+}
+
+// masks beyond the LDS kernels: one 1024-thread block per mask (dynamic queue over the batch),
+// a two-buffer Jacobi over the mask's pixel list in a block-private slice of global scratch
+// (L2-resident for the masks that reach here); the centre's +1 is applied by the thread that
+// writes the centre, so each iteration needs one barrier.  Masks that do not fit a slice (and
+// are not flagged yet) are left to k_flow_error_fov.
+constexpr int kBigThreads = 1024;
+
+__global__ __launch_bounds__(kBigThreads) void k_flow_error_big(
+    const int* __restrict__ m0, const float2* __restrict__ dpf, int Dy, int Dx, int B, int max_label,
+    const cpx_object* __restrict__ objects, const int* __restrict__ off, int* __restrict__ ctr,
+    int lo_threads, int lo_units, int lo_cells, double thr, double* __restrict__ gscratch,
+    long long slice, unsigned char* __restrict__ bad) {
+  __shared__ int rowc[2112];
+  __shared__ int colc[2112];
+  __shared__ double sred[kBigThreads / 64][2];
+  __shared__ unsigned long long sbest[kBigThreads / 64];
+  __shared__ double smed[2];
+  __shared__ int sitem, snpix;
+  const long long n = (long long)Dy * Dx;
+  const int total = off[B];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  double* T0 = gscratch + (long long)blockIdx.x * slice;
+  while (true) {
+    if (tid == 0) sitem = atomicAdd(ctr, 1);
+    __syncthreads();
+    const int item = sitem;
+    __syncthreads();
+    if (item >= total) break;
+    int fov = 0;
+    while (fov + 1 < B && off[fov + 1] <= item) ++fov;
+    const int kobj = item - off[fov];
+    const cpx_object o = objects[(long long)fov * max_label + kobj];
+    const int L = o.label;
+    const int r0 = o.bbox[0], c0 = o.bbox[1];
+    const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
+    if (fe_fits(bh, bw, lo_threads, lo_units, lo_cells)) continue;       // the small kernels'
+    if (bad[(long long)fov * (max_label + 1) + L] != 0) continue;        // k_flow_error_cmp's
+    const int ly = bh + 2, lx = bw + 2;
+    const long long ncell = (long long)ly * lx;
+    const int nb = bh * bw;
+    if (bh > 2112 || bw > 2112 || 2 * ncell + (nb + 1) / 2 + 2 > slice) continue;  // k_flow_error_fov
+    double* Tc = T0;
+    double* Tn = T0 + ncell;
+    int* plist = reinterpret_cast<int*>(T0 + 2 * ncell);
+    for (long long i = tid; i < 2 * ncell; i += kBigThreads) T0[i] = 0.0;
+    for (int i = tid; i < bh + bw; i += kBigThreads) (i < bh ? rowc[i] : colc[i - bh]) = 0;
+    if (tid == 0) snpix = 0;
+    __syncthreads();
+    const int* lab = m0 + (long long)fov * n;
+    for (int p = tid; p < nb; p += kBigThreads) {
+      const int rr = p / bw, cc = p - rr * bw;
+      const bool in = lab[(long long)(r0 + rr) * Dx + c0 + cc] == L;
+      if (in) {
+        atomicAdd(&rowc[rr], 1);
+        atomicAdd(&colc[cc], 1);
+      }
+      const unsigned long long bal = __ballot(in);
+      int base = 0;
+      if (lane == 0 && bal) base = atomicAdd(&snpix, __popcll(bal));
+      base = __shfl(base, 0);
+      if (in) plist[base + __popcll(bal & ((1ull << lane) - 1ull))] = (rr + 1) * lx + cc + 1;
+    }
+    __syncthreads();
+    const int npix = snpix;
+    if (tid < 2) {
+      const int* hc = tid == 0 ? rowc : colc;
+      const int len = tid == 0 ? bh : bw;
+      const long long cntn = o.area;
+      const long long ka = (cntn - 1) / 2, kb = cntn / 2;
+      long long cum = 0;
+      int va = -1, vb = -1;
+      for (int i = 0; i < len; ++i) {
+        cum += hc[i];
+        if (va < 0 && cum > ka) va = i;
+        if (vb < 0 && cum > kb) { vb = i; break; }
+      }
+      smed[tid] = ((double)(va + 1) + (double)(vb + 1)) / 2.0;
+    }
+    __syncthreads();
+    const double ymed = smed[0], xmed = smed[1];
+    unsigned long long best = ~0ull;
+    for (int p = tid; p < nb; p += kBigThreads) {
+      const int rr = p / bw, cc = p - rr * bw;
+      if (lab[(long long)(r0 + rr) * Dx + c0 + cc] != L) continue;
+      const double dy = (double)(rr + 1) - ymed, dx = (double)(cc + 1) - xmed;
+      const double dist = dx * dx + dy * dy;
+      const unsigned long long key = ((unsigned long long)(dist * 4.0) << 32) | (unsigned int)p;
+      best = key < best ? key : best;
+    }
+    best = wave_min(best);
+    if (lane == 0) sbest[wid] = best;
+    __syncthreads();
+    unsigned long long bsel = sbest[0];
+    for (int w = 1; w < kBigThreads / 64; ++w) bsel = sbest[w] < bsel ? sbest[w] : bsel;
+    const int pbest = (int)(bsel & 0xffffffffu);
+    const int cidx = (pbest / bw + 1) * lx + pbest % bw + 1;
+    const int niter = 2 * ((bw - 1) + (bh - 1));
+    if (tid == 0 && niter > 0) Tc[cidx] = 1.0;
+    __syncthreads();
+    for (int it = 0; it < niter; ++it) {
+      const bool inc = it + 1 < niter;
+      for (int i = tid; i < npix; i += kBigThreads) {
+        const int q = plist[i];
+        double v = 1 / 9. * (Tc[q] + Tc[q - lx] + Tc[q + lx] + Tc[q - 1] + Tc[q + 1] + Tc[q - lx - 1] +
+                             Tc[q - lx + 1] + Tc[q + lx - 1] + Tc[q + lx + 1]);
+        if (q == cidx && inc) v = v + 1.0;  // the next iteration's T[centre] += 1
+        Tn[q] = v;
+      }
+      __syncthreads();
+      double* t = Tc;
+      Tc = Tn;
+      Tn = t;
+    }
+    const float2* F = dpf + (long long)fov * n;
+    double e0 = 0.0, e1 = 0.0;
+    for (int i = tid; i < npix; i += kBigThreads) {
+      const int q = plist[i];
+      const int y = q / lx, x = q - (q / lx) * lx;
+      const double dy = Tc[q + lx] - Tc[q - lx];
+      const double dx = Tc[q + 1] - Tc[q - 1];
+      const double nrm = 1e-20 + sqrt(dy * dy + dx * dx);
+      const double my = dy / nrm, mx = dx / nrm;
+      const float2 f = F[(long long)(r0 + y - 1) * Dx + c0 + x - 1];
+      const double ty = my - (double)(f.x / 5.0f);
+      const double tx = mx - (double)(f.y / 5.0f);
+      e0 += ty * ty;
+      e1 += tx * tx;
+    }
+    e0 = wave_sum(e0);
+    e1 = wave_sum(e1);
+    if (lane == 0) {
+      sred[wid][0] = e0;
+      sred[wid][1] = e1;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int w = 0; w < kBigThreads / 64; ++w) {
+        s0 += sred[w][0];
+        s1 += sred[w][1];
+      }
+      const double err = 0.0 + s0 / (double)o.area + s1 / (double)o.area;
+      bad[(long long)fov * (max_label + 1) + L] = err > thr ? 1 : 2;
+    }
+    __syncthreads();
+  }
+}
+
+// last resort for masks no block slice holds: one block per FOV walks them with a two-buffer
+// Jacobi in the FOV's whole scratch (no two blocks share a scratch area)
 constexpr int kFlowThreads = 256;
 
-__global__ __launch_bounds__(kFlowThreads) void k_flow_error_big(
+__global__ __launch_bounds__(kFlowThreads) void k_flow_error_fov(
     const int* __restrict__ m0, const float2* __restrict__ dpf, int Dy, int Dx, int max_label,
     const cpx_object* __restrict__ objects, const cpx_fov_objects* __restrict__ hdr, int lds_threads,
     int lds_units, int lds_cells, double thr, double* __restrict__ gscratch,
@@ -1083,6 +1482,7 @@ __global__ __launch_bounds__(kFlowThreads) void k_flow_error_big(
   const int r0 = o.bbox[0], c0 = o.bbox[1];
   const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
   if (fe_fits(bh, bw, lds_threads, lds_units, lds_cells)) continue;  // block-uniform: an LDS kernel's
+  if (bad[(long long)fov * (max_label + 1) + L] != 0) continue;      // or an earlier kernel's
   const int ly = bh + 2, lx = bw + 2;
   const int ncell = ly * lx;
   double* T0 = gscratch + (long long)fov * gscratch_per_fov;
@@ -1188,7 +1588,7 @@ __global__ __launch_bounds__(kFlowThreads) void k_flow_error_big(
       s1 += sred[w][1];
     }
     const double err = 0.0 + s0 / (double)o.area + s1 / (double)o.area;
-    bad[(long long)fov * (max_label + 1) + L] = err > thr ? 1 : 0;
+    bad[(long long)fov * (max_label + 1) + L] = err > thr ? 1 : 2;
   }
   __syncthreads();
   }  // object loop
@@ -1202,14 +1602,14 @@ __global__ __launch_bounds__(kT) void k_apply_bad(long long n, int max_label,
   if (q >= n) return;
   int* m = m0 + (long long)fov * n + q;
   const int l = *m;
-  if (l > 0 && l <= max_label && bad[(long long)fov * (max_label + 1) + l]) *m = 0;
+  if (l > 0 && l <= max_label && bad[(long long)fov * (max_label + 1) + l] == 1) *m = 0;
 }
 
 __global__ void k_count_bad(int max_label, const unsigned char* __restrict__ bad,
                             cpx_seg_stats* __restrict__ st) {
   const int fov = blockIdx.x;
   int c = 0;
-  for (int l = threadIdx.x; l <= max_label; l += blockDim.x) c += bad[(long long)fov * (max_label + 1) + l];
+  for (int l = threadIdx.x; l <= max_label; l += blockDim.x) c += bad[(long long)fov * (max_label + 1) + l] == 1;
   c = wave_sum(c);
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(&st[fov].n_bad_flow, c);
 }
@@ -1449,7 +1849,7 @@ int seg_tables(cpx_ctx* ctx, int H, int W, int Ly, int Lx, SegTabs& t) {
   t.ux.i1 = up + 3 * H + W;
   t.ux.w = (const float*)(up + 3 * H + 2 * W);
   const int key[6] = {H, W, Ly, Lx, 2, 0};
-  bool same = ctx->seg_tab == buf;
+  bool same = ctx->seg_gen == ctx->ws_gen[WS_SEG_TAB];
   for (int i = 0; i < 6; ++i) same = same && ctx->seg_key[i] == key[i];
   if (same) return CPX_OK;
   std::vector<int> h(words);
@@ -1464,7 +1864,7 @@ int seg_tables(cpx_ctx* ctx, int H, int W, int Ly, int Lx, SegTabs& t) {
   CPX_CHECK_HIP(hipMemcpyAsync(buf, h.data(), words * 4, hipMemcpyHostToDevice, ctx->stream));
   CPX_CHECK_HIP(hipStreamSynchronize(ctx->stream));
   for (int i = 0; i < 6; ++i) ctx->seg_key[i] = key[i];
-  ctx->seg_tab = buf;
+  ctx->seg_gen = ctx->ws_gen[WS_SEG_TAB];
   return CPX_OK;
 }
 
@@ -1511,8 +1911,8 @@ extern "C" int cpx_seg_tiles(cpx_ctx* ctx, const float* corr_dev, int B, int C, 
   CPX_REQUIRE(geom_ok(geom), CPX_ERR_ARG, "cpx_seg_tiles: bad geometry");
   CPX_REQUIRE(B > 0 && B <= 65535 && nchan > 0 && nchan <= C && H > 0 && W > 0, CPX_ERR_ARG,
               "cpx_seg_tiles: bad sizes");
-  CPX_REQUIRE(layout == CPX_TILE_F32_NCHW || layout == CPX_TILE_BF16_NHWC, CPX_ERR_ARG,
-              "cpx_seg_tiles: bad layout %d", layout);
+  CPX_REQUIRE(layout == CPX_TILE_F32_NCHW || layout == CPX_TILE_BF16_NHWC || layout == CPX_TILE_F32_NHWC,
+              CPX_ERR_ARG, "cpx_seg_tiles: bad layout %d", layout);
   SegTabs t;
   int rc = seg_tables(ctx, H, W, geom->Ly, geom->Lx, t);
   if (rc) return rc;
@@ -1558,6 +1958,7 @@ __global__ void k_seed_count(int B, const int* __restrict__ totals, cpx_seg_stat
 constexpr int kFeSmallThreads = 256, kFeSmallCells = 5000;    // 40 KiB: 4 blocks per CU
 constexpr int kFeMidThreads = 512, kFeMidCells = 10176;       // 80 KiB: 2 blocks per CU
 constexpr int kFeLargeThreads = 1024, kFeLargeCells = 20224;  // 158 KiB: 1 block per CU
+constexpr int kFeCmpThreads = 1024, kFeCmpU = 1, kFeCmpCells = 19968;  // compact rows: 156 KiB + rows
 constexpr int kFeU = 1;                                        // 2-column x 12-row units per thread
 
 extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx_seg_geom* geom,
@@ -1567,7 +1968,9 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   CPX_REQUIRE(ctx && yf_dev && labels_dev && stats_dev, CPX_ERR_ARG, "cpx_seg_masks: null argument");
   CPX_REQUIRE(geom_ok(geom), CPX_ERR_ARG, "cpx_seg_masks: bad geometry");
   CPX_REQUIRE(B > 0 && B <= 65535 && H > 0 && W > 0 && niter >= 0 && max_objects > 0 &&
-                  (long long)(H + 2 * kRpad) * (W + 2 * kRpad) < (1LL << 31),
+                  (long long)(H + 2 * kRpad) * (W + 2 * kRpad) < (1LL << 31) &&
+                  // k_dyn_follow addresses the float2 field with 32-bit byte offsets
+                  (long long)H * W * (long long)sizeof(float2) < (1LL << 32),
               CPX_ERR_ARG, "cpx_seg_masks: bad sizes");
   const int Ly = geom->Ly, Lx = geom->Lx;
   const int Dy = resample ? H : Ly, Dx = resample ? W : Lx;  // dynamics resolution
@@ -1675,7 +2078,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   const size_t sz_l2i = al(sizeof(int) * (size_t)B * (ML + 1));
   const size_t sz_abs = al(sizeof(int) * (size_t)B * ML);
   const size_t sz_nl = sz_abs;
-  const size_t sz_off = al(sizeof(int) * (size_t)(B + 1 + 3));
+  const size_t sz_off = al(sizeof(int) * (size_t)(B + 1 + 4));  // prefix + 4 queue counters
   const size_t gscr_per = (size_t)2 * (Dy + 2) * (Dx + 2);  // doubles per FOV (oversize masks)
   const size_t sz_gscr = al(sizeof(double) * B * gscr_per);
   unsigned char* o = (unsigned char*)cpx_ws(ctx, WS_SEG_OBJ,
@@ -1694,7 +2097,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
     rc = cpx_objects(ctx, d.m0, B, Dy, Dx, ML, 0, lst, obj, hdr);
     if (rc) return rc;
     CPX_CHECK_HIP(hipMemsetAsync(bad, 0, sz_bad, ctx->stream));
-    CPX_CHECK_HIP(hipMemsetAsync(off + B + 1, 0, 3 * sizeof(int), ctx->stream));
+    CPX_CHECK_HIP(hipMemsetAsync(off + B + 1, 0, 4 * sizeof(int), ctx->stream));
     hipLaunchKernelGGL(k_obj_prefix, dim3(1), dim3(64), 0, ctx->stream, B,
                        (const cpx_fov_objects*)hdr, off);
     hipLaunchKernelGGL((k_flow_error_lds<kFeSmallThreads, kFeSmallCells, kFeU>), dim3(4 * ctx->n_cu),
@@ -1705,13 +2108,21 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
                        dim3(kFeMidThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
                        Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 2,
                        kFeSmallThreads, kFeU, kFeSmallCells, flow_threshold, bad);
-    hipLaunchKernelGGL((k_flow_error_lds<kFeLargeThreads, kFeLargeCells, kFeU>), dim3(ctx->n_cu),
-                       dim3(kFeLargeThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
+    hipLaunchKernelGGL((k_flow_error_cmp<kFeCmpThreads, kFeCmpCells, kFeCmpU>), dim3(ctx->n_cu),
+                       dim3(kFeCmpThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
                        Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 3,
                        kFeMidThreads, kFeU, kFeMidCells, flow_threshold, bad);
-    hipLaunchKernelGGL(k_flow_error_big, dim3(B), dim3(kFlowThreads), 0, ctx->stream,
+    {
+      const int nbig = std::max(1, std::min(ctx->n_cu, 4 * B));
+      const long long slice = (long long)(B * gscr_per / nbig) & ~1LL;
+      hipLaunchKernelGGL(k_flow_error_big, dim3(nbig), dim3(kBigThreads), 0, ctx->stream,
+                         (const int*)d.m0, (const float2*)d.dpf, Dy, Dx, B, ML, (const cpx_object*)obj,
+                         (const int*)off, off + B + 4, kFeMidThreads, kFeU, kFeMidCells, flow_threshold,
+                         gscr, slice, bad);
+    }
+    hipLaunchKernelGGL(k_flow_error_fov, dim3(B), dim3(kFlowThreads), 0, ctx->stream,
                        (const int*)d.m0, (const float2*)d.dpf, Dy, Dx, ML, (const cpx_object*)obj,
-                       (const cpx_fov_objects*)hdr, kFeLargeThreads, kFeU, kFeLargeCells,
+                       (const cpx_fov_objects*)hdr, kFeMidThreads, kFeU, kFeMidCells,
                        flow_threshold, gscr, (long long)gscr_per, bad);
     hipLaunchKernelGGL(k_apply_bad, gp, dim3(kT), 0, ctx->stream, n, ML,
                        (const unsigned char*)bad, d.m0);

@@ -327,6 +327,7 @@ typedef struct cpx_seg_stats {
 
 #define CPX_TILE_F32_NCHW 0  /* tiles/net output as float32 [n][c][by][bx]                   */
 #define CPX_TILE_BF16_NHWC 1 /* tiles/net output as bfloat16 [n][by][bx][c] (channels_last)  */
+#define CPX_TILE_F32_NHWC 2  /* tiles/net output as float32 [n][by][bx][c] (channels_last)    */
 
 /* normalize99 statistics: pct_dev float64 [B][nchan][2] = (p1, p99) of channels 0..nchan-1 of
  * each FOV (exact order statistics of the fp32 corrected planes, linear interpolation).       */
@@ -405,6 +406,40 @@ int cpx_cpnet_conv3x3_head(cpx_ctx* ctx, const void* in, int N, int H, int W, in
 int cpx_cpnet_stem(cpx_ctx* ctx, const void* x, int N, int H, int W, const float* scale0,
                    const float* shift0, const float* w0, const float* bias0, const float* scale1,
                    const float* shift1, const float* wp, void* p_out, void* z_out);
+
+/* ---- a6 CPnet at the reference's precision (split fp16, "f16x3") ---------------------------
+ * The fp32 U-Net the reference runs (Cellpose_GPU_s3fs.py:108,143: CellposeModel without half
+ * precision) on the fp16 matrix cores.  Activations are "split" tensors: NHWC, channels in slabs
+ * of 16, per pixel and slab 16 f16 hi halves then 16 f16 lo halves (4 bytes per channel), value
+ * = hi + lo * 2^-11 (hi = f16(a), lo = f16((a - hi) * 2^11)); weights are packed split by the
+ * host as [cout/bm][cin/16][ky][kx][bm][hi|lo][16] f16 (bm from cpx_cpnet_x3_cfg).  Every
+ * product is formed as wh*xh + (wh*xl + wl*xh) * 2^-11 in fp32 (three v_mfma_f32_32x32x16_f16
+ * per 16 channels), ~2^-22 relative per operand: the fp32 network to its rounding noise.
+ * *ovf (device int, optional) is OR-ed with 1 when a stored activation is not below 65504.
+ * cpx_cpnet_x3_conv: ks = 3 (pad 1) or 1 (the block projections); the epilogue of
+ * cpx_cpnet_conv3x3 (bias, res [split, res_up], y_out, style [N][style_stride], scale/shift,
+ * relu, z_out [z_up]) or, for the last 3x3 convolution (cout 32), the output head:
+ * head_out fp32 [N][H][W][n_head] = head_b + head_w [n_head][32] . z (z in fp32).             */
+int cpx_cpnet_x3_cfg(int ks, int cin, int cout, int variant, int* bm);
+int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* in, int N, int H, int W,
+                      int cin, int cout, const void* wpk, const float* bias, const void* res,
+                      int res_up, const float* style, int style_stride, const float* scale,
+                      const float* shift, int relu, void* y_out, void* z_out, int z_up,
+                      const float* head_w, const float* head_b, int n_head, float* head_out,
+                      int* ovf);
+/* stem on the fp32 network input x [N][H][W][2] (CPX_TILE_F32_NHWC tiles): z0 = relu(scale0 x
+ * + shift0), z_out = relu(scale1 (conv3x3(z0, w0) + bias0) + shift1), p_out = conv1x1(x, wp),
+ * fp32 arithmetic, split stores (32 channels).                                               */
+int cpx_cpnet_x3_stem(cpx_ctx* ctx, const float* x, int N, int H, int W, const float* scale0,
+                      const float* shift0, const float* w0, const float* bias0, const float* scale1,
+                      const float* shift1, const float* wp, void* p_out, void* z_out, int* ovf);
+/* 2x2/2 max-pool of split [N][2Hh][2Ww][Cn] -> x_out (exact) and z_out = relu?(scale x + shift). */
+int cpx_cpnet_x3_pool(cpx_ctx* ctx, const void* in, const float* scale, const float* shift,
+                      int relu, int N, int Hh, int Ww, int Cn, void* x_out, void* z_out, int* ovf);
+/* style vector of split x [N][H][W][C] (mean over pixels, L2-normalised; CPnet.forward) and the
+ * up path's Linear layers: out [N][J] = lin_b + lin_w [J][C] . style.                          */
+int cpx_cpnet_x3_style(cpx_ctx* ctx, const void* x, int N, int H, int W, int C, const float* lin_w,
+                       const float* lin_b, int J, float* out);
 
 /* ==== per-FOV drop-in boundary ============================================
  * Host planes in, host tables out, one context per GPU and one FOV at a time — the shape of the

@@ -8,9 +8,9 @@ on the same inputs.
   * Cells / Cytoplasm (marker watershed) bit-identical to ws_oracle.cells_watershed of those
     Nuclei (the sequential heap flood, pinned to skimage 0.18.3);
   * object tables bit-exact and all three feature tables within rtol 1e-5 of cpx_oracle.features;
-  * the bf16 CPnet's (and an fp32 GPU CPnet's) masks vs the same network in fp32 on the CPU,
-    then the oracle's dynamics: identical-mask and IoU-matched fractions (north_star asks for
-    identical IDs; recorded in DESIGN.md §6 and gpurun_out/e2e_seg_agreement.json).
+  * pipeline parity at the reference's precision: the default (f16x3) masks and object IDs
+    bit-identical to the fp32 CPU network + the restated dynamics on 8 FOVs of a bench batch,
+    two runs bit-identical; the bf16 variant recorded beside it.
 """
 import json
 import os
@@ -125,41 +125,85 @@ def _agreement(a, b):
             "matched_same_id": int(same_id), "mean_iou_matched": float(np.mean(ious)) if ious else 0.0}
 
 
-def test_e2e_network_precision_agreement(e2e, dev):
-    """Masks of the bf16 MFMA CPnet and of the same weights in fp32 on the GPU (eager PyTorch)
-    vs fp32 on the CPU, all followed by the same restated dynamics.  The dynamics amplify any
-    flow difference at mask boundaries, so identical masks need identical flows; the numbers
-    are recorded in DESIGN.md §6 (gpurun_out/e2e_seg_agreement.json).  Required: >= 90 % of the
-    fp32-CPU objects matched one-to-one (IoU >= 0.5) by the bf16 masks."""
+@pytest.fixture(scope="module")
+def ids8(dev):
+    """8 FOVs of the bench plate through the default pipeline (CPnet f16x3) twice, and the same
+    FOVs through Cellpose's CPnet in fp32 on the CPU followed by the restated dynamics."""
+    from cpx import shard
     from cpx.cpnet import build_cpnet
-    from cpx.segment import Segmenter
+    from cpx.pipeline import FovPipeline, PipelineConfig
+    from cpx.synth import synth_fovs, synth_illum
+    H = W = 2080
+    C, B = 5, 8
+    weights = os.path.join(REPO, "image-processing-suite_amd", "cpx", "weights", "cpnet_nuclei_synth.pt")
+    cfg = PipelineConfig(H=H, W=W, C=C, batch=B, weights=weights if os.path.exists(weights) else None)
+    assert cfg.cpnet_precision == "f16x3"
+    illum = synth_illum(C, H, W, seed=1)
+    pipe = FovPipeline(dev, cfg, illum)
+    mine = shard.shard(shard.plate_fovs(n_wells=384), 0, 1)
+    raw = synth_fovs(B, C, H, W, dev.torch_device, seed=shard.fov_seed(mine[0]) + 7919)  # bench batch 1
+    runs = []
+    for _ in range(2):
+        pipe.fetch(pipe.run(raw))
+        dev.sync()
+        runs.append(pipe.labels["Nuclei"].cpu().numpy().copy())
+    corr = pipe.corr.cpu().numpy()
+    del pipe
     torch.set_num_threads(16)
-    cfg = e2e["cfg"]
     net = build_cpnet(seed=cfg.seed, model=cfg.model, state_dict_path=cfg.weights)
-    H, W = cfg.H, cfg.W
-    B = e2e["yf"].shape[0]
     Ly, Lx = so.net_size(H, W, cfg.model, cfg.diameter)
-    seg32 = Segmenter(dev, H, W, B, model=cfg.model, diameter=cfg.diameter, weights=cfg.weights,
-                      seed=cfg.seed, use_graph=False, max_objects=cfg.max_objects,
-                      net_dtype=torch.float32, fused=False)
-    lab32 = seg32.segment(torch.from_numpy(e2e["corr"]).to(dev.torch_device)).cpu().numpy()
-    rows = []
+    cpu = []
     for b in range(B):
-        tiles, g = so.make_net_input(e2e["corr"][b], Ly, Lx)
+        tiles, g = so.make_net_input(corr[b], Ly, Lx)
         with torch.no_grad():
             y = net(torch.from_numpy(tiles)).numpy()
-        yf32 = so.average_tiles(y, g)
-        m_cpu = so.compute_masks(yf32, H, W)
-        r = {"fov": b, "max_abs_flow_diff_bf16": float(np.abs(yf32 - e2e["yf"][b]).max()),
-             "bf16_gpu_vs_fp32_cpu": _agreement(m_cpu, e2e["labels"]["Nuclei"][b]),
-             "fp32_gpu_vs_fp32_cpu": _agreement(m_cpu, lab32[b])}
+        cpu.append(so.compute_masks(so.average_tiles(y, g), H, W))
+    return dict(runs=runs, cpu=cpu, corr=corr, cfg=cfg)
+
+
+@pytest.mark.timeout(900)
+def test_e2e_object_ids_identical_to_fp32_cpu(ids8):
+    """north_star's bar: object IDs (and masks) identical to the CPU path.  The reference runs
+    the U-Net in fp32 (Cellpose_GPU_s3fs.py:108,143); the default CPnet precision (f16x3, native
+    split-fp16 MFMA kernels) gives labels bit-identical to the fp32 CPU network + the restated
+    dynamics on all 8 FOVs of a bench batch (recorded in gpurun_out/e2e_seg_agreement.json)."""
+    rows = []
+    for b, m_cpu in enumerate(ids8["cpu"]):
+        got = ids8["runs"][0][b]
+        r = {"fov": b, "objects": int(m_cpu.max()), "f16x3_gpu_vs_fp32_cpu": _agreement(m_cpu, got),
+             "pixels_differing": int((got != m_cpu).sum())}
         rows.append(r)
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     with open(os.path.join(REPO, "gpurun_out", "e2e_seg_agreement.json"), "w") as f:
         json.dump(rows, f, indent=1)
     print(json.dumps(rows))
     for r in rows:
-        assert r["bf16_gpu_vs_fp32_cpu"]["fraction_matched"] >= 0.9, r
+        assert r["objects"] >= 150
+        assert r["f16x3_gpu_vs_fp32_cpu"]["fraction_identical"] == 1.0, r
+        assert r["pixels_differing"] == 0, r
+
+
+def test_e2e_default_cpnet_deterministic(ids8):
+    """Two runs of the default pipeline on one batch: bit-identical masks (no float atomics in
+    the CPnet or the dynamics)."""
+    np.testing.assert_array_equal(ids8["runs"][0], ids8["runs"][1])
+
+
+@pytest.mark.timeout(600)
+def test_e2e_bf16_variant_agreement(ids8, dev):
+    """The named bf16 variant (not the default): recorded, with a loose bar — >= 90 % of the
+    fp32-CPU objects matched one-to-one (IoU >= 0.5); its IDs are not identical."""
+    from cpx.segment import Segmenter
+    cfg = ids8["cfg"]
+    H, W, B = cfg.H, cfg.W, len(ids8["cpu"])
+    seg = Segmenter(dev, H, W, B, model=cfg.model, diameter=cfg.diameter, weights=cfg.weights, seed=cfg.seed,
+                    use_graph=False, max_objects=cfg.max_objects, precision="bf16")
+    lab = seg.segment(torch.from_numpy(ids8["corr"]).to(dev.torch_device)).cpu().numpy()
+    rows = [_agreement(m, lab[b]) for b, m in enumerate(ids8["cpu"])]
+    with open(os.path.join(REPO, "gpurun_out", "e2e_seg_agreement_bf16.json"), "w") as f:
+        json.dump(rows, f, indent=1)
+    for r in rows:
+        assert r["fraction_matched"] >= 0.9, r
 
 
 def test_e2e_csv_tables(e2e, tmp_path):

@@ -131,6 +131,36 @@ def test_masks_full_resolution_bit_exact_vs_oracle(dev, H, W, rmax):
     assert st[2]["n_final"] == 0 and st[2]["n_moving"] == 0
 
 
+def test_flow_error_threshold_all_mask_sizes(dev):
+    """The flow-error decision for masks of every size class — the LDS kernels (bbox grid), the
+    compact-row LDS kernel (~110-155 px masks), the per-mask global kernel and the per-FOV last
+    resort — on flows scaled per object so that the error lands on either side of 0.4 ((1 - s)^2
+    sums to ~0.45 at s = 0.33 and ~0.36 at s = 0.40): labels bit-identical to the oracle, and
+    masks removed on both sides."""
+    H, W = 1400, 1400
+    g = make_geom(H, W)
+    yfs, n_obj = [], []
+    for seed in (5, 6):
+        lab = sg.labels(seed, g.Ly, g.Lx, n=14, rmin=6, rmax=24, skip_every=0)
+        mu = so.masks_to_flows(lab)
+        rng = np.random.default_rng(seed)
+        scale = np.ones(lab.max() + 1, np.float32)
+        scale[1:] = rng.choice(np.float32([0.33, 0.40, 0.6, 1.0]), lab.max())
+        s = scale[lab]
+        yf = np.zeros((3, g.Ly, g.Lx), np.float32)
+        yf[0] = 5.0 * mu[0] * s + 0.02 * rng.standard_normal((g.Ly, g.Lx))
+        yf[1] = 5.0 * mu[1] * s + 0.02 * rng.standard_normal((g.Ly, g.Lx))
+        yf[2] = np.where(lab > 0, 3.0, -3.0)
+        yfs.append(yf)
+        n_obj.append(int(lab.max()))
+    yf = np.stack(yfs)
+    got, st = _gpu_masks(dev, yf, g, H, W)
+    for b in range(yf.shape[0]):
+        ref = so.compute_masks(yf[b], H, W)
+        np.testing.assert_array_equal(got[b], ref, err_msg=f"fov {b}")
+    assert st["n_bad_flow"].sum() >= 2 and st["n_final"].sum() >= 4, st
+
+
 def test_masks_network_resolution_bit_exact_vs_oracle(dev):
     """resample=False (named option): dynamics at network size (200 steps), nearest resize."""
     H, W = 700, 760

@@ -23,7 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--out", required=True)
-    ap.add_argument("--match", default="k_conv3x3,k_cpnet_,Cijk,igemm",
+    ap.add_argument("--match", default="k_conv3x3,k_conv_x3,k_cpnet_,Cijk,igemm",
                     help="comma-separated kernel-name substrings to report")
     a = ap.parse_args()
     path = glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True)

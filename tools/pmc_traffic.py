@@ -22,7 +22,7 @@ FAMILIES = [
     ("illum", ("k_illum_correct", "k_illum_finish")),
     ("qc_rps", ("k_qc_",)),
     ("seg_prep", ("k_pct_", "k_seg_tiles")),
-    ("cpnet", ("k_conv3x3", "k_cpnet_", "igemm", "SubTensorOp", "Cijk", "at::native", "native::",
+    ("cpnet", ("k_conv3x3", "k_conv_x3", "k_cpnet_", "igemm", "SubTensorOp", "Cijk", "at::native", "native::",
                "elementwise", "reduce_kernel", "naive_conv")),
     ("seg_post", ("k_seg_average", "k_dyn_", "k_seed_", "k_assign", "k_relabel", "k_flow_error",
                   "k_apply_bad", "k_count_bad", "k_upsample", "k_lab2idx", "k_fill_")),
@@ -66,6 +66,7 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--out", required=True)
     ap.add_argument("--batch", type=int, default=32, help="FOVs per bench step (bench.py --batch)")
+    ap.add_argument("--precision", default="f16x3", help="bench.py --cpnet-precision of the passes")
     a = ap.parse_args()
     fk, ff, n1 = load(a.fetch_dir, "FETCH_SIZE")
     wk, wf, n2 = load(a.write_dir, "WRITE_SIZE")
@@ -75,6 +76,7 @@ def main():
                   "one step = dispatches between consecutive k_illum_correct launches; "
                   "bytes = 2 x FETCH_SIZE (gfx950 wide-read correction) + WRITE_SIZE, KB x 1024",
         "fovs_per_step": a.batch,
+        "cpnet_precision": a.precision,
         "dispatches_per_step": [n1, n2],
         "per_family_bytes_per_step": {f: {"read": 2.0 * ff.get(f, 0.0), "write": wf.get(f, 0.0),
                                           "total": 2.0 * ff.get(f, 0.0) + wf.get(f, 0.0)} for f in fams},
