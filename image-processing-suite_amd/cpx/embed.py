@@ -80,25 +80,29 @@ class Embedder:
         torch = self.torch
         B, ML, _, S, _ = crops8.shape
         index = [((b * ML + k) * C + c) for b in range(B) for k in range(int(n_kept[b])) for c in range(C)]
-        feats = []
-        i, step = 0, self.batch
-        while i < len(index):
-            j = min(i + step, len(index))
-            try:
-                x = self.pixel_values(crops8, index[i:j], S)
-                feats.append(self.forward(x).cpu().numpy())
-                i = j
-            except torch.cuda.OutOfMemoryError:  # Cellpose_GPU_s3fs.py:196-202
-                torch.cuda.empty_cache()
-                step = max(1, step // 2)
-                if step == 1:
-                    raise
-        allf = np.concatenate(feats) if feats else np.zeros((0, effnet.FEATURE_LENGTH), np.float32)
-        out, o = [], 0
-        for b in range(B):
-            n = int(n_kept[b]) * C
-            out.append(allf[o:o + n].reshape(int(n_kept[b]), C, effnet.FEATURE_LENGTH))
-            o += n
+        out = []
+        for b in range(B):  # per site, as the reference's consumer (Cellpose_GPU_s3fs.py:184-206)
+            idx = index[sum(int(n_kept[k]) for k in range(b)) * C:][: int(n_kept[b]) * C]
+            feats = []
+            i = 0
+            while i < len(idx):
+                j = min(i + self.batch, len(idx))
+                try:
+                    x = self.pixel_values(crops8, idx[i:j], S)
+                    feats.append(self.forward(x).cpu().numpy())
+                    i = j
+                except torch.cuda.OutOfMemoryError:  # Cellpose_GPU_s3fs.py:196-202
+                    torch.cuda.empty_cache()
+                    # the halved batch size is kept for later sites; at 1 the site is given up
+                    self.batch = max(1, self.batch // 2)
+                    if self.batch == 1:
+                        feats = None
+                        break
+            if feats is None:  # the reference's empty result for this site
+                out.append(None)
+                continue
+            allf = np.concatenate(feats) if feats else np.zeros((0, effnet.FEATURE_LENGTH), np.float32)
+            out.append(allf.reshape(int(n_kept[b]), C, effnet.FEATURE_LENGTH))
         return out
 
 
@@ -280,7 +284,7 @@ def run(argv=None):
             kept += [0] * (B - len(chunk))
             feats = emb.embed(pipe.crops8, kept, C)
             for k, (idx, _) in enumerate(chunk):
-                if fovs[k] is None or kept[k] == 0:
+                if fovs[k] is None or kept[k] == 0 or feats[k] is None:
                     results[idx] = {"status": "empty", "n_cells": 0}
                     continue
                 o = res.objects["Nuclei"][k]

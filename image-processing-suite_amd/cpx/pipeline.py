@@ -18,6 +18,7 @@ for the event only — so the host can fetch step i while the GPU already runs s
 from __future__ import annotations
 
 import dataclasses
+import logging
 
 import numpy as np
 import torch
@@ -27,6 +28,7 @@ from .device import Device, as_numpy, n_features
 from .segment import CELLPOSE_MODEL, DIAMETER, Segmenter
 
 OBJECT_SETS = ("Nuclei", "Cells", "Cytoplasm")
+log = logging.getLogger("cpx.pipeline")
 
 
 @dataclasses.dataclass
@@ -76,6 +78,9 @@ class FovResults:
     objects: dict                    # set -> list of structured arrays (per FOV)
     feats: dict                      # set -> list of float64 [n_objects, F]
     seg_stats: np.ndarray
+    failed: np.ndarray | None = None  # [B] bool: the FOV's Cells watershed did not converge within
+                                      # ws_rounds; its object tables are emptied (the reference's
+                                      # per-site 'empty' result, Cellpose_GPU_s3fs.py:225-232)
 
 
 class FovPipeline:
@@ -244,7 +249,18 @@ class FovPipeline:
         if int(hb["cpnet_ovf"][0]) != 0:
             raise RuntimeError("CPnet (f16x3): an activation left the fp16 range (|a| >= 65504); "
                                "run this plate with cpnet_precision='fp32'")
-        if self.cfg.cells == "watershed" and (seg_stats["cells_status"] < 0).any():
-            raise RuntimeError("cpx_watershed_cells: the flood did not converge within ws_rounds "
-                               f"{self.cfg.ws_rounds} (status {seg_stats['cells_status'].ravel().tolist()})")
-        return FovResults(qc=qc, hdr=hdrs, objects=objs, feats=feats, seg_stats=seg_stats)
+        failed = np.zeros(B, dtype=bool)
+        if self.cfg.cells == "watershed":
+            failed = seg_stats["cells_status"].ravel()[:B] < 0
+            if failed.any():
+                # per-site failure, not a failed batch: those FOVs get no object rows, every other
+                # FOV of the batch is kept (the reference logs a site's error and moves on)
+                log.error("cpx_watershed_cells: no convergence within ws_rounds %s for FOV(s) %s of the batch; "
+                          "recorded as empty sites", self.cfg.ws_rounds, np.nonzero(failed)[0].tolist())
+                for s in OBJECT_SETS:
+                    for b in np.nonzero(failed)[0]:
+                        objs[s][b] = objs[s][b][:0]
+                        feats[s][b] = feats[s][b][:0]
+                        hdrs[s][b]["n_objects"] = 0
+                        hdrs[s][b]["n_kept"] = 0
+        return FovResults(qc=qc, hdr=hdrs, objects=objs, feats=feats, seg_stats=seg_stats, failed=failed)

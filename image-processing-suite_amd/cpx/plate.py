@@ -31,10 +31,15 @@ import json
 import logging
 import os
 import shutil
+import time
 
 import numpy as np
 
 log = logging.getLogger("cpx.plate")
+# per job of the last run(): {"job", "fovs", "seconds", "threads", "batch", "pipes"} — decode, upload,
+# GPU pipeline and table assembly, from the first decode to the last recorded site (pipeline
+# construction excluded); the I/O-inclusive throughput of the drop-in (tools/plate_bench.py)
+LAST_TIMING: list = []
 PARTS = ".parts"
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(prog="python -m cpx.plate", description="GPU per-object measurement of one plate/time")
@@ -59,6 +64,8 @@ def parse_args(argv=None):
                     help="processes (GPUs) sharing the jobs; default $WORLD_SIZE")
     ap.add_argument("--no-merge", action="store_true",
                     help="with --world > 1: leave the parts for cpx.launch / merge_parts")
+    ap.add_argument("--ws-rounds", type=int, nargs=2, default=None, metavar=("RELAX", "LABEL"),
+                    help="Cells watershed rounds enqueued per batch (default: PipelineConfig.ws_rounds)")
     return ap.parse_args(argv)
 
 
@@ -157,6 +164,7 @@ def run(argv=None):
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s: %(message)s")
     chans = list(a.channels)
     C = len(chans)
+    LAST_TIMING.clear()
     state = {}  # pipelines, created for the first job's plane geometry and reused
     dirs = []
     for load_data in a.load_data:
@@ -167,6 +175,7 @@ def run(argv=None):
         status = []  # per site: the reference's results_dict entry (Cellpose_GPU_s3fs.py:123-125,219-223)
         if files:
             _run_sites(a, table, mine, files, chans, state, out, status)
+            LAST_TIMING.append({"job": os.path.basename(load_data), "fovs": len(files), **state["timing"]})
         d = job_dir(a.out, plate, time)
         frames = out.frames()
         frames["site_status"] = pd.DataFrame(status, columns=["ImageNumber", "status", "n_cells"]) \
@@ -207,22 +216,29 @@ def _run_sites(a, table, mine, files, chans, state, out, status):
     from .device import Device
     from .pipeline import OBJECT_SETS, FovPipeline, PipelineConfig
     C = len(chans)
+    H = W = None
+    for fs in files:  # this job's plane geometry, from its first readable plane
+        try:
+            H, W = tiffio.imread(fs[0]).shape
+            break
+        except Exception:  # noqa: BLE001
+            continue
+    if H is None:
+        raise RuntimeError("no readable plane in this job")
+    if "pipes" in state and (state["H"], state["W"]) != (H, W):
+        # pipelines are sized for one plane geometry: rebuild them for this job's
+        log.info("plane geometry %s -> %s: rebuilding the GPU pipelines", (state["H"], state["W"]), (H, W))
+        state.clear()
+        torch.cuda.synchronize()
     if "pipes" not in state:
-        H = W = None
-        for fs in files:  # the plane geometry from the first readable plane
-            try:
-                H, W = tiffio.imread(fs[0]).shape
-                break
-            except Exception:  # noqa: BLE001
-                continue
-        if H is None:
-            raise RuntimeError("no readable plane in this job")
         weights = a.weights
         if weights is None:
             cand = os.path.join(os.path.dirname(__file__), "weights", "cpnet_nuclei_synth.pt")
             weights = cand if os.path.exists(cand) else None
         B = max(1, a.batch)
         cfg = PipelineConfig(H=H, W=W, C=C, batch=B, channels=tuple(chans), weights=weights)
+        if a.ws_rounds:
+            cfg.ws_rounds = tuple(a.ws_rounds)
         illum = _illum(a.illum_path, chans, H, W)
         streams, pipes = [], []
         for _ in range(max(1, a.pipes)):
@@ -255,6 +271,7 @@ def _run_sites(a, table, mine, files, chans, state, out, status):
 
     batches = [list(range(i, min(i + B, len(files)))) for i in range(0, len(files), B)]
     inflight = []  # (batch index, pipeline, slot, upload event, empty flags)
+    t_start = time.perf_counter()
 
     def record(bi, res, empty):
         idx = batches[bi]
@@ -269,6 +286,10 @@ def _run_sites(a, table, mine, files, chans, state, out, status):
                 continue
             q = res.qc[k * C:(k + 1) * C]
             counts = {s: int(res.hdr[s][k]["n_objects"]) for s in OBJECT_SETS}
+            if res.failed is not None and res.failed[k]:  # segmentation step failed for this site
+                out.add_image(img_no, meta, q["slope"], q["pct_max"], counts)
+                status.append({"ImageNumber": img_no, "status": "empty", "n_cells": 0})
+                continue
             out.add_image(img_no, meta, q["slope"], q["pct_max"], counts)
             for s in OBJECT_SETS:
                 out.add_objects(s, img_no, res.objects[s][k]["label"], res.feats[s][k])
@@ -305,6 +326,10 @@ def _run_sites(a, table, mine, files, chans, state, out, status):
         while inflight:
             obi, q, sl, _, em = inflight.pop(0)
             record(obi, q.fetch(sl), em)
+    secs = time.perf_counter() - t_start
+    state["timing"] = {"seconds": secs, "threads": a.threads, "batch": B, "pipes": n_pipes}
+    log.info("%d sites in %.2f s: %.1f FOV/s (decode threads %d, batch %d, pipelines %d)",
+             len(files), secs, len(files) / max(secs, 1e-9), a.threads, B, n_pipes)
 
 
 if __name__ == "__main__":

@@ -118,3 +118,24 @@ def test_embed_cli_end_to_end(dev, tmp_path):
     assert len(sc) == counts["Cell_Count"].sum() and len(sc["single_cell_features"].iloc[0]) == C * 1280
     assert sc["Cell_Index"].tolist()[:2] == [0, 1]
     assert any(p.endswith("_single_cell.parquet") for p in out)
+
+
+@pytest.mark.gpu
+def test_preprocess_table_survives_workspace_regrowth(dev):
+    """the bicubic coefficient table lives in a workspace slot that is freed and
+    re-allocated when a later call needs more room (more images); the table cache is keyed by
+    the slot's allocation generation, so the regrown slot gets the table again even when the
+    allocator hands back the same address.  Small N, then a much larger N: both bit-exact."""
+    from cpx.embed import Embedder
+    S = 200
+    rng = np.random.default_rng(12)
+    emb = Embedder.__new__(Embedder)
+    emb.dev, emb.torch, emb.size = dev, torch, 384
+    for n in (1, 24):
+        c8 = rng.integers(0, 256, (n, S, S), dtype=np.uint8)
+        t = torch.from_numpy(c8).to(dev.torch_device)
+        idx = list(range(n))[::-1]
+        got = emb.pixel_values(t, idx, S).cpu().numpy()
+        for j, i in enumerate(idx):
+            ref = eo.pixel_values(c8[i], 384).astype(np.float16)
+            np.testing.assert_array_equal(got[j].view(np.uint16), ref.view(np.uint16))

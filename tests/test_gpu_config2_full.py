@@ -1,0 +1,103 @@
+"""BASELINE configs[2] at its FOV size: one plate x 2 timepoints x 4 wells x 4 sites of
+2080 x 2080 x 5-channel synthetic FOVs as uncompressed TIFFs, through the plate CLI on two ranks
+(cpx.launch, both ranks on the test GPU) and on one; the two outputs are byte-identical, the
+<plate>/<time>/{Image,Nuclei,Cells,Cytoplasm}.csv tables of two FOVs equal the CPU path
+(oracle/cpu_pipeline.run_fov: QC, the fp32 CPnet on the CPU, the restated dynamics, the
+heap-flood watershed, skimage-pinned features) row for row, and the per-time profiles run on the
+sharded output.
+
+Reference: Feature_extraction_opt.py:63-76,147-178 (per (plate, time) jobs writing the four
+tables), Cellpose_GPU_s3fs.py:269-300 (one consumer per GPU), Pycyto_pertime.py:29-172."""
+import filecmp
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+import cpu_pipeline
+from csv_tables import CHANNELS, cpu_tables
+
+pytestmark = pytest.mark.gpu
+
+TIMES = [6, 24]
+WELLS = ["B01", "B02", "B03", "B04"]
+SITES = 4
+
+
+@pytest.mark.timeout(1200)
+def test_config2_full_size_two_ranks_cpu_parity_profiles(tmp_path, dev):
+    from cpx import launch, plate, profiles, shard, tiffio
+    from cpx.cpnet import build_cpnet
+    from cpx.csvout import OBJECT_TABLES
+    from cpx.synth import synth_fovs, synth_illum
+    C, H, W = len(CHANNELS), 2080, 2080
+    imgdir, illdir = tmp_path / "images", tmp_path / "illum"
+    imgdir.mkdir()
+    illdir.mkdir()
+    illum = synth_illum(C, H, W, seed=1)
+    for c, ch in enumerate(CHANNELS):
+        np.save(illdir / f"{ch}_illum.npy", illum[c])
+    lds, raws = [], {}
+    for t in TIMES:
+        n = len(WELLS) * SITES
+        raw = synth_fovs(n, C, H, W, dev.torch_device,
+                         seed=shard.fov_seed(shard.Fov("P01", "B01", 1, t))).cpu().numpy().view(np.uint16)
+        raws[t] = raw.reshape(n, C, H, W)
+        rows = []
+        for wi, well in enumerate(WELLS):
+            for s in range(SITES):
+                f = wi * SITES + s
+                row = {"Metadata_Plate": "P01", "Metadata_Well": well, "Metadata_Site": s + 1,
+                       "Metadata_Timepoint": t, "Metadata_Compound": ["DMSO", "CmpA", "DMSO", "CmpB"][wi],
+                       "Metadata_ConcLevel": 0 if wi % 2 == 0 else 1}
+                for c, ch in enumerate(CHANNELS):
+                    name = f"t{t}_f{f}_c{c}.tiff"
+                    tiffio.imwrite(str(imgdir / name), raws[t][f, c])
+                    row[f"FileName_{ch}"] = name
+                rows.append(row)
+        ld = tmp_path / f"ld_t{t}.csv"
+        pd.DataFrame(rows).to_csv(ld, index=False)
+        lds.append(str(ld))
+    common = ["--load-data", *lds, "--data-path", str(imgdir), "--illum-path", str(illdir),
+              "--channels", *CHANNELS, "--batch", "8", "--threads", "8", "--pipes", "1"]
+    two = launch.main(["--gpus", "2", "--devices", "0,0", "--", *common, "--out", str(tmp_path / "two")])
+    one = plate.run(common + ["--out", str(tmp_path / "one"), "--world", "1", "--rank", "0"])
+    assert [os.path.relpath(d, tmp_path / "two") for d in two] == [f"P01/{t}" for t in TIMES]
+    for d1, d2 in zip(one, two):
+        for name in ("Image", *OBJECT_TABLES, "site_status"):
+            assert filecmp.cmp(os.path.join(d1, f"{name}.csv"), os.path.join(d2, f"{name}.csv"),
+                               shallow=False), (d1, name)
+        st = pd.read_csv(os.path.join(d2, "site_status.csv"))
+        assert (st.status == "success").all() and len(st) == len(WELLS) * SITES
+    # CPU path on two FOVs (first site of each well at the first timepoint): every table row
+    torch.set_num_threads(16)
+    net = build_cpnet(state_dict_path=os.path.join(os.path.dirname(plate.__file__), "weights",
+                                                   "cpnet_nuclei_synth.pt"))
+    d = two[0]
+    gpu = {name: pd.read_csv(os.path.join(d, f"{name}.csv")) for name in ("Image", *OBJECT_TABLES)}
+    for f in (0, SITES):
+        img_no = f + 1  # LoadData row + 1
+        ref = cpu_pipeline.run_fov(raws[TIMES[0]][f], illum, net, cell_channel=CHANNELS.index("AGP"))
+        cdir = cpu_tables(ref, image_number=img_no).write(str(tmp_path / f"cpu{f}"), "P01", TIMES[0])
+        for name in OBJECT_TABLES:
+            c = pd.read_csv(os.path.join(cdir, f"{name}.csv"))
+            g = gpu[name][gpu[name].ImageNumber == img_no].reset_index(drop=True)
+            assert len(c) == len(g) and len(c) > 100, (name, len(c), len(g))
+            np.testing.assert_array_equal(c.ObjectNumber.to_numpy(), g.ObjectNumber.to_numpy())
+            feat = [k for k in c.columns if k not in ("ImageNumber", "ObjectNumber")]
+            assert all(k in g.columns for k in feat)
+            np.testing.assert_allclose(g[feat].to_numpy(np.float64), c[feat].to_numpy(np.float64),
+                                       rtol=1e-5, atol=1e-9, err_msg=name)
+        ci = pd.read_csv(os.path.join(cdir, "Image.csv"))
+        gi = gpu["Image"][gpu["Image"].ImageNumber == img_no]
+        for k in ci.columns:
+            if k.startswith("ImageQuality_PercentMaximal") or k.startswith("Count_"):
+                assert ci[k].iloc[0] == gi[k].iloc[0], k
+            elif k.startswith("ImageQuality_PowerLogLogSlope"):
+                assert abs(ci[k].iloc[0] - gi[k].iloc[0]) <= 1e-9 * abs(ci[k].iloc[0]), k
+    # per-time profiles (Pycyto_pertime.py) of the sharded output
+    written = profiles.concatenate_csv(str(tmp_path / "two"), [str(t) for t in TIMES], "P01",
+                                       str(tmp_path / "prof"), "P01_profiles", local_dir=str(tmp_path / "tmp"))
+    assert len(written) == 3 * len(TIMES)

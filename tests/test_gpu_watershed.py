@@ -115,3 +115,24 @@ def test_status_reports_unresolved_labels(dev, full_size):
     nuc, corr, _ = full_size
     _, _, st = _ws_gpu(dev, nuc, corr, 0, 15, rounds=(24, 1))  # levels converge, chains do not
     assert (st == -1).all(), st
+
+
+def test_pipeline_unconverged_watershed_is_a_per_site_failure(dev):
+    """a FOV whose Cells flood did not converge within ws_rounds is a failed site (no
+    object rows, FovResults.failed), not a failed batch — the reference records a site error and
+    carries on (Cellpose_GPU_s3fs.py:225-232)."""
+    from cpx.pipeline import FovPipeline, PipelineConfig
+    from cpx.synth import synth_fovs, synth_illum
+    H = W = 768
+    C, B = 5, 2
+    cfg = PipelineConfig(H=H, W=W, C=C, batch=B, ws_rounds=(1, 1))
+    pipe = FovPipeline(dev, cfg, synth_illum(C, H, W, seed=1))
+    res = pipe.fetch(pipe.run(synth_fovs(B, C, H, W, dev.torch_device, seed=3)))
+    assert res.failed is not None and res.failed.all()
+    for s in ("Nuclei", "Cells", "Cytoplasm"):
+        for b in range(B):
+            assert len(res.objects[s][b]) == 0 and len(res.feats[s][b]) == 0
+            assert res.hdr[s][b]["n_objects"] == 0
+    ok = FovPipeline(dev, PipelineConfig(H=H, W=W, C=C, batch=B), synth_illum(C, H, W, seed=1))
+    res2 = ok.fetch(ok.run(synth_fovs(B, C, H, W, dev.torch_device, seed=3)))
+    assert not res2.failed.any() and all(len(res2.objects["Cells"][b]) > 0 for b in range(B))
