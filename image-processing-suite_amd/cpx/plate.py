@@ -252,25 +252,23 @@ def _run_sites(a, table, mine, files, chans, state, out, status):
     B, H, W = state["B"], state["H"], state["W"]
     n_pipes = len(pipes)
 
-    def read_fov(paths):
-        """The site's C planes, or None when any of them cannot be read (missing, undecodable,
-        other shape): the reference's producer then sends (site_id, None) and the consumer
-        records the site as {'status': 'empty', 'n_cells': 0} (Cellpose_GPU_s3fs.py:76-87,
-        123-136)."""
+    def read_fov(paths, dst):
+        """Decode the site's C planes straight into dst [C][H][W] (a slice of the pinned staging
+        buffer); False when any of them cannot be read (missing, undecodable, other shape): the
+        reference's producer then sends (site_id, None) and the consumer records the site as
+        {'status': 'empty', 'n_cells': 0} (Cellpose_GPU_s3fs.py:76-87, 123-136)."""
         try:
-            planes = []
-            for p in paths:
-                x = tiffio.imread(p)
-                if x.shape != (H, W):
-                    raise ValueError(f"{p}: shape {x.shape}, expected {(H, W)}")
-                planes.append(x.astype(np.uint16, copy=False))
-            return np.stack(planes)
+            for c, p in enumerate(paths):
+                tiffio.read_into(p, dst[c])
+            return True
         except Exception as e:  # noqa: BLE001
             log.error("failed on site %s: %s", paths, e)
-            return None
+            dst[...] = 0
+            return False
 
     batches = [list(range(i, min(i + B, len(files)))) for i in range(0, len(files), B)]
     inflight = []  # (batch index, pipeline, slot, upload event, empty flags)
+    uploads = [None] * n_pipes  # last upload event per staging buffer
     t_start = time.perf_counter()
 
     def record(bi, res, empty):
@@ -297,29 +295,31 @@ def _run_sites(a, table, mine, files, chans, state, out, status):
             status.append({"ImageNumber": img_no, "status": "success" if n else "empty", "n_cells": n})
         log.info("batch %d/%d: %d FOVs", bi + 1, len(batches), len(idx))
 
+    def decode(bi, pool):
+        """Decode batch bi into its pipeline's pinned staging buffer (after that buffer's last
+        upload completed); the tail of a short batch is zero-filled."""
+        p_i = bi % n_pipes
+        if uploads[p_i] is not None:
+            uploads[p_i].synchronize()
+        hn = hosts[p_i].numpy().view(np.uint16).reshape(B, C, H, W)
+        idx = batches[bi]
+        hn[len(idx):] = 0
+        return [pool.submit(read_fov, files[i], hn[k]) for k, i in enumerate(idx)]
+
     with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, a.threads)) as pool:
-        pending = [pool.submit(read_fov, files[i]) for i in batches[0]]
+        pending = decode(0, pool)
         for bi, idx in enumerate(batches):
-            fovs = [f.result() for f in pending]
-            if bi + 1 < len(batches):  # decode the next batch while this one runs
-                pending = [pool.submit(read_fov, files[i]) for i in batches[bi + 1]]
+            empty = [not f.result() for f in pending]
             p_i = bi % n_pipes
-            # the pinned staging buffer of this pipeline is free once its last upload completed
-            for _, q, _, up, _ in inflight:
-                if q is pipes[p_i]:
-                    up.synchronize()
-            host = hosts[p_i]
-            hn = host.numpy().view(np.uint16).reshape(B, C, H, W)
-            empty = [f is None for f in fovs]
-            for k, f in enumerate(fovs):
-                hn[k] = 0 if f is None else f
-            hn[len(fovs):] = 0
             with torch.cuda.stream(streams[p_i]):
-                pipes[p_i].raw.copy_(host, non_blocking=True)
+                pipes[p_i].raw.copy_(hosts[p_i], non_blocking=True)
                 up = torch.cuda.Event()
                 up.record(streams[p_i])
+                uploads[p_i] = up
                 slot = pipes[p_i].run()
             inflight.append((bi, pipes[p_i], slot, up, empty))
+            if bi + 1 < len(batches):  # decode the next batch while this one runs
+                pending = decode(bi + 1, pool)
             if len(inflight) > n_pipes:   # results in batch order, one step behind the GPU
                 obi, q, sl, _, em = inflight.pop(0)
                 record(obi, q.fetch(sl), em)

@@ -69,6 +69,58 @@ def imread(src) -> np.ndarray:
     return arr.astype(dt.newbyteorder("="), copy=True)
 
 
+def read_into(path: str, out: np.ndarray) -> None:
+    """Decode the first page of the TIFF at `path` into `out` (a writable C-contiguous 2-D array,
+    e.g. a slice of a pinned staging buffer).  Uncompressed strips whose sample type and byte
+    order match `out` are read straight from the file into `out` (readinto: no intermediate
+    copies, the GIL released during the reads); anything else goes through imread and a copy.
+    Raises ValueError on a shape mismatch."""
+    with open(path, "rb") as f:
+        head = f.read(65536)
+        if head[:2] not in (b"II", b"MM"):
+            raise ValueError(f"{path}: not a TIFF file")
+        bo = "<" if head[:2] == b"II" else ">"
+        if struct.unpack(bo + "H", head[2:4])[0] != 42:
+            raise ValueError(f"{path}: BigTIFF/unknown TIFF version not supported")
+        ifd = struct.unpack(bo + "I", head[4:8])[0]
+        tags = None
+        if ifd + 2 <= len(head):
+            n = struct.unpack(bo + "H", head[ifd:ifd + 2])[0]
+            if ifd + 2 + 12 * n + 4 <= len(head):
+                try:
+                    tags = _read_ifd(head, ifd, bo)
+                except struct.error:
+                    tags = None
+        direct = False
+        if tags is not None and 256 in tags and 257 in tags and 273 in tags:
+            W, H = tags[256][0], tags[257][0]
+            bits = tags.get(258, (1,))[0]
+            kind = {1: "u", 2: "i", 3: "f"}.get(tags.get(339, (1,))[0], "u")
+            dt = np.dtype(f"{bo}{kind}{bits // 8}")
+            direct = (tags.get(259, (1,))[0] == 1 and tags.get(277, (1,))[0] == 1 and 322 not in tags
+                      and dt.newbyteorder("=") == out.dtype and dt.isnative and out.flags.c_contiguous
+                      and len(tags.get(279, ())) == len(tags[273]))
+            if (H, W) != out.shape:
+                raise ValueError(f"{path}: shape {(H, W)}, expected {out.shape}")
+        if direct:
+            mv = memoryview(out.reshape(-1).view(np.uint8))
+            pos = 0
+            for o, c in zip(tags[273], tags[279]):
+                c = min(c, out.nbytes - pos)
+                f.seek(o)
+                got = f.readinto(mv[pos:pos + c])
+                if got != c:
+                    raise ValueError(f"{path}: truncated strip")
+                pos += c
+            if pos != out.nbytes:
+                raise ValueError(f"{path}: strips hold {pos} of {out.nbytes} bytes")
+            return
+    arr = imread(path)
+    if arr.shape != out.shape:
+        raise ValueError(f"{path}: shape {arr.shape}, expected {out.shape}")
+    out[...] = arr
+
+
 def _pil_read(buf: bytes) -> np.ndarray:
     from PIL import Image
     with Image.open(io.BytesIO(buf)) as im:

@@ -448,7 +448,9 @@ struct X3Cfg {
   int bm, ty, tx;
 };
 
-// tile configuration per (KS, CIN, COUT, variant); must match the instances in x3_launch()
+// tile configuration per (KS, CIN, COUT, variant); must match the instances in x3_launch().
+// Variant 0 (default) is the faster one per level on the box (tools/conv_bench_x3.py, r03):
+// 224^2 BM 32 on 8 x 32 tiles, deeper levels BM 32 with 2 blocks per CU; variant 1 the others.
 bool x3_cfg(int ks, int cin, int cout, int variant, X3Cfg* c) {
   if (!((cin == 32 || cin == 64 || cin == 128 || cin == 256) && (cout == 32 || cout == 64 || cout == 128 || cout == 256)))
     return false;
@@ -457,9 +459,9 @@ bool x3_cfg(int ks, int cin, int cout, int variant, X3Cfg* c) {
     return true;
   }
   if (ks != 3) return false;
-  if (cout == 32) *c = {32, 8, 32};
-  else if (cout == 64) *c = variant == 1 ? X3Cfg{32, 16, 16} : X3Cfg{64, 16, 16};
-  else *c = variant == 1 ? X3Cfg{32, 8, 28} : X3Cfg{64, 14, 28};
+  if (cout == 32) *c = variant == 1 ? X3Cfg{32, 16, 32} : X3Cfg{32, 8, 32};
+  else if (cout == 64) *c = variant == 1 ? X3Cfg{64, 16, 16} : X3Cfg{32, 16, 16};
+  else *c = variant == 1 ? X3Cfg{64, 14, 28} : X3Cfg{32, 8, 28};
   return true;
 }
 
@@ -485,24 +487,26 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
   // 224^2 level
   X3_3(32, 32, 0, 32, 8, 32, 1, 1, 4)
   X3_3(64, 32, 0, 32, 8, 32, 1, 1, 4)
+  X3_3(32, 32, 1, 32, 16, 32, 1, 2, 2)
+  X3_3(64, 32, 1, 32, 16, 32, 1, 2, 2)
   // 112^2 level
-  X3_3(32, 64, 0, 64, 16, 16, 2, 1, 2)
-  X3_3(64, 64, 0, 64, 16, 16, 2, 1, 2)
-  X3_3(128, 64, 0, 64, 16, 16, 2, 1, 2)
-  X3_3(32, 64, 1, 32, 16, 16, 1, 1, 4)
-  X3_3(64, 64, 1, 32, 16, 16, 1, 1, 4)
-  X3_3(128, 64, 1, 32, 16, 16, 1, 1, 4)
+  X3_3(32, 64, 1, 64, 16, 16, 2, 1, 2)
+  X3_3(64, 64, 1, 64, 16, 16, 2, 1, 2)
+  X3_3(128, 64, 1, 64, 16, 16, 2, 1, 2)
+  X3_3(32, 64, 0, 32, 16, 16, 1, 1, 4)
+  X3_3(64, 64, 0, 32, 16, 16, 1, 1, 4)
+  X3_3(128, 64, 0, 32, 16, 16, 1, 1, 4)
   // 56^2 / 28^2 levels
-  X3_3(64, 128, 0, 64, 14, 28, 2, 2, 2)
-  X3_3(128, 128, 0, 64, 14, 28, 2, 2, 2)
-  X3_3(256, 128, 0, 64, 14, 28, 2, 2, 2)
-  X3_3(128, 256, 0, 64, 14, 28, 2, 2, 2)
-  X3_3(256, 256, 0, 64, 14, 28, 2, 2, 2)
-  X3_3(64, 128, 1, 32, 8, 28, 1, 1, 4)
-  X3_3(128, 128, 1, 32, 8, 28, 1, 1, 4)
-  X3_3(256, 128, 1, 32, 8, 28, 1, 1, 4)
-  X3_3(128, 256, 1, 32, 8, 28, 1, 1, 4)
-  X3_3(256, 256, 1, 32, 8, 28, 1, 1, 4)
+  X3_3(64, 128, 1, 64, 14, 28, 2, 2, 2)
+  X3_3(128, 128, 1, 64, 14, 28, 2, 2, 2)
+  X3_3(256, 128, 1, 64, 14, 28, 2, 2, 2)
+  X3_3(128, 256, 1, 64, 14, 28, 2, 2, 2)
+  X3_3(256, 256, 1, 64, 14, 28, 2, 2, 2)
+  X3_3(64, 128, 0, 32, 8, 28, 1, 1, 4)
+  X3_3(128, 128, 0, 32, 8, 28, 1, 1, 4)
+  X3_3(256, 128, 0, 32, 8, 28, 1, 1, 4)
+  X3_3(128, 256, 0, 32, 8, 28, 1, 1, 4)
+  X3_3(256, 256, 0, 32, 8, 28, 1, 1, 4)
   // 1x1 block projections (BatchNorm folded into the weights)
   X3_1(32, 64)
   X3_1(64, 128)

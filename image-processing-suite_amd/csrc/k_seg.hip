@@ -877,7 +877,11 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
     // block-uniform: objects of the smaller variant or of k_flow_error_big are skipped
     if (!fe_fits(bh, bw, THREADS, U, CELLS)) continue;
     if (lo_threads > 0 && fe_fits(bh, bw, lo_threads, lo_units, lo_cells)) continue;
-    const int nsr = (bh + kFeKS - 1) / kFeKS;
+    // rows per unit: the fewest (<= kFeKS) that keep the units within the block, so small masks
+    // spread over more lanes (shorter per-iteration chains) instead of idling most of them
+    const int ncp0 = (bw + 1) / 2;
+    const int R = min(kFeKS, max(1, (bh + max(1, THREADS * U / ncp0) - 1) / max(1, THREADS * U / ncp0)));
+    const int nsr = (bh + R - 1) / R;
     const int ly = bh + 2;
     const int* lab = m0 + (long long)fov * n;
     // ---- medians of the pixel coordinates (row / column counts in the T area, as ints)
@@ -942,17 +946,17 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
       uy0[i] = 1;
       ujc[i] = -1;
       if (u < ncp * nsr) {
-        const int X = 2 * (u % ncp) + 1, Y0 = 1 + (u / ncp) * kFeKS;
+        const int X = 2 * (u % ncp) + 1, Y0 = 1 + (u / ncp) * R;
         ux[i] = X;
         uy0[i] = Y0;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           if (X + h > bw) continue;  // bw odd: the last pair's second column is the border
           unsigned int m = 0u;
-          for (int j = 0; j < kFeKS && Y0 + j <= bh; ++j)
+          for (int j = 0; j < R && Y0 + j <= bh; ++j)
             if (lab[(long long)(r0 + Y0 - 1 + j) * Dx + c0 + X + h - 1] == L) m |= 1u << j;
           um[i][h] = m;
-          if (X + h == xm && ym >= Y0 && ym < Y0 + kFeKS) ujc[i] = 2 * (ym - Y0) + h;
+          if (X + h == xm && ym >= Y0 && ym < Y0 + R) ujc[i] = 2 * (ym - Y0) + h;
         }
       }
     }
@@ -987,20 +991,23 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
         double2 da = T2[r], db = T2[r + 1];
 #pragma unroll
         for (int j = 0; j < kFeKS; ++j) {
-          // the next row's loads are issued before this row's sums (latency hidden); the
-          // scheduling barrier keeps the compiler from hoisting more rows (register budget)
-          double2 na = {0.0, 0.0}, nb = {0.0, 0.0};
-          if (j + 1 < kFeKS) {
-            r = min(r + rs, rmax);
-            na = T2[r];
-            nb = T2[r + 1];
+          // rows beyond R: predicated off (block-uniform), the loop stays unrolled so nv stays in
+          // registers.  The next row's loads are issued before this row's sums (latency hidden);
+          // the scheduling barrier keeps the compiler from hoisting more rows (register budget)
+          if (j < R) {
+            double2 na = {0.0, 0.0}, nb = {0.0, 0.0};
+            if (j + 1 < R) {
+              r = min(r + rs, rmax);
+              na = T2[r];
+              nb = T2[r + 1];
+            }
+            // column X: l = .x of a, c = .y of a, r = .x of b;  column X + 1: l = a.y, c = b.x, r = b.y
+            nv[i][0][j] = 1 / 9. * (ca.y + ua.y + da.y + ca.x + cb.x + ua.x + ub.x + da.x + db.x);
+            nv[i][1][j] = 1 / 9. * (cb.x + ub.x + db.x + ca.y + cb.y + ua.y + ub.y + da.y + db.y);
+            ua = ca; ub = cb;
+            ca = da; cb = db;
+            da = na; db = nb;
           }
-          // column X: l = .x of a, c = .y of a, r = .x of b;  column X + 1: l = a.y, c = b.x, r = b.y
-          nv[i][0][j] = 1 / 9. * (ca.y + ua.y + da.y + ca.x + cb.x + ua.x + ub.x + da.x + db.x);
-          nv[i][1][j] = 1 / 9. * (cb.x + ub.x + db.x + ca.y + cb.y + ua.y + ub.y + da.y + db.y);
-          ua = ca; ub = cb;
-          ca = da; cb = db;
-          da = na; db = nb;
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -1101,9 +1108,11 @@ __global__ __launch_bounds__(THREADS, 1) void k_flow_error_cmp(
     const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
     // block-uniform: the smaller kernels' masks, and masks beyond this kernel's limits
     if (fe_fits(bh, bw, lo_threads, lo_units, lo_cells)) continue;
-    const int nsr = (bh + kFeKS - 1) / kFeKS;
     const int ncp = (bw + 1) / 2;
-    if (bh > kCmpRows || (long long)ncp * nsr > (long long)THREADS * U) continue;
+    if (bh > kCmpRows || (long long)ncp * ((bh + kFeKS - 1) / kFeKS) > (long long)THREADS * U) continue;
+    const int G = max(1, THREADS * U / ncp);  // row groups the block holds
+    const int R = min(kFeKS, (bh + G - 1) / G);  // rows per unit
+    const int nsr = (bh + R - 1) / R;
     const int* lab = m0 + (long long)fov * n;
     // ---- coordinate counts (medians) and per-row column extents, in the T area as ints
     int* rowc = reinterpret_cast<int*>(T);
@@ -1191,15 +1200,15 @@ __global__ __launch_bounds__(THREADS, 1) void k_flow_error_cmp(
       Y0[i] = 1;
       if (u < ncp * nsr) {
         X[i] = 2 * (u % ncp) + 1;
-        Y0[i] = 1 + (u / ncp) * kFeKS;
+        Y0[i] = 1 + (u / ncp) * R;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           if (X[i] + h > bw) continue;
           unsigned int m = 0u;
-          for (int j = 0; j < kFeKS && Y0[i] + j <= bh; ++j)
+          for (int j = 0; j < R && Y0[i] + j <= bh; ++j)
             if (lab[(long long)(r0 + Y0[i] - 1 + j) * Dx + c0 + X[i] + h - 1] == L) m |= 1u << j;
           um[i][h] = m;
-          if (X[i] + h == xm && ym >= Y0[i] && ym < Y0[i] + kFeKS) cown = true;
+          if (X[i] + h == xm && ym >= Y0[i] && ym < Y0[i] + R) cown = true;
         }
       }
     }
@@ -1231,14 +1240,16 @@ __global__ __launch_bounds__(THREADS, 1) void k_flow_error_cmp(
         ldrow(min(Y0[i] + 1, bh + 1), pa, da, db);
 #pragma unroll
         for (int j = 0; j < kFeKS; ++j) {
-          double2 na = z2, nb2 = z2;
-          if (j + 1 < kFeKS) ldrow(min(Y0[i] + j + 2, bh + 1), pa, na, nb2);
-          // column X: l = a.x, c = a.y, r = b.x;  column X + 1: l = a.y, c = b.x, r = b.y
-          nv[i][0][j] = 1 / 9. * (ca.y + ua.y + da.y + ca.x + cb.x + ua.x + ub.x + da.x + db.x);
-          nv[i][1][j] = 1 / 9. * (cb.x + ub.x + db.x + ca.y + cb.y + ua.y + ub.y + da.y + db.y);
-          ua = ca; ub = cb;
-          ca = da; cb = db;
-          da = na; db = nb2;
+          if (j < R) {  // block-uniform predicate: the loop stays unrolled, nv in registers
+            double2 na = z2, nb2 = z2;
+            if (j + 1 < R) ldrow(min(Y0[i] + j + 2, bh + 1), pa, na, nb2);
+            // column X: l = a.x, c = a.y, r = b.x;  column X + 1: l = a.y, c = b.x, r = b.y
+            nv[i][0][j] = 1 / 9. * (ca.y + ua.y + da.y + ca.x + cb.x + ua.x + ub.x + da.x + db.x);
+            nv[i][1][j] = 1 / 9. * (cb.x + ub.x + db.x + ca.y + cb.y + ua.y + ub.y + da.y + db.y);
+            ua = ca; ub = cb;
+            ca = da; cb = db;
+            da = na; db = nb2;
+          }
           __builtin_amdgcn_sched_barrier(0);
         }
       }

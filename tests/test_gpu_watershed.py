@@ -127,12 +127,15 @@ def test_pipeline_unconverged_watershed_is_a_per_site_failure(dev):
     C, B = 5, 2
     cfg = PipelineConfig(H=H, W=W, C=C, batch=B, ws_rounds=(1, 1))
     pipe = FovPipeline(dev, cfg, synth_illum(C, H, W, seed=1))
-    res = pipe.fetch(pipe.run(synth_fovs(B, C, H, W, dev.torch_device, seed=3)))
+    # 768^2 FOVs with a plausible nucleus count for that area (synth_fovs' default targets 2080^2)
+    raw = synth_fovs(B, C, H, W, dev.torch_device, seed=3, nuclei=(30, 45))
+    res = pipe.fetch(pipe.run(raw))
+    assert res.seg_stats["n_final"].min() >= 10
     assert res.failed is not None and res.failed.all()
     for s in ("Nuclei", "Cells", "Cytoplasm"):
         for b in range(B):
             assert len(res.objects[s][b]) == 0 and len(res.feats[s][b]) == 0
             assert res.hdr[s][b]["n_objects"] == 0
     ok = FovPipeline(dev, PipelineConfig(H=H, W=W, C=C, batch=B), synth_illum(C, H, W, seed=1))
-    res2 = ok.fetch(ok.run(synth_fovs(B, C, H, W, dev.torch_device, seed=3)))
+    res2 = ok.fetch(ok.run(raw))
     assert not res2.failed.any() and all(len(res2.objects["Cells"][b]) > 0 for b in range(B))

@@ -1,0 +1,85 @@
+"""Development timing of every convolution of the split-fp16 (f16x3) CPnet forward, in isolation,
+for each tile-configuration variant of k_conv_x3 (cpx_cpnet_x3_cfg): one forward over N tiles of
+224^2, every cpx_cpnet_x3_conv call replayed `reps` times between HIP events.  Per call: kernel
+size, channels, level, us, network TFLOP/s (x3 = f16 MFMA rate) and the minimum HBM bytes (4 B
+per channel: input, residual, outputs once) per us.
+
+python tools/conv_bench_x3.py [--tiles 144] [--reps 10] [--variants 0 1]"""
+import argparse
+import ctypes as ct
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "image-processing-suite_amd"))
+import torch  # noqa: E402
+
+from cpx.cpnet import build_cpnet  # noqa: E402
+from cpx.cpnet_x3 import FusedCPnetX3  # noqa: E402
+from cpx.device import Device  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tiles", type=int, default=144)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--forward", type=int, default=5)
+    ap.add_argument("--variants", type=int, nargs="+", default=[0, 1])
+    a = ap.parse_args()
+    dev = Device(0)
+    td = dev.torch_device
+    w = os.path.join(REPO, "image-processing-suite_amd", "cpx", "weights", "cpnet_nuclei_synth.pt")
+    net = build_cpnet(state_dict_path=w if os.path.exists(w) else None)
+    x = torch.rand(a.tiles, 224, 224, 2, device=td)
+    lib = dev.lib
+    real = lib.cpx_cpnet_x3_conv
+    for v in a.variants:
+        f = FusedCPnetX3(net, dev, variant=v)
+        rows = []
+
+        def wrap(*args):
+            (h, ks, var, xin, N, H, W, cin, cout, pk, bias, res, res_up, sty, sts, sc, sh, relu, y, z, z_up,
+             hw, hb, nh, ho, ovf) = args
+            rc = real(*args)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.reps):
+                real(*args)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / a.reps * 1e3
+
+            def on(p):
+                return p is not None and (not isinstance(p, ct.c_void_p) or p.value is not None)
+            flops = 2.0 * N * H * W * cin * cout * ks * ks
+            px = N * H * W
+            byt = px * cin * 4 + px * cout * 4 * (on(y) + on(z) * (4 if z_up else 1)) + (px * 12 if on(ho) else 0)
+            if on(res):
+                byt += px * cout * 4 // (4 if res_up else 1)
+            rows.append((ks, cin, cout, H, int(on(res)), int(on(y)), int(on(z)), int(on(ho)), us,
+                         flops / us / 1e6, byt / us / 1e3))
+            return rc
+
+        with torch.no_grad():
+            f(x)
+            torch.cuda.synchronize()
+            lib.cpx_cpnet_x3_conv = wrap
+            f(x)
+            lib.cpx_cpnet_x3_conv = real
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.forward):
+                f(x)
+            e1.record()
+            torch.cuda.synchronize()
+        print(f"variant={v} tiles={a.tiles}")
+        print(" ks  cin cout   H res y z head       us  netTFLOP/s  GB/s(min)")
+        tot = 0.0
+        for r in rows:
+            tot += r[8]
+            print(f"{r[0]:3d} {r[1]:4d} {r[2]:4d} {r[3]:3d} {r[4]:3d} {r[5]} {r[6]} {r[7]:4d} {r[8]:8.1f} {r[9]:10.1f} {r[10]:9.1f}")
+        print(f"sum of convs: {tot / 1e3:.3f} ms; whole forward: {e0.elapsed_time(e1) / a.forward:.3f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()

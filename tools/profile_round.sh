@@ -7,6 +7,7 @@ set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/round
 BATCH=${BATCH:-48}  # bench.py's default --batch
+PREC=${PREC:-f16x3}  # bench.py's default --cpnet-precision
 mkdir -p $O
 cd $R
 timeout -k 10 420 python -u bench.py > $O/bench_default.log 2>&1
@@ -31,7 +32,7 @@ python tools/prof_summary.py $O/kt/run_kernel_trace.csv --steps 4 --md > $O/kern
 python tools/prof_summary.py $O/kt2/run_kernel_trace.csv --steps 4 --md > $O/kernels_concurrent.md
 cp $O/kt/run_kernel_stats.csv $O/kernel_stats.csv
 cp $O/kt2/run_kernel_stats.csv $O/kernel_stats_concurrent.csv
-python tools/pmc_traffic.py $O/fetch $O/write --batch $BATCH --out $O/pmc_traffic.json > $O/pmc_traffic.log
+python tools/pmc_traffic.py $O/fetch $O/write --batch $BATCH --precision ${PREC:-f16x3} --out $O/pmc_traffic.json > $O/pmc_traffic.log
 python tools/pmc_mfma.py $O/mfma --out $O/pmc_mfma.json > $O/pmc_mfma.log
 rm -rf $O/kt $O/kt2 $O/fetch $O/write $O/mfma
 echo done
