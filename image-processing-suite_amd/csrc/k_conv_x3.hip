@@ -135,8 +135,13 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   const int mw = wid % MWV, pg = wid / MWV;
   const int h = lane >> 5, l32 = lane & 31;
   const int tiles = tiles_x * tiles_y;
-  const int n = blockIdx.x / tiles;
-  const int t = blockIdx.x - n * tiles;
+  // XCD-aware order: the hardware deals consecutive block ids round-robin over the 8 XCDs, so
+  // block b runs on XCD b % 8; give each XCD a contiguous run of tiles instead, so vertically
+  // adjacent tiles (which share halo rows) meet in the same L2
+  const int G = gridDim.x, xq = G >> 3, xr = G & 7, xb = blockIdx.x & 7;
+  const int bid = xb * xq + min(xb, xr) + (blockIdx.x >> 3);
+  const int n = bid / tiles;
+  const int t = bid - n * tiles;
   const int ty0 = (t / tiles_x) * TY, tx0 = (t % tiles_x) * TX;
   const int nb = blockIdx.y;
   const uint4* inb = in + (long long)n * H * W * QI;
@@ -532,12 +537,14 @@ __global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem_x3(
     const float* __restrict__ shift0, const float* __restrict__ w0, const float* __restrict__ bias0,
     const float* __restrict__ scale1, const float* __restrict__ shift1, const float* __restrict__ wp,
     uint4* __restrict__ p_out, uint4* __restrict__ z_out, int tiles_x, int tiles_y, int* ovf) {
+  constexpr int NP = kSTY * kSTX;  // pixels (threads) per block
   __shared__ float sz[2][kSTY + 2][kSTX + 2];
+  __shared__ uint4 so[2][NP * 8];   // z and p tiles: 8 chunks (2 slabs x hi/lo x 2) per pixel
   const int tiles = tiles_x * tiles_y;
   const int n = blockIdx.x / tiles, t = blockIdx.x - n * tiles;
   const int ty0 = (t / tiles_x) * kSTY, tx0 = (t % tiles_x) * kSTX;
   const float s00 = scale0[0], s01 = scale0[1], h00 = shift0[0], h01 = shift0[1];
-  for (int i = threadIdx.x; i < (kSTY + 2) * (kSTX + 2); i += kSTY * kSTX) {
+  for (int i = threadIdx.x; i < (kSTY + 2) * (kSTX + 2); i += NP) {
     const int hy = i / (kSTX + 2), hx = i - hy * (kSTX + 2);
     const int gy = ty0 + hy - 1, gx = tx0 + hx - 1;
     float a = 0.0f, b = 0.0f;
@@ -553,6 +560,7 @@ __global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem_x3(
   const int ly = threadIdx.x / kSTX, lx = threadIdx.x - ly * kSTX;
   const int gy = ty0 + ly, gx = tx0 + lx;
   bool bad = false;
+  const int px = threadIdx.x;
   if (gy < H && gx < W) {
     const long long pix = ((long long)n * H + gy) * W + gx;
     float in[18];
@@ -561,8 +569,6 @@ __global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem_x3(
 #pragma unroll
       for (int k = 0; k < 9; ++k) in[c * 9 + k] = sz[c][ly + k / 3][lx + k % 3];
     const float2 xv = *reinterpret_cast<const float2*>(x + pix * 2);
-    uint4* zo = z_out + pix * 8;
-    uint4* po = p_out + pix * 8;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // 8 channels per q: slab q >> 1, chunk q & 1
       float zf[8], pf[8];
@@ -577,12 +583,26 @@ __global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem_x3(
       }
       uint4 hi, lo;
       const int base = (q >> 1) * 4 + (q & 1);
+      // chunk slots swizzled by pixel (8 chunks = 128 B per pixel row)
       split8(zf, hi, lo, bad);
-      zo[base] = hi;
-      zo[base + 2] = lo;
+      so[0][px * 8 + (base ^ (px & 7))] = hi;
+      so[0][px * 8 + ((base + 2) ^ (px & 7))] = lo;
       split8(pf, hi, lo, bad);
-      po[base] = hi;
-      po[base + 2] = lo;
+      so[1][px * 8 + (base ^ (px & 7))] = hi;
+      so[1][px * 8 + ((base + 2) ^ (px & 7))] = lo;
+    }
+  }
+  __syncthreads();
+  // whole 16-byte chunks, consecutive threads -> consecutive chunks of a tile row (2 KiB runs)
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int i = threadIdx.x + r * NP;
+    const int p = i >> 3, k = i & 7;
+    const int py = ty0 + p / kSTX, pxg = tx0 + p % kSTX;
+    if (py < H && pxg < W) {
+      const long long g = (((long long)n * H + py) * W + pxg) * 8 + k;
+      z_out[g] = so[0][p * 8 + (k ^ (p & 7))];
+      p_out[g] = so[1][p * 8 + (k ^ (p & 7))];
     }
   }
   if (ovf && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);

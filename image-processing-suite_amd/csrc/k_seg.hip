@@ -877,10 +877,13 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
     // block-uniform: objects of the smaller variant or of k_flow_error_big are skipped
     if (!fe_fits(bh, bw, THREADS, U, CELLS)) continue;
     if (lo_threads > 0 && fe_fits(bh, bw, lo_threads, lo_units, lo_cells)) continue;
-    // rows per unit: the fewest (<= kFeKS) that keep the units within the block, so small masks
-    // spread over more lanes (shorter per-iteration chains) instead of idling most of them
+    // rows per unit: the one-block-per-CU variant (latency-bound: one mask at a time) takes the
+    // fewest (<= kFeKS) that keep the units within the block, so a mask spreads over more lanes
+    // with shorter per-iteration chains; the multi-block variants keep kFeKS (throughput-bound:
+    // shorter units only add halo-row reads)
     const int ncp0 = (bw + 1) / 2;
-    const int R = min(kFeKS, max(1, (bh + max(1, THREADS * U / ncp0) - 1) / max(1, THREADS * U / ncp0)));
+    const int R = THREADS < 1024 ? kFeKS
+                                 : min(kFeKS, max(1, (bh + max(1, THREADS * U / ncp0) - 1) / max(1, THREADS * U / ncp0)));
     const int nsr = (bh + R - 1) / R;
     const int ly = bh + 2;
     const int* lab = m0 + (long long)fov * n;
@@ -1070,7 +1073,7 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
 }
 
 // k_flow_error_cmp: the same per-mask diffusion for masks whose full (bh + 2) x stride grid does
-// not fit the large LDS kernel: T holds only each row's span of mask cells (row y keeps the
+// not fit the large LDS kernel (kFeLargeCells; its per-row span lookups make it slower there): T holds only each row's span of mask cells (row y keeps the
 // column pairs [pb, pe] covering its mask pixels, at T2[base + p]); every cell outside a row's
 // span is a non-mask cell of the reference's grid, which stays 0.0 for the whole diffusion, so
 // reads there return zero.  Round masks keep ~80 % of their bbox, which takes masks up to about
@@ -2089,7 +2092,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   const size_t sz_l2i = al(sizeof(int) * (size_t)B * (ML + 1));
   const size_t sz_abs = al(sizeof(int) * (size_t)B * ML);
   const size_t sz_nl = sz_abs;
-  const size_t sz_off = al(sizeof(int) * (size_t)(B + 1 + 4));  // prefix + 4 queue counters
+  const size_t sz_off = al(sizeof(int) * (size_t)(B + 1 + 5));  // prefix + 5 queue counters
   const size_t gscr_per = (size_t)2 * (Dy + 2) * (Dx + 2);  // doubles per FOV (oversize masks)
   const size_t sz_gscr = al(sizeof(double) * B * gscr_per);
   unsigned char* o = (unsigned char*)cpx_ws(ctx, WS_SEG_OBJ,
@@ -2108,7 +2111,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
     rc = cpx_objects(ctx, d.m0, B, Dy, Dx, ML, 0, lst, obj, hdr);
     if (rc) return rc;
     CPX_CHECK_HIP(hipMemsetAsync(bad, 0, sz_bad, ctx->stream));
-    CPX_CHECK_HIP(hipMemsetAsync(off + B + 1, 0, 4 * sizeof(int), ctx->stream));
+    CPX_CHECK_HIP(hipMemsetAsync(off + B + 1, 0, 5 * sizeof(int), ctx->stream));
     hipLaunchKernelGGL(k_obj_prefix, dim3(1), dim3(64), 0, ctx->stream, B,
                        (const cpx_fov_objects*)hdr, off);
     hipLaunchKernelGGL((k_flow_error_lds<kFeSmallThreads, kFeSmallCells, kFeU>), dim3(4 * ctx->n_cu),
@@ -2119,21 +2122,25 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
                        dim3(kFeMidThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
                        Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 2,
                        kFeSmallThreads, kFeU, kFeSmallCells, flow_threshold, bad);
-    hipLaunchKernelGGL((k_flow_error_cmp<kFeCmpThreads, kFeCmpCells, kFeCmpU>), dim3(ctx->n_cu),
-                       dim3(kFeCmpThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
+    hipLaunchKernelGGL((k_flow_error_lds<kFeLargeThreads, kFeLargeCells, kFeU>), dim3(ctx->n_cu),
+                       dim3(kFeLargeThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
                        Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 3,
                        kFeMidThreads, kFeU, kFeMidCells, flow_threshold, bad);
+    hipLaunchKernelGGL((k_flow_error_cmp<kFeCmpThreads, kFeCmpCells, kFeCmpU>), dim3(ctx->n_cu),
+                       dim3(kFeCmpThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
+                       Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 4,
+                       kFeLargeThreads, kFeU, kFeLargeCells, flow_threshold, bad);
     {
       const int nbig = std::max(1, std::min(ctx->n_cu, 4 * B));
       const long long slice = (long long)(B * gscr_per / nbig) & ~1LL;
       hipLaunchKernelGGL(k_flow_error_big, dim3(nbig), dim3(kBigThreads), 0, ctx->stream,
                          (const int*)d.m0, (const float2*)d.dpf, Dy, Dx, B, ML, (const cpx_object*)obj,
-                         (const int*)off, off + B + 4, kFeMidThreads, kFeU, kFeMidCells, flow_threshold,
+                         (const int*)off, off + B + 5, kFeLargeThreads, kFeU, kFeLargeCells, flow_threshold,
                          gscr, slice, bad);
     }
     hipLaunchKernelGGL(k_flow_error_fov, dim3(B), dim3(kFlowThreads), 0, ctx->stream,
                        (const int*)d.m0, (const float2*)d.dpf, Dy, Dx, ML, (const cpx_object*)obj,
-                       (const cpx_fov_objects*)hdr, kFeMidThreads, kFeU, kFeMidCells,
+                       (const cpx_fov_objects*)hdr, kFeLargeThreads, kFeU, kFeLargeCells,
                        flow_threshold, gscr, (long long)gscr_per, bad);
     hipLaunchKernelGGL(k_apply_bad, gp, dim3(kT), 0, ctx->stream, n, ML,
                        (const unsigned char*)bad, d.m0);

@@ -125,7 +125,9 @@ def test_pipeline_unconverged_watershed_is_a_per_site_failure(dev):
     from cpx.synth import synth_fovs, synth_illum
     H = W = 768
     C, B = 5, 2
-    cfg = PipelineConfig(H=H, W=W, C=C, batch=B, ws_rounds=(1, 1))
+    w = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "image-processing-suite_amd",
+                     "cpx", "weights", "cpnet_nuclei_synth.pt")
+    cfg = PipelineConfig(H=H, W=W, C=C, batch=B, ws_rounds=(1, 1), weights=w)
     pipe = FovPipeline(dev, cfg, synth_illum(C, H, W, seed=1))
     # 768^2 FOVs with a plausible nucleus count for that area (synth_fovs' default targets 2080^2)
     raw = synth_fovs(B, C, H, W, dev.torch_device, seed=3, nuclei=(30, 45))
@@ -136,6 +138,6 @@ def test_pipeline_unconverged_watershed_is_a_per_site_failure(dev):
         for b in range(B):
             assert len(res.objects[s][b]) == 0 and len(res.feats[s][b]) == 0
             assert res.hdr[s][b]["n_objects"] == 0
-    ok = FovPipeline(dev, PipelineConfig(H=H, W=W, C=C, batch=B), synth_illum(C, H, W, seed=1))
+    ok = FovPipeline(dev, PipelineConfig(H=H, W=W, C=C, batch=B, weights=w), synth_illum(C, H, W, seed=1))
     res2 = ok.fetch(ok.run(raw))
     assert not res2.failed.any() and all(len(res2.objects["Cells"][b]) > 0 for b in range(B))
