@@ -211,8 +211,7 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
     auto mma = [&](auto cnt) {
       constexpr int C = decltype(cnt)::value;
       if constexpr (C > 0) {
-#pragma unroll 1
-        for (int tap = 0; tap < T; ++tap) {
+        auto tapbody = [&](int tap) {
           const int ky = tap / KS, kx = tap - KS * (tap / KS);
           f16x8 ah[WM], al[WM];
 #pragma unroll
@@ -233,6 +232,15 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
               acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bh, acc1[m][j], 0, 0, 0);
             }
           }
+        };
+        // single-fragment waves: all taps unrolled, the next tap's reads scheduled under this
+        // tap's MFMAs; larger wave tiles keep one tap per iteration (register budget)
+        if constexpr (WM * WN == 1) {
+#pragma unroll
+          for (int tap = 0; tap < T; ++tap) tapbody(tap);
+        } else {
+#pragma unroll 1
+          for (int tap = 0; tap < T; ++tap) tapbody(tap);
         }
       }
     };
