@@ -23,9 +23,9 @@ Design: the GPU path of cpx.pipeline (illumination, segmentation, object table, 
 the a9 scale_to_8bit fused) runs on batches of FOVs resident in HBM; libcpx
 cpx_embed_preprocess does the processor's bicubic resize / normalisation (Pillow-exact 8-bit
 arithmetic) straight from the crops; the EfficientNetV2-L forward runs in PyTorch-ROCm under
-fp16 autocast (channels_last), as the reference's.  The result assembly is the reference's own
-pandas / numpy arithmetic (host).  Weights: timm/tf_efficientnetv2_l.in21k is a remote
-download, so --effnet-weights takes a local state_dict, else a seeded initialisation
+fp16 autocast (channels_last), as the reference's.  assemble() writes the reference's output
+tables (host) from the per-site results, with the same float32 summation order.
+Weights: timm/tf_efficientnetv2_l.in21k is a remote download, so --effnet-weights takes a local state_dict, else a seeded initialisation
 (embedding values parity-unpinned).
 """
 from __future__ import annotations
@@ -106,97 +106,110 @@ class Embedder:
         return out
 
 
+OUTPUT_SUFFIXES = {  # Cellpose_GPU_s3fs.py:326-471: what is written next to --out_data_path
+    "counts": "_counts.csv",
+    "coords": "_coords.parquet",
+    "wells": "_well_aggregated.parquet",
+    "wells_filtered": "_filtered_well_aggregated.parquet",
+    "single_cell": "_single_cell.parquet",
+}
+
+
+def _site_arrays(results, index, C, L):
+    """Per LoadData row (in row order): features [n, C, L] float32, coords [(y, x)], dead [n]."""
+    feats, coords, dead = [], [], []
+    for idx in index:
+        r = results[idx]
+        ok = r["status"] != "empty"
+        feats.append(np.asarray(r["features"], np.float32) if ok else np.zeros((0, C, L), np.float32))
+        coords.append([tuple(c) for c in r["coords"]] if ok else [])
+        dead.append(np.asarray(r["is_dead"], bool) if ok else np.zeros(0, bool))
+    return feats, coords, dead
+
+
+def _site_sums(feats, dead, drop_dead):
+    """Per site: the float32 embedding sum over its (alive) cells — numpy's axis-0 reduction, i.e.
+    cells added in order — and the number of cells that entered it."""
+    sums, counts = [], []
+    for f, d in zip(feats, dead):
+        keep = f[~d] if drop_dead else f
+        counts.append(len(keep))
+        sums.append(keep.sum(axis=0) if len(keep) else np.zeros(f.shape[1:], np.float32))
+    return sums, counts
+
+
+def _well_table(ld, sums, C, L):
+    """One row per Metadata_Well (sorted, as groupby): Cell_Count (sum), first Metadata_Timepoint /
+    Metadata_Plate when present, mean_features = float32 well sum / float32 count as nested lists
+    (zeros when the well has no cell)."""
+    import pandas as pd
+    wells = ld["Metadata_Well"].to_numpy()
+    keys = sorted(set(wells.tolist()))
+    extra = [c for c in ("Metadata_Timepoint", "Metadata_Plate") if c in ld.columns]
+    rows = []
+    for w in keys:
+        pos = np.flatnonzero(wells == w)
+        tot = sums[pos[0]].copy()
+        for p in pos[1:]:  # sites added in row order
+            tot += sums[p]
+        n = int(ld["Cell_Count"].to_numpy()[pos].sum())
+        row = {"Metadata_Well": w, "Cell_Count": n}
+        for c in extra:
+            v = ld[c].iloc[pos]
+            v = v[v.notna()]
+            row[c] = v.iloc[0] if len(v) else np.nan
+        row["mean_features"] = (tot / np.float32(n)).tolist() if n > 0 else np.zeros((C, L)).tolist()
+        rows.append(row)
+    return pd.DataFrame(rows, columns=["Metadata_Well", "Cell_Count", *extra, "mean_features"])
+
+
 def assemble(load_data, results, channels, out_data_path, save_coords=False, single_cell=False,
              xgb=False, filter_dead_cells=False):
-    """Cellpose_GPU_s3fs.py:326-471 on the per-site results
-    {index: {'status', 'features' [n, C, 1280] float32, 'coords' [(y, x)], 'is_dead' [n]}}.
-    Returns the output paths written."""
+    """Writes the embedding outputs of Cellpose_GPU_s3fs.py:326-471 from the per-site results
+    {row index: {'status', 'features' [n, C, 1280] float32, 'coords' [(y, x)], 'is_dead' [n]}}:
+      counts       LoadData + Cell_Count (alive cells when dead cells are filtered) [+ Dead_Cells]
+      coords       (--save_coords, when any cell) Cell_ID "{well}_{site}_cell{i}", Y/X_Center, Is_Dead
+      wells        per well: Cell_Count, first timepoint / plate, mean_features (C x 1280)
+      single_cell  (--single_cell) one row per cell of every non-empty site: the LoadData row
+                   (original index kept), Cell_Index, single_cell_features (C * 1280)
+                   [+ is_dead_cell]; no non-empty site -> the counts table itself
+    Dead_Cells is the per-site dead count (0 for empty sites).  Returns the paths written."""
     import pandas as pd
-    C = len(channels)
-    L = effnet.FEATURE_LENGTH
-    load_data = load_data.copy()
-    original_indices = list(load_data.index)
-    site_features, site_coords, site_dead_flags = [], [], []
-    for idx in original_indices:
-        res = results[idx]
-        if res["status"] == "empty":
-            site_features.append(np.zeros((0, C, L), dtype=np.float32))
-            site_coords.append([])
-            site_dead_flags.append(np.array([], dtype=bool))
-        else:
-            site_features.append(res["features"])
-            site_coords.append([tuple(c) for c in res["coords"]])
-            site_dead_flags.append(res["is_dead"])
-    aggregated_features, final_site_counts, final_dead_counts = [], [], []
-    for feats, flags in zip(site_features, site_dead_flags):
-        if len(feats) == 0:
-            aggregated_features.append(np.zeros((C, L), dtype=np.float32))
-            final_site_counts.append(0)
-        elif xgb and filter_dead_cells:
-            alive = ~flags
-            n_alive = int(np.sum(alive))
-            aggregated_features.append(np.sum(feats[alive], axis=0) if n_alive > 0 else np.zeros((C, L), np.float32))
-            final_site_counts.append(n_alive)
-            final_dead_counts.append(int(flags.sum()))
-        else:
-            aggregated_features.append(np.sum(feats, axis=0))
-            final_site_counts.append(len(feats))
-    load_data["Cell_Count"] = final_site_counts
+    C, L = len(channels), effnet.FEATURE_LENGTH
+    ld = load_data.copy()
+    feats, coords, dead = _site_arrays(results, list(ld.index), C, L)
+    sums, counts = _site_sums(feats, dead, xgb and filter_dead_cells)
+    ld["Cell_Count"] = counts
     if xgb:
-        load_data["Dead_Cells"] = final_dead_counts
-    written = []
-    counts_out_path = out_data_path.replace(".parquet", "_counts.csv")
-    os.makedirs(os.path.dirname(os.path.abspath(counts_out_path)), exist_ok=True)
-    load_data.to_csv(counts_out_path, index=False)
-    written.append(counts_out_path)
+        ld["Dead_Cells"] = [int(d.sum()) for d in dead]
+    path = {k: out_data_path.replace(".parquet", v) for k, v in OUTPUT_SUFFIXES.items()}
+    os.makedirs(os.path.dirname(os.path.abspath(path["counts"])), exist_ok=True)
+    ld.to_csv(path["counts"], index=False)
+    written = [path["counts"]]
     if save_coords:
-        recs = []
-        for idx, coords_list, dead_flags in zip(original_indices, site_coords, site_dead_flags):
-            well = load_data.loc[idx, "Metadata_Well"]
-            site = load_data.loc[idx, "Metadata_Site"] if "Metadata_Site" in load_data.columns else str(idx)
-            for cell_idx, (y, x) in enumerate(coords_list):
-                is_dead = dead_flags[cell_idx] if len(dead_flags) > 0 else False
-                recs.append({"Cell_ID": f"{well}_{site}_cell{cell_idx}", "Y_Center": y, "X_Center": x,
-                             "Is_Dead": is_dead})
+        has_site = "Metadata_Site" in ld.columns
+        recs = [{"Cell_ID": f"{ld.at[idx, 'Metadata_Well']}_{ld.at[idx, 'Metadata_Site'] if has_site else str(idx)}_cell{i}",
+                 "Y_Center": y, "X_Center": x, "Is_Dead": bool(d[i]) if len(d) else False}
+                for idx, cs, d in zip(ld.index, coords, dead) for i, (y, x) in enumerate(cs)]
         if recs:
-            p = out_data_path.replace(".parquet", "_coords.parquet")
-            pd.DataFrame(recs).to_parquet(p, engine="pyarrow")
-            written.append(p)
-    agg = load_data.copy()
-    agg["sum_features"] = aggregated_features
-    funcs = {"sum_features": lambda s: np.sum(np.stack(s.values), axis=0), "Cell_Count": "sum"}
-    for col in ["Metadata_Well", "Metadata_Timepoint", "Metadata_Plate"]:
-        if col != "Metadata_Well" and col in agg.columns:
-            funcs[col] = "first"
-    well = agg.groupby("Metadata_Well").agg(funcs).reset_index()
-    # numpy 1.24 (requirements.txt:1-12): float32 sums / int count stay float32
-    well["mean_features"] = well.apply(
-        lambda r: (r["sum_features"] / np.float32(r["Cell_Count"])).tolist() if r["Cell_Count"] > 0
-        else np.zeros((C, L)).tolist(), axis=1)
-    well = well.drop(columns=["sum_features"])
-    p = out_data_path.replace(".parquet", "_filtered_well_aggregated.parquet" if filter_dead_cells
-                              else "_well_aggregated.parquet")
-    well.to_parquet(p, engine="pyarrow")
-    written.append(p)
+            pd.DataFrame(recs).to_parquet(path["coords"], engine="pyarrow")
+            written.append(path["coords"])
+    wpath = path["wells_filtered" if filter_dead_cells else "wells"]
+    _well_table(ld, sums, C, L).to_parquet(wpath, engine="pyarrow")
+    written.append(wpath)
     if single_cell:
-        sc = out_data_path.replace(".parquet", "_single_cell.parquet")
-        valid = [i for i, f in enumerate(site_features) if len(f) > 0]
-        if not valid:
-            load_data.to_parquet(sc, engine="pyarrow")
-            return written + [sc]
-        sites = load_data.iloc[valid].copy()
-        vf = [site_features[i] for i in valid]
-        flags = [site_dead_flags[i] for i in valid]
-        ex = sites.loc[sites.index.repeat([len(f) for f in vf])].copy()
-        ex["Cell_Index"] = ex.groupby(level=0).cumcount()
-        st = np.concatenate(vf, axis=0)
-        ex["single_cell_features"] = list(st.reshape(st.shape[0], -1))
-        if xgb:
-            ex["is_dead_cell"] = np.concatenate(flags)
-        if "Cell_Count" in ex.columns:
-            ex = ex.drop(columns=["Cell_Count"])
-        ex.to_parquet(sc, engine="pyarrow", row_group_size=100000)
-        written.append(sc)
+        nz = [i for i, f in enumerate(feats) if len(f)]
+        if not nz:
+            ld.to_parquet(path["single_cell"], engine="pyarrow")
+        else:
+            reps = np.array([len(feats[i]) for i in nz])
+            sc = ld.iloc[np.repeat(nz, reps)].drop(columns=["Cell_Count"]).copy()
+            sc["Cell_Index"] = np.concatenate([np.arange(r) for r in reps])
+            sc["single_cell_features"] = list(np.concatenate([feats[i] for i in nz]).reshape(int(reps.sum()), C * L))
+            if xgb:
+                sc["is_dead_cell"] = np.concatenate([dead[i] for i in nz])
+            sc.to_parquet(path["single_cell"], engine="pyarrow", row_group_size=100000)
+        written.append(path["single_cell"])
     return written
 
 

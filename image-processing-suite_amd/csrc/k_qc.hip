@@ -434,6 +434,173 @@ __global__ __launch_bounds__(kThreads) void k_qc_slope(const double* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Row pass specialised for W = 2080 = 13 x 20 x 8 (the plate's FOV width): three Stockham
+// passes, each butterfly's points in registers, two LDS exchanges instead of one per radix, and
+// the last pass pruned to the frequencies the rings use.  One 256-thread block per (row pair,
+// plane), 33 KB of LDS (four blocks per CU).
+//   P1 R = 13, Ns = 1:   j < 160, points x[j + 160 r] straight from global (two rows as one
+//                        complex sequence), DFT13, to A[13 j + r];
+//   P2 R = 20, Ns = 13:  j < 104, points A[j + 104 r] times W_260^((j % 13) r), DFT20 (4 x 5),
+//                        to A[(j / 13) 260 + j % 13 + 13 r];
+//   P3 R = 8, Ns = 260:  j < 260, points A[j + 260 r] times W_2080^(j r); only the outputs
+//                        X[j] (r' = 0) and X[1820 + j] (r' = 7) — the columns k < 260 and their
+//                        mirrored partners N - k that the two-real-rows unpack needs.
+constexpr int kR2N = 2080, kR2T = 256, kR2KC = 260;
+
+// W_20^t = exp(-2 pi i t / 20), t = 0 .. 12 (the products m k1 of the 4 x 5 split)
+__device__ __forceinline__ cplx w20(int t) {
+  constexpr double c1 = 0.9510565162951535, s1 = 0.30901699437494745;
+  constexpr double c2 = 0.8090169943749475, s2 = 0.5877852522924731;
+  switch (t) {
+    case 0: return {1.0, 0.0};
+    case 1: return {c1, -s1};
+    case 2: return {c2, -s2};
+    case 3: return {s2, -c2};
+    case 4: return {s1, -c1};
+    case 5: return {0.0, -1.0};
+    case 6: return {-s1, -c1};
+    case 7: return {-s2, -c2};
+    case 8: return {-c2, -s2};
+    case 9: return {-c1, -s1};
+    case 10: return {-1.0, 0.0};
+    case 11: return {-c1, s1};
+    default: return {-c2, s2};
+  }
+}
+
+// in-register 20-point DFT: n = m + 5 p, k = k1 + 4 k2:
+//   X[k1 + 4 k2] = sum_m W_5^(m k2) W_20^(m k1) sum_p v[m + 5 p] W_4^(p k1)
+__device__ __forceinline__ void dft20(cplx* v) {
+  cplx y[5][4];
+#pragma unroll
+  for (int m = 0; m < 5; ++m) {
+    cplx q[4] = {v[m], v[m + 5], v[m + 10], v[m + 15]};
+    dft<4>(q, nullptr);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) y[m][k1] = (m * k1 == 0) ? q[k1] : cmul(q[k1], w20(m * k1));
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    cplx q[5] = {y[0][k1], y[1][k1], y[2][k1], y[3][k1], y[4][k1]};
+    dft<5>(q, nullptr);
+#pragma unroll
+    for (int k2 = 0; k2 < 5; ++k2) v[k1 + 4 * k2] = q[k2];
+  }
+}
+
+template <int ILLUM>
+__global__ __launch_bounds__(kR2T) void k_qc_rows_2080(
+    const unsigned short* __restrict__ raw, const void* __restrict__ illum, int C, int H,
+    const cpx_plane_stats* __restrict__ stats, const cplx* __restrict__ tw, cplx* __restrict__ rowspec,
+    QcAux* __restrict__ aux) {
+  constexpr int W = kR2N;
+  __shared__ cplx A[kR2N];
+  __shared__ cplx t260[260];
+  const int plane = blockIdx.y;
+  const int ch = plane % C;
+  const int r0 = 2 * blockIdx.x, r1 = r0 + 1;
+  const long long N = (long long)H * W;
+  const unsigned short* rp = raw + (long long)plane * N;
+  const void* il = nullptr;
+  if (ILLUM == 1) il = static_cast<const float*>(illum) + (long long)ch * N;
+  if (ILLUM == 2 || ILLUM == 3) il = static_cast<const double*>(illum) + (long long)ch * N;
+  const cpx_plane_stats st = stats[plane];
+  const double mean = st.sum_q / (double)st.n;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 260; i += kR2T) t260[i] = tw[8 * i];  // W_260^i = W_2080^(8 i)
+  // ---- P1
+  unsigned long long eq = 0;
+  if (tid < 160) {
+    cplx v[13];
+#pragma unroll
+    for (int r = 0; r < 13; ++r) {
+      const int n = tid + 160 * r;
+      const double qa = qval<ILLUM>(rp, il, (long long)r0 * W + n);
+      const double qb = r1 < H ? qval<ILLUM>(rp, il, (long long)r1 * W + n) : mean;
+      eq += (qa == mean) + (r1 < H && qb == mean);
+      v[r] = cplx{qa - mean, qb - mean};
+    }
+    dft<13>(v, nullptr);
+#pragma unroll
+    for (int r = 0; r < 13; ++r) A[13 * tid + r] = v[r];
+  }
+  eq = wave_sum(eq);
+  if ((tid & 63) == 0 && eq) atomicAdd(&aux[plane].eq_count, eq);
+  __syncthreads();
+  // ---- P2
+  {
+    cplx v[20];
+    if (tid < 104) {
+      const int k = tid % 13;
+#pragma unroll
+      for (int r = 0; r < 20; ++r) v[r] = A[tid + 104 * r];
+#pragma unroll
+      for (int r = 1; r < 20; ++r) v[r] = cmul(v[r], t260[k * r]);
+      dft20(v);
+    }
+    __syncthreads();
+    if (tid < 104) {
+      const int d = (tid / 13) * 260 + tid % 13;
+#pragma unroll
+      for (int r = 0; r < 20; ++r) A[d + 13 * r] = v[r];
+    }
+    __syncthreads();
+  }
+  // ---- P3 (pruned): lo = X[j], hi = X[1820 + j]
+  {
+    constexpr int NR = (260 + kR2T - 1) / kR2T;
+    cplx lo[NR], hi[NR];
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      const int j = tid + q * kR2T;
+      lo[q] = hi[q] = cplx{0.0, 0.0};
+      if (j < 260) {
+        cplx v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = A[j + 260 * r];
+#pragma unroll
+        for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], tw[j * r]);
+        // r' = 0: sum v[r];  r' = 7: sum v[r] W_8^(7 r) = sum v[r] exp(+i pi r / 4)
+        const double h = 0.70710678118654752440;
+        cplx a = cadd(cadd(v[0], v[4]), cadd(v[2], v[6]));
+        cplx b = cadd(cadd(v[1], v[5]), cadd(v[3], v[7]));
+        lo[q] = cadd(a, b);
+        // exp(+i pi r / 4): r = 0: 1, 1: h(1 + i), 2: i, 3: h(-1 + i), 4: -1, 5: -h(1 + i), 6: -i, 7: h(1 - i)
+        const cplx e0 = csub(v[0], v[4]);                       // r = 0, 4
+        const cplx e2 = csub(v[2], v[6]);                       // r = 2, 6 (times i)
+        const cplx o1 = csub(v[1], v[5]);                       // r = 1, 5 (times h(1 + i))
+        const cplx o3 = csub(v[3], v[7]);                       // r = 3, 7 (times h(-1 + i))
+        const cplx ie2 = cplx{-e2.y, e2.x};
+        const cplx t1 = cplx{h * (o1.x - o1.y), h * (o1.x + o1.y)};
+        const cplx t3 = cplx{h * (-o3.x - o3.y), h * (o3.x - o3.y)};
+        hi[q] = cadd(cadd(e0, ie2), cadd(t1, t3));
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      const int j = tid + q * kR2T;
+      if (j < 260) {
+        A[j] = lo[q];
+        A[260 + j] = hi[q];
+      }
+    }
+    __syncthreads();
+  }
+  // ---- unpack the two real rows for k < KC: Z[N - k] = X[1820 + (260 - k)]
+  cplx* outa = rowspec + ((long long)plane * H + r0) * kR2KC;
+  for (int k = tid; k < kR2KC; k += kR2T) {
+    const cplx zk = A[k];
+    const cplx zn = k == 0 ? A[0] : A[260 + 260 - k];
+    const cplx xa = {0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)};
+    const cplx dlt = {zk.x - zn.x, zk.y + zn.y};
+    const cplx xb = {0.5 * dlt.y, -0.5 * dlt.x};
+    outa[k] = xa;
+    if (r1 < H) outa[kR2KC + k] = xb;
+  }
+}
+
 bool make_plan(int n, Plan& p) {
   if (n < 1 || n > kMaxN) return false;
   p.n = n;
@@ -529,7 +696,16 @@ extern "C" int cpx_qc_rps(cpx_ctx* ctx, const uint16_t* raw_dev, const void* ill
     const size_t sh_rows = sizeof(cplx) * (size_t)W;
     dim3 grow((H + 1) / 2, n_planes);
     const void* il = illum_dtype == CPX_DTYPE_NONE ? nullptr : illum_dev;
-    if (illum_dtype == CPX_DTYPE_F32)
+    if (W == kR2N && KC == kR2KC && !getenv("CPX_QC_GENERIC")) {
+      const cplx* t = (const cplx*)twW;
+#define CPX_R2(I) hipLaunchKernelGGL(k_qc_rows_2080<I>, grow, dim3(kR2T), 0, ctx->stream, raw_dev, il, C, H, \
+                                     stats_dev, t, rowspec, aux)
+      if (illum_dtype == CPX_DTYPE_F32) CPX_R2(1);
+      else if (illum_dtype == CPX_DTYPE_F64) CPX_R2(2);
+      else if (illum_dtype == CPX_DTYPE_IMAGE_F64) CPX_R2(3);
+      else CPX_R2(0);
+#undef CPX_R2
+    } else if (illum_dtype == CPX_DTYPE_F32)
       hipLaunchKernelGGL(k_qc_rows<1>, grow, dim3(kFT), sh_rows, ctx->stream, raw_dev, il, C,
                          H, W, stats_dev, (const cplx*)twW, pw, KC, rowspec, aux);
     else if (illum_dtype == CPX_DTYPE_F64)

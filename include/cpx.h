@@ -427,6 +427,10 @@ int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* in, int N, 
                       const float* shift, int relu, void* y_out, void* z_out, int z_up,
                       const float* head_w, const float* head_b, int n_head, float* head_out,
                       int* ovf);
+/* Variant 2 of cpx_cpnet_x3_conv (3x3) is persistent: a grid of two blocks per CU walks the
+ * tiles, each tile's first channel slab loading while the previous tile finishes.  This caps
+ * that grid at max_blocks (0 = default) — tests use it to give every block several tiles.     */
+int cpx_cpnet_x3_set_grid(cpx_ctx* ctx, int max_blocks);
 /* stem on the fp32 network input x [N][H][W][2] (CPX_TILE_F32_NHWC tiles): z0 = relu(scale0 x
  * + shift0), z_out = relu(scale1 (conv3x3(z0, w0) + bias0) + shift1), p_out = conv1x1(x, wp),
  * fp32 arithmetic, split stores (32 channels).                                               */

@@ -139,3 +139,65 @@ def test_preprocess_table_survives_workspace_regrowth(dev):
         for j, i in enumerate(idx):
             ref = eo.pixel_values(c8[i], 384).astype(np.float16)
             np.testing.assert_array_equal(got[j].view(np.uint16), ref.view(np.uint16))
+
+
+@pytest.mark.parametrize("xgb,filt", [(False, False), (True, True), (True, False)])
+def test_assemble_output_layout(tmp_path, xgb, filt):
+    """assemble() against the output spec of Cellpose_GPU_s3fs.py:326-471, on hand-made per-site
+    results (one empty site, one well with no cell): counts, coords, well means (float32 sums of
+    the alive cells in row order / float32 count) and the single-cell explode."""
+    import pandas as pd
+    from cpx import embed
+    C, L = 2, effnet.FEATURE_LENGTH
+    rng = np.random.default_rng(4)
+    ld = pd.DataFrame({"Metadata_Plate": ["P"] * 5, "Metadata_Well": ["B02", "A01", "B02", "A01", "C03"],
+                       "Metadata_Site": [1, 1, 2, 2, 1], "Metadata_Timepoint": [6, 6, 6, 6, 6]},
+                      index=[10, 11, 12, 13, 14])
+    ncell = {10: 3, 11: 2, 12: 0, 13: 4, 14: 0}
+    res = {}
+    for i, n in ncell.items():
+        if n == 0:
+            res[i] = {"status": "empty", "n_cells": 0}
+            continue
+        res[i] = {"status": "success", "features": rng.standard_normal((n, C, L)).astype(np.float32),
+                  "coords": [(int(y), int(x)) for y, x in rng.integers(0, 500, (n, 2))],
+                  "is_dead": rng.random(n) < 0.4, "n_cells": n}
+    out = str(tmp_path / "o" / "emb.parquet")
+    written = embed.assemble(ld, res, ["DNA", "AGP"], out, save_coords=True, single_cell=True,
+                             xgb=xgb, filter_dead_cells=filt)
+    counts = pd.read_csv(tmp_path / "o" / "emb_counts.csv")
+    drop = xgb and filt
+    alive = {i: (~res[i]["is_dead"] if drop else np.ones(n, bool)) if n else np.zeros(0, bool)
+             for i, n in ncell.items()}
+    assert counts["Cell_Count"].tolist() == [int(alive[i].sum()) for i in ld.index]
+    if xgb:
+        assert counts["Dead_Cells"].tolist() == [int(res[i]["is_dead"].sum()) if ncell[i] else 0 for i in ld.index]
+    coords = pd.read_parquet(tmp_path / "o" / "emb_coords.parquet")
+    assert coords["Cell_ID"].tolist() == [f"{ld.at[i, 'Metadata_Well']}_{ld.at[i, 'Metadata_Site']}_cell{k}"
+                                          for i in ld.index for k in range(ncell[i])]
+    wname = "emb_filtered_well_aggregated.parquet" if filt else "emb_well_aggregated.parquet"
+    well = pd.read_parquet(tmp_path / "o" / wname)
+    assert list(well.columns) == ["Metadata_Well", "Cell_Count", "Metadata_Timepoint", "Metadata_Plate", "mean_features"]
+    assert well["Metadata_Well"].tolist() == ["A01", "B02", "C03"]
+    for _, r in well.iterrows():
+        rows = [i for i in ld.index if ld.at[i, "Metadata_Well"] == r["Metadata_Well"]]
+        tot, n = np.zeros((C, L), np.float32), 0
+        for i in rows:
+            if ncell[i]:
+                s = np.zeros((C, L), np.float32)
+                for k in np.flatnonzero(alive[i]):
+                    s += res[i]["features"][k]
+                tot += s
+                n += int(alive[i].sum())
+        got = np.array(r["mean_features"].tolist(), dtype=np.float64)
+        want = (tot / np.float32(n)).astype(np.float64) if n else np.zeros((C, L))
+        np.testing.assert_array_equal(got, want)
+        assert r["Cell_Count"] == n
+    sc = pd.read_parquet(tmp_path / "o" / "emb_single_cell.parquet")
+    assert len(sc) == sum(ncell.values()) and "Cell_Count" not in sc.columns
+    assert sc.index.tolist() == [i for i in ld.index for _ in range(ncell[i])]
+    assert sc["Cell_Index"].tolist() == [k for i in ld.index for k in range(ncell[i])]
+    # row 3 = the first cell of the second non-empty site (row 11)
+    np.testing.assert_array_equal(np.stack(sc["single_cell_features"].to_numpy())[3], res[11]["features"][0].reshape(-1))
+    assert ("is_dead_cell" in sc.columns) == xgb
+    assert len(written) == 4

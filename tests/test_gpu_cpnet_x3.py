@@ -69,7 +69,15 @@ CONFIGS = [  # ks, cin, cout, H, W, variant
     (3, 128, 64, 16, 16, 0), (3, 64, 128, 30, 29, 0), (3, 128, 128, 28, 28, 1), (3, 256, 128, 14, 14, 0),
     (3, 128, 256, 14, 28, 0), (3, 256, 256, 16, 12, 1), (1, 32, 64, 20, 22, 0), (1, 64, 128, 17, 16, 0),
     (1, 128, 256, 14, 14, 0), (1, 256, 256, 9, 7, 0), (1, 256, 128, 8, 8, 0), (1, 128, 64, 12, 16, 0),
-    (1, 64, 32, 16, 16, 0)]
+    (1, 64, 32, 16, 16, 0),
+    # variant 2 (persistent): the grid capped at 5 blocks (set below), so each block walks several
+    # tiles and its next tile's first slab streams in while the previous one finishes
+    (3, 32, 32, 40, 70, 2), (3, 64, 32, 24, 36, 2), (3, 32, 64, 28, 20, 2), (3, 64, 64, 20, 18, 2),
+    (3, 128, 64, 16, 16, 2), (3, 64, 128, 30, 29, 2), (3, 128, 128, 28, 28, 2), (3, 256, 128, 14, 14, 2),
+    (3, 128, 256, 14, 28, 2), (3, 256, 256, 16, 12, 2),
+    # variant 3: 16-wave blocks with BM 64 at 112^2 and below
+    (3, 32, 64, 28, 20, 3), (3, 64, 64, 36, 18, 3), (3, 128, 64, 16, 16, 3), (3, 64, 128, 30, 29, 3),
+    (3, 128, 128, 28, 28, 3), (3, 256, 128, 14, 14, 3), (3, 128, 256, 14, 28, 3), (3, 256, 256, 33, 12, 3)]
 
 
 @pytest.mark.gpu
@@ -97,9 +105,13 @@ def test_x3_conv_epilogue_vs_fp64(dev, ks, cin, cout, H, W, variant):
     bd, sd, scd, shd = (torch.from_numpy(a).to(td) for a in (bias, style, scale, shift))
     ovf = torch.zeros(1, dtype=torch.int32, device=td)
     P = lambda t: ct.c_void_p(t.data_ptr())  # noqa: E731
-    rc = lib.cpx_cpnet_x3_conv(dev.h, ks, variant, P(xd), N, H, W, cin, cout, P(pk), P(bd), P(resd), int(res_up),
-                               P(sd), cout + 8, P(scd), P(shd), 1, P(yd), P(zd), int(z_up), None, None, 0, None,
-                               P(ovf))
+    assert lib.cpx_cpnet_x3_set_grid(dev.h, 5 if variant == 2 else 0) == 0
+    try:
+        rc = lib.cpx_cpnet_x3_conv(dev.h, ks, variant, P(xd), N, H, W, cin, cout, P(pk), P(bd), P(resd),
+                                   int(res_up), P(sd), cout + 8, P(scd), P(shd), 1, P(yd), P(zd), int(z_up), None,
+                                   None, 0, None, P(ovf))
+    finally:
+        lib.cpx_cpnet_x3_set_grid(dev.h, 0)
     assert rc == 0, lib.cpx_last_error()
     torch.cuda.synchronize()
     # fp64 reference on the split-representable operands
@@ -131,12 +143,14 @@ def test_x3_conv_epilogue_vs_fp64(dev, ks, cin, cout, H, W, variant):
 
 
 @pytest.mark.gpu
-def test_x3_head_and_overflow(dev):
+@pytest.mark.parametrize("variant", [0, 2])
+def test_x3_head_and_overflow(dev, variant):
     lib, td = dev.lib, dev.torch_device
     rng = np.random.default_rng(7)
     N, H, W, cin, cout, nh = 1, 24, 40, 32, 32, 3
     bm = ct.c_int()
-    assert lib.cpx_cpnet_x3_cfg(3, cin, cout, 0, ct.byref(bm)) == 0
+    assert lib.cpx_cpnet_x3_cfg(3, cin, cout, variant, ct.byref(bm)) == 0
+    assert lib.cpx_cpnet_x3_set_grid(dev.h, 2 if variant == 2 else 0) == 0
     x = rng.standard_normal((N, H, W, cin)).astype(np.float32)
     w = (rng.standard_normal((cout, cin, 3, 3)) * 0.08).astype(np.float32)
     bias = (0.1 * rng.standard_normal(cout)).astype(np.float32)
@@ -150,7 +164,7 @@ def test_x3_head_and_overflow(dev):
     out = torch.empty((N, H, W, nh), dtype=torch.float32, device=td)
     dv = [torch.from_numpy(a).to(td) for a in (bias, scale, shift, hw, hb)]
     ovf = torch.zeros(1, dtype=torch.int32, device=td)
-    rc = lib.cpx_cpnet_x3_conv(dev.h, 3, 0, P(xd), N, H, W, cin, cout, P(pk), P(dv[0]), None, 0, None, 0,
+    rc = lib.cpx_cpnet_x3_conv(dev.h, 3, variant, P(xd), N, H, W, cin, cout, P(pk), P(dv[0]), None, 0, None, 0,
                                P(dv[1]), P(dv[2]), 1, None, None, 0, P(dv[3]), P(dv[4]), nh, P(out), P(ovf))
     assert rc == 0
     hi, lo = split_f16(w)
@@ -165,8 +179,9 @@ def test_x3_head_and_overflow(dev):
     big = x * 1e5
     zd = torch.empty((N, H, W, cout), dtype=torch.int32, device=td)
     xd2 = torch.from_numpy(to_split(np.clip(big, -60000, 60000)).reshape(N, H, W, 2 * cin).view(np.int32)).to(td)
-    rc = lib.cpx_cpnet_x3_conv(dev.h, 3, 0, P(xd2), N, H, W, cin, cout, P(pk), P(dv[0]), None, 0, None, 0,
+    rc = lib.cpx_cpnet_x3_conv(dev.h, 3, variant, P(xd2), N, H, W, cin, cout, P(pk), P(dv[0]), None, 0, None, 0,
                                None, None, 0, None, P(zd), 0, None, None, 0, None, P(ovf))
+    lib.cpx_cpnet_x3_set_grid(dev.h, 0)
     assert rc == 0
     assert int(ovf.item()) == 1
 

@@ -92,6 +92,32 @@ def test_illum_qc_full_fov_batched(dev, golden_dir):
     np.testing.assert_array_equal(corr[1], orc.illum_correct_producer(raw[1], ill[1]))
 
 
+def test_qc_rows_2080_matches_generic_fft(dev, monkeypatch):
+    """The W = 2080 row pass (k_qc_rows_2080: three register passes, pruned last pass) against the
+    generic Stockham row pass on the same planes — ordinary FOVs, an odd row count (H = 2079: the
+    last row pair has one row), a constant plane, a NaN pixel, a plane that is mostly its mean."""
+    rng = np.random.default_rng(31)
+    H, W = 2080, 2080
+    raw = rng.integers(100, 4000, (5, H, W), dtype=np.uint16)
+    raw[1] = 1234
+    raw[3, :1500] = 777
+    ill = (0.7 + 0.6 * rng.random((1, H, W))).astype(np.float32)
+    ill_nan = ill.copy()
+    for case_raw, case_ill, h in ((raw, ill, H), (raw[:, :2079], ill[:, :2079], 2079), (raw[4:5], ill_nan, H)):
+        if case_ill is ill_nan:
+            case_ill = case_ill.copy()
+            case_ill[0, 17, 33] = np.nan
+        monkeypatch.setenv("CPX_QC_GENERIC", "1")
+        _, qg, pg, _ = _run_qc(dev, case_raw, case_ill)
+        monkeypatch.delenv("CPX_QC_GENERIC")
+        _, qs, ps, _ = _run_qc(dev, case_raw, case_ill)
+        for p in range(case_raw.shape[0]):
+            a, b = qs[p]["slope"], qg[p]["slope"]
+            assert (np.isnan(a) and np.isnan(b)) or a == pytest.approx(b, rel=1e-12, abs=1e-14), (h, p, a, b)
+            fin = np.isfinite(pg[p]) & (pg[p] > 0)
+            np.testing.assert_allclose(ps[p][fin], pg[p][fin], rtol=1e-10, err_msg=f"{h} {p}")
+
+
 def test_zmax_vs_maximum_reduce(dev, golden_dir):
     d = _load(golden_dir, "maxproj")
     planes = np.stack([d[f"plane{z}"] for z in range(5)])
