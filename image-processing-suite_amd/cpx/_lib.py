@@ -125,7 +125,7 @@ SIGNATURES = {
                                     _P, _P, _I, _P]),
     "cpx_cpnet_stem": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cpx_cpnet_x3_cfg": (_I, [_I, _I, _I, _I, _P]),
-    "cpx_cpnet_x3_conv": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _I, _P, _P, _I,
+    "cpx_cpnet_x3_conv": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _I, _P, _P, _I,
                                _P, _P, _I, _P, _P, _I, _P, _P]),
     "cpx_cpnet_x3_set_grid": (_I, [_P, _I]),
     "cpx_cpnet_x3_stem": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -155,8 +155,10 @@ class FusedCPnetX3:
         return torch.empty((N, H, W, C), dtype=torch.int32, device=self.td)  # split: 4 B per channel
 
     def _conv(self, x, pk, cout, bias, ks=3, res=None, res_up=False, style=None, bn=None, relu=True,
-              y=False, z=True, z_up=False, head=False):
+              y=False, z=True, z_up=False, head=False, in_up=False):
         N, H, W, cin = x.shape
+        if in_up:  # x is read 2x nearest-upsampled: the output has twice its size
+            H, W = 2 * H, 2 * W
         yo = self._empty(N, H, W, cout) if y else None
         zo = None
         if z and not head:
@@ -165,7 +167,7 @@ class FusedCPnetX3:
         scale, shift = bn if bn is not None else (None, None)
         st, st_stride = (None, 0) if style is None else style
         check(self.lib.cpx_cpnet_x3_conv(
-            self.dev.h, ks, self.variant, _p(x), N, H, W, cin, cout, _p(pk), _p(bias), _p(res), int(res_up),
+            self.dev.h, ks, self.variant, _p(x), int(in_up), N, H, W, cin, cout, _p(pk), _p(bias), _p(res), int(res_up),
             st, st_stride, _p(scale), _p(shift), int(relu), _p(yo), _p(zo), int(z_up),
             _p(self.head_w) if head else None, _p(self.head_b) if head else None, self.nout if head else 0,
             _p(ho), _p(self.ovf)), "cpx_cpnet_x3_conv")
@@ -231,12 +233,15 @@ class FusedCPnetX3:
             so = self.style_off[n]
             sty = [(ct.c_void_p(S.data_ptr() + 4 * o), J) for o in so]
             p = self._proj(x_small, u)
-            _, z = self._conv(z0, u["pk"][0], u["cout"], u["b"][0], res=xd[n], style=sty[0], bn=u["bn"][1])
+            # below the deepest level the block input is nn.Upsample(x_small): z0 (its
+            # BatchNorm+ReLU, pointwise) stays at the small size and is read upsampled
+            _, z = self._conv(z0, u["pk"][0], u["cout"], u["b"][0], res=xd[n], style=sty[0], bn=u["bn"][1],
+                              in_up=(n < len(self.up) - 1))
             x1, z = self._conv(z, u["pk"][1], u["cout"], u["b1p"], res=p, res_up=(n < len(self.up) - 1),
                                style=sty[1], bn=u["bn"][2], y=True)
             _, z = self._conv(z, u["pk"][2], u["cout"], u["b"][2], style=sty[2], bn=u["bn"][3])
             if n > 0:
                 x_small, z0 = self._conv(z, u["pk"][3], u["cout"], u["b"][3], res=x1, bn=self.up[n - 1]["bn"][0],
-                                         y=True, z_up=True)
+                                         y=True)
             else:
                 return self._conv(z, u["pk"][3], u["cout"], u["b"][3], res=x1, bn=self.bn_out, head=True)[0]

@@ -103,9 +103,21 @@ struct X3Epi {
   float* head;          // fp32 [N][h][w][n_head]
   int n_head;
   int* ovf;
+  int in_up;  // the input is the (H/2) x (W/2) tensor read 2x nearest-upsampled
 };
 
-template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, bool PS, int NT>
+// s_waitcnt vmcnt for "all but the `younger` most recent slabs' DMA" (C instructions per slab per
+// wave; the waits need immediates)
+template <int NBUF, int C>
+__device__ __forceinline__ void x3_vm_wait(int younger) {
+  if (younger <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (NBUF >= 3 && younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C) : "memory");
+  else if (NBUF >= 4 && younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * C) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 1) * C) : "memory");
+}
+
+template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, bool PS, int NT,
+          int NBUF = 2>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, int N, int H,
                int W, int tiles_x, int tiles_y) {
@@ -130,8 +142,13 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   // output staging: both slab buffers (one tile per block), or the buffer of the slab just
   // consumed (persistent: the other one is receiving the next tile's first slab)
   static_assert(P * QB <= (PS ? SB : 2 * SB), "output tile must fit the staging LDS");
-  static_assert(2 * SB * 16 <= 163840, "LDS");
-  __shared__ uint4 smem[2 * SB];
+  // persistent ring of NBUF slab buffers (+ one 1 KiB sink for the padding DMAs that give every
+  // wave the same number of DMA instructions per slab, so counted vmcnt waits are exact)
+  static_assert(NBUF >= 2 && (PS || NBUF == 2) && NBUF <= 4, "slab ring");
+  constexpr int DSINK = PS ? 64 : 0;
+  static_assert((NBUF * SB + DSINK) * 16 <= 163840, "LDS");
+  static_assert((NBUF - 1) * (JW + JI) <= 63, "vmcnt");
+  __shared__ uint4 smem[NBUF * SB + DSINK];
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int mw = wid % MWV, pg = wid / MWV;
@@ -166,11 +183,14 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
 
   // DMA sources: weights (lane-constant swizzle), halo chunks of the tile (zero chunk outside)
   const int fW = (lane & ~3) | ((lane & 3) ^ ((lane >> 4) & 3));
+  // in_up: the source pixel of (gy, gx) is (gy / 2, gx / 2) of the half-size input (nearest
+  // 2x upsampling folded into the halo DMA; the L2 serves each source line to four output pixels)
+  const int iu = ep.in_up, Wi = W >> iu;
   auto issue = [&](int item, int ch, int buf) {
     const int tile = item / NB, nb = item - tile * NB;
     const int n = tile / tiles, t = tile - n * tiles;
     const int ty0 = (t / tiles_x) * TY, tx0 = (t % tiles_x) * TX;
-    const uint4* inb = in + (long long)n * H * W * QI + ch * 4;
+    const uint4* inb = in + (long long)n * (H >> iu) * Wi * QI + ch * 4;
     const uint4* wsl = wpk + (long long)(nb * NCH + ch) * SW;
     uint4* dst = smem + buf * SB;
     int ln = lane;  // opaque in the persistent loop: the halo offsets are recomputed per tile
@@ -180,6 +200,8 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
       const int j = wid + NWV * jj;
       if (j < NWW)
         __builtin_amdgcn_global_load_lds((glb_void_t*)(wsl + j * 64 + fW), (lds_void_t*)(dst + j * 64), 16, 0, 0);
+      else if (PS)
+        __builtin_amdgcn_global_load_lds((glb_void_t*)&g_x3_zero16, (lds_void_t*)(smem + NBUF * SB), 16, 0, 0);
     }
 #pragma unroll
     for (int jj = 0; jj < JI; ++jj) {
@@ -190,8 +212,10 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
         const int hy = hp / HX, hx = hp - (hp / HX) * HX;
         const int gy = ty0 + hy - HALO, gx = tx0 + hx - HALO;
         const uint4* src = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-                               ? inb + (gy * W + gx) * QI + (cq ^ swz4(hp)) : &g_x3_zero16;
+                               ? inb + ((gy >> iu) * Wi + (gx >> iu)) * QI + (cq ^ swz4(hp)) : &g_x3_zero16;
         __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(dst + SW + j * 64), 16, 0, 0);
+      } else if (PS) {
+        __builtin_amdgcn_global_load_lds((glb_void_t*)&g_x3_zero16, (lds_void_t*)(smem + NBUF * SB), 16, 0, 0);
       }
     }
   };
@@ -417,11 +441,20 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   };
 
   // slab sequence over this block's tiles: slab s = (tile k = s / NCH, channel slab s % NCH) lives
-  // in buffer s & 1; slab s + 1 (possibly the next tile's first) is in flight while slab s is
-  // multiplied
-  issue(first, 0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // in buffer s % NBUF.  One tile per block: slab s + 1 streams in while slab s is multiplied.
+  // Persistent: NBUF - 1 slabs (across tile boundaries) are in flight while slab s is multiplied,
+  // each wave waiting (counted vmcnt) only for its own share of slab s before the barrier.
+  const int S = (PS ? count : 1) * NCH;
+  auto slab_issue = [&](int q) { issue(first + (q / NCH) * step, q % NCH, q % NBUF); };
+  if constexpr (PS) {
+#pragma unroll
+    for (int q = 0; q < NBUF - 1; ++q)
+      if (q < S) slab_issue(q);
+  } else {
+    issue(first, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   const int ntile = PS ? count : 1;
   for (int k = 0; k < ntile; ++k) {
     const int item = first + k * step;
@@ -438,10 +471,9 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
 #pragma unroll 1
     for (int ch = 0; ch < NCH; ++ch) {
       const int s = k * NCH + ch;
-      if (ch + 1 < NCH) issue(item, ch + 1, (s + 1) & 1);
-      else if (PS && k + 1 < ntile) issue(item + step, 0, (s + 1) & 1);
-      // persistent: the tile's residual chunks are loaded under its last slab's products
       if constexpr (PS) {
+        // the tile's residual chunks are loaded under its last slab's products, issued before the
+        // next slab's DMA so that waiting for them leaves that DMA in flight
         if (ch == NCH - 1 && ep.res) {
           const int tile = item / NB, nb = item - tile * NB;
           const int n = tile / tiles, t = tile - n * tiles;
@@ -461,8 +493,13 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
             }
           }
         }
+        if (s + NBUF - 1 < S) slab_issue(s + NBUF - 1);
+        x3_vm_wait<NBUF, JW + JI>(min(NBUF - 1, S - 1 - s));
+        __syncthreads();
+      } else {
+        if (ch + 1 < NCH) issue(item, ch + 1, (s + 1) & 1);
       }
-      const uint4* sb = smem + (s & 1) * SB;
+    const uint4* sb = smem + (s % NBUF) * SB;
       auto mma = [&](auto cnt) {
         constexpr int C = decltype(cnt)::value;
         if constexpr (C > 0) {
@@ -507,11 +544,13 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
       } else {
         static_assert(WN <= 2, "WN");
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // every wave done with buffer s % NBUF (persistent: the next slab's DMA or the staging
+      // reuses it); one tile: slab s + 1 landed
+      if constexpr (!PS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
-    epilogue(item, PS ? smem + ((k * NCH + NCH - 1) & 1) * SB : smem, rv);
-    if (PS) __syncthreads();  // staging drained before the buffer receives the slab after next
+    epilogue(item, PS ? smem + ((k * NCH + NCH - 1) % NBUF) * SB : smem, rv);
+    if (PS) __syncthreads();  // staging drained before its buffer receives a slab again
   }
   if (ep.ovf && __ballot(bad)) {
     if (lane == 0) atomicOr(ep.ovf, 1);
@@ -540,7 +579,7 @@ bool x3_cfg(int ks, int cin, int cout, int variant, X3Cfg* c) {
 }
 
 template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, bool PS = false,
-          int NT = 512>
+          int NT = 512, int NBUF = 2>
 int x3_run(cpx_ctx* ctx, const void* in, const void* wpk, const X3Epi& ep, int N, int H, int W) {
   const int tx = cpx_div_up(W, TX), ty = cpx_div_up(H, TY);
   const long long tiles = (long long)N * tx * ty;
@@ -552,7 +591,7 @@ int x3_run(cpx_ctx* ctx, const void* in, const void* wpk, const X3Epi& ep, int N
     blocks = std::min<long long>(blocks, (long long)std::max(1, WPE * 256 / NT) * ctx->n_cu);
     if (ctx->x3_grid_cap > 0) blocks = std::min<long long>(blocks, ctx->x3_grid_cap);
   }
-  hipLaunchKernelGGL((k_conv_x3<KS, CIN, COUT, BM, TY, TX, WM, WN, WPE, PS, NT>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((k_conv_x3<KS, CIN, COUT, BM, TY, TX, WM, WN, WPE, PS, NT, NBUF>), dim3((unsigned)blocks),
                      dim3(NT), 0, ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N, H, W, tx, ty);
   CPX_CHECK_LAUNCH("k_conv_x3");
   return CPX_OK;
@@ -569,6 +608,9 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
 #define X3_3W(CI, CO, V, BM_, TY_, TX_, WM_, WN_)                                      \
   if (ks == 3 && cin == CI && cout == CO && variant == V)                                \
     return x3_run<3, CI, CO, BM_, TY_, TX_, WM_, WN_, 4, false, 1024>(ctx, in, wpk, ep, N, H, W);
+#define X3_3R(CI, CO, V, BM_, TY_, TX_, NB_)                                           \
+  if (ks == 3 && cin == CI && cout == CO && variant == V)                                \
+    return x3_run<3, CI, CO, BM_, TY_, TX_, 1, 1, 2, true, 512, NB_>(ctx, in, wpk, ep, N, H, W);
 #define X3_1(CI, CO)                                                                     \
   if (ks == 1 && cin == CI && cout == CO)                                                \
     return x3_run<1, CI, CO, 32, 16, 16, 1, 1, 4>(ctx, in, wpk, ep, N, H, W);
@@ -581,6 +623,9 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
   X3_3P(64, 32, 2, 32, 8, 32, 4)
   X3_3(32, 32, 3, 32, 8, 32, 1, 1, 4)
   X3_3(64, 32, 3, 32, 8, 32, 1, 1, 4)
+  // variant 4: persistent, one 8-wave block per CU, a ring of three / four slab buffers
+  X3_3R(32, 32, 4, 32, 8, 32, 3)
+  X3_3R(64, 32, 4, 32, 8, 32, 3)
   // 112^2 level
   X3_3(32, 64, 1, 64, 16, 16, 2, 1, 2)
   X3_3(64, 64, 1, 64, 16, 16, 2, 1, 2)
@@ -595,6 +640,9 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
   X3_3W(32, 64, 3, 64, 16, 16, 1, 1)
   X3_3W(64, 64, 3, 64, 16, 16, 1, 1)
   X3_3W(128, 64, 3, 64, 16, 16, 1, 1)
+  X3_3R(32, 64, 4, 32, 16, 16, 4)
+  X3_3R(64, 64, 4, 32, 16, 16, 4)
+  X3_3R(128, 64, 4, 32, 16, 16, 4)
   // 56^2 / 28^2 levels
   X3_3(64, 128, 1, 64, 14, 28, 2, 2, 2)
   X3_3(128, 128, 1, 64, 14, 28, 2, 2, 2)
@@ -616,6 +664,11 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
   X3_3W(256, 128, 3, 64, 16, 28, 1, 2)
   X3_3W(128, 256, 3, 64, 16, 28, 1, 2)
   X3_3W(256, 256, 3, 64, 16, 28, 1, 2)
+  X3_3R(64, 128, 4, 32, 8, 28, 4)
+  X3_3R(128, 128, 4, 32, 8, 28, 4)
+  X3_3R(256, 128, 4, 32, 8, 28, 4)
+  X3_3R(128, 256, 4, 32, 8, 28, 4)
+  X3_3R(256, 256, 4, 32, 8, 28, 4)
   // 1x1 block projections (BatchNorm folded into the weights)
   X3_1(32, 64)
   X3_1(64, 128)
@@ -627,6 +680,7 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
 #undef X3_3
 #undef X3_3P
 #undef X3_3W
+#undef X3_3R
 #undef X3_1
   cpx_set_error("cpx_cpnet_x3_conv: no instance for ks %d, %d -> %d channels (variant %d)", ks, cin, cout, variant);
   return CPX_ERR_SHAPE;
@@ -833,8 +887,8 @@ extern "C" int cpx_cpnet_x3_set_grid(cpx_ctx* ctx, int max_blocks) {
   return CPX_OK;
 }
 
-extern "C" int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* in, int N, int H,
-                                 int W, int cin, int cout, const void* wpk, const float* bias,
+extern "C" int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* in, int in_up, int N,
+                                 int H, int W, int cin, int cout, const void* wpk, const float* bias,
                                  const void* res, int res_up, const float* style, int style_stride,
                                  const float* scale, const float* shift, int relu, void* y_out,
                                  void* z_out, int z_up, const float* head_w, const float* head_b,
@@ -844,8 +898,9 @@ extern "C" int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* 
   CPX_REQUIRE(N > 0 && H > 0 && W > 0, CPX_ERR_ARG, "cpx_cpnet_x3_conv: bad sizes");
   CPX_REQUIRE(!(scale == nullptr) == !(shift == nullptr), CPX_ERR_ARG,
               "cpx_cpnet_x3_conv: scale and shift go together");
-  CPX_REQUIRE(!res_up || ((H % 2) == 0 && (W % 2) == 0), CPX_ERR_ARG,
-              "cpx_cpnet_x3_conv: res_up needs even sizes");
+  CPX_REQUIRE(!(res_up || in_up) || ((H % 2) == 0 && (W % 2) == 0), CPX_ERR_ARG,
+              "cpx_cpnet_x3_conv: res_up / in_up need even sizes");
+  CPX_REQUIRE(in_up == 0 || in_up == 1, CPX_ERR_ARG, "cpx_cpnet_x3_conv: in_up is 0 or 1");
   CPX_REQUIRE(((uintptr_t)in | (uintptr_t)wpk | (uintptr_t)res | (uintptr_t)y_out | (uintptr_t)z_out) % 16 == 0,
               CPX_ERR_ARG, "cpx_cpnet_x3_conv: misaligned buffers");
   CPX_REQUIRE(!style || (style_stride >= cout && style_stride % 4 == 0 && ((uintptr_t)style % 16) == 0),
@@ -854,7 +909,7 @@ extern "C" int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* 
               CPX_ERR_ARG, "cpx_cpnet_x3_conv: head needs a 3x3 conv with cout 32, no z_out, 1..4 outputs");
   CPX_REQUIRE(!z_up || z_out, CPX_ERR_ARG, "cpx_cpnet_x3_conv: z_up without z_out");
   X3Epi ep{bias, (const uint4*)res, style, scale, shift, (uint4*)y_out, (uint4*)z_out, res_up, relu,
-           z_up, style_stride, head_w, head_b, head_out, n_head, ovf};
+           z_up, style_stride, head_w, head_b, head_out, n_head, ovf, in_up};
   return x3_launch(ctx, ks, cin, cout, variant, in, wpk, ep, N, H, W);
 }
 

@@ -42,40 +42,60 @@ __global__ __launch_bounds__(kT) void k_edt_cols(const int* __restrict__ labels,
   const long long base = (long long)fov * H * W + col;
   const int* lab = labels + base;
   int* o = off + base;
-  // down sweep: distance to the last feature at or above (stored), capped at D+1
+  // the tile's labels and candidates stay in registers between the two sweeps (one label read
+  // and one store per pixel); the D-row halos above and below are only read
+  int lv[kColTile], cur[kColTile];
+#pragma unroll
+  for (int u = 0; u < kColTile; ++u) lv[u] = r0 + u < r1 ? lab[(long long)(r0 + u) * W] : 0;
+  // down sweep: distance to the last feature at or above, capped at D+1
   int last = -0x40000000, last_l = 0;
-  for (int rb = max(0, r0 - D); rb < r1; rb += 8) {  // eight label loads in flight
-    int lv[8];
+  for (int rb = max(0, r0 - D); rb < r0; rb += 8) {  // eight halo loads in flight
+    int hv[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) lv[u] = rb + u < r1 ? lab[(long long)(rb + u) * W] : 0;
+    for (int u = 0; u < 8; ++u) hv[u] = rb + u < r0 ? lab[(long long)(rb + u) * W] : 0;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = rb + u;
-      if (r >= r1) break;
-      if (lv[u] != 0) {
-        last = r;
-        last_l = lv[u];
+    for (int u = 0; u < 8; ++u)
+      if (rb + u < r0 && hv[u] != 0) {
+        last = rb + u;
+        last_l = hv[u];
       }
-      if (r < r0) continue;
-      const int du = r - last;
-      o[(long long)r * W] = du <= D ? pack_ft(-du, last_l) : pack_ft(kNone, 0);  // feature above (or here)
+  }
+#pragma unroll
+  for (int u = 0; u < kColTile; ++u) {
+    if (lv[u] != 0) {
+      last = r0 + u;
+      last_l = lv[u];
     }
+    const int du = r0 + u - last;
+    cur[u] = du <= D ? pack_ft(-du, last_l) : pack_ft(kNone, 0);  // feature above (or here)
   }
   // up sweep: next feature at or below; keep the above one on ties (smaller row)
   int next = 0x40000000, next_l = 0;
-  for (int r = min(H, r1 + D) - 1; r >= r0; --r) {
-    const int l = lab[(long long)r * W];
-    if (l != 0) {
-      next = r;
-      next_l = l;
-    }
-    if (r >= r1) continue;
-    const int dd = next - r;
-    if (dd > D) continue;
-    const int cur = ft_dr(o[(long long)r * W]);
-    const int du = cur == kNone ? 0x7fffffff : -cur;
-    if (dd < du) o[(long long)r * W] = pack_ft(dd, next_l);
+  for (int rb = min(H, r1 + D) - 1; rb >= r1; rb -= 8) {
+    int hv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) hv[u] = rb - u >= r1 ? lab[(long long)(rb - u) * W] : 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (rb - u >= r1 && hv[u] != 0) {
+        next = rb - u;
+        next_l = hv[u];
+      }
   }
+#pragma unroll
+  for (int u = kColTile - 1; u >= 0; --u) {
+    if (lv[u] != 0) {
+      next = r0 + u;
+      next_l = lv[u];
+    }
+    const int dd = next - (r0 + u);
+    const int c = ft_dr(cur[u]);
+    const int du = c == kNone ? 0x7fffffff : -c;
+    if (dd <= D && dd < du) cur[u] = pack_ft(dd, next_l);
+  }
+#pragma unroll
+  for (int u = 0; u < kColTile; ++u)
+    if (r0 + u < r1) o[(long long)(r0 + u) * W] = cur[u];
 }
 
 // pass 2: per pixel, lexicographic min of (d^2, column) over the 2D+1 columns.  A block owns

@@ -264,6 +264,8 @@ __device__ __forceinline__ int ceil_sqrt_ll(long long v) {
 
 // Sum of p[row(i)] over rows i whose folded index fi gives radius R for the given fj.
 // row(i) = i (direct) or (H - i) % H (mirrored partner).
+// compact: p holds rows 0 .. 259 then rows 1820 .. 2079 (H = 2080, k_qc_cols_2080)
+template <bool COMPACT = false>
 __device__ __forceinline__ double ring_rows(const double* __restrict__ p, int H, int R, int fj,
                                             bool mirrored) {
   const long long fj2 = (long long)fj * fj;
@@ -278,10 +280,10 @@ __device__ __forceinline__ double ring_rows(const double* __restrict__ p, int H,
   for (int fi = lo; fi <= hi; ++fi) {
     const int i0 = fi, i1 = H - 1 - fi;
     const int s0 = mirrored ? (H - i0) % H : i0;
-    s += p[s0];
+    s += p[COMPACT && s0 >= 260 ? s0 - 1560 : s0];
     if (i1 != i0) {
       const int s1 = mirrored ? (H - i1) % H : i1;
-      s += p[s1];
+      s += p[COMPACT && s1 >= 260 ? s1 - 1560 : s1];
     }
   }
   return s;
@@ -489,44 +491,23 @@ __device__ __forceinline__ void dft20(cplx* v) {
   }
 }
 
-template <int ILLUM>
-__global__ __launch_bounds__(kR2T) void k_qc_rows_2080(
-    const unsigned short* __restrict__ raw, const void* __restrict__ illum, int C, int H,
-    const cpx_plane_stats* __restrict__ stats, const cplx* __restrict__ tw, cplx* __restrict__ rowspec,
-    QcAux* __restrict__ aux) {
-  constexpr int W = kR2N;
-  __shared__ cplx A[kR2N];
-  __shared__ cplx t260[260];
-  const int plane = blockIdx.y;
-  const int ch = plane % C;
-  const int r0 = 2 * blockIdx.x, r1 = r0 + 1;
-  const long long N = (long long)H * W;
-  const unsigned short* rp = raw + (long long)plane * N;
-  const void* il = nullptr;
-  if (ILLUM == 1) il = static_cast<const float*>(illum) + (long long)ch * N;
-  if (ILLUM == 2 || ILLUM == 3) il = static_cast<const double*>(illum) + (long long)ch * N;
-  const cpx_plane_stats st = stats[plane];
-  const double mean = st.sum_q / (double)st.n;
+// The three passes on one 2080-point sequence: load(n) gives point n (P1 threads call it for
+// their 13 points); on return A[j] = X[j] and A[260 + j] = X[1820 + j] (j < 260) and the block
+// is synchronised.  t260 must hold W_260^i (filled and synchronised by the caller's first
+// barrier: P1 does not read it).
+template <typename Load>
+__device__ __forceinline__ void fft2080_pruned(cplx* A, const cplx* t260, const cplx* __restrict__ tw,
+                                               Load load) {
   const int tid = threadIdx.x;
-  for (int i = tid; i < 260; i += kR2T) t260[i] = tw[8 * i];  // W_260^i = W_2080^(8 i)
   // ---- P1
-  unsigned long long eq = 0;
   if (tid < 160) {
     cplx v[13];
 #pragma unroll
-    for (int r = 0; r < 13; ++r) {
-      const int n = tid + 160 * r;
-      const double qa = qval<ILLUM>(rp, il, (long long)r0 * W + n);
-      const double qb = r1 < H ? qval<ILLUM>(rp, il, (long long)r1 * W + n) : mean;
-      eq += (qa == mean) + (r1 < H && qb == mean);
-      v[r] = cplx{qa - mean, qb - mean};
-    }
+    for (int r = 0; r < 13; ++r) v[r] = load(tid + 160 * r);
     dft<13>(v, nullptr);
 #pragma unroll
     for (int r = 0; r < 13; ++r) A[13 * tid + r] = v[r];
   }
-  eq = wave_sum(eq);
-  if ((tid & 63) == 0 && eq) atomicAdd(&aux[plane].eq_count, eq);
   __syncthreads();
   // ---- P2
   {
@@ -548,47 +529,78 @@ __global__ __launch_bounds__(kR2T) void k_qc_rows_2080(
     __syncthreads();
   }
   // ---- P3 (pruned): lo = X[j], hi = X[1820 + j]
-  {
-    constexpr int NR = (260 + kR2T - 1) / kR2T;
-    cplx lo[NR], hi[NR];
+  constexpr int NR = (260 + kR2T - 1) / kR2T;
+  cplx lo[NR], hi[NR];
 #pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      const int j = tid + q * kR2T;
-      lo[q] = hi[q] = cplx{0.0, 0.0};
-      if (j < 260) {
-        cplx v[8];
+  for (int q = 0; q < NR; ++q) {
+    const int j = tid + q * kR2T;
+    lo[q] = hi[q] = cplx{0.0, 0.0};
+    if (j < 260) {
+      cplx v[8];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = A[j + 260 * r];
+      for (int r = 0; r < 8; ++r) v[r] = A[j + 260 * r];
 #pragma unroll
-        for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], tw[j * r]);
-        // r' = 0: sum v[r];  r' = 7: sum v[r] W_8^(7 r) = sum v[r] exp(+i pi r / 4)
-        const double h = 0.70710678118654752440;
-        cplx a = cadd(cadd(v[0], v[4]), cadd(v[2], v[6]));
-        cplx b = cadd(cadd(v[1], v[5]), cadd(v[3], v[7]));
-        lo[q] = cadd(a, b);
-        // exp(+i pi r / 4): r = 0: 1, 1: h(1 + i), 2: i, 3: h(-1 + i), 4: -1, 5: -h(1 + i), 6: -i, 7: h(1 - i)
-        const cplx e0 = csub(v[0], v[4]);                       // r = 0, 4
-        const cplx e2 = csub(v[2], v[6]);                       // r = 2, 6 (times i)
-        const cplx o1 = csub(v[1], v[5]);                       // r = 1, 5 (times h(1 + i))
-        const cplx o3 = csub(v[3], v[7]);                       // r = 3, 7 (times h(-1 + i))
-        const cplx ie2 = cplx{-e2.y, e2.x};
-        const cplx t1 = cplx{h * (o1.x - o1.y), h * (o1.x + o1.y)};
-        const cplx t3 = cplx{h * (-o3.x - o3.y), h * (o3.x - o3.y)};
-        hi[q] = cadd(cadd(e0, ie2), cadd(t1, t3));
-      }
+      for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], tw[j * r]);
+      // r' = 0: sum v[r];  r' = 7: sum v[r] W_8^(7 r) = sum v[r] exp(+i pi r / 4)
+      const double h = 0.70710678118654752440;
+      const cplx a = cadd(cadd(v[0], v[4]), cadd(v[2], v[6]));
+      const cplx b = cadd(cadd(v[1], v[5]), cadd(v[3], v[7]));
+      lo[q] = cadd(a, b);
+      // exp(+i pi r / 4): r = 0: 1, 1: h(1 + i), 2: i, 3: h(-1 + i), 4: -1, 5: -h(1 + i), 6: -i,
+      // 7: h(1 - i)
+      const cplx e0 = csub(v[0], v[4]);  // r = 0, 4
+      const cplx e2 = csub(v[2], v[6]);  // r = 2, 6 (times i)
+      const cplx o1 = csub(v[1], v[5]);  // r = 1, 5 (times h(1 + i))
+      const cplx o3 = csub(v[3], v[7]);  // r = 3, 7 (times h(-1 + i))
+      const cplx ie2 = cplx{-e2.y, e2.x};
+      const cplx t1 = cplx{h * (o1.x - o1.y), h * (o1.x + o1.y)};
+      const cplx t3 = cplx{h * (-o3.x - o3.y), h * (o3.x - o3.y)};
+      hi[q] = cadd(cadd(e0, ie2), cadd(t1, t3));
     }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      const int j = tid + q * kR2T;
-      if (j < 260) {
-        A[j] = lo[q];
-        A[260 + j] = hi[q];
-      }
-    }
-    __syncthreads();
   }
-  // ---- unpack the two real rows for k < KC: Z[N - k] = X[1820 + (260 - k)]
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NR; ++q) {
+    const int j = tid + q * kR2T;
+    if (j < 260) {
+      A[j] = lo[q];
+      A[260 + j] = hi[q];
+    }
+  }
+  __syncthreads();
+}
+
+template <int ILLUM>
+__global__ __launch_bounds__(kR2T) void k_qc_rows_2080(
+    const unsigned short* __restrict__ raw, const void* __restrict__ illum, int C, int H,
+    const cpx_plane_stats* __restrict__ stats, const cplx* __restrict__ tw, cplx* __restrict__ rowspec,
+    QcAux* __restrict__ aux) {
+  constexpr int W = kR2N;
+  __shared__ cplx A[kR2N];
+  __shared__ cplx t260[260];
+  const int plane = blockIdx.y;
+  const int ch = plane % C;
+  const int r0 = 2 * blockIdx.x, r1 = r0 + 1;
+  const long long N = (long long)H * W;
+  const unsigned short* rp = raw + (long long)plane * N;
+  const void* il = nullptr;
+  if (ILLUM == 1) il = static_cast<const float*>(illum) + (long long)ch * N;
+  if (ILLUM == 2 || ILLUM == 3) il = static_cast<const double*>(illum) + (long long)ch * N;
+  const cpx_plane_stats st = stats[plane];
+  const double mean = st.sum_q / (double)st.n;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 260; i += kR2T) t260[i] = tw[8 * i];  // W_260^i = W_2080^(8 i)
+  unsigned long long eq = 0;
+  // the two rows as one complex sequence (real-input pair trick), mean removed
+  fft2080_pruned(A, t260, tw, [&](int n) {
+    const double qa = qval<ILLUM>(rp, il, (long long)r0 * W + n);
+    const double qb = r1 < H ? qval<ILLUM>(rp, il, (long long)r1 * W + n) : mean;
+    eq += (qa == mean) + (r1 < H && qb == mean);
+    return cplx{qa - mean, qb - mean};
+  });
+  eq = wave_sum(eq);
+  if ((tid & 63) == 0 && eq) atomicAdd(&aux[plane].eq_count, eq);
+  // unpack the two real rows for k < KC: Z[N - k] = X[1820 + (260 - k)]
   cplx* outa = rowspec + ((long long)plane * H + r0) * kR2KC;
   for (int k = tid; k < kR2KC; k += kR2T) {
     const cplx zk = A[k];
@@ -598,6 +610,54 @@ __global__ __launch_bounds__(kR2T) void k_qc_rows_2080(
     const cplx xb = {0.5 * dlt.y, -0.5 * dlt.x};
     outa[k] = xa;
     if (r1 < H) outa[kR2KC + k] = xb;
+  }
+}
+
+// Column pass for H = 2080: the same pruned transform of column j (the rows the rings use are
+// i <= 258, the mirrored ones >= 1821 and their partners (H - i) % H: all within X[0 .. 259] and
+// X[1820 .. 2079]), power into A's doubles at the row index, ring sums as k_qc_cols.
+__global__ __launch_bounds__(kR2T) void k_qc_cols_2080(const cplx* __restrict__ rowspec, int W, int KC,
+                                                       const cplx* __restrict__ tw, int n_rings,
+                                                       double* __restrict__ ringpart) {
+  constexpr int H = kR2N;
+  __shared__ cplx A[kR2N];
+  __shared__ cplx t260[260];
+  double* pw = reinterpret_cast<double*>(A);  // rows 0 .. 259, 1820 .. 2079 (compact), after the FFT
+  int j = blockIdx.x, plane = blockIdx.y;
+  const int total = gridDim.x * gridDim.y;
+  if ((total & 7) == 0) {  // XCD-aware order, as k_qc_cols
+    const int L = blockIdx.y * gridDim.x + blockIdx.x;
+    const int V = (L & 7) * (total >> 3) + (L >> 3);
+    plane = V / KC;
+    j = V - plane * KC;
+  }
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 260; i += kR2T) t260[i] = tw[8 * i];
+  const cplx* src = rowspec + (long long)plane * H * KC + j;
+  fft2080_pruned(A, t260, tw, [&](int n) { return src[(long long)n * KC]; });
+  constexpr int NP = (520 + kR2T - 1) / kR2T;
+  double pv[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const int i = tid + q * kR2T;
+    pv[q] = 0.0;
+    if (i < 520) {
+      const cplx v = A[i];
+      pv[q] = v.x * v.x + v.y * v.y;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NP; ++q)
+    if (tid + q * kR2T < 520) pw[tid + q * kR2T] = pv[q];
+  __syncthreads();
+  double* out = ringpart + ((long long)plane * KC + j) * n_rings;
+  for (int t = tid; t < n_rings; t += kR2T) {
+    const int R = t + 2;
+    double s = 0.0;
+    s += ring_rows<true>(pw, H, R, min(j, W - 1 - j), false);
+    if (j >= 1) s += ring_rows<true>(pw, H, R, min(W - j, j - 1), true);
+    out[t] = s;
   }
 }
 
@@ -719,8 +779,12 @@ extern "C" int cpx_qc_rps(cpx_ctx* ctx, const uint16_t* raw_dev, const void* ill
                          H, W, stats_dev, (const cplx*)twW, pw, KC, rowspec, aux);
     CPX_CHECK_LAUNCH("k_qc_rows");
     const size_t sh_cols = sizeof(cplx) * (size_t)H;
-    hipLaunchKernelGGL(k_qc_cols, dim3(KC, n_planes), dim3(kFT), sh_cols, ctx->stream,
-                       (const cplx*)rowspec, H, W, KC, (const cplx*)twH, ph, n_rings, ringpart);
+    if (H == kR2N && !getenv("CPX_QC_GENERIC"))
+      hipLaunchKernelGGL(k_qc_cols_2080, dim3(KC, n_planes), dim3(kR2T), 0, ctx->stream,
+                         (const cplx*)rowspec, W, KC, (const cplx*)twH, n_rings, ringpart);
+    else
+      hipLaunchKernelGGL(k_qc_cols, dim3(KC, n_planes), dim3(kFT), sh_cols, ctx->stream,
+                         (const cplx*)rowspec, H, W, KC, (const cplx*)twH, ph, n_rings, ringpart);
     CPX_CHECK_LAUNCH("k_qc_cols");
   }
   hipLaunchKernelGGL(k_qc_slope, dim3(n_planes), dim3(kThreads),

@@ -141,19 +141,26 @@ __device__ __forceinline__ int border_pixel(int k) {
 }
 
 
-// Tiles of this block for this round: t = blockIdx.x + k * gridDim.x.  Every thread evaluates one
-// tile's activity at once (flags of the previous round), writes the flags of inactive tiles and
-// appends active ones to the LDS list — an idle round costs one pass over the flags, not a
-// serial walk.  Active: every tile in round 0, later a tile with free pixels whose facing
+// Tiles of this block for this round: XCD x (the blocks b with b % 8 == x) owns the contiguous
+// tile range [total x / 8, total (x + 1) / 8) and block b takes the tiles lo + b / 8 + k * (blocks
+// on its XCD), so horizontally and vertically adjacent tiles run on one XCD at about the same
+// time and the 4-byte column halos they read from each other's lines hit that XCD's L2 (dealt
+// round-robin, every tile's halo columns pulled three lines per row from HBM).  Every thread
+// evaluates one tile's activity at once (flags of the previous round), writes the flags of
+// inactive tiles and appends active ones to the LDS list — an idle round costs one pass over the
+// flags, not a serial walk.  Active: every tile in round 0, later a tile with free pixels whose facing
 // neighbour's border changed (or whose own queue overflowed: kSelf).
 __device__ int schedule_tiles(const WsArgs& a, int round, const unsigned char* Fp,
                               unsigned char* Fn, int* list, int* s_n) {
   if (threadIdx.x == 0) *s_n = 0;
   __syncthreads();
   const int per = a.nty * a.ntx;
+  const int G = gridDim.x, xb = blockIdx.x & 7, xi = blockIdx.x >> 3;
+  const int ng = G < 8 ? G : 8, gx = (G - xb + 7) >> 3;
+  const int lo = (int)((long long)a.total * xb / ng), hi = (int)((long long)a.total * (xb + 1) / ng);
   for (int k = threadIdx.x;; k += blockDim.x) {
-    const int t = blockIdx.x + k * gridDim.x;
-    if (t >= a.total) break;
+    const int t = lo + xi + k * gx;
+    if (t >= hi) break;
     const int fov = t / per, tt = t - fov * per, ty = tt / a.ntx, tx = tt - ty * a.ntx;
     // all flags loaded before use (clamped neighbour indices; edges masked after)
     const int base = fov * per;
@@ -446,7 +453,9 @@ __global__ __launch_bounds__(kJumpThreads) void k_ws_ptr_init(WsArgs a, int* __r
                                                               int* __restrict__ list, int* __restrict__ cnt) {
   __shared__ int s_buf[kT * kT];
   __shared__ int s_cnt, s_base;
-  const int t = blockIdx.x;
+  // XCD-aware: each XCD labels a contiguous run of tiles (neighbour level reads stay in its L2)
+  const int G = gridDim.x, xb = blockIdx.x & 7;
+  const int t = xb * (G >> 3) + min(xb, G & 7) + (blockIdx.x >> 3);
   if (!a.tfree[t]) return;
   const int per = a.nty * a.ntx;
   const int fov = t / per, tt = t - fov * per, ty = tt / a.ntx, tx = tt - ty * a.ntx;

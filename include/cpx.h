@@ -419,10 +419,12 @@ int cpx_cpnet_stem(cpx_ctx* ctx, const void* x, int N, int H, int W, const float
  * cpx_cpnet_x3_conv: ks = 3 (pad 1) or 1 (the block projections); the epilogue of
  * cpx_cpnet_conv3x3 (bias, res [split, res_up], y_out, style [N][style_stride], scale/shift,
  * relu, z_out [z_up]) or, for the last 3x3 convolution (cout 32), the output head:
- * head_out fp32 [N][H][W][n_head] = head_b + head_w [n_head][32] . z (z in fp32).             */
+ * head_out fp32 [N][H][W][n_head] = head_b + head_w [n_head][32] . z (z in fp32).  N, H, W are
+ * the output sizes; in_up = 1 reads `in` as the [N][H/2][W/2][cin] tensor, 2x nearest-upsampled
+ * on the fly (the up path's nn.Upsample(scale_factor=2) is never materialised).              */
 int cpx_cpnet_x3_cfg(int ks, int cin, int cout, int variant, int* bm);
-int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* in, int N, int H, int W,
-                      int cin, int cout, const void* wpk, const float* bias, const void* res,
+int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* in, int in_up, int N, int H,
+                      int W, int cin, int cout, const void* wpk, const float* bias, const void* res,
                       int res_up, const float* style, int style_stride, const float* scale,
                       const float* shift, int relu, void* y_out, void* z_out, int z_up,
                       const float* head_w, const float* head_b, int n_head, float* head_out,

@@ -38,8 +38,8 @@ def main():
         rows = []
 
         def wrap(*args):
-            (h, ks, var, xin, N, H, W, cin, cout, pk, bias, res, res_up, sty, sts, sc, sh, relu, y, z, z_up,
-             hw, hb, nh, ho, ovf) = args
+            (h, ks, var, xin, in_up, N, H, W, cin, cout, pk, bias, res, res_up, sty, sts, sc, sh, relu, y, z,
+             z_up, hw, hb, nh, ho, ovf) = args
             rc = real(*args)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -53,7 +53,8 @@ def main():
                 return p is not None and (not isinstance(p, ct.c_void_p) or p.value is not None)
             flops = 2.0 * N * H * W * cin * cout * ks * ks
             px = N * H * W
-            byt = px * cin * 4 + px * cout * 4 * (on(y) + on(z) * (4 if z_up else 1)) + (px * 12 if on(ho) else 0)
+            byt = px * cin * 4 // (4 if in_up else 1) + px * cout * 4 * (on(y) + on(z) * (4 if z_up else 1)) + \
+                (px * 12 if on(ho) else 0)
             if on(res):
                 byt += px * cout * 4 // (4 if res_up else 1)
             rows.append((ks, cin, cout, H, int(on(res)), int(on(y)), int(on(z)), int(on(ho)), us,
