@@ -107,6 +107,12 @@ SIGNATURES = {
     "cpx_seg_tiles": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P]),
     "cpx_seg_average": (_I, [_P, _P, _I, _I, _I, _P, _P, _P]),
     "cpx_embed_preprocess": (_I, [_P, _P, _P, _I, _I, _I, ct.c_float, ct.c_float, _P]),
+    "cpx_effnet_stem": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
+    "cpx_effnet_conv": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P]),
+    "cpx_effnet_dw": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "cpx_effnet_dw_blocks": (_I, [_I, _I, _I]),
+    "cpx_effnet_se": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "cpx_effnet_pool": (_I, [_P, _P, _I, _I, _I, _P]),
     "cpx_seg_masks": (_I, [_P, _P, _I, _P, _I, _I, _I, ct.c_double, _I, _I, _I, _P, _P]),
     "cpx_cpnet_epilogue": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I]),
     "cpx_cpnet_pool": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
@@ -127,7 +133,6 @@ SIGNATURES = {
     "cpx_cpnet_x3_cfg": (_I, [_I, _I, _I, _I, _P]),
     "cpx_cpnet_x3_conv": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _I, _P, _P, _I,
                                _P, _P, _I, _P, _P, _I, _P, _P]),
-    "cpx_cpnet_x3_set_grid": (_I, [_P, _I]),
     "cpx_cpnet_x3_stem": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cpx_cpnet_x3_pool": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cpx_cpnet_x3_style": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _I, _P]),

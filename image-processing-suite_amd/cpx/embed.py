@@ -22,8 +22,8 @@ Same contract as the reference script:
 Design: the GPU path of cpx.pipeline (illumination, segmentation, object table, a7 crops with
 the a9 scale_to_8bit fused) runs on batches of FOVs resident in HBM; libcpx
 cpx_embed_preprocess does the processor's bicubic resize / normalisation (Pillow-exact 8-bit
-arithmetic) straight from the crops; the EfficientNetV2-L forward runs in PyTorch-ROCm under
-fp16 autocast (channels_last), as the reference's.  assemble() writes the reference's output
+arithmetic) straight from the crops; the EfficientNetV2-L forward runs on libcpx's fp16 MFMA
+kernels (cpx.effnet_hip: k_effnet.hip), the counterpart of the reference's fp16-autocast model.  assemble() writes the reference's output
 tables (host) from the per-site results, with the same float32 summation order.
 Weights: timm/tf_efficientnetv2_l.in21k is a remote download, so --effnet-weights takes a local state_dict, else a seeded initialisation
 (embedding values parity-unpinned).
@@ -37,6 +37,7 @@ import os
 import numpy as np
 
 from . import effnet
+from .effnet_hip import EffNetHip
 
 log = logging.getLogger("cpx.embed")
 BOX_SIZE = 200                 # Cellpose_GPU_s3fs.py:30
@@ -52,8 +53,8 @@ class Embedder:
         self.dev, self.torch = dev, torch
         self.size = size
         self.batch = batch_images
-        self.model = effnet.build_effnet(seed=seed, state_dict_path=weights).to(dev.torch_device)
-        self.model = self.model.to(memory_format=torch.channels_last)
+        # the module (host) holds the architecture and weights; the forward runs natively
+        self.net = EffNetHip(effnet.build_effnet(seed=seed, state_dict_path=weights), dev)
 
     def pixel_values(self, crops8, index, S):
         """Preprocessed fp16 [len(index), 3, D, D] for the crop images at `index` (int64 image
@@ -70,10 +71,8 @@ class Embedder:
         return out
 
     def forward(self, x):
-        torch = self.torch
-        with torch.no_grad(), torch.autocast(device_type="cuda", dtype=torch.float16):
-            y = self.model(x.contiguous(memory_format=torch.channels_last))
-        return y.float()
+        """fp16 [n, 3, D, D] pixel values (device) -> fp32 [n, 1280]."""
+        return self.net(x.half().contiguous())
 
     def embed(self, crops8, n_kept, C: int):
         """crops8: device uint8 [B][ML][C][S][S] (slot = cell_idx); n_kept: cells per FOV."""

@@ -25,8 +25,6 @@ struct cpx_ctx {
   // it was uploaded into (a regrown slot can come back at the same address, with fresh contents)
   unsigned int ws_gen[kWsSlots] = {0};
   int n_cu = 256;
-  // cap on the persistent x3 convolution grid (0: WPE / 2 blocks per CU); cpx_cpnet_x3_set_grid
-  int x3_grid_cap = 0;
   // QC FFT twiddle tables currently uploaded (WS_QC_MISC)
   int qc_H = 0, qc_W = 0;
   unsigned int qc_gen = 0;

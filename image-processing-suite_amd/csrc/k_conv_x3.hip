@@ -106,22 +106,11 @@ struct X3Epi {
   int in_up;  // the input is the (H/2) x (W/2) tensor read 2x nearest-upsampled
 };
 
-// s_waitcnt vmcnt for "all but the `younger` most recent slabs' DMA" (C instructions per slab per
-// wave; the waits need immediates)
-template <int NBUF, int C>
-__device__ __forceinline__ void x3_vm_wait(int younger) {
-  if (younger <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if (NBUF >= 3 && younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C) : "memory");
-  else if (NBUF >= 4 && younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * C) : "memory");
-  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 1) * C) : "memory");
-}
-
-template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, bool PS, int NT,
-          int NBUF = 2>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE)))
+template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, int N, int H,
                int W, int tiles_x, int tiles_y) {
-  constexpr int NWV = NT / 64;
+  constexpr int NT = 512, NWV = NT / 64;
   constexpr int T = KS * KS, HALO = KS / 2;
   constexpr int MWV = BM / (32 * WM), PW = NWV / MWV;
   constexpr int HY = TY + KS - 1, HX = TX + KS - 1, NPIX = HY * HX;
@@ -139,88 +128,73 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   static_assert(CIN % 16 == 0 && COUT % BM == 0 && BM % (32 * WM) == 0 && NWV % MWV == 0, "shape");
   static_assert(PW * WN >= NS, "every subtile needs a wave");
   static_assert(SW % 64 == 0, "weight DMA rows");
-  // output staging: both slab buffers (one tile per block), or the buffer of the slab just
-  // consumed (persistent: the other one is receiving the next tile's first slab)
-  static_assert(P * QB <= (PS ? SB : 2 * SB), "output tile must fit the staging LDS");
-  // persistent ring of NBUF slab buffers (+ one 1 KiB sink for the padding DMAs that give every
-  // wave the same number of DMA instructions per slab, so counted vmcnt waits are exact)
-  static_assert(NBUF >= 2 && (PS || NBUF == 2) && NBUF <= 4, "slab ring");
-  constexpr int DSINK = PS ? 64 : 0;
-  static_assert((NBUF * SB + DSINK) * 16 <= 163840, "LDS");
-  static_assert((NBUF - 1) * (JW + JI) <= 63, "vmcnt");
-  __shared__ uint4 smem[NBUF * SB + DSINK];
+  static_assert(P * QB <= 2 * SB, "output tile must fit the staging LDS");
+  static_assert(2 * SB * 16 <= 163840, "LDS");
+  __shared__ uint4 smem[2 * SB];
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int mw = wid % MWV, pg = wid / MWV;
   const int h = lane >> 5, l32 = lane & 31;
   const int tiles = tiles_x * tiles_y;
-  constexpr int NB = COUT / BM;  // output-channel blocks; item = tile * NB + nb, so the NB blocks
-                                 // of one tile run together on one XCD and share its input in L2
-  // XCD-aware order: the hardware deals consecutive block ids round-robin over the 8 XCDs
-  // (block b runs on XCD b % 8); each XCD gets a contiguous run of tiles instead, so vertically
-  // adjacent tiles (which share halo rows) meet in the same L2.  Persistent (PS): a block walks
-  // the tiles first, first + step, ... of its XCD's run, the next tile's first slab streaming in
-  // while the current tile finishes.
-  int first, step, count;
-  {
-    const int G = gridDim.x, xb = blockIdx.x & 7, xi = blockIdx.x >> 3;
-    if constexpr (PS) {
-      const int nitem = N * tiles * NB;
-      const int ng = G < 8 ? G : 8;      // XCD groups that hold a block
-      const int gx = (G - xb + 7) >> 3;  // blocks on this XCD
-      const int lo = (int)((long long)nitem * xb / ng), hi = (int)((long long)nitem * (xb + 1) / ng);
-      first = lo + xi;
-      step = gx;
-      count = first < hi ? (hi - first + gx - 1) / gx : 0;
-    } else {
-      const int xq = G >> 3, xr = G & 7;
-      first = xb * xq + min(xb, xr) + xi;
-      step = 0;
-      count = 1;
-    }
-  }
-  if (count == 0) return;  // block-uniform
-
-  // DMA sources: weights (lane-constant swizzle), halo chunks of the tile (zero chunk outside)
-  const int fW = (lane & ~3) | ((lane & 3) ^ ((lane >> 4) & 3));
-  // in_up: the source pixel of (gy, gx) is (gy / 2, gx / 2) of the half-size input (nearest
-  // 2x upsampling folded into the halo DMA; the L2 serves each source line to four output pixels)
+  // XCD-aware order: the hardware deals consecutive block ids round-robin over the 8 XCDs, so
+  // block b runs on XCD b % 8; give each XCD a contiguous run of items instead.  An item is
+  // (tile, output-channel block nb) with nb fastest, so the COUT / BM blocks of one tile run
+  // together on one XCD and read its input halo once from HBM (the rest from that XCD's L2), and
+  // vertically adjacent tiles (which share halo rows) meet in the same L2
+  constexpr int NB = COUT / BM;
+  const int G = gridDim.x, xq = G >> 3, xr = G & 7, xb = blockIdx.x & 7;
+  const int bid = xb * xq + min(xb, xr) + (blockIdx.x >> 3);
+  const int tile = bid / NB, nb = bid - tile * NB;
+  const int n = tile / tiles;
+  const int t = tile - n * tiles;
+  const int ty0 = (t / tiles_x) * TY, tx0 = (t % tiles_x) * TX;
+  // in_up: the source pixel of (gy, gx) is (gy / 2, gx / 2) of the half-size input (nearest 2x
+  // upsampling folded into the halo DMA; the L2 serves each source line to four output pixels)
   const int iu = ep.in_up, Wi = W >> iu;
-  auto issue = [&](int item, int ch, int buf) {
-    const int tile = item / NB, nb = item - tile * NB;
-    const int n = tile / tiles, t = tile - n * tiles;
-    const int ty0 = (t / tiles_x) * TY, tx0 = (t % tiles_x) * TX;
-    const uint4* inb = in + (long long)n * (H >> iu) * Wi * QI + ch * 4;
+  const uint4* inb = in + (long long)n * (H >> iu) * Wi * QI;
+
+  // DMA sources: weights (lane-constant swizzle), halo chunk offsets (slab-independent)
+  const int fW = (lane & ~3) | ((lane & 3) ^ ((lane >> 4) & 3));
+  int inOff[JI];
+#pragma unroll
+  for (int jj = 0; jj < JI; ++jj) {
+    const int si = (wid + NWV * jj) * 64 + lane;
+    const int hp = si >> 2, cq = si & 3;
+    const int hy = hp / HX, hx = hp - (hp / HX) * HX;
+    const int gy = ty0 + hy - HALO, gx = tx0 + hx - HALO;
+    inOff[jj] = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+                    ? ((gy >> iu) * Wi + (gx >> iu)) * QI + (cq ^ swz4(hp)) : -1;
+  }
+  auto issue = [&](int ch, int buf) {
     const uint4* wsl = wpk + (long long)(nb * NCH + ch) * SW;
     uint4* dst = smem + buf * SB;
-    int ln = lane;  // opaque in the persistent loop: the halo offsets are recomputed per tile
-    if constexpr (PS) asm volatile("" : "+v"(ln));
 #pragma unroll
     for (int jj = 0; jj < JW; ++jj) {
       const int j = wid + NWV * jj;
       if (j < NWW)
         __builtin_amdgcn_global_load_lds((glb_void_t*)(wsl + j * 64 + fW), (lds_void_t*)(dst + j * 64), 16, 0, 0);
-      else if (PS)
-        __builtin_amdgcn_global_load_lds((glb_void_t*)&g_x3_zero16, (lds_void_t*)(smem + NBUF * SB), 16, 0, 0);
     }
 #pragma unroll
     for (int jj = 0; jj < JI; ++jj) {
       const int j = wid + NWV * jj;
       if (j < NWIN) {
-        const int si = j * 64 + ln;
-        const int hp = si >> 2, cq = si & 3;
-        const int hy = hp / HX, hx = hp - (hp / HX) * HX;
-        const int gy = ty0 + hy - HALO, gx = tx0 + hx - HALO;
-        const uint4* src = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-                               ? inb + ((gy >> iu) * Wi + (gx >> iu)) * QI + (cq ^ swz4(hp)) : &g_x3_zero16;
+        const uint4* src = inOff[jj] >= 0 ? inb + inOff[jj] + ch * 4 : &g_x3_zero16;
         __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(dst + SW + j * 64), 16, 0, 0);
-      } else if (PS) {
-        __builtin_amdgcn_global_load_lds((glb_void_t*)&g_x3_zero16, (lds_void_t*)(smem + NBUF * SB), 16, 0, 0);
       }
     }
   };
 
   f32x16 acc0[WM][WN], acc1[WM][WN];
+#pragma unroll
+  for (int m = 0; m < WM; ++m)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc0[m][j][r] = 0.0f;
+        acc1[m][j][r] = 0.0f;
+      }
+
   const int nsub = max(0, min(WN, NS - pg * WN));
   int aS[WM];
 #pragma unroll
@@ -235,326 +209,259 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
     hp0[j] = (px / TX) * HX + (px % TX);
   }
 
-  bool bad = false;
-  auto slice = [&](int m) { return mw * WM + m; };
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int ch = 0; ch < NCH; ++ch) {
+    if (ch + 1 < NCH) issue(ch + 1, (ch + 1) & 1);
+    const uint4* sb = smem + (ch & 1) * SB;
+    auto mma = [&](auto cnt) {
+      constexpr int C = decltype(cnt)::value;
+      if constexpr (C > 0) {
+        auto tapbody = [&](int tap) {
+          const int ky = tap / KS, kx = tap - KS * (tap / KS);
+          f16x8 ah[WM], al[WM];
+#pragma unroll
+          for (int m = 0; m < WM; ++m) {
+            ah[m] = __builtin_bit_cast(f16x8, sb[aS[m] + tap * BM * 4]);
+            al[m] = __builtin_bit_cast(f16x8, sb[(aS[m] ^ 2) + tap * BM * 4]);
+          }
+#pragma unroll
+          for (int j = 0; j < C; ++j) {
+            const int hp = hp0[j] + ky * HX + kx;
+            const int bs = SW + hp * 4 + (h ^ swz4(hp));
+            const f16x8 bh = __builtin_bit_cast(f16x8, sb[bs]);
+            const f16x8 bl = __builtin_bit_cast(f16x8, sb[bs ^ 2]);
+#pragma unroll
+            for (int m = 0; m < WM; ++m) {
+              acc0[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh, acc0[m][j], 0, 0, 0);
+              acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bl, acc1[m][j], 0, 0, 0);
+              acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bh, acc1[m][j], 0, 0, 0);
+            }
+          }
+        };
+        // single-fragment waves: all taps unrolled, the next tap's reads scheduled under this
+        // tap's MFMAs; larger wave tiles keep one tap per iteration (register budget)
+        if constexpr (WM * WN == 1) {
+#pragma unroll
+          for (int tap = 0; tap < T; ++tap) tapbody(tap);
+        } else {
+#pragma unroll 1
+          for (int tap = 0; tap < T; ++tap) tapbody(tap);
+        }
+      }
+    };
+    if constexpr (WN == 1) {
+      if (nsub == 1) mma(std::integral_constant<int, 1>{});
+    } else if constexpr (WN == 2) {
+      if (nsub == 2) mma(std::integral_constant<int, 2>{});
+      else if (nsub == 1) mma(std::integral_constant<int, 1>{});
+    } else {
+      static_assert(WN <= 2, "WN");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
 
-  // epilogue of one tile on the fp32 values (acc0), staging through stg
-  auto epilogue = [&](int item, uint4* stg, const uint4* rv) {
-    // thread-derived indices recomputed from an opaque copy of the thread id: in the persistent
-    // loop they would otherwise be hoisted out of it and held across the products (spills)
-    int tid = threadIdx.x;
-    if constexpr (PS) asm volatile("" : "+v"(tid));
-    const int h = (tid >> 5) & 1, l32 = tid & 31;
-    const int tile = item / NB, nb = item - tile * NB;
-    const int n = tile / tiles, t = tile - n * tiles;
-    auto chan = [&](int m, int g) { return nb * BM + slice(m) * 32 + 8 * g + 4 * h; };
-    const int ty0 = (t / tiles_x) * TY, tx0 = (t % tiles_x) * TX;
-    auto gpix = [&](int px) -> long long {
-      const int gy = ty0 + px / TX, gx = tx0 + px % TX;
-      if (px >= P || gy >= H || gx >= W) return -1;
-      return ((long long)n * H + gy) * W + gx;
-    };
-    // lane's channel group (m, g): channels cb(m) + 8 g + {0..3} of the block, slab (m', g >> 1)
-    auto piece = [&](int px, int m, int g, int lo) -> uint2* {
-      const int q = (slice(m) * 2 + (g >> 1)) * 4 + 2 * lo + (g & 1);
-      return reinterpret_cast<uint2*>(stg + px * QB + (q ^ swzq<QB>(px))) + h;
-    };
+  // ---- epilogue on the fp32 values ----
+#pragma unroll
+  for (int m = 0; m < WM; ++m)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc0[m][j][r] += acc1[m][j][r] * kLoInv;  // exact product, one rounding
+
+  bool bad = false;
+  auto gpix = [&](int px) -> long long {
+    const int gy = ty0 + px / TX, gx = tx0 + px % TX;
+    if (px >= P || gy >= H || gx >= W) return -1;
+    return ((long long)n * H + gy) * W + gx;
+  };
+  // lane's channel group (m, g): channels cb(m) + 8 g + {0..3} of the block, slab (m', g >> 1)
+  auto slice = [&](int m) { return mw * WM + m; };
+  auto piece = [&](int px, int m, int g, int lo) -> uint2* {
+    const int q = (slice(m) * 2 + (g >> 1)) * 4 + 2 * lo + (g & 1);
+    return reinterpret_cast<uint2*>(smem + px * QB + (q ^ swzq<QB>(px))) + h;
+  };
+  auto chan = [&](int m, int g) { return nb * BM + slice(m) * 32 + 8 * g + 4 * h; };
+  if (ep.bias) {
 #pragma unroll
     for (int m = 0; m < WM; ++m)
 #pragma unroll
-      for (int j = 0; j < WN; ++j)
+      for (int g = 0; g < 4; ++g) {
+        const float4 bv = *reinterpret_cast<const float4*>(ep.bias + chan(m, g));
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc0[m][j][r] += acc1[m][j][r] * kLoInv;  // exact product, one rounding
-    if (ep.bias) {
+        for (int j = 0; j < WN; ++j) {
+          acc0[m][j][4 * g + 0] += bv.x;
+          acc0[m][j][4 * g + 1] += bv.y;
+          acc0[m][j][4 * g + 2] += bv.z;
+          acc0[m][j][4 * g + 3] += bv.w;
+        }
+      }
+  }
+  if (ep.res) {
+#pragma unroll
+    for (int r = 0; r < OUT_R; ++r) {
+      const int i = threadIdx.x + r * NT;
+      if (i < P * QB) {
+        const int px = i / QB, k = i - px * QB;
+        const int gy = ty0 + px / TX, gx = tx0 + px % TX;
+        uint4 v = {0u, 0u, 0u, 0u};
+        if (gy < H && gx < W) {
+          const long long rp = ep.res_up ? ((long long)n * (H >> 1) + (gy >> 1)) * (W >> 1) + (gx >> 1)
+                                         : ((long long)n * H + gy) * W + gx;
+          v = ep.res[rp * QC + nb * QB + k];
+        }
+        smem[px * QB + (k ^ swzq<QB>(px))] = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int px = min((pg * WN + j) * 32 + l32, P - 1);
 #pragma unroll
       for (int m = 0; m < WM; ++m)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const float4 bv = *reinterpret_cast<const float4*>(ep.bias + chan(m, g));
+          float rv[4];
+          join4(*piece(px, m, g, 0), *piece(px, m, g, 1), rv);
 #pragma unroll
-          for (int j = 0; j < WN; ++j) {
-            acc0[m][j][4 * g + 0] += bv.x;
-            acc0[m][j][4 * g + 1] += bv.y;
-            acc0[m][j][4 * g + 2] += bv.z;
-            acc0[m][j][4 * g + 3] += bv.w;
-          }
+          for (int k = 0; k < 4; ++k) acc0[m][j][4 * g + k] += rv[k];
         }
     }
-    if (ep.res) {
+    __syncthreads();
+  }
+  auto stage = [&]() {
 #pragma unroll
-      for (int r = 0; r < OUT_R; ++r) {
-        const int i = tid + r * NT;
-        if (i < P * QB) {
-          const int px = i / QB, k = i - px * QB;
-          uint4 v;
-          if constexpr (PS) {
-            v = rv[r];
-          } else {
-            const int gy = ty0 + px / TX, gx = tx0 + px % TX;
-            v = {0u, 0u, 0u, 0u};
-            if (gy < H && gx < W) {
-              const long long rp = ep.res_up ? ((long long)n * (H >> 1) + (gy >> 1)) * (W >> 1) + (gx >> 1)
-                                             : ((long long)n * H + gy) * W + gx;
-              v = ep.res[rp * QC + nb * QB + k];
-            }
-          }
-          stg[px * QB + (k ^ swzq<QB>(px))] = v;
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < WN; ++j) {
-        const int px = min((pg * WN + j) * 32 + l32, P - 1);
+    for (int j = 0; j < WN; ++j) {
+      const int px = (pg * WN + j) * 32 + l32;
+      if (j < nsub && px < P) {
 #pragma unroll
         for (int m = 0; m < WM; ++m)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            float rvv[4];
-            join4(*piece(px, m, g, 0), *piece(px, m, g, 1), rvv);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) acc0[m][j][4 * g + k] += rvv[k];
+            uint2 hi, lo;
+            split4(acc0[m][j][4 * g], acc0[m][j][4 * g + 1], acc0[m][j][4 * g + 2], acc0[m][j][4 * g + 3],
+                   hi, lo, bad);
+            *piece(px, m, g, 0) = hi;
+            *piece(px, m, g, 1) = lo;
           }
-      }
-      __syncthreads();
-    }
-    auto stage = [&]() {
-#pragma unroll
-      for (int j = 0; j < WN; ++j) {
-        const int px = (pg * WN + j) * 32 + l32;
-        if (j < nsub && px < P) {
-#pragma unroll
-          for (int m = 0; m < WM; ++m)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              uint2 hi, lo;
-              split4(acc0[m][j][4 * g], acc0[m][j][4 * g + 1], acc0[m][j][4 * g + 2], acc0[m][j][4 * g + 3],
-                     hi, lo, bad);
-              *piece(px, m, g, 0) = hi;
-              *piece(px, m, g, 1) = lo;
-            }
-        }
-      }
-    };
-    auto drain = [&](uint4* dst) {
-#pragma unroll
-      for (int r = 0; r < OUT_R; ++r) {
-        const int i = tid + r * NT;
-        const int px = i / QB, k = i - px * QB;
-        const long long gp = gpix(px);
-        if (i < P * QB && gp >= 0) dst[gp * QC + nb * QB + k] = stg[px * QB + (k ^ swzq<QB>(px))];
-      }
-    };
-    if (ep.y) {
-      stage();
-      __syncthreads();
-      drain(ep.y);
-      __syncthreads();
-    }
-    if (!ep.z && !ep.head) return;
-    if (ep.style) {
-#pragma unroll
-      for (int m = 0; m < WM; ++m)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 sv = *reinterpret_cast<const float4*>(ep.style + (long long)n * ep.style_stride + chan(m, g));
-#pragma unroll
-          for (int j = 0; j < WN; ++j) {
-            acc0[m][j][4 * g + 0] += sv.x;
-            acc0[m][j][4 * g + 1] += sv.y;
-            acc0[m][j][4 * g + 2] += sv.z;
-            acc0[m][j][4 * g + 3] += sv.w;
-          }
-        }
-    }
-    if (ep.scale) {
-#pragma unroll
-      for (int m = 0; m < WM; ++m)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 sc = *reinterpret_cast<const float4*>(ep.scale + chan(m, g));
-          const float4 sh = *reinterpret_cast<const float4*>(ep.shift + chan(m, g));
-#pragma unroll
-          for (int j = 0; j < WN; ++j) {
-            acc0[m][j][4 * g + 0] = sc.x * acc0[m][j][4 * g + 0] + sh.x;
-            acc0[m][j][4 * g + 1] = sc.y * acc0[m][j][4 * g + 1] + sh.y;
-            acc0[m][j][4 * g + 2] = sc.z * acc0[m][j][4 * g + 2] + sh.z;
-            acc0[m][j][4 * g + 3] = sc.w * acc0[m][j][4 * g + 3] + sh.w;
-          }
-        }
-    }
-    if (ep.relu) {
-#pragma unroll
-      for (int m = 0; m < WM; ++m)
-#pragma unroll
-        for (int j = 0; j < WN; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc0[m][j][r] = fmaxf(acc0[m][j][r], 0.0f);
-    }
-    if constexpr (COUT == 32 && BM == 32 && WM == 1) {
-      if (ep.head) {
-        // fp32 output 1x1 convolution: lane l and l ^ 32 hold the two halves of a pixel's channels
-#pragma unroll
-        for (int j = 0; j < WN; ++j) {
-          float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const int c = 8 * g + 4 * h + k;
-#pragma unroll
-              for (int q = 0; q < 4; ++q)
-                if (q < ep.n_head) o[q] = __builtin_fmaf(ep.head_w[q * 32 + c], acc0[0][j][4 * g + k], o[q]);
-            }
-#pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] += __shfl_xor(o[q], 32, 64);
-          const int px = (pg * WN + j) * 32 + l32;
-          const long long gp = gpix(px);
-          if (h == 0 && j < nsub && gp >= 0) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (q < ep.n_head) ep.head[gp * ep.n_head + q] = o[q] + ep.head_b[q];
-          }
-        }
-        return;
-      }
-    }
-    stage();
-    __syncthreads();
-    if (!ep.z_up) {
-      drain(ep.z);
-    } else {
-      const long long W2 = 2LL * W;
-#pragma unroll
-      for (int r = 0; r < 4 * OUT_R; ++r) {
-        const int i = tid + r * NT;
-        if (i >= 4 * P * QB) continue;
-        const int k = i % QB;
-        const int d = i / QB;
-        const int dy = d / (2 * TX), dx = d - dy * (2 * TX);
-        const int px = (dy >> 1) * TX + (dx >> 1);
-        const int gy = ty0 + (dy >> 1), gx = tx0 + (dx >> 1);
-        if (gy >= H || gx >= W) continue;
-        const long long dp = ((long long)n * 2 * H + 2LL * ty0 + dy) * W2 + 2LL * tx0 + dx;
-        ep.z[dp * QC + nb * QB + k] = stg[px * QB + (k ^ swzq<QB>(px))];
       }
     }
   };
-
-  // slab sequence over this block's tiles: slab s = (tile k = s / NCH, channel slab s % NCH) lives
-  // in buffer s % NBUF.  One tile per block: slab s + 1 streams in while slab s is multiplied.
-  // Persistent: NBUF - 1 slabs (across tile boundaries) are in flight while slab s is multiplied,
-  // each wave waiting (counted vmcnt) only for its own share of slab s before the barrier.
-  const int S = (PS ? count : 1) * NCH;
-  auto slab_issue = [&](int q) { issue(first + (q / NCH) * step, q % NCH, q % NBUF); };
-  if constexpr (PS) {
+  auto drain = [&](uint4* dst) {
 #pragma unroll
-    for (int q = 0; q < NBUF - 1; ++q)
-      if (q < S) slab_issue(q);
-  } else {
-    issue(first, 0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int r = 0; r < OUT_R; ++r) {
+      const int i = threadIdx.x + r * NT;
+      const int px = i / QB, k = i - px * QB;
+      const long long gp = gpix(px);
+      if (i < P * QB && gp >= 0) dst[gp * QC + nb * QB + k] = smem[px * QB + (k ^ swzq<QB>(px))];
+    }
+  };
+  auto flag = [&]() {
+    if (ep.ovf && __ballot(bad)) {
+      if (lane == 0) atomicOr(ep.ovf, 1);
+    }
+  };
+  if (ep.y) {
+    stage();
+    __syncthreads();
+    drain(ep.y);
     __syncthreads();
   }
-  const int ntile = PS ? count : 1;
-  for (int k = 0; k < ntile; ++k) {
-    const int item = first + k * step;
+  if (!ep.z && !ep.head) {
+    flag();
+    return;
+  }
+  if (ep.style) {
+#pragma unroll
+    for (int m = 0; m < WM; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 sv = *reinterpret_cast<const float4*>(ep.style + (long long)n * ep.style_stride + chan(m, g));
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          acc0[m][j][4 * g + 0] += sv.x;
+          acc0[m][j][4 * g + 1] += sv.y;
+          acc0[m][j][4 * g + 2] += sv.z;
+          acc0[m][j][4 * g + 3] += sv.w;
+        }
+      }
+  }
+  if (ep.scale) {
+#pragma unroll
+    for (int m = 0; m < WM; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 sc = *reinterpret_cast<const float4*>(ep.scale + chan(m, g));
+        const float4 sh = *reinterpret_cast<const float4*>(ep.shift + chan(m, g));
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          acc0[m][j][4 * g + 0] = sc.x * acc0[m][j][4 * g + 0] + sh.x;
+          acc0[m][j][4 * g + 1] = sc.y * acc0[m][j][4 * g + 1] + sh.y;
+          acc0[m][j][4 * g + 2] = sc.z * acc0[m][j][4 * g + 2] + sh.z;
+          acc0[m][j][4 * g + 3] = sc.w * acc0[m][j][4 * g + 3] + sh.w;
+        }
+      }
+  }
+  if (ep.relu) {
 #pragma unroll
     for (int m = 0; m < WM; ++m)
 #pragma unroll
       for (int j = 0; j < WN; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          acc0[m][j][r] = 0.0f;
-          acc1[m][j][r] = 0.0f;
-        }
-    uint4 rv[PS ? OUT_R : 1];
-#pragma unroll 1
-    for (int ch = 0; ch < NCH; ++ch) {
-      const int s = k * NCH + ch;
-      if constexpr (PS) {
-        // the tile's residual chunks are loaded under its last slab's products, issued before the
-        // next slab's DMA so that waiting for them leaves that DMA in flight
-        if (ch == NCH - 1 && ep.res) {
-          const int tile = item / NB, nb = item - tile * NB;
-          const int n = tile / tiles, t = tile - n * tiles;
-          const int ty0 = (t / tiles_x) * TY, tx0 = (t % tiles_x) * TX;
-          int tid = threadIdx.x;
-          asm volatile("" : "+v"(tid));
+        for (int r = 0; r < 16; ++r) acc0[m][j][r] = fmaxf(acc0[m][j][r], 0.0f);
+  }
+  if constexpr (COUT == 32 && BM == 32 && WM == 1) {
+    if (ep.head) {
+      // fp32 output 1x1 convolution: lane l and l ^ 32 hold the two halves of a pixel's channels
 #pragma unroll
-          for (int r = 0; r < OUT_R; ++r) {
-            const int i = tid + r * NT;
-            const int px = i / QB, kq = i - px * QB;
-            const int gy = ty0 + px / TX, gx = tx0 + px % TX;
-            rv[r] = {0u, 0u, 0u, 0u};
-            if (i < P * QB && gy < H && gx < W) {
-              const long long rp = ep.res_up ? ((long long)n * (H >> 1) + (gy >> 1)) * (W >> 1) + (gx >> 1)
-                                             : ((long long)n * H + gy) * W + gx;
-              rv[r] = ep.res[rp * QC + nb * QB + kq];
-            }
+      for (int j = 0; j < WN; ++j) {
+        float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int c = 8 * g + 4 * h + k;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (q < ep.n_head) o[q] = __builtin_fmaf(ep.head_w[q * 32 + c], acc0[0][j][4 * g + k], o[q]);
           }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] += __shfl_xor(o[q], 32, 64);
+        const int px = (pg * WN + j) * 32 + l32;
+        const long long gp = gpix(px);
+        if (h == 0 && j < nsub && gp >= 0) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (q < ep.n_head) ep.head[gp * ep.n_head + q] = o[q] + ep.head_b[q];
         }
-        if (s + NBUF - 1 < S) slab_issue(s + NBUF - 1);
-        x3_vm_wait<NBUF, JW + JI>(min(NBUF - 1, S - 1 - s));
-        __syncthreads();
-      } else {
-        if (ch + 1 < NCH) issue(item, ch + 1, (s + 1) & 1);
       }
-    const uint4* sb = smem + (s % NBUF) * SB;
-      auto mma = [&](auto cnt) {
-        constexpr int C = decltype(cnt)::value;
-        if constexpr (C > 0) {
-          auto tapbody = [&](int tap) {
-            const int ky = tap / KS, kx = tap - KS * (tap / KS);
-            f16x8 ah[WM], al[WM];
-#pragma unroll
-            for (int m = 0; m < WM; ++m) {
-              ah[m] = __builtin_bit_cast(f16x8, sb[aS[m] + tap * BM * 4]);
-              al[m] = __builtin_bit_cast(f16x8, sb[(aS[m] ^ 2) + tap * BM * 4]);
-            }
-#pragma unroll
-            for (int j = 0; j < C; ++j) {
-              const int hp = hp0[j] + ky * HX + kx;
-              const int bs = SW + hp * 4 + (h ^ swz4(hp));
-              const f16x8 bh = __builtin_bit_cast(f16x8, sb[bs]);
-              const f16x8 bl = __builtin_bit_cast(f16x8, sb[bs ^ 2]);
-#pragma unroll
-              for (int m = 0; m < WM; ++m) {
-                acc0[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh, acc0[m][j], 0, 0, 0);
-                acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bl, acc1[m][j], 0, 0, 0);
-                acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bh, acc1[m][j], 0, 0, 0);
-              }
-            }
-          };
-          // single-fragment waves: all taps unrolled, the next tap's reads scheduled under this
-          // tap's MFMAs; larger wave tiles keep one tap per iteration (register budget)
-          if constexpr (WM * WN == 1) {
-#pragma unroll
-            for (int tap = 0; tap < T; ++tap) tapbody(tap);
-          } else {
-#pragma unroll 1
-            for (int tap = 0; tap < T; ++tap) tapbody(tap);
-          }
-        }
-      };
-      if constexpr (WN == 1) {
-        if (nsub == 1) mma(std::integral_constant<int, 1>{});
-      } else if constexpr (WN == 2) {
-        if (nsub == 2) mma(std::integral_constant<int, 2>{});
-        else if (nsub == 1) mma(std::integral_constant<int, 1>{});
-      } else {
-        static_assert(WN <= 2, "WN");
-      }
-      // every wave done with buffer s % NBUF (persistent: the next slab's DMA or the staging
-      // reuses it); one tile: slab s + 1 landed
-      if constexpr (!PS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      flag();
+      return;
     }
-    epilogue(item, PS ? smem + ((k * NCH + NCH - 1) % NBUF) * SB : smem, rv);
-    if (PS) __syncthreads();  // staging drained before its buffer receives a slab again
   }
-  if (ep.ovf && __ballot(bad)) {
-    if (lane == 0) atomicOr(ep.ovf, 1);
+  stage();
+  __syncthreads();
+  if (!ep.z_up) {
+    drain(ep.z);
+  } else {
+    const long long W2 = 2LL * W;
+#pragma unroll
+    for (int r = 0; r < 4 * OUT_R; ++r) {
+      const int i = threadIdx.x + r * NT;
+      if (i >= 4 * P * QB) continue;
+      const int k = i % QB;
+      const int d = i / QB;
+      const int dy = d / (2 * TX), dx = d - dy * (2 * TX);
+      const int px = (dy >> 1) * TX + (dx >> 1);
+      const int gy = ty0 + (dy >> 1), gx = tx0 + (dx >> 1);
+      if (gy >= H || gx >= W) continue;
+      const long long dp = ((long long)n * 2 * H + 2LL * ty0 + dy) * W2 + 2LL * tx0 + dx;
+      ep.z[dp * QC + nb * QB + k] = smem[px * QB + (k ^ swzq<QB>(px))];
+    }
   }
+  flag();
 }
 
 struct X3Cfg {
@@ -573,26 +480,18 @@ bool x3_cfg(int ks, int cin, int cout, int variant, X3Cfg* c) {
   }
   if (ks != 3) return false;
   if (cout == 32) *c = variant == 1 ? X3Cfg{32, 16, 32} : X3Cfg{32, 8, 32};
-  else if (cout == 64) *c = variant == 1 || variant == 3 ? X3Cfg{64, 16, 16} : X3Cfg{32, 16, 16};
-  else *c = variant == 1 ? X3Cfg{64, 14, 28} : variant == 3 ? X3Cfg{64, 16, 28} : X3Cfg{32, 8, 28};
+  else if (cout == 64) *c = variant == 1 ? X3Cfg{64, 16, 16} : X3Cfg{32, 16, 16};
+  else *c = variant == 1 ? X3Cfg{64, 14, 28} : X3Cfg{32, 8, 28};
   return true;
 }
 
-template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, bool PS = false,
-          int NT = 512, int NBUF = 2>
+template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE>
 int x3_run(cpx_ctx* ctx, const void* in, const void* wpk, const X3Epi& ep, int N, int H, int W) {
   const int tx = cpx_div_up(W, TX), ty = cpx_div_up(H, TY);
-  const long long tiles = (long long)N * tx * ty;
-  CPX_REQUIRE(tiles * (COUT / BM) < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv: too many tiles");
-  // persistent: as many blocks as fit on a CU (WPE waves per SIMD), every block walks a stride
-  // of its XCD's (tile, output-channel block) items
-  long long blocks = tiles * (COUT / BM);
-  if (PS) {
-    blocks = std::min<long long>(blocks, (long long)std::max(1, WPE * 256 / NT) * ctx->n_cu);
-    if (ctx->x3_grid_cap > 0) blocks = std::min<long long>(blocks, ctx->x3_grid_cap);
-  }
-  hipLaunchKernelGGL((k_conv_x3<KS, CIN, COUT, BM, TY, TX, WM, WN, WPE, PS, NT, NBUF>), dim3((unsigned)blocks),
-                     dim3(NT), 0, ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N, H, W, tx, ty);
+  const long long blocks = (long long)N * tx * ty * (COUT / BM);  // (tile, output-channel block) items
+  CPX_REQUIRE(blocks < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv: too many tiles");
+  hipLaunchKernelGGL((k_conv_x3<KS, CIN, COUT, BM, TY, TX, WM, WN, WPE>), dim3((unsigned)blocks),
+                     dim3(512), 0, ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N, H, W, tx, ty);
   CPX_CHECK_LAUNCH("k_conv_x3");
   return CPX_OK;
 }
@@ -602,15 +501,6 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
 #define X3_3(CI, CO, V, BM_, TY_, TX_, WM_, WN_, WPE_)                                  \
   if (ks == 3 && cin == CI && cout == CO && variant == V)                                \
     return x3_run<3, CI, CO, BM_, TY_, TX_, WM_, WN_, WPE_>(ctx, in, wpk, ep, N, H, W);
-#define X3_3P(CI, CO, V, BM_, TY_, TX_, WPE_)                                          \
-  if (ks == 3 && cin == CI && cout == CO && variant == V)                                \
-    return x3_run<3, CI, CO, BM_, TY_, TX_, 1, 1, WPE_, true>(ctx, in, wpk, ep, N, H, W);
-#define X3_3W(CI, CO, V, BM_, TY_, TX_, WM_, WN_)                                      \
-  if (ks == 3 && cin == CI && cout == CO && variant == V)                                \
-    return x3_run<3, CI, CO, BM_, TY_, TX_, WM_, WN_, 4, false, 1024>(ctx, in, wpk, ep, N, H, W);
-#define X3_3R(CI, CO, V, BM_, TY_, TX_, NB_)                                           \
-  if (ks == 3 && cin == CI && cout == CO && variant == V)                                \
-    return x3_run<3, CI, CO, BM_, TY_, TX_, 1, 1, 2, true, 512, NB_>(ctx, in, wpk, ep, N, H, W);
 #define X3_1(CI, CO)                                                                     \
   if (ks == 1 && cin == CI && cout == CO)                                                \
     return x3_run<1, CI, CO, 32, 16, 16, 1, 1, 4>(ctx, in, wpk, ep, N, H, W);
@@ -619,13 +509,6 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
   X3_3(64, 32, 0, 32, 8, 32, 1, 1, 4)
   X3_3(32, 32, 1, 32, 16, 32, 1, 2, 2)
   X3_3(64, 32, 1, 32, 16, 32, 1, 2, 2)
-  X3_3P(32, 32, 2, 32, 8, 32, 4)
-  X3_3P(64, 32, 2, 32, 8, 32, 4)
-  X3_3(32, 32, 3, 32, 8, 32, 1, 1, 4)
-  X3_3(64, 32, 3, 32, 8, 32, 1, 1, 4)
-  // variant 4: persistent, one 8-wave block per CU, a ring of three / four slab buffers
-  X3_3R(32, 32, 4, 32, 8, 32, 3)
-  X3_3R(64, 32, 4, 32, 8, 32, 3)
   // 112^2 level
   X3_3(32, 64, 1, 64, 16, 16, 2, 1, 2)
   X3_3(64, 64, 1, 64, 16, 16, 2, 1, 2)
@@ -633,16 +516,6 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
   X3_3(32, 64, 0, 32, 16, 16, 1, 1, 4)
   X3_3(64, 64, 0, 32, 16, 16, 1, 1, 4)
   X3_3(128, 64, 0, 32, 16, 16, 1, 1, 4)
-  X3_3P(32, 64, 2, 32, 16, 16, 4)
-  X3_3P(64, 64, 2, 32, 16, 16, 4)
-  X3_3P(128, 64, 2, 32, 16, 16, 4)
-  // variant 3: one 16-wave block per CU, BM 64 (weights and halo reused over twice the work)
-  X3_3W(32, 64, 3, 64, 16, 16, 1, 1)
-  X3_3W(64, 64, 3, 64, 16, 16, 1, 1)
-  X3_3W(128, 64, 3, 64, 16, 16, 1, 1)
-  X3_3R(32, 64, 4, 32, 16, 16, 4)
-  X3_3R(64, 64, 4, 32, 16, 16, 4)
-  X3_3R(128, 64, 4, 32, 16, 16, 4)
   // 56^2 / 28^2 levels
   X3_3(64, 128, 1, 64, 14, 28, 2, 2, 2)
   X3_3(128, 128, 1, 64, 14, 28, 2, 2, 2)
@@ -654,21 +527,6 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
   X3_3(256, 128, 0, 32, 8, 28, 1, 1, 4)
   X3_3(128, 256, 0, 32, 8, 28, 1, 1, 4)
   X3_3(256, 256, 0, 32, 8, 28, 1, 1, 4)
-  X3_3P(64, 128, 2, 32, 8, 28, 4)
-  X3_3P(128, 128, 2, 32, 8, 28, 4)
-  X3_3P(256, 128, 2, 32, 8, 28, 4)
-  X3_3P(128, 256, 2, 32, 8, 28, 4)
-  X3_3P(256, 256, 2, 32, 8, 28, 4)
-  X3_3W(64, 128, 3, 64, 16, 28, 1, 2)
-  X3_3W(128, 128, 3, 64, 16, 28, 1, 2)
-  X3_3W(256, 128, 3, 64, 16, 28, 1, 2)
-  X3_3W(128, 256, 3, 64, 16, 28, 1, 2)
-  X3_3W(256, 256, 3, 64, 16, 28, 1, 2)
-  X3_3R(64, 128, 4, 32, 8, 28, 4)
-  X3_3R(128, 128, 4, 32, 8, 28, 4)
-  X3_3R(256, 128, 4, 32, 8, 28, 4)
-  X3_3R(128, 256, 4, 32, 8, 28, 4)
-  X3_3R(256, 256, 4, 32, 8, 28, 4)
   // 1x1 block projections (BatchNorm folded into the weights)
   X3_1(32, 64)
   X3_1(64, 128)
@@ -678,9 +536,6 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
   X3_1(128, 64)
   X3_1(64, 32)
 #undef X3_3
-#undef X3_3P
-#undef X3_3W
-#undef X3_3R
 #undef X3_1
   cpx_set_error("cpx_cpnet_x3_conv: no instance for ks %d, %d -> %d channels (variant %d)", ks, cin, cout, variant);
   return CPX_ERR_SHAPE;
@@ -878,12 +733,6 @@ extern "C" int cpx_cpnet_x3_cfg(int ks, int cin, int cout, int variant, int* bm)
   X3Cfg c;
   if (!x3_cfg(ks, cin, cout, variant, &c)) return CPX_ERR_SHAPE;
   if (bm) *bm = c.bm;
-  return CPX_OK;
-}
-
-extern "C" int cpx_cpnet_x3_set_grid(cpx_ctx* ctx, int max_blocks) {
-  CPX_REQUIRE(ctx && max_blocks >= 0, CPX_ERR_ARG, "cpx_cpnet_x3_set_grid: bad argument");
-  ctx->x3_grid_cap = max_blocks;
   return CPX_OK;
 }
 

@@ -106,7 +106,8 @@ __device__ __forceinline__ unsigned int bytes_sub(unsigned int x, unsigned int y
   return ((x | 0x80808080u) - (y & 0x7f7f7f7fu)) ^ ((x ^ ~y) & 0x80808080u);
 }
 
-// Background and masked pairs (key 0) go to a per-lane sink word instead of a branch.
+// Background and masked pairs (key 0) go to a per-lane sink word instead of a branch (a
+// predicated-off atomic measured the same, tools/tex_bench.py r03).
 __device__ __forceinline__ void glcm_add(unsigned int* tab, unsigned int* sink, unsigned int key) {
   atomicAdd(key ? &tab[key >> 1] : sink, (key & 1u) * 0xffffu + 1u);  // half = i & 1
 }
@@ -568,7 +569,7 @@ __device__ __forceinline__ bool shape_fits(const cpx_object& o) {
 }
 
 // Membership bitmask of object o over its bbox + 2-px margin (rows x wpr words in M): each
-// 32-lane half-wave builds one 32-bit word (r, cw); four words per half-wave are loaded before
+// 32-lane half-wave builds one 32-bit word (r, cw); eight words per half-wave are loaded before
 // the first ballot so the label loads overlap.
 template <int NT>
 __device__ __forceinline__ void shape_mask(const int* __restrict__ lab, int H, int W, const cpx_object& o,
@@ -580,10 +581,10 @@ __device__ __forceinline__ void shape_mask(const int* __restrict__ lab, int H, i
   const int rows = o.bbox[2] - o.bbox[0] + 4, cols = o.bbox[3] - o.bbox[1] + 4;
   const int wpr = (cols + 31) >> 5;
   const int nw = rows * wpr;
-  for (int w0 = 0; w0 < nw; w0 += 4 * (NT / 32)) {
-    int lv[4];
+  for (int w0 = 0; w0 < nw; w0 += 8 * (NT / 32)) {
+    int lv[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       const int w = w0 + u * (NT / 32) + ty;
       const int r = w / wpr, cw = w - r * wpr;
       const int c = cw * 32 + tx;
@@ -592,7 +593,7 @@ __device__ __forceinline__ void shape_mask(const int* __restrict__ lab, int H, i
       lv[u] = ok ? lab[(long long)gr * W + gc] : -1;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       const int w = w0 + u * (NT / 32) + ty;
       const unsigned long long b = __ballot(lv[u] == L);
       if (w < nw) {
@@ -729,6 +730,7 @@ __global__ __launch_bounds__(256) void k_shape_props(int max_label, int F,
 // the block's working set (one channel of one bbox, two blocks per CU) L2-resident in between.
 constexpr int kOT = 512;
 constexpr int kOG = 1;
+constexpr int kOR = 4;  // groups per iteration beyond the register-held ones
 
 // in-bbox membership of the 4 pixels (r, c .. c + 3) from the bbox + 2-px margin bitmask
 __device__ __forceinline__ unsigned int member4(const unsigned int* M, int wpr, int r, int c) {
@@ -856,16 +858,26 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
           if ((unsigned int)u < nv) int_acc(a, v[i][u], (mb >> u) & 1u);
       }
       // groups past the register-held ones (large bboxes) are read twice; the block's working
-      // set (one channel of one bbox) stays in L2 between the two passes
-      for (int g = threadIdx.x + kOG * kOT; g < ng; g += kOT) {
-        const unsigned int d = group_desc(M, wpr, bw, bwp, W, g);
-        const unsigned int o0 = d & 0xffffffu, mb = (d >> 24) & 15u, nv = d >> 28;
-        float w4[4];
+      // set (one channel of one bbox) stays in L2 between the two passes.  kOR groups per
+      // iteration, all their loads issued before any is used (one memory latency per kOR groups)
+      for (int g0 = threadIdx.x + kOG * kOT; g0 < ng; g0 += kOR * kOT) {
+        unsigned int d[kOR];
+        float w4[kOR][4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) w4[u] = ldg_b(img, 4u * (o0 + min((unsigned int)u, nv - 1u)));
+        for (int r = 0; r < kOR; ++r) {
+          d[r] = group_desc(M, wpr, bw, bwp, W, min(g0 + r * kOT, ng - 1));
+          const unsigned int o0 = d[r] & 0xffffffu, nv = d[r] >> 28;
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if ((unsigned int)u < nv) int_acc(a, w4[u], (mb >> u) & 1u);
+          for (int u = 0; u < 4; ++u) w4[r][u] = ldg_b(img, 4u * (o0 + min((unsigned int)u, nv - 1u)));
+        }
+#pragma unroll
+        for (int r = 0; r < kOR; ++r) {
+          if (g0 + r * kOT >= ng) continue;
+          const unsigned int mb = (d[r] >> 24) & 15u, nv = d[r] >> 28;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if ((unsigned int)u < nv) int_acc(a, w4[r][u], (mb >> u) & 1u);
+        }
       }
       a.n = wave_sum(a.n);
       a.sm = wave_sum(a.sm);
@@ -925,17 +937,29 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
         }
         *reinterpret_cast<unsigned int*>(dst + 4 * g) = word;
       }
-      for (int g = threadIdx.x + kOG * kOT; g < ng; g += kOT) {
-        const unsigned int d = group_desc(M, wpr, bw, bwp, W, g);
-        const unsigned int o0 = d & 0xffffffu, mb = (d >> 24) & 15u, nv = d >> 28;
-        unsigned int word = 0u;
+      for (int g0 = threadIdx.x + kOG * kOT; g0 < ng; g0 += kOR * kOT) {
+        unsigned int d[kOR];
+        float w4[kOR][4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float x = ldg_b(img, 4u * (o0 + min((unsigned int)u, nv - 1u)));
-          const unsigned int q = (unsigned int)quantize(x, (mb >> u) & 1u, mmin, rng, flat);
-          word |= ((unsigned int)u < nv ? q : 0u) << (8 * u);
+        for (int r = 0; r < kOR; ++r) {
+          d[r] = group_desc(M, wpr, bw, bwp, W, min(g0 + r * kOT, ng - 1));
+          const unsigned int o0 = d[r] & 0xffffffu, nv = d[r] >> 28;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) w4[r][u] = ldg_b(img, 4u * (o0 + min((unsigned int)u, nv - 1u)));
         }
-        *reinterpret_cast<unsigned int*>(dst + 4 * g) = word;
+#pragma unroll
+        for (int r = 0; r < kOR; ++r) {
+          const int g = g0 + r * kOT;
+          if (g >= ng) continue;
+          const unsigned int mb = (d[r] >> 24) & 15u, nv = d[r] >> 28;
+          unsigned int word = 0u;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const unsigned int q = (unsigned int)quantize(w4[r][u], (mb >> u) & 1u, mmin, rng, flat);
+            word |= ((unsigned int)u < nv ? q : 0u) << (8 * u);
+          }
+          *reinterpret_cast<unsigned int*>(dst + 4 * g) = word;
+        }
       }
     }
   }

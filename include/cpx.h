@@ -363,6 +363,32 @@ int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx_seg_geom* 
 int cpx_embed_preprocess(cpx_ctx* ctx, const uint8_t* crops8_dev, const int64_t* index_dev, int N,
                          int S, int D, float mean, float stdv, void* out_dev);
 
+/* ---- f3: the EfficientNetV2-L forward (Cellpose_GPU_s3fs.py:109-110,184-194: timm
+ * tf_efficientnetv2_l, fp16 autocast, pooler_output) -------------------------------------- *
+ * NHWC fp16 activations, fp16 MFMA products with fp32 accumulation; BatchNorm folded to fp32
+ * scale/shift [C]; TF 'same' padding (output ceil(i / stride), pad_lo = total / 2).
+ * cpx_effnet_stem: x = cpx_embed_preprocess output fp16 [N][3][H][W]; w fp32 [32][3][3][3];
+ *   out fp16 [N][ceil(H/2)][ceil(W/2)][32] = silu(scale conv + shift).
+ * cpx_effnet_conv: ks 1 or 3, stride 1 or 2, cin % 32 == 0; w fp16 [cout][ks*ks][cin];
+ *   out [N][Ho][Wo][cout] = (act ? silu : id)(scale conv(in, w * gate) + shift) + res, with the
+ *   optional squeeze-excite gate fp32 [N][cin] and residual fp16 [N][Ho][Wo][cout] (stride 1).
+ * cpx_effnet_dw: depthwise 3x3, C % 64 == 0, w fp32 [C][9]; out = silu(scale dw + shift);
+ *   partial fp32 [N][cpx_effnet_dw_blocks(H, W, stride)][C] = per-block channel sums of out.
+ * cpx_effnet_se: gate fp32 [N][C] = sigmoid(be + we [C][rd] . silu(br + wr [rd][C] . mean)),
+ *   mean = sum of partial / HW.
+ * cpx_effnet_pool: out fp32 [N][C] = mean over HW of in fp16 [N][HW][C] (pooler_output).   */
+int cpx_effnet_stem(cpx_ctx* ctx, const void* x, int N, int H, int W, const float* w,
+                    const float* scale, const float* shift, void* out);
+int cpx_effnet_conv(cpx_ctx* ctx, const void* in, int N, int H, int W, int cin, int cout, int ks,
+                    int stride, const void* w, const float* scale, const float* shift, int act,
+                    const void* res, const float* gate, void* out);
+int cpx_effnet_dw(cpx_ctx* ctx, const void* in, int N, int H, int W, int C, int stride,
+                  const float* w, const float* scale, const float* shift, void* out, float* partial);
+int cpx_effnet_dw_blocks(int H, int W, int stride);
+int cpx_effnet_se(cpx_ctx* ctx, const float* partial, int N, int pblks, int HW, int C, int rd,
+                  const float* wr, const float* br, const float* we, const float* be, float* gate);
+int cpx_effnet_pool(cpx_ctx* ctx, const void* in, int N, int HW, int C, float* out);
+
 /* ---- a4 CPnet glue (bf16 NHWC activations around MIOpen convolutions) ----------------------
  * Cellpose resnet_torch.CPnet forward (used at Cellpose_GPU_s3fs.py:108-110 through
  * models.CellposeModel.eval): every batchconv is BatchNorm -> ReLU -> Conv2d, blocks add
@@ -429,10 +455,6 @@ int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* in, int in_
                       const float* shift, int relu, void* y_out, void* z_out, int z_up,
                       const float* head_w, const float* head_b, int n_head, float* head_out,
                       int* ovf);
-/* Variant 2 of cpx_cpnet_x3_conv (3x3) is persistent: a grid of two blocks per CU walks the
- * tiles, each tile's first channel slab loading while the previous tile finishes.  This caps
- * that grid at max_blocks (0 = default) — tests use it to give every block several tiles.     */
-int cpx_cpnet_x3_set_grid(cpx_ctx* ctx, int max_blocks);
 /* stem on the fp32 network input x [N][H][W][2] (CPX_TILE_F32_NHWC tiles): z0 = relu(scale0 x
  * + shift0), z_out = relu(scale1 (conv3x3(z0, w0) + bias0) + shift1), p_out = conv1x1(x, wp),
  * fp32 arithmetic, split stores (32 channels).                                               */

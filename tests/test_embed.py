@@ -1,7 +1,8 @@
 """f3 embeddings: EfficientNetV2-L restated (timm tf_efficientnetv2_l
 architecture, parameter count exact), the preprocessing restatement pinned to Pillow, the HIP
-preprocessing kernel bit-exact vs the restatement, the fp16 GPU forward vs the fp32 CPU module,
-and the reference's parquet / CSV layout (Cellpose_GPU_s3fs.py:326-471)."""
+preprocessing kernel bit-exact vs the restatement, the native fp16 forward (k_effnet.hip,
+cpx.effnet_hip) vs the fp32 PyTorch module on the CPU, and the reference's parquet / CSV layout
+(Cellpose_GPU_s3fs.py:326-471)."""
 import numpy as np
 import pytest
 import torch
@@ -59,7 +60,8 @@ def test_preprocess_kernel_bit_exact(dev):
 
 @pytest.mark.gpu
 def test_effnet_fp16_gpu_vs_fp32_cpu(dev):
-    """The fp16-autocast channels_last forward on the GPU vs the fp32 module on the CPU."""
+    """The native fp16 forward (libcpx k_effnet.hip kernels) on the GPU vs the fp32 module on the
+    CPU, same weights."""
     m_cpu = effnet.build_effnet(seed=5)
     from cpx.embed import Embedder
     emb = Embedder(dev, seed=5)
