@@ -491,13 +491,26 @@ __device__ __forceinline__ void dft20(cplx* v) {
   }
 }
 
+// W_2080^s, s = 0 .. 7: with W_260^q = W_2080^(8 q) they give every P3 twiddle W_2080^m =
+// W_260^(m >> 3) W_2080^(m & 7) from LDS (one extra rounding, no global load in P3)
+__constant__ double kW8[8][2] = {
+    {1.0, -0.0}, {0.9999954375014348, -0.0030207575728375146}, {0.9999817500473723, -0.006041487581270846},
+    {0.9999589377627102, -0.009062162461147334}, {0.9999270008556107, -0.012082754648817372},
+    {0.9998859396174979, -0.015103236581385914}, {0.9998357544230555, -0.018123580696963994},
+    {0.9997764457302234, -0.021143759434920226}};
+constexpr int kT260 = 268;  // W_260^i (i < 260), then W_2080^s (s < 8)
+
+__device__ __forceinline__ void fill_t260(cplx* t260, const cplx* __restrict__ tw) {
+  for (int i = threadIdx.x; i < kT260; i += kR2T)
+    t260[i] = i < 260 ? tw[8 * i] : cplx{kW8[i - 260][0], kW8[i - 260][1]};
+}
+
 // The three passes on one 2080-point sequence: load(n) gives point n (P1 threads call it for
 // their 13 points); on return A[j] = X[j] and A[260 + j] = X[1820 + j] (j < 260) and the block
-// is synchronised.  t260 must hold W_260^i (filled and synchronised by the caller's first
+// is synchronised.  t260 must hold fill_t260's table (filled before, and synchronised by, P1's
 // barrier: P1 does not read it).
 template <typename Load>
-__device__ __forceinline__ void fft2080_pruned(cplx* A, const cplx* t260, const cplx* __restrict__ tw,
-                                               Load load) {
+__device__ __forceinline__ void fft2080_pruned(cplx* A, const cplx* t260, Load load) {
   const int tid = threadIdx.x;
   // ---- P1
   if (tid < 160) {
@@ -540,7 +553,10 @@ __device__ __forceinline__ void fft2080_pruned(cplx* A, const cplx* t260, const 
 #pragma unroll
       for (int r = 0; r < 8; ++r) v[r] = A[j + 260 * r];
 #pragma unroll
-      for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], tw[j * r]);
+      for (int r = 1; r < 8; ++r) {
+        const int m = j * r;
+        v[r] = cmul(v[r], cmul(t260[m >> 3], t260[260 + (m & 7)]));
+      }
       // r' = 0: sum v[r];  r' = 7: sum v[r] W_8^(7 r) = sum v[r] exp(+i pi r / 4)
       const double h = 0.70710678118654752440;
       const cplx a = cadd(cadd(v[0], v[4]), cadd(v[2], v[6]));
@@ -577,7 +593,7 @@ __global__ __launch_bounds__(kR2T) void k_qc_rows_2080(
     QcAux* __restrict__ aux) {
   constexpr int W = kR2N;
   __shared__ cplx A[kR2N];
-  __shared__ cplx t260[260];
+  __shared__ cplx t260[kT260];
   const int plane = blockIdx.y;
   const int ch = plane % C;
   const int r0 = 2 * blockIdx.x, r1 = r0 + 1;
@@ -589,10 +605,10 @@ __global__ __launch_bounds__(kR2T) void k_qc_rows_2080(
   const cpx_plane_stats st = stats[plane];
   const double mean = st.sum_q / (double)st.n;
   const int tid = threadIdx.x;
-  for (int i = tid; i < 260; i += kR2T) t260[i] = tw[8 * i];  // W_260^i = W_2080^(8 i)
+  fill_t260(t260, tw);
   unsigned long long eq = 0;
   // the two rows as one complex sequence (real-input pair trick), mean removed
-  fft2080_pruned(A, t260, tw, [&](int n) {
+  fft2080_pruned(A, t260, [&](int n) {
     const double qa = qval<ILLUM>(rp, il, (long long)r0 * W + n);
     const double qb = r1 < H ? qval<ILLUM>(rp, il, (long long)r1 * W + n) : mean;
     eq += (qa == mean) + (r1 < H && qb == mean);
@@ -621,7 +637,7 @@ __global__ __launch_bounds__(kR2T) void k_qc_cols_2080(const cplx* __restrict__ 
                                                        double* __restrict__ ringpart) {
   constexpr int H = kR2N;
   __shared__ cplx A[kR2N];
-  __shared__ cplx t260[260];
+  __shared__ cplx t260[kT260];
   double* pw = reinterpret_cast<double*>(A);  // rows 0 .. 259, 1820 .. 2079 (compact), after the FFT
   int j = blockIdx.x, plane = blockIdx.y;
   const int total = gridDim.x * gridDim.y;
@@ -632,9 +648,9 @@ __global__ __launch_bounds__(kR2T) void k_qc_cols_2080(const cplx* __restrict__ 
     j = V - plane * KC;
   }
   const int tid = threadIdx.x;
-  for (int i = tid; i < 260; i += kR2T) t260[i] = tw[8 * i];
+  fill_t260(t260, tw);
   const cplx* src = rowspec + (long long)plane * H * KC + j;
-  fft2080_pruned(A, t260, tw, [&](int n) { return src[(long long)n * KC]; });
+  fft2080_pruned(A, t260, [&](int n) { return src[(long long)n * KC]; });
   constexpr int NP = (520 + kR2T - 1) / kR2T;
   double pv[NP];
 #pragma unroll
