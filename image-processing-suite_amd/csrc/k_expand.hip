@@ -18,6 +18,7 @@
 //          ascending order with a strict `<` (smaller column wins ties), threshold d^2 <= D^2.
 // Bit-identical to skimage/scipy (tests/test_gpu_parity.py, including equidistant ties).
 #include "cpx_internal.h"
+#include "ws_levels.h"
 
 namespace {
 
@@ -103,9 +104,15 @@ __global__ __launch_bounds__(kT) void k_edt_cols(const int* __restrict__ labels,
 // dispatch-bound); all its rows' candidate segments are staged in LDS at once.
 constexpr int kRowsPB = 8;
 
+// With `ring` (the Cells watershed, k_watershed.hip): every pixel on the border ring of its
+// 32 x 32 watershed tile also stores its initial flood level (from the Nuclei label, this
+// footprint label and the cell channel `corr` at plane stride `cstride`) into the tile's ring, so
+// the first relax round reads its halo as four contiguous vectors.
 __global__ __launch_bounds__(kT) void k_edt_rows(const int* __restrict__ nuc, int H, int W, int D,
                                                  const int* __restrict__ off,
-                                                 int* __restrict__ cells, int* __restrict__ cyto) {
+                                                 int* __restrict__ cells, int* __restrict__ cyto,
+                                                 const float* __restrict__ corr, long long cstride,
+                                                 unsigned long long* __restrict__ ring, int ntx, int nty) {
   extern __shared__ int seg[];  // kRowsPB x (kT + 2D) packed candidates
   const int fov = blockIdx.z, r0 = blockIdx.y * kRowsPB;
   const int nr = min(kRowsPB, H - r0);
@@ -135,15 +142,27 @@ __global__ __launch_bounds__(kT) void k_edt_rows(const int* __restrict__ nuc, in
     }
     const int lab = best <= D * D ? blab : 0;
     const long long px = ((long long)fov * H + r0 + rr) * W + c;
+    const int nv = nuc[px];
     if (cells) cells[px] = lab;
-    if (cyto) cyto[px] = (nuc[px] == 0) ? lab : 0;
+    if (cyto) cyto[px] = (nv == 0) ? lab : 0;
+    if (ring) {
+      const int y = r0 + rr, ly = y % wsl::kT, lx = c % wsl::kT;
+      if (ly == 0 || ly == wsl::kT - 1 || lx == 0 || lx == wsl::kT - 1) {
+        const long long pix = (long long)y * W + c;
+        const unsigned long long v =
+            wsl::init_level(wsl::info_of(nv, lab, corr[fov * cstride + pix]), pix);
+        const long long tile = ((long long)fov * nty + y / wsl::kT) * ntx + c / wsl::kT;
+        wsl::ring_store(ring, tile, ly, lx, v);
+      }
+    }
   }
 }
 
 }  // namespace
 
-extern "C" int cpx_expand_labels(cpx_ctx* ctx, const int32_t* nuclei_dev, int B, int H, int W,
-                                 int distance, int32_t* cells_dev, int32_t* cyto_dev) {
+int cpx_expand_labels_ring(cpx_ctx* ctx, const int32_t* nuclei_dev, int B, int H, int W, int distance,
+                           int32_t* cells_dev, int32_t* cyto_dev, const float* corr_cell,
+                           long long corr_stride, unsigned long long* ring) {
   CPX_REQUIRE(ctx && nuclei_dev && (cells_dev || cyto_dev), CPX_ERR_ARG,
               "cpx_expand_labels: null argument");
   CPX_REQUIRE(B > 0 && B <= 65535 && H > 0 && H <= 65535 && W > 0 && distance >= 0 && distance <= 127,
@@ -156,7 +175,13 @@ extern "C" int cpx_expand_labels(cpx_ctx* ctx, const int32_t* nuclei_dev, int B,
   CPX_CHECK_LAUNCH("k_edt_cols");
   hipLaunchKernelGGL(k_edt_rows, dim3(cpx_div_up(W, kT), cpx_div_up(H, kRowsPB), B), dim3(kT),
                      sizeof(int) * kRowsPB * (kT + 2 * distance), ctx->stream,
-                     (const int*)nuclei_dev, H, W, distance, (const int*)off, cells_dev, cyto_dev);
+                     (const int*)nuclei_dev, H, W, distance, (const int*)off, cells_dev, cyto_dev,
+                     corr_cell, corr_stride, ring, cpx_div_up(W, wsl::kT), cpx_div_up(H, wsl::kT));
   CPX_CHECK_LAUNCH("k_edt_rows");
   return CPX_OK;
+}
+
+extern "C" int cpx_expand_labels(cpx_ctx* ctx, const int32_t* nuclei_dev, int B, int H, int W,
+                                 int distance, int32_t* cells_dev, int32_t* cyto_dev) {
+  return cpx_expand_labels_ring(ctx, nuclei_dev, B, H, W, distance, cells_dev, cyto_dev, nullptr, 0, nullptr);
 }

@@ -963,6 +963,13 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
         }
       }
     }
+    // Chebyshev distance of each unit from the centre: T is exactly 0.0 beyond distance it before
+    // iteration it (the support grows by one cell per iteration), so a unit further than it + 1
+    // would compute and store 0.0 over 0.0 — it is skipped until the support reaches it
+    int ud[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i)
+      ud[i] = max(max(max(0, uy0[i] - ym), ym - (uy0[i] + R - 1)), max(max(0, ux[i] - xm), xm - (ux[i] + 1)));
     __syncthreads();  // rowc / colc / sbest reads done before T is cleared
     for (int i = tid; i < ly * lxp; i += THREADS) T[i] = 0.0;
     __syncthreads();
@@ -978,7 +985,8 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
     for (int it = 0; it < niter; ++it) {
 #pragma unroll
       for (int i = 0; i < U; ++i) {
-        if (!(um[i][0] | um[i][1])) continue;  // no mask cell in this unit (or no unit)
+        if (!(um[i][0] | um[i][1]) || ud[i] > it + 1) continue;  // no mask cell (or no unit), or
+                                                                  // beyond the support
         // double2 offsets of the unit's rows (columns X - 1 .. X + 2 = two 16-byte words); the
         // opaque base keeps the compiler from holding every row address across the loop, and
         // rows past the object's last row read the zero border row (clamped): their sums are
@@ -1017,7 +1025,7 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < U; ++i) {
-        if (!(um[i][0] | um[i][1])) continue;
+        if (!(um[i][0] | um[i][1]) || ud[i] > it + 1) continue;
         int wb = uy0[i] * lxp + ux[i];
         asm volatile("" : "+v"(wb));
 #pragma unroll
@@ -1215,6 +1223,10 @@ __global__ __launch_bounds__(THREADS, 1) void k_flow_error_cmp(
         }
       }
     }
+    int ud[U];  // Chebyshev distance of the unit from the centre (see k_flow_error_lds)
+#pragma unroll
+    for (int i = 0; i < U; ++i)
+      ud[i] = max(max(max(0, Y0[i] - ym), ym - (Y0[i] + R - 1)), max(max(0, X[i] - xm), xm - (X[i] + 1)));
     __syncthreads();  // rowc / colc / extents read: T is cleared next
     for (int i = tid; i < 2 * tot2; i += THREADS) T[i] = 0.0;
     __syncthreads();
@@ -1235,7 +1247,7 @@ __global__ __launch_bounds__(THREADS, 1) void k_flow_error_cmp(
     for (int it = 0; it < niter; ++it) {
 #pragma unroll
       for (int i = 0; i < U; ++i) {
-        if (!(um[i][0] | um[i][1])) continue;
+        if (!(um[i][0] | um[i][1]) || ud[i] > it + 1) continue;
         const int pa = (X[i] - 1) >> 1;  // column pairs (X - 1, X) and (X + 1, X + 2)
         double2 ua, ub, ca, cb, da, db;
         ldrow(Y0[i] - 1, pa, ua, ub);
@@ -1259,7 +1271,7 @@ __global__ __launch_bounds__(THREADS, 1) void k_flow_error_cmp(
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < U; ++i) {
-        if (!(um[i][0] | um[i][1])) continue;
+        if (!(um[i][0] | um[i][1]) || ud[i] > it + 1) continue;
         const int pa = (X[i] - 1) >> 1;
         // opaque copies: the per-row write predicates are not hoisted out of the iteration loop
         unsigned int m0 = um[i][0], m1 = um[i][1];

@@ -27,21 +27,18 @@
 // (oracle) and tests/test_gpu_watershed.py (this kernel), pinned to skimage itself by
 // tests/golden/watershed_cases.npz.
 #include "cpx_internal.h"
+#include "ws_levels.h"
 #include <stdio.h>
 #include <stdlib.h>
 
 namespace {
 
-constexpr int kT = 32;                 // tile edge
+using namespace wsl;
 constexpr int kThreads = 64;           // one wave per tile: no block barrier on the hop path,
 constexpr int kWaves = kThreads / 64;  // ~9 independent tiles per CU (17-19 KB of LDS each)
 constexpr int kLS = kT + 3;            // LDS row stride (odd)
 constexpr int kLRows = kT + 2;
 constexpr int kPerThread = kT * kT / kThreads;
-constexpr unsigned long long kBlocked = ~0ull;          // outside the mask / the image
-constexpr unsigned long long kUnreached = ~0ull - 1ull; // free pixel the flood has not reached
-constexpr unsigned kMark = 1u << 16, kBlk = 1u << 17;
-constexpr int kKeyShift = 23;
 // tile flag bits (per round)
 constexpr unsigned char kUp = 1, kLeft = 2, kRight = 4, kDown = 8;  // that border changed
 constexpr unsigned char kSelf = 16;   // a wave queue overflowed: re-run the whole tile
@@ -59,24 +56,10 @@ struct WsArgs {
   unsigned long long* Bg;  // [B][H][W] stored levels: kBlocked | key | kMarkBit (markers) | B
   unsigned short* inv;     // [B][H][W] 65535 - q16 of free pixels (tiles with free pixels)
   unsigned char* tfree;    // [B * tiles] tile has free pixels
+  unsigned long long* ring;  // [B * tiles][4][kT] border levels (ws_levels.h); initial ones from k_edt_rows
   int* last;               // [B][2] last active relax / label round
   unsigned long long* dbg; // optional counters (CPX_WS_DEBUG): [kernel][round][4]
 };
-
-__device__ __forceinline__ unsigned q16(float v) {
-  if (!(v < 65535.0f)) return 65535u;  // NaN, inf, >= 65535
-  return v > 0.0f ? (unsigned)v : 0u;  // truncation
-}
-
-__device__ __forceinline__ unsigned long long key_of(unsigned inf, long long pix) {
-  return ((unsigned long long)(inf & 0xffffu) << kKeyShift) | (unsigned long long)pix;
-}
-
-__device__ __forceinline__ unsigned long long init_level(unsigned inf, long long pix) {
-  if (inf & kBlk) return kBlocked;
-  if (inf & kMark) return key_of(inf, pix);
-  return kUnreached;
-}
 
 __device__ __forceinline__ unsigned char border_bits(int y, int x) {
   unsigned char m = 0;
@@ -179,13 +162,6 @@ __device__ int schedule_tiles(const WsArgs& a, int round, const unsigned char* F
   return *s_n;
 }
 
-// info word from the three inputs: (65535 - q) | marker | blocked
-__device__ __forceinline__ unsigned info_of(int n, int f, float v) {
-  if (n != 0) return (65535u - q16(v)) | kMark;
-  if (f == 0) return kBlk;
-  return 65535u - q16(v);
-}
-
 // border bits of a padded LDS offset (tile rows / columns 1..kT)
 __device__ __forceinline__ unsigned char border_bits_off(int o) {
   return border_bits(o / kLS - 1, o % kLS - 1);
@@ -235,27 +211,25 @@ __global__ __launch_bounds__(kThreads, 2) void k_ws_relax(WsArgs a, int round,
         w1_[k] = a.inv[fov * hw + pix];
       }
     }
-    // halo: loads from clamped addresses issued unconditionally with the tile's, resolved after
-    constexpr int kHalo = (4 * kT + kThreads - 1) / kThreads;
-    unsigned long long hw0[kHalo];
-    int hw1[kHalo], ho[kHalo];
-    bool hin[kHalo];
+    // halo: the facing border vectors of the four neighbour tiles' rings (contiguous; the initial
+    // rings come from k_edt_rows, later ones from the neighbours' previous visits — any of them is
+    // an upper bound of the final level, and a changed border flags this tile for the next round)
+    constexpr int kHalo = kRing / kThreads;
+    static_assert(kRing % kThreads == 0, "whole halo per lane");
+    unsigned long long hv[kHalo];
+    int ho[kHalo];
 #pragma unroll
     for (int k = 0; k < kHalo; ++k) {
-      const int h = lane + k * kThreads;
-      int hy = 0, hx = 0;
-      if (h < 4 * kT) halo_pos(h, hy, hx);
-      ho[k] = h < 4 * kT ? (1 + hy) * kLS + 1 + hx : -1;
-      const int y = y0 + hy, x = x0 + hx;
-      hin[k] = h < 4 * kT && y >= 0 && y < a.H && x >= 0 && x < a.W;
-      const long long pix = hin[k] ? (long long)y * a.W + x : 0;
-      if (R0) {
-        hw0[k] = ((unsigned long long)(unsigned)nucf[pix] << 32) | (unsigned)footf[pix];
-        hw1[k] = __float_as_int(cf[pix]);
-      } else {
-        hw0[k] = Bf[pix];
-        hw1[k] = 0;
-      }
+      const int h = lane + k * kThreads, side = h / kT, j = h % kT;
+      int hy, hx;
+      halo_pos(h, hy, hx);
+      ho[k] = (1 + hy) * kLS + 1 + hx;
+      long long src = -1;
+      if (side == 0) { if (ty > 0 && x0 + j < a.W) src = (long long)(t - a.ntx) * kRing + kT + j; }
+      else if (side == 1) { if (ty + 1 < a.nty && x0 + j < a.W) src = (long long)(t + a.ntx) * kRing + j; }
+      else if (side == 2) { if (tx > 0 && y0 + j < a.H) src = (long long)(t - 1) * kRing + 3 * kT + j; }
+      else if (tx + 1 < a.ntx && y0 + j < a.H) src = (long long)(t + 1) * kRing + 2 * kT + j;
+      hv[k] = src >= 0 ? a.ring[src] : kBlocked;
     }
     int any_free = 0;
 #pragma unroll
@@ -280,17 +254,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_ws_relax(WsArgs a, int round,
     }
 #pragma unroll
     for (int k = 0; k < kHalo; ++k) {
-      if (ho[k] < 0) continue;
-      unsigned long long hb = kBlocked;
-      if (hin[k]) {
-        const int hh = lane + k * kThreads;
-        int hy, hx;
-        halo_pos(hh, hy, hx);
-        const long long pix = (long long)(y0 + hy) * a.W + x0 + hx;
-        hb = R0 ? init_level(info_of((int)(hw0[k] >> 32), (int)(unsigned)hw0[k], __int_as_float(hw1[k])), pix)
-                : level_of(hw0[k]);
-      }
-      sB[ho[k]] = hb;
+      sB[ho[k]] = hv[k];
       sK[ho[k]] = kBlocked;
     }
     any_free = __syncthreads_or(any_free);
@@ -400,6 +364,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_ws_relax(WsArgs a, int round,
       } else if (R0) {
         a.Bg[pix] = b == kBlocked ? b : (b | kMarkBit);
       }
+    }
+    // this tile's border levels for its neighbours' halos
+    for (int h = lane; h < kRing; h += kThreads) {
+      const int side = h / kT, j = h % kT;
+      const int ly = side == 0 ? 0 : side == 1 ? kT - 1 : j, lx = side == 2 ? 0 : side == 3 ? kT - 1 : j;
+      if (y0 + ly < a.H && x0 + lx < a.W) a.ring[(long long)t * kRing + h] = sB[(1 + ly) * kLS + 1 + lx];
     }
     if (lane == 0) {
       Fn[t] = (unsigned char)s_bits;
@@ -574,17 +544,21 @@ extern "C" int cpx_watershed_cells(cpx_ctx* ctx, const int32_t* nuclei_dev, cons
                   W > 0 && (long long)H * W <= (1ll << kKeyShift) && relax_rounds > 0 &&
                   label_rounds > 0 && status_stride > 0,
               CPX_ERR_ARG, "cpx_watershed_cells: bad sizes (H*W <= 2^23, 0 <= cell_channel < C, rounds 1..64)");
-  // the footprint (mask) and the Cytoplasm of every pixel the flood does not relabel
-  int rc = cpx_expand_labels(ctx, nuclei_dev, B, H, W, distance, cells_dev, cyto_dev);
-  if (rc != CPX_OK) return rc;
   const int ntx = cpx_div_up(W, kT), nty = cpx_div_up(H, kT), per = ntx * nty, total = B * per;
   const size_t nB = sizeof(unsigned long long) * (size_t)B * H * W;
   const size_t nF = (size_t)total;
   const size_t nI = (sizeof(unsigned short) * (size_t)B * H * W + 255) / 256 * 256;
   const size_t nP = (sizeof(int) * (size_t)B * H * W + 255) / 256 * 256;  // ptr, two lists
   CPX_REQUIRE((long long)B * H * W < (1ll << 31), CPX_ERR_ARG, "cpx_watershed_cells: batch too large");
-  char* ws = (char*)cpx_ws(ctx, WS_WATERSHED, nB + nI + 3 * nP + 5 * nF + sizeof(int) * (2 * B + 80) + 2048);
+  const size_t nR = sizeof(unsigned long long) * kRing * (size_t)total;
+  char* ws = (char*)cpx_ws(ctx, WS_WATERSHED, nB + nI + 3 * nP + nR + 5 * nF + sizeof(int) * (2 * B + 80) + 2048);
   if (!ws) return CPX_ERR_OOM;
+  // the footprint (mask), the Cytoplasm of every pixel the flood does not relabel, and every
+  // tile's initial border ring
+  unsigned long long* ring = (unsigned long long*)(ws + nB + nI + 3 * nP);
+  int rc = cpx_expand_labels_ring(ctx, nuclei_dev, B, H, W, distance, cells_dev, cyto_dev,
+                                  corr_dev + (size_t)cell_channel * H * W, (long long)C * H * W, ring);
+  if (rc != CPX_OK) return rc;
   WsArgs a;
   a.nuc = nuclei_dev;
   a.foot = cells_dev;
@@ -600,7 +574,8 @@ extern "C" int cpx_watershed_cells(cpx_ctx* ctx, const int32_t* nuclei_dev, cons
   a.inv = (unsigned short*)(ws + nB);
   int* ptr = (int*)(ws + nB + nI);
   int* lists[2] = {(int*)(ws + nB + nI + nP), (int*)(ws + nB + nI + 2 * nP)};
-  unsigned char* F = (unsigned char*)(ws + nB + nI + 3 * nP);  // relax ping-pong, tile-free
+  a.ring = ring;
+  unsigned char* F = (unsigned char*)(ws + nB + nI + 3 * nP + nR);  // relax ping-pong, tile-free
   unsigned char* Fr[2] = {F, F + nF};
   a.tfree = F + 4 * nF;
   a.last = (int*)(((uintptr_t)(F + 5 * nF) + 255) & ~(uintptr_t)255);
