@@ -5,8 +5,9 @@
 
 Starts N `cpx.plate` processes (rank r sees only GPU devices[r] through HIP_VISIBLE_DEVICES,
 as the reference pins each consumer with CUDA_VISIBLE_DEVICES, Cellpose_GPU_s3fs.py:97,295);
-each drains its own queue of (plate, time, well shard) jobs and writes its rows as parts; once
-all exit cleanly the launcher merges every job's parts into the final CSVs.  The launcher itself
+the ranks claim the batches of every (plate, time) job from shared per-job counters (a fresh
+cpx.plate --queue directory per run: a rank that finishes sooner claims more) and write their rows
+as parts; once all exit cleanly the launcher merges every job's parts into the final CSVs.  The launcher itself
 never touches a GPU.  --devices repeats a device to run several ranks on one GPU (tests).
 """
 from __future__ import annotations
@@ -16,8 +17,10 @@ import glob
 import json
 import logging
 import os
+import shutil
 import subprocess
 import sys
+import time
 
 from .plate import merge_parts, parse_args as plate_args
 
@@ -44,15 +47,19 @@ def main(argv=None):
     for f in glob.glob(os.path.join(pa.out, ".cpx_jobs_r*.json")):
         os.remove(f)
     pkg_root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    # fresh shared batch counters for this run (cpx.plate.WorkQueue): ranks claim batches
+    qdir = os.path.join(pa.out, f".cpx_queue_{os.getpid()}_{time.time_ns()}")
+    os.makedirs(qdir)
     procs = []
     for r in range(n):
         env = dict(os.environ, HIP_VISIBLE_DEVICES=str(devs[r]), RANK=str(r), WORLD_SIZE=str(n))
         env.pop("MASTER_ADDR", None)  # no process group: the launcher merges
         env["PYTHONPATH"] = pkg_root + os.pathsep + env.get("PYTHONPATH", "")
         cmd = [sys.executable, "-m", "cpx.plate", *rest, "--rank", str(r), "--world", str(n),
-               "--device", "0", "--no-merge"]
+               "--device", "0", "--no-merge", "--queue", qdir]
         procs.append(subprocess.Popen(cmd, env=env))
     rcs = [p.wait() for p in procs]
+    shutil.rmtree(qdir, ignore_errors=True)
     if any(rcs):
         raise SystemExit(f"rank exit codes {rcs}: parts left unmerged under {pa.out}")
     dirs = []

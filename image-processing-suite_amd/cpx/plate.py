@@ -15,9 +15,10 @@ Metadata_Timepoint unless given.  Every LoadData file is one (plate, time) job.
 
 Multi-GPU (the reference's per-GPU consumers Cellpose_GPU_s3fs.py:269-300 and
 per-(plate, time) jobs Feature_extraction_opt.py:63-76): one process per GPU (`cpx.launch`, or
-torchrun with RANK / WORLD_SIZE), each draining its own queue of (plate, time, well shard)
-jobs — wells are dealt round-robin in first-appearance order, so all sites of a well stay on one
-GPU — and writing its rows as parquet parts; the parts are merged into the final CSVs sorted by
+torchrun with RANK / WORLD_SIZE); the ranks claim the batches of each (plate, time) job from a
+shared per-job counter (WorkQueue, --queue: a rank that finishes sooner claims more) or, without
+--queue, each drains its static well shard (wells dealt round-robin in first-appearance order);
+each writes its rows as parquet parts; the parts are merged into the final CSVs sorted by
 (ImageNumber, ObjectNumber), byte-identical for any number of processes.  No collective touches
 the data path.  Batches always hold --batch FOVs (the tail is zero-padded), so every process runs
 the same kernels on the same batch shape.
@@ -62,6 +63,9 @@ def parse_args(argv=None):
                     help="this process's rank (well shard); default $RANK")
     ap.add_argument("--world", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
                     help="processes (GPUs) sharing the jobs; default $WORLD_SIZE")
+    ap.add_argument("--queue", default=None,
+                    help="with --world > 1: directory of the shared per-job batch counters (dynamic work "
+                         "queue across the ranks; cpx.launch creates a fresh one); default: static well shards")
     ap.add_argument("--no-merge", action="store_true",
                     help="with --world > 1: leave the parts for cpx.launch / merge_parts")
     ap.add_argument("--ws-rounds", type=int, nargs=2, default=None, metavar=("RELAX", "LABEL"),
@@ -79,6 +83,50 @@ def shard_rows(table, rank: int, world: int):
         wells = [order.setdefault(w, len(order)) for w in table["Metadata_Well"].astype(str)]
         return [i for i, w in enumerate(wells) if w % world == rank]
     return [i for i in range(len(table)) if i % world == rank]
+
+
+class WorkQueue:
+    """Batch counter of one (plate, time) job shared by the ranks of one node: a file advanced
+    under an exclusive flock, so each rank claims the next unclaimed batch of --batch consecutive
+    LoadData rows and a rank whose batches finish sooner claims more (the reference's GPU consumers
+    draw sites from one shared queue, Cellpose_GPU_s3fs.py:269-300).  The merged tables do not
+    depend on which rank measured a site (merge_parts sorts the rows)."""
+
+    def __init__(self, qdir: str, key: str):
+        os.makedirs(qdir, exist_ok=True)
+        self.path = os.path.join(qdir, f"{key}.ctr")
+
+    def take(self) -> int:
+        import fcntl
+        fd = os.open(self.path, os.O_RDWR | os.O_CREAT, 0o644)
+        try:
+            fcntl.flock(fd, fcntl.LOCK_EX)
+            raw = os.read(fd, 32)
+            k = int(raw) if raw.strip() else 0
+            os.lseek(fd, 0, os.SEEK_SET)
+            os.ftruncate(fd, 0)
+            os.write(fd, str(k + 1).encode())
+            return k
+        finally:
+            os.close(fd)  # releases the lock
+
+
+def batch_source(table, a, job_index: int):
+    """Lists of table row positions, one per GPU batch, for this rank: claimed from the job's
+    WorkQueue (--queue, world > 1) or this rank's static well shard (shard_rows)."""
+    B = max(1, a.batch)
+    if a.queue and a.world > 1:
+        q = WorkQueue(a.queue, f"job{job_index:04d}")
+        nb = (len(table) + B - 1) // B
+        while True:
+            k = q.take()
+            if k >= nb:
+                return
+            yield list(range(k * B, min(len(table), (k + 1) * B)))
+    else:
+        mine = shard_rows(table, a.rank, a.world)
+        for i in range(0, len(mine), B):
+            yield mine[i:i + B]
 
 
 def job_dir(out, plate, time):
@@ -167,15 +215,13 @@ def run(argv=None):
     LAST_TIMING.clear()
     state = {}  # pipelines, created for the first job's plane geometry and reused
     dirs = []
-    for load_data in a.load_data:
+    for ji, load_data in enumerate(a.load_data):
         table, plate, time = _job_meta(a, load_data)
-        mine = shard_rows(table, a.rank, a.world)
-        files = [[os.path.join(a.data_path, str(table.iloc[i][f"FileName_{ch}"])) for ch in chans] for i in mine]
         out = PlateTables(chans)
         status = []  # per site: the reference's results_dict entry (Cellpose_GPU_s3fs.py:123-125,219-223)
-        if files:
-            _run_sites(a, table, mine, files, chans, state, out, status)
-            LAST_TIMING.append({"job": os.path.basename(load_data), "fovs": len(files), **state["timing"]})
+        nsites = _run_sites(a, table, batch_source(table, a, ji), chans, state, out, status)
+        if nsites:
+            LAST_TIMING.append({"job": os.path.basename(load_data), "fovs": nsites, **state["timing"]})
         d = job_dir(a.out, plate, time)
         frames = out.frames()
         frames["site_status"] = pd.DataFrame(status, columns=["ImageNumber", "status", "n_cells"]) \
@@ -186,7 +232,7 @@ def run(argv=None):
             os.makedirs(d, exist_ok=True)
             for name, df in frames.items():
                 df.to_csv(os.path.join(d, f"{name}.csv"), index=False)
-        log.info("rank %d/%d: %d sites of %s/%s -> %s", a.rank, a.world, len(files), plate, time, d)
+        log.info("rank %d/%d: %d sites of %s/%s -> %s", a.rank, a.world, nsites, plate, time, d)
         dirs.append(d)
     if a.world > 1:
         with open(os.path.join(a.out, f".cpx_jobs_r{a.rank:04d}.json"), "w") as f:
@@ -210,14 +256,25 @@ def _torchrun_merge(a, dirs):
     dist.barrier()
 
 
-def _run_sites(a, table, mine, files, chans, state, out, status):
+def _run_sites(a, table, source, chans, state, out, status):
+    """Measure the batches `source` yields (lists of table row positions); returns the number of
+    sites measured."""
     import torch
     from . import tiffio
     from .device import Device
     from .pipeline import OBJECT_SETS, FovPipeline, PipelineConfig
     C = len(chans)
+    source = iter(source)
+    first = next(source, None)
+    if first is None:
+        return 0
+
+    def site_files(r):
+        return [os.path.join(a.data_path, str(table.iloc[r][f"FileName_{ch}"])) for ch in chans]
+
     H = W = None
-    for fs in files:  # this job's plane geometry, from its first readable plane
+    # this job's plane geometry, from the first readable plane of this batch (else of the job)
+    for fs in map(site_files, [*first, *range(len(table))]):
         try:
             H, W = tiffio.imread(fs[0]).shape
             break
@@ -266,15 +323,14 @@ def _run_sites(a, table, mine, files, chans, state, out, status):
             dst[...] = 0
             return False
 
-    batches = [list(range(i, min(i + B, len(files)))) for i in range(0, len(files), B)]
+    batches = [first]  # row positions per batch, grown as batches are claimed
     inflight = []  # (batch index, pipeline, slot, upload event, empty flags)
     uploads = [None] * n_pipes  # last upload event per staging buffer
     t_start = time.perf_counter()
 
     def record(bi, res, empty):
         idx = batches[bi]
-        for k, j in enumerate(idx):
-            row_i = mine[j]
+        for k, row_i in enumerate(idx):
             img_no = int(table.index[row_i]) + 1   # the LoadData row, also after QC filtering
             meta = table.iloc[row_i].to_dict()
             if empty[k]:  # unreadable site: no measurements, no object rows
@@ -293,7 +349,7 @@ def _run_sites(a, table, mine, files, chans, state, out, status):
                 out.add_objects(s, img_no, res.objects[s][k]["label"], res.feats[s][k])
             n = counts["Nuclei"]
             status.append({"ImageNumber": img_no, "status": "success" if n else "empty", "n_cells": n})
-        log.info("batch %d/%d: %d FOVs", bi + 1, len(batches), len(idx))
+        log.info("batch %d: %d FOVs", bi + 1, len(idx))
 
     def decode(bi, pool):
         """Decode batch bi into its pipeline's pinned staging buffer (after that buffer's last
@@ -304,11 +360,12 @@ def _run_sites(a, table, mine, files, chans, state, out, status):
         hn = hosts[p_i].numpy().view(np.uint16).reshape(B, C, H, W)
         idx = batches[bi]
         hn[len(idx):] = 0
-        return [pool.submit(read_fov, files[i], hn[k]) for k, i in enumerate(idx)]
+        return [pool.submit(read_fov, site_files(r), hn[k]) for k, r in enumerate(idx)]
 
     with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, a.threads)) as pool:
         pending = decode(0, pool)
-        for bi, idx in enumerate(batches):
+        bi = 0
+        while bi < len(batches):
             empty = [not f.result() for f in pending]
             p_i = bi % n_pipes
             with torch.cuda.stream(streams[p_i]):
@@ -318,18 +375,23 @@ def _run_sites(a, table, mine, files, chans, state, out, status):
                 uploads[p_i] = up
                 slot = pipes[p_i].run()
             inflight.append((bi, pipes[p_i], slot, up, empty))
-            if bi + 1 < len(batches):  # decode the next batch while this one runs
+            nxt = next(source, None)  # claim and decode the next batch while this one runs
+            if nxt is not None:
+                batches.append(nxt)
                 pending = decode(bi + 1, pool)
             if len(inflight) > n_pipes:   # results in batch order, one step behind the GPU
                 obi, q, sl, _, em = inflight.pop(0)
                 record(obi, q.fetch(sl), em)
+            bi += 1
         while inflight:
             obi, q, sl, _, em = inflight.pop(0)
             record(obi, q.fetch(sl), em)
     secs = time.perf_counter() - t_start
+    nsites = sum(len(b) for b in batches)
     state["timing"] = {"seconds": secs, "threads": a.threads, "batch": B, "pipes": n_pipes}
     log.info("%d sites in %.2f s: %.1f FOV/s (decode threads %d, batch %d, pipelines %d)",
-             len(files), secs, len(files) / max(secs, 1e-9), a.threads, B, n_pipes)
+             nsites, secs, nsites / max(secs, 1e-9), a.threads, B, n_pipes)
+    return nsites
 
 
 if __name__ == "__main__":

@@ -35,7 +35,7 @@ namespace {
 
 using namespace wsl;
 constexpr int kThreads = 64;           // one wave per tile: no block barrier on the hop path,
-constexpr int kWaves = kThreads / 64;  // ~9 independent tiles per CU (17-19 KB of LDS each)
+constexpr int kWaves = kThreads / 64;  // eight independent tiles per CU (18 KiB of LDS each)
 constexpr int kLS = kT + 3;            // LDS row stride (odd)
 constexpr int kLRows = kT + 2;
 constexpr int kPerThread = kT * kT / kThreads;
@@ -45,6 +45,7 @@ constexpr unsigned char kSelf = 16;   // a wave queue overflowed: re-run the who
 constexpr int kQCap = 2048;           // per-wave LDS queue (tile-local pixel indices)
 static_assert(kQCap >= kT * kT + 3 * 64, "the seeds of a whole tile plus one drain step fit");
 static_assert(kWaves == 1, "one wave per tile");
+constexpr unsigned kNoKey = 0xffffffffu;             // sK of a pixel without a key
 constexpr unsigned long long kMarkBit = 1ull << 40;  // stored level of a marker: key | kMarkBit
 static_assert(kKeyShift + 16 < 40, "keys stay below the marker bit");
 
@@ -174,10 +175,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_ws_relax(WsArgs a, int round,
   // levels of the tile + halo, and the key of every free tile pixel (kBlocked for markers,
   // blocked pixels and the halo: max(kBlocked, .) never lowers them, so the pushes need no
   // bounds or type checks); the queue holds padded LDS offsets
+  // sK holds a free pixel's inverted intensity (its key without the pixel index, which follows
+  // from the LDS offset) or kNoKey; the seed candidates share the queue's storage (a seed is read
+  // before the queue's tail can reach its slot): 18 KiB per tile, eight tiles per CU
   __shared__ unsigned long long sB[kLRows * kLS];
-  __shared__ unsigned long long sK[kLRows * kLS];
+  __shared__ unsigned sK[kLRows * kLS];
   __shared__ unsigned short sQ[kQCap];
-  __shared__ unsigned short sS[kT * kT];  // seed candidates
+  unsigned short* sS = sQ;  // seed candidates
   __shared__ unsigned s_bits;
   __shared__ int s_list[kThreads], s_n;
   const int lane = threadIdx.x;
@@ -190,6 +194,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_ws_relax(WsArgs a, int round,
     const int fov = t / per, tt = t - fov * per, ty = tt / a.ntx, tx = tt - ty * a.ntx;
     const bool full = R0 || (Fp[t] & kSelf) != 0;
     const int y0 = ty * kT, x0 = tx * kT;
+    // key of the pixel at padded LDS offset o (kBlocked for markers, blocked pixels, the halo)
+    auto key_at = [&](int o) -> unsigned long long {
+      const unsigned v = sK[o];
+      if (v == kNoKey) return kBlocked;
+      const int oy = o / kLS - 1, ox = o - (o / kLS) * kLS - 1;
+      return ((unsigned long long)v << kKeyShift) | (unsigned long long)((long long)(y0 + oy) * a.W + x0 + ox);
+    };
     if (lane == 0) s_bits = 0;
     const int* nucf = a.nuc + fov * hw;
     const int* footf = a.foot + fov * hw;
@@ -250,12 +261,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_ws_relax(WsArgs a, int round,
       }
       any_free |= key != kBlocked;
       sB[lds_off(i)] = b;
-      sK[lds_off(i)] = key;
+      sK[lds_off(i)] = key != kBlocked ? (unsigned)(key >> kKeyShift) : kNoKey;
     }
 #pragma unroll
     for (int k = 0; k < kHalo; ++k) {
       sB[ho[k]] = hv[k];
-      sK[ho[k]] = kBlocked;
+      sK[ho[k]] = kNoKey;
     }
     any_free = __syncthreads_or(any_free);
     if (R0) {
@@ -282,7 +293,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_ws_relax(WsArgs a, int round,
 #pragma unroll
       for (int k = 0; k < kPerThread; ++k) {
         const int o = lds_off(lane + k * kThreads);
-        const bool c = sK[o] != kBlocked;
+        const bool c = sK[o] != kNoKey;
         const unsigned long long m = __ballot(c);
         if (c) sS[nseed + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)o;
         nseed += __popcll(m);
@@ -294,7 +305,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_ws_relax(WsArgs a, int round,
     __syncthreads();
     for (int base = 0; base < nseed; base += kThreads) {
       const int o = base + lane < nseed ? (int)sS[base + lane] : kLS + 1;
-      const unsigned long long key = base + lane < nseed ? sK[o] : kBlocked;
+      const unsigned long long key = base + lane < nseed ? key_at(o) : kBlocked;
       bool imp = false;
       if (key != kBlocked) {
         const unsigned long long u = sB[o - kLS], l = sB[o - 1], r = sB[o + 1], d = sB[o + kLS];
@@ -326,7 +337,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_ws_relax(WsArgs a, int round,
       unsigned long long kk[4], bb[4];
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        kk[d] = sK[nb[d]];
+        kk[d] = key_at(nb[d]);
         bb[d] = sB[nb[d]];
       }
       bool imp[4];
@@ -357,10 +368,11 @@ __global__ __launch_bounds__(kThreads, 2) void k_ws_relax(WsArgs a, int round,
       if (y >= a.H || x >= a.W) continue;
       const long long pix = fov * hw + (long long)y * a.W + x;
       const int o = lds_off(i);
-      const unsigned long long b = sB[o], key = sK[o];
-      if (key != kBlocked) {
+      const unsigned long long b = sB[o];
+      const unsigned kv = sK[o];
+      if (kv != kNoKey) {
         a.Bg[pix] = b;
-        if (R0) a.inv[pix] = (unsigned short)(key >> kKeyShift);
+        if (R0) a.inv[pix] = (unsigned short)kv;
       } else if (R0) {
         a.Bg[pix] = b == kBlocked ? b : (b | kMarkBit);
       }
@@ -588,9 +600,9 @@ extern "C" int cpx_watershed_cells(cpx_ctx* ctx, const int32_t* nuclei_dev, cons
   }
   CPX_CHECK_HIP(hipMemsetAsync(a.last, 0xff, sizeof(int) * 2 * B, ctx->stream));
   CPX_CHECK_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (label_rounds + 1), ctx->stream));
-  // ~9 one-wave blocks per CU fit the LDS; each block schedules its tiles t = block + k * grid
+  // eight one-wave blocks per CU fit the LDS; each block schedules its tiles t = block + k * grid
   // (at most kThreads of them: the LDS list)
-  const int grid = std::max(std::min(total, ctx->n_cu * 9), cpx_div_up(total, kThreads));
+  const int grid = std::max(std::min(total, ctx->n_cu * 8), cpx_div_up(total, kThreads));
   // The expand footprint is read in every relax round; the label rounds then overwrite the
   // free pixels of cells / cyto (the footprint is no longer needed: blocked <=> B == kBlocked).
   for (int r = 0; r < relax_rounds; ++r)

@@ -7,6 +7,7 @@ import os
 
 import numpy as np
 import pandas as pd
+import pytest
 
 import cpu_pipeline
 from csv_tables import cpu_tables
@@ -14,12 +15,15 @@ from csv_tables import cpu_tables
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_config0_cpu_results_csv(tmp_path):
+@pytest.mark.parametrize("size", [416, pytest.param(2080, marks=pytest.mark.gpu)])
+def test_config0_cpu_results_csv(tmp_path, size):
+    """416^2 in the CPU suite; configs[0]'s own 2080^2 x 5ch FOV in the GPU suite (no GPU is used:
+    it runs there for the box's host cores, ~1 min)."""
     import torch
     from cpx.cpnet import build_cpnet
     from cpx.synth import synth_fovs, synth_illum
-    torch.set_num_threads(4)
-    H = W = 416
+    torch.set_num_threads(4 if size < 1000 else 16)
+    H = W = size
     C = 5
     raw = synth_fovs(1, C, H, W, "cpu", seed=21).numpy().view(np.uint16).reshape(C, H, W)
     illum = synth_illum(C, H, W, seed=1)

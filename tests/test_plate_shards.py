@@ -2,7 +2,9 @@
 per-rank parquet parts, merge into CSVs sorted by (ImageNumber, ObjectNumber) — byte-identical
 to one process.  CPU: world-2 gloo ranks with a stub measurement; GPU: two real pipeline
 processes on the one GPU vs one process."""
+import argparse
 import filecmp
+import json
 import os
 import socket
 
@@ -127,3 +129,34 @@ def test_launch_two_processes_one_gpu_byte_identical(tmp_path, dev):
     assert st.loc[st.ImageNumber == 4, "status"].item() == "empty"
     for name in ("Image", *OBJECT_TABLES, "site_status"):
         assert filecmp.cmp(os.path.join(d1, f"{name}.csv"), os.path.join(d2, f"{name}.csv"), shallow=False), name
+
+
+def _claimer(qdir, n_batches, out_path, delay):
+    import time as _t
+    a = argparse.Namespace(queue=qdir, world=3, rank=0, batch=4)
+    table = pd.DataFrame({"x": range(4 * n_batches - 1)})  # last batch short
+    got = []
+    for rows in plate.batch_source(table, a, 0):
+        got.append(rows)
+        _t.sleep(delay)
+    with open(out_path, "w") as f:
+        json.dump(got, f)
+
+
+def test_work_queue_claims_every_batch_once(tmp_path):
+    """Three processes drain one job's WorkQueue: every batch (4 consecutive rows, the last one
+    short) is claimed by exactly one of them, and the slow claimer takes fewer."""
+    ctx = mp.get_context("spawn")
+    n = 23
+    outs = [str(tmp_path / f"r{r}.json") for r in range(3)]
+    procs = [ctx.Process(target=_claimer, args=(str(tmp_path / "q"), n, outs[r], d))
+             for r, d in enumerate((0.002, 0.002, 0.05))]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    claimed = [json.load(open(o)) for o in outs]
+    flat = sorted((b for c in claimed for b in c), key=lambda b: b[0])
+    assert flat == [list(range(4 * k, min(4 * n - 1, 4 * k + 4))) for k in range(n)]
+    assert len(claimed[2]) < len(claimed[0]) + len(claimed[1])

@@ -11,6 +11,7 @@ PREC=${PREC:-f16x3}  # bench.py's default --cpnet-precision
 mkdir -p $O
 cd $R
 timeout -k 10 420 python -u bench.py > $O/bench_default.log 2>&1
+timeout -k 10 200 python -u tools/flow_error_flops.py > $O/flow_error_flops.json 2> $O/flow_error_flops.log
 cd /tmp && export TMPDIR=/tmp
 cd $R
 # per-kernel durations: one pipeline (steps run back to back, as the bench's instrumented
