@@ -824,6 +824,31 @@ __global__ __launch_bounds__(kT) void k_apply_newlab(int Dy, int Dx, DynBufs d) 
 // consecutive column pairs).
 // Sums keep the reference's term order; rows are computed unconditionally (compile-time loop)
 // and only mask cells are written.
+// The two cells of a column pair (X, X + 1) from the 3 x 4 window (rows u, c, d; words a =
+// columns X - 1, X and b = X + 1, X + 2): the reference's 9-term sums in its own order, the two
+// dependent fp64 chains interleaved so each wave has two additions in flight (the adds of one
+// chain wait on each other's results)
+__device__ __forceinline__ void fe_pair(const double2& ua, const double2& ub, const double2& ca, const double2& cb,
+                                        const double2& da, const double2& db, double& n0, double& n1) {
+  double s0 = ca.y + ua.y, s1 = cb.x + ub.x;
+  s0 = s0 + da.y;
+  s1 = s1 + db.x;
+  s0 = s0 + ca.x;
+  s1 = s1 + ca.y;
+  s0 = s0 + cb.x;
+  s1 = s1 + cb.y;
+  s0 = s0 + ua.x;
+  s1 = s1 + ua.y;
+  s0 = s0 + ub.x;
+  s1 = s1 + ub.y;
+  s0 = s0 + da.x;
+  s1 = s1 + da.y;
+  s0 = s0 + db.x;
+  s1 = s1 + db.y;
+  n0 = 1 / 9. * s0;  // column X: c + u + d + l + r + ul + ur + dl + dr
+  n1 = 1 / 9. * s1;  // column X + 1
+}
+
 constexpr int kFeKS = 12;
 static_assert(kFeKS <= 32, "unit mask bits");
 
@@ -1013,8 +1038,7 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
               nb = T2[r + 1];
             }
             // column X: l = .x of a, c = .y of a, r = .x of b;  column X + 1: l = a.y, c = b.x, r = b.y
-            nv[i][0][j] = 1 / 9. * (ca.y + ua.y + da.y + ca.x + cb.x + ua.x + ub.x + da.x + db.x);
-            nv[i][1][j] = 1 / 9. * (cb.x + ub.x + db.x + ca.y + cb.y + ua.y + ub.y + da.y + db.y);
+            fe_pair(ua, ub, ca, cb, da, db, nv[i][0][j], nv[i][1][j]);
             ua = ca; ub = cb;
             ca = da; cb = db;
             da = na; db = nb;
@@ -1259,8 +1283,7 @@ __global__ __launch_bounds__(THREADS, 1) void k_flow_error_cmp(
             double2 na = z2, nb2 = z2;
             if (j + 1 < R) ldrow(min(Y0[i] + j + 2, bh + 1), pa, na, nb2);
             // column X: l = a.x, c = a.y, r = b.x;  column X + 1: l = a.y, c = b.x, r = b.y
-            nv[i][0][j] = 1 / 9. * (ca.y + ua.y + da.y + ca.x + cb.x + ua.x + ub.x + da.x + db.x);
-            nv[i][1][j] = 1 / 9. * (cb.x + ub.x + db.x + ca.y + cb.y + ua.y + ub.y + da.y + db.y);
+            fe_pair(ua, ub, ca, cb, da, db, nv[i][0][j], nv[i][1][j]);
             ua = ca; ub = cb;
             ca = da; cb = db;
             da = na; db = nb2;
