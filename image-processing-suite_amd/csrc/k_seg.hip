@@ -11,6 +11,8 @@
 #include "cpx_internal.h"
 #include <limits.h>
 #include <math.h>
+#include <stdio.h>
+#include <type_traits>
 #include <vector>
 
 #pragma clang fp contract(off)
@@ -828,9 +830,10 @@ __global__ __launch_bounds__(kT) void k_apply_newlab(int Dy, int Dx, DynBufs d) 
 // columns X - 1, X and b = X + 1, X + 2): the reference's 9-term sums in its own order, the two
 // dependent fp64 chains interleaved so each wave has two additions in flight (the adds of one
 // chain wait on each other's results)
-__device__ __forceinline__ void fe_pair(const double2& ua, const double2& ub, const double2& ca, const double2& cb,
-                                        const double2& da, const double2& db, double& n0, double& n1) {
-  double s0 = ca.y + ua.y, s1 = cb.x + ub.x;
+template <typename E, typename E2>
+__device__ __forceinline__ void fe_pair(const E2& ua, const E2& ub, const E2& ca, const E2& cb, const E2& da,
+                                        const E2& db, E& n0, E& n1) {
+  E s0 = ca.y + ua.y, s1 = cb.x + ub.x;
   s0 = s0 + da.y;
   s1 = s1 + db.x;
   s0 = s0 + ca.x;
@@ -845,8 +848,8 @@ __device__ __forceinline__ void fe_pair(const double2& ua, const double2& ub, co
   s1 = s1 + da.y;
   s0 = s0 + db.x;
   s1 = s1 + db.y;
-  n0 = 1 / 9. * s0;  // column X: c + u + d + l + r + ul + ur + dl + dr
-  n1 = 1 / 9. * s1;  // column X + 1
+  n0 = (E)(1 / 9.) * s0;  // column X: c + u + d + l + r + ul + ur + dl + dr
+  n1 = (E)(1 / 9.) * s1;  // column X + 1
 }
 
 constexpr int kFeKS = 12;
@@ -873,18 +876,32 @@ __global__ void k_obj_prefix(int B, const cpx_fov_objects* __restrict__ hdr, int
   }
 }
 
-template <int THREADS, int CELLS, int U>
-__global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per SIMD: <= 128 VGPRs
+// E = double: the reference's arithmetic, the decision err > thr.  E = float (screening pass):
+// the same sweeps in fp32 — half the LDS per mask, so twice the masks in flight per CU — and a
+// decision only where it is certain: every operation of a sweep adds non-negative terms, so
+// each fp32 cell stays within a relative (1 + 11u)^niter of the exact value (u = 2^-24; plus an
+// absolute n 2^-126 for underflow), and so does the fp64 reference (u = 2^-53); from that bound
+// on both grids every pixel's normalised gradient gets a bound on its error contribution (a
+// pixel whose gradient is not clearly above its own uncertainty counts its whole range
+// (1 + |dP/5|)^2).  A mask whose fp32 error is further from thr than the summed bound gets its
+// flag (1 bad, 2 kept) — the same flag the fp64 sweeps give it; any other mask is flagged 3 and
+// appended to `und` ([0] = count, then fov << 20 | object), which the fp64 pass (list = und)
+// then decides exactly.
+template <int THREADS, int CELLS, int U, typename E = double, int WPE = 4>
+__global__ __launch_bounds__(THREADS, WPE) void k_flow_error_lds(  // WPE waves per SIMD: <= 512 / WPE VGPRs
     const int* __restrict__ m0, const float2* __restrict__ dpf, int Dy, int Dx, int B, int max_label,
     const cpx_object* __restrict__ objects, const int* __restrict__ off, int* __restrict__ ctr,
-    int lo_threads, int lo_units, int lo_cells, double thr, unsigned char* __restrict__ bad) {
-  __shared__ __attribute__((aligned(16))) double T[CELLS];
-  __shared__ double sred[THREADS / 64][2];
+    int lo_threads, int lo_units, int lo_cells, double thr, unsigned char* __restrict__ bad,
+    const int* __restrict__ list, int* __restrict__ und) {
+  constexpr bool kScreen = std::is_same<E, float>::value;
+  typedef typename std::conditional<kScreen, float2, double2>::type E2;
+  __shared__ __attribute__((aligned(16))) E T[CELLS];
+  __shared__ double sred[THREADS / 64][3];
   __shared__ unsigned long long sbest[THREADS / 64];
   __shared__ double smed[2];
   __shared__ int sitem;
   const long long n = (long long)Dy * Dx;
-  const int total = off[B];
+  const int total = list ? list[0] : off[B];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   while (true) {
     if (tid == 0) sitem = atomicAdd(ctr, 1);
@@ -892,9 +909,15 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
     const int item = sitem;
     __syncthreads();
     if (item >= total) break;
-    int fov = 0;
-    while (fov + 1 < B && off[fov + 1] <= item) ++fov;
-    const int kobj = item - off[fov];
+    int fov = 0, kobj;
+    if (list) {  // the screening pass's undecided masks
+      const int code = list[1 + item];
+      fov = code >> 20;
+      kobj = code & 0xfffff;
+    } else {
+      while (fov + 1 < B && off[fov + 1] <= item) ++fov;
+      kobj = item - off[fov];
+    }
     const cpx_object o = objects[(long long)fov * max_label + kobj];
     const int L = o.label;
     const int r0 = o.bbox[0], c0 = o.bbox[1];
@@ -996,23 +1019,23 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
     for (int i = 0; i < U; ++i)
       ud[i] = max(max(max(0, uy0[i] - ym), ym - (uy0[i] + R - 1)), max(max(0, ux[i] - xm), xm - (ux[i] + 1)));
     __syncthreads();  // rowc / colc / sbest reads done before T is cleared
-    for (int i = tid; i < ly * lxp; i += THREADS) T[i] = 0.0;
+    for (int i = tid; i < ly * lxp; i += THREADS) T[i] = (E)0;
     __syncthreads();
-    if (tid == 0 && niter > 0) T[ym * lxp + xm] = 1.0;  // the first iteration's T[centre] += 1
+    if (tid == 0 && niter > 0) T[ym * lxp + xm] = (E)1;  // the first iteration's T[centre] += 1
     __syncthreads();
-    double nv[U][2][kFeKS];
+    E nv[U][2][kFeKS];
     const int cidx = ym * lxp + xm;
     bool cown = false;  // this thread owns the centre cell
 #pragma unroll
     for (int i = 0; i < U; ++i)
       if (ujc[i] >= 0) cown = true;
-    const double2* T2 = reinterpret_cast<const double2*>(T);
+    const E2* T2 = reinterpret_cast<const E2*>(T);
     for (int it = 0; it < niter; ++it) {
 #pragma unroll
       for (int i = 0; i < U; ++i) {
         if (!(um[i][0] | um[i][1]) || ud[i] > it + 1) continue;  // no mask cell (or no unit), or
                                                                   // beyond the support
-        // double2 offsets of the unit's rows (columns X - 1 .. X + 2 = two 16-byte words); the
+        // E2 offsets of the unit's rows (columns X - 1 .. X + 2 = two 16-byte words); the
         // opaque base keeps the compiler from holding every row address across the loop, and
         // rows past the object's last row read the zero border row (clamped): their sums are
         // never written
@@ -1020,25 +1043,25 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
         int rmax = ((ly - 1) * lxp + ux[i] - 1) >> 1;
         const int rs = lxp >> 1;
         asm volatile("" : "+v"(r), "+v"(rmax));
-        double2 ua = T2[r], ub = T2[r + 1];
+        E2 ua = T2[r], ub = T2[r + 1];
         r += rs;
-        double2 ca = T2[r], cb = T2[r + 1];
+        E2 ca = T2[r], cb = T2[r + 1];
         r = min(r + rs, rmax);
-        double2 da = T2[r], db = T2[r + 1];
+        E2 da = T2[r], db = T2[r + 1];
 #pragma unroll
         for (int j = 0; j < kFeKS; ++j) {
           // rows beyond R: predicated off (block-uniform), the loop stays unrolled so nv stays in
           // registers.  The next row's loads are issued before this row's sums (latency hidden);
           // the scheduling barrier keeps the compiler from hoisting more rows (register budget)
           if (j < R) {
-            double2 na = {0.0, 0.0}, nb = {0.0, 0.0};
+            E2 na = {(E)0, (E)0}, nb = {(E)0, (E)0};
             if (j + 1 < R) {
               r = min(r + rs, rmax);
               na = T2[r];
               nb = T2[r + 1];
             }
             // column X: l = .x of a, c = .y of a, r = .x of b;  column X + 1: l = a.y, c = b.x, r = b.y
-            fe_pair(ua, ub, ca, cb, da, db, nv[i][0][j], nv[i][1][j]);
+            fe_pair<E, E2>(ua, ub, ca, cb, da, db, nv[i][0][j], nv[i][1][j]);
             ua = ca; ub = cb;
             ca = da; cb = db;
             da = na; db = nb;
@@ -1059,12 +1082,20 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
         }
       }
       // the next iteration's T[centre] += 1, by the centre's owner after its own store
-      if (cown && it + 1 < niter) T[cidx] = T[cidx] + 1.0;
+      if (cown && it + 1 < niter) T[cidx] = T[cidx] + (E)1;
       __syncthreads();
     }
     // ---- gradients, normalisation, error vs dP/5
     const float2* F = dpf + (long long)fov * n;
-    double e0 = 0.0, e1 = 0.0;
+    // screening: relative bound rho on |T32 - T64| per cell (both vs the exact sweeps, see above)
+    // and the absolute underflow allowance alpha
+    double rho = 0.0, alpha = 0.0;
+    if constexpr (kScreen) {
+      const double g32 = 11.0 * 0x1p-24 * (1.0 + 1e-6), g64 = 11.0 * 0x1p-53 * (1.0 + 1e-6);
+      rho = (expm1((double)niter * g32) + expm1((double)niter * g64)) / (1.0 - (double)niter * g32);
+      alpha = 4.0 * (double)niter * 0x1p-126;
+    }
+    double e0 = 0.0, e1 = 0.0, eb = 0.0;
 #pragma unroll
     for (int i = 0; i < U; ++i) {
 #pragma unroll
@@ -1072,33 +1103,59 @@ __global__ __launch_bounds__(THREADS, 4) void k_flow_error_lds(  // 4 waves per 
         for (int j = 0; j < kFeKS; ++j) {
           if (!((um[i][h] >> j) & 1u)) continue;
           const int Y = uy0[i] + j, X = ux[i] + h;
-          const double dy = T[(Y + 1) * lxp + X] - T[(Y - 1) * lxp + X];
-          const double dx = T[Y * lxp + X + 1] - T[Y * lxp + X - 1];
-          const double nrm = 1e-20 + sqrt(dy * dy + dx * dx);
+          const double tdn = (double)T[(Y + 1) * lxp + X], tup = (double)T[(Y - 1) * lxp + X];
+          const double trt = (double)T[Y * lxp + X + 1], tlf = (double)T[Y * lxp + X - 1];
+          const double dy = tdn - tup;
+          const double dx = trt - tlf;
+          const double g = sqrt(dy * dy + dx * dx);
+          const double nrm = 1e-20 + g;
           const double my = dy / nrm, mx = dx / nrm;
           const float2 f = F[(long long)(r0 + Y - 1) * Dx + c0 + X - 1];
-          const double ty = my - (double)(f.x / 5.0f);
-          const double tx = mx - (double)(f.y / 5.0f);
+          const double fy = (double)(f.x / 5.0f), fx = (double)(f.y / 5.0f);
+          const double ty = my - fy;
+          const double tx = mx - fx;
           e0 += ty * ty;
           e1 += tx * tx;
+          if constexpr (kScreen) {
+            // |grad32 - grad64| <= D; unit vectors then differ by <= 2 D / |grad32| (+ the 1e-20)
+            const double Dy_ = rho * (tdn + tup) + 2.0 * alpha, Dx_ = rho * (trt + tlf) + 2.0 * alpha;
+            const double D = sqrt(Dy_ * Dy_ + Dx_ * Dx_) * (1.0 + 1e-9);
+            const double ff = sqrt(fy * fy + fx * fx);
+            if (g > 3.0 * D && g > 1e-12) {
+              const double ep = 2.0 * D / g + 1e-7;
+              eb += ep * (2.0 * sqrt(ty * ty + tx * tx) + ep);
+            } else {
+              eb += (1.0 + ff) * (1.0 + ff);
+            }
+          }
         }
       }
     }
     e0 = wave_sum(e0);
     e1 = wave_sum(e1);
+    if constexpr (kScreen) eb = wave_sum(eb);
     if (lane == 0) {
       sred[wid][0] = e0;
       sred[wid][1] = e1;
+      sred[wid][2] = eb;
     }
     __syncthreads();
     if (tid == 0) {
-      double s0 = 0.0, s1 = 0.0;
+      double s0 = 0.0, s1 = 0.0, sb = 0.0;
       for (int w = 0; w < THREADS / 64; ++w) {
         s0 += sred[w][0];
         s1 += sred[w][1];
+        sb += sred[w][2];
       }
       const double err = 0.0 + s0 / (double)o.area + s1 / (double)o.area;
-      bad[(long long)fov * (max_label + 1) + L] = err > thr ? 1 : 2;
+      unsigned char v = err > thr ? 1 : 2;
+      if constexpr (kScreen) {
+        // + the two fp64 error sums' own rounding (orders differ) with a wide margin
+        const double bnd = sb / (double)o.area + 1e-9 * (1.0 + err);
+        v = err - thr > bnd ? 1 : thr - err > bnd ? 2 : 3;
+        if (v == 3) und[1 + atomicAdd(&und[0], 1)] = (fov << 20) | kobj;
+      }
+      bad[(long long)fov * (max_label + 1) + L] = v;
     }
     __syncthreads();
   }
@@ -1283,7 +1340,7 @@ __global__ __launch_bounds__(THREADS, 1) void k_flow_error_cmp(
             double2 na = z2, nb2 = z2;
             if (j + 1 < R) ldrow(min(Y0[i] + j + 2, bh + 1), pa, na, nb2);
             // column X: l = a.x, c = a.y, r = b.x;  column X + 1: l = a.y, c = b.x, r = b.y
-            fe_pair(ua, ub, ca, cb, da, db, nv[i][0][j], nv[i][1][j]);
+            fe_pair<double, double2>(ua, ub, ca, cb, da, db, nv[i][0][j], nv[i][1][j]);
             ua = ca; ub = cb;
             ca = da; cb = db;
             da = na; db = nb2;
@@ -2127,11 +2184,12 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   const size_t sz_l2i = al(sizeof(int) * (size_t)B * (ML + 1));
   const size_t sz_abs = al(sizeof(int) * (size_t)B * ML);
   const size_t sz_nl = sz_abs;
-  const size_t sz_off = al(sizeof(int) * (size_t)(B + 1 + 5));  // prefix + 5 queue counters
+  const size_t sz_off = al(sizeof(int) * (size_t)(B + 1 + 8));  // prefix + 8 queue counters
+  const size_t sz_und = al(sizeof(int) * ((size_t)B * ML + 1));  // screening: undecided masks
   const size_t gscr_per = (size_t)2 * (Dy + 2) * (Dx + 2);  // doubles per FOV (oversize masks)
   const size_t sz_gscr = al(sizeof(double) * B * gscr_per);
   unsigned char* o = (unsigned char*)cpx_ws(ctx, WS_SEG_OBJ,
-      sz_lst + sz_obj + sz_hdr + sz_bad + sz_l2i + sz_abs + sz_nl + sz_off + sz_gscr);
+      sz_lst + sz_obj + sz_hdr + sz_bad + sz_l2i + sz_abs + sz_nl + sz_off + sz_und + sz_gscr);
   if (!o) return CPX_ERR_OOM;
   cpx_label_stats* lst = (cpx_label_stats*)o; o += sz_lst;
   cpx_object* obj = (cpx_object*)o; o += sz_obj;
@@ -2141,26 +2199,53 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   int* absorber = (int*)o; o += sz_abs;
   int* newlab = (int*)o; o += sz_nl;
   int* off = (int*)o; o += sz_off;
+  int* und = (int*)o; o += sz_und;
   double* gscr = (double*)o;
   if (flow_threshold > 0.0) {
     rc = cpx_objects(ctx, d.m0, B, Dy, Dx, ML, 0, lst, obj, hdr);
     if (rc) return rc;
     CPX_CHECK_HIP(hipMemsetAsync(bad, 0, sz_bad, ctx->stream));
-    CPX_CHECK_HIP(hipMemsetAsync(off + B + 1, 0, 5 * sizeof(int), ctx->stream));
+    CPX_CHECK_HIP(hipMemsetAsync(off + B + 1, 0, 8 * sizeof(int), ctx->stream));
+    CPX_CHECK_HIP(hipMemsetAsync(und, 0, sizeof(int), ctx->stream));
     hipLaunchKernelGGL(k_obj_prefix, dim3(1), dim3(64), 0, ctx->stream, B,
                        (const cpx_fov_objects*)hdr, off);
+    // fp32 screening of every mask the LDS kernels hold (half the LDS: twice the masks per CU),
+    // then the fp64 sweeps for the masks it could not decide
+    static const bool screen = !getenv("CPX_FE_NOSCREEN");
+    const int* lst_in = nullptr;
+    if (screen && B < 2048 && ML <= (1 << 20)) {  // list codes: fov << 20 | object
+#define FE_SCREEN(TH, CE, U_, WPE, G, CTR, LT, LU, LC)                                                  \
+  hipLaunchKernelGGL((k_flow_error_lds<TH, CE, U_, float, WPE>), dim3((G) * ctx->n_cu), dim3(TH), 0,    \
+                     ctx->stream, (const int*)d.m0, (const float2*)d.dpf, Dy, Dx, B, ML,             \
+                     (const cpx_object*)obj, (const int*)off, off + B + (CTR), LT, LU, LC, flow_threshold, \
+                     bad, (const int*)nullptr, und)
+      // six waves per SIMD for the small and mid classes; the large class as 512 threads with two
+      // units each (the same masks as the fp64 1024 x 1 kernel), two 79 KiB blocks per CU
+      FE_SCREEN(kFeSmallThreads, kFeSmallCells, kFeU, 6, 6, 6, 0, 0, 0);
+      FE_SCREEN(kFeMidThreads, kFeMidCells, kFeU, 6, 3, 7, kFeSmallThreads, kFeU, kFeSmallCells);
+      FE_SCREEN(kFeLargeThreads / 2, kFeLargeCells, 2 * kFeU, 4, 2, 8, kFeMidThreads, kFeU, kFeMidCells);
+#undef FE_SCREEN
+      lst_in = und;
+      if (getenv("CPX_FE_DEBUG")) {  // profiling aid: masks the screening left undecided
+        int nu = 0, nm = 0;
+        CPX_CHECK_HIP(hipMemcpyAsync(&nu, und, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        CPX_CHECK_HIP(hipMemcpyAsync(&nm, off + B, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        CPX_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        fprintf(stderr, "flow error: %d of %d masks undecided by the fp32 screening\n", nu, nm);
+      }
+    }
     hipLaunchKernelGGL((k_flow_error_lds<kFeSmallThreads, kFeSmallCells, kFeU>), dim3(4 * ctx->n_cu),
                        dim3(kFeSmallThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
                        Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 1, 0, 0, 0,
-                       flow_threshold, bad);
+                       flow_threshold, bad, lst_in, (int*)nullptr);
     hipLaunchKernelGGL((k_flow_error_lds<kFeMidThreads, kFeMidCells, kFeU>), dim3(2 * ctx->n_cu),
                        dim3(kFeMidThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
                        Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 2,
-                       kFeSmallThreads, kFeU, kFeSmallCells, flow_threshold, bad);
+                       kFeSmallThreads, kFeU, kFeSmallCells, flow_threshold, bad, lst_in, (int*)nullptr);
     hipLaunchKernelGGL((k_flow_error_lds<kFeLargeThreads, kFeLargeCells, kFeU>), dim3(ctx->n_cu),
                        dim3(kFeLargeThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
                        Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 3,
-                       kFeMidThreads, kFeU, kFeMidCells, flow_threshold, bad);
+                       kFeMidThreads, kFeU, kFeMidCells, flow_threshold, bad, lst_in, (int*)nullptr);
     hipLaunchKernelGGL((k_flow_error_cmp<kFeCmpThreads, kFeCmpCells, kFeCmpU>), dim3(ctx->n_cu),
                        dim3(kFeCmpThreads), 0, ctx->stream, (const int*)d.m0, (const float2*)d.dpf,
                        Dy, Dx, B, ML, (const cpx_object*)obj, (const int*)off, off + B + 4,

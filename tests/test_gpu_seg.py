@@ -161,6 +161,39 @@ def test_flow_error_threshold_all_mask_sizes(dev):
     assert st["n_bad_flow"].sum() >= 2 and st["n_final"].sum() >= 4, st
 
 
+def test_flow_error_screening_defers_near_threshold(dev):
+    """The fp32 screening pass decides a mask only when its error is certified to lie on one side
+    of the threshold; with thresholds placed 1e-7 either side of the fp64 errors of masks of
+    three sizes (smallest, median, largest), those masks must be deferred to the fp64 sweeps and
+    the labels stay bit-identical to the oracle on both sides."""
+    H, W = 1400, 1400
+    g = make_geom(H, W)
+    lab = sg.labels(7, g.Ly, g.Lx, n=14, rmin=6, rmax=24, skip_every=0)
+    mu = so.masks_to_flows(lab)
+    rng = np.random.default_rng(7)
+    yf = np.zeros((3, g.Ly, g.Lx), np.float32)
+    yf[0] = 5.0 * mu[0] * 0.37 + 0.02 * rng.standard_normal((g.Ly, g.Lx))
+    yf[1] = 5.0 * mu[1] * 0.37 + 0.02 * rng.standard_normal((g.Ly, g.Lx))
+    yf[2] = np.where(lab > 0, 3.0, -3.0)
+    # the oracle's masks before the filter and their fp64 flow errors
+    f = so.upsample_flows(yf, H, W)
+    p, _ = so.follow_flows(f[:2], f[2] > so.CELLPROB_THRESHOLD, so.default_niter())
+    m = so.get_masks(p, f[2] > so.CELLPROB_THRESHOLD)
+    err = so.flow_errors(m, f[:2])
+    area = np.bincount(m.ravel(), minlength=len(err) + 1)[1:]
+    order = np.argsort(area)
+    picks = [order[0], order[len(order) // 2], order[-1]]
+    removed_somewhere = False
+    for k in picks:
+        for d in (-1e-7, 1e-7):
+            thr = float(err[k] + d)
+            got, st = _gpu_masks(dev, yf[None], g, H, W, flow_threshold=thr)
+            ref = so.compute_masks(yf, H, W, flow_threshold=thr)
+            np.testing.assert_array_equal(got[0], ref, err_msg=f"mask {k + 1} threshold {thr}")
+            removed_somewhere |= d < 0
+    assert removed_somewhere and len(err) >= 6
+
+
 def test_masks_network_resolution_bit_exact_vs_oracle(dev):
     """resample=False (named option): dynamics at network size (200 steps), nearest resize."""
     H, W = 700, 760
