@@ -28,6 +28,7 @@
 // (fp32), all on the fp32 values; output tiles go through LDS as whole 16-byte chunks.
 #include "cpx_internal.h"
 #include <type_traits>
+#include <stdlib.h>
 
 namespace {
 
@@ -106,171 +107,20 @@ struct X3Epi {
   int in_up;  // the input is the (H/2) x (W/2) tensor read 2x nearest-upsampled
 };
 
-template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE)))
-void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, int N, int H,
-               int W, int tiles_x, int tiles_y) {
-  constexpr int NT = 512, NWV = NT / 64;
-  constexpr int T = KS * KS, HALO = KS / 2;
-  constexpr int MWV = BM / (32 * WM), PW = NWV / MWV;
-  constexpr int HY = TY + KS - 1, HX = TX + KS - 1, NPIX = HY * HX;
-  constexpr int NCH = CIN / 16;
-  constexpr int P = TY * TX, NS = (P + 31) / 32;
-  constexpr int SW = T * BM * 4;                      // 16-byte slots [tap][BM][4 chunks]
-  constexpr int SI = (NPIX * 4 + 63) / 64 * 64;       // [halo pixel][4 chunks]
-  constexpr int SB = SW + SI;
-  constexpr int NWW = SW / 64, NWIN = SI / 64;
-  constexpr int JW = (NWW + NWV - 1) / NWV, JI = (NWIN + NWV - 1) / NWV;
-  constexpr int QB = BM / 4;                          // output chunks per pixel (hi + lo)
-  constexpr int QC = COUT / 4;                        // chunks per pixel of a COUT tensor
-  constexpr int QI = CIN / 4;
+// Epilogue of a 3x3 / 1x1 convolution tile on its fp32 values (acc0 = the joined sums): bias,
+// residual, residual-stream store, style, eval BatchNorm, ReLU, next-input store or output head.
+// Every thread of the block takes part (the output tile is staged through smem); waves without a
+// subtile (j >= nsub) only move data.
+template <int COUT, int BM, int TY, int TX, int WM, int WN>
+__device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi& ep, uint4* smem, int n,
+                                            int nb, int ty0, int tx0, int H, int W, int mw, int pg, int nsub) {
+  constexpr int NT = 512;
+  constexpr int P = TY * TX;
+  constexpr int QB = BM / 4;
+  constexpr int QC = COUT / 4;
   constexpr int OUT_R = (P * QB + NT - 1) / NT;
-  static_assert(CIN % 16 == 0 && COUT % BM == 0 && BM % (32 * WM) == 0 && NWV % MWV == 0, "shape");
-  static_assert(PW * WN >= NS, "every subtile needs a wave");
-  static_assert(SW % 64 == 0, "weight DMA rows");
-  static_assert(P * QB <= 2 * SB, "output tile must fit the staging LDS");
-  static_assert(2 * SB * 16 <= 163840, "LDS");
-  __shared__ uint4 smem[2 * SB];
-
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int mw = wid % MWV, pg = wid / MWV;
+  const int lane = threadIdx.x & 63;
   const int h = lane >> 5, l32 = lane & 31;
-  const int tiles = tiles_x * tiles_y;
-  // XCD-aware order: the hardware deals consecutive block ids round-robin over the 8 XCDs, so
-  // block b runs on XCD b % 8; give each XCD a contiguous run of items instead.  An item is
-  // (tile, output-channel block nb) with nb fastest, so the COUT / BM blocks of one tile run
-  // together on one XCD and read its input halo once from HBM (the rest from that XCD's L2), and
-  // vertically adjacent tiles (which share halo rows) meet in the same L2
-  constexpr int NB = COUT / BM;
-  const int G = gridDim.x, xq = G >> 3, xr = G & 7, xb = blockIdx.x & 7;
-  const int bid = xb * xq + min(xb, xr) + (blockIdx.x >> 3);
-  const int tile = bid / NB, nb = bid - tile * NB;
-  const int n = tile / tiles;
-  const int t = tile - n * tiles;
-  const int ty0 = (t / tiles_x) * TY, tx0 = (t % tiles_x) * TX;
-  // in_up: the source pixel of (gy, gx) is (gy / 2, gx / 2) of the half-size input (nearest 2x
-  // upsampling folded into the halo DMA; the L2 serves each source line to four output pixels)
-  const int iu = ep.in_up, Wi = W >> iu;
-  const uint4* inb = in + (long long)n * (H >> iu) * Wi * QI;
-
-  // DMA sources: weights (lane-constant swizzle), halo chunk offsets (slab-independent)
-  const int fW = (lane & ~3) | ((lane & 3) ^ ((lane >> 4) & 3));
-  int inOff[JI];
-#pragma unroll
-  for (int jj = 0; jj < JI; ++jj) {
-    const int si = (wid + NWV * jj) * 64 + lane;
-    const int hp = si >> 2, cq = si & 3;
-    const int hy = hp / HX, hx = hp - (hp / HX) * HX;
-    const int gy = ty0 + hy - HALO, gx = tx0 + hx - HALO;
-    inOff[jj] = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-                    ? ((gy >> iu) * Wi + (gx >> iu)) * QI + (cq ^ swz4(hp)) : -1;
-  }
-  auto issue = [&](int ch, int buf) {
-    const uint4* wsl = wpk + (long long)(nb * NCH + ch) * SW;
-    uint4* dst = smem + buf * SB;
-#pragma unroll
-    for (int jj = 0; jj < JW; ++jj) {
-      const int j = wid + NWV * jj;
-      if (j < NWW)
-        __builtin_amdgcn_global_load_lds((glb_void_t*)(wsl + j * 64 + fW), (lds_void_t*)(dst + j * 64), 16, 0, 0);
-    }
-#pragma unroll
-    for (int jj = 0; jj < JI; ++jj) {
-      const int j = wid + NWV * jj;
-      if (j < NWIN) {
-        const uint4* src = inOff[jj] >= 0 ? inb + inOff[jj] + ch * 4 : &g_x3_zero16;
-        __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(dst + SW + j * 64), 16, 0, 0);
-      }
-    }
-  };
-
-  f32x16 acc0[WM][WN], acc1[WM][WN];
-#pragma unroll
-  for (int m = 0; m < WM; ++m)
-#pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc0[m][j][r] = 0.0f;
-        acc1[m][j][r] = 0.0f;
-      }
-
-  const int nsub = max(0, min(WN, NS - pg * WN));
-  int aS[WM];
-#pragma unroll
-  for (int m = 0; m < WM; ++m) {
-    const int r = (mw * WM + m) * 32 + l32;
-    aS[m] = r * 4 + (h ^ swz4(r));
-  }
-  int hp0[WN];
-#pragma unroll
-  for (int j = 0; j < WN; ++j) {
-    const int px = min((pg * WN + j) * 32 + l32, P - 1);
-    hp0[j] = (px / TX) * HX + (px % TX);
-  }
-
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int ch = 0; ch < NCH; ++ch) {
-    if (ch + 1 < NCH) issue(ch + 1, (ch + 1) & 1);
-    const uint4* sb = smem + (ch & 1) * SB;
-    auto mma = [&](auto cnt) {
-      constexpr int C = decltype(cnt)::value;
-      if constexpr (C > 0) {
-        auto tapbody = [&](int tap) {
-          const int ky = tap / KS, kx = tap - KS * (tap / KS);
-          f16x8 ah[WM], al[WM];
-#pragma unroll
-          for (int m = 0; m < WM; ++m) {
-            ah[m] = __builtin_bit_cast(f16x8, sb[aS[m] + tap * BM * 4]);
-            al[m] = __builtin_bit_cast(f16x8, sb[(aS[m] ^ 2) + tap * BM * 4]);
-          }
-#pragma unroll
-          for (int j = 0; j < C; ++j) {
-            const int hp = hp0[j] + ky * HX + kx;
-            const int bs = SW + hp * 4 + (h ^ swz4(hp));
-            const f16x8 bh = __builtin_bit_cast(f16x8, sb[bs]);
-            const f16x8 bl = __builtin_bit_cast(f16x8, sb[bs ^ 2]);
-#pragma unroll
-            for (int m = 0; m < WM; ++m) {
-              acc0[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh, acc0[m][j], 0, 0, 0);
-              acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bl, acc1[m][j], 0, 0, 0);
-              acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bh, acc1[m][j], 0, 0, 0);
-            }
-          }
-        };
-        // single-fragment waves: all taps unrolled, the next tap's reads scheduled under this
-        // tap's MFMAs; larger wave tiles keep one tap per iteration (register budget)
-        if constexpr (WM * WN == 1) {
-#pragma unroll
-          for (int tap = 0; tap < T; ++tap) tapbody(tap);
-        } else {
-#pragma unroll 1
-          for (int tap = 0; tap < T; ++tap) tapbody(tap);
-        }
-      }
-    };
-    if constexpr (WN == 1) {
-      if (nsub == 1) mma(std::integral_constant<int, 1>{});
-    } else if constexpr (WN == 2) {
-      if (nsub == 2) mma(std::integral_constant<int, 2>{});
-      else if (nsub == 1) mma(std::integral_constant<int, 1>{});
-    } else {
-      static_assert(WN <= 2, "WN");
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  // ---- epilogue on the fp32 values ----
-#pragma unroll
-  for (int m = 0; m < WM; ++m)
-#pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc0[m][j][r] += acc1[m][j][r] * kLoInv;  // exact product, one rounding
-
   bool bad = false;
   auto gpix = [&](int px) -> long long {
     const int gy = ty0 + px / TX, gx = tx0 + px % TX;
@@ -464,6 +314,280 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   flag();
 }
 
+template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, int N, int H,
+               int W, int tiles_x, int tiles_y) {
+  constexpr int NT = 512, NWV = NT / 64;
+  constexpr int T = KS * KS, HALO = KS / 2;
+  constexpr int MWV = BM / (32 * WM), PW = NWV / MWV;
+  constexpr int HY = TY + KS - 1, HX = TX + KS - 1, NPIX = HY * HX;
+  constexpr int NCH = CIN / 16;
+  constexpr int P = TY * TX, NS = (P + 31) / 32;
+  constexpr int SW = T * BM * 4;                      // 16-byte slots [tap][BM][4 chunks]
+  constexpr int SI = (NPIX * 4 + 63) / 64 * 64;       // [halo pixel][4 chunks]
+  constexpr int SB = SW + SI;
+  constexpr int NWW = SW / 64, NWIN = SI / 64;
+  constexpr int JW = (NWW + NWV - 1) / NWV, JI = (NWIN + NWV - 1) / NWV;
+  constexpr int QB = BM / 4;                          // output chunks per pixel (hi + lo)
+  constexpr int QC = COUT / 4;                        // chunks per pixel of a COUT tensor
+  constexpr int QI = CIN / 4;
+  constexpr int OUT_R = (P * QB + NT - 1) / NT;
+  static_assert(CIN % 16 == 0 && COUT % BM == 0 && BM % (32 * WM) == 0 && NWV % MWV == 0, "shape");
+  static_assert(PW * WN >= NS, "every subtile needs a wave");
+  static_assert(SW % 64 == 0, "weight DMA rows");
+  static_assert(P * QB <= 2 * SB, "output tile must fit the staging LDS");
+  static_assert(2 * SB * 16 <= 163840, "LDS");
+  __shared__ uint4 smem[2 * SB];
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int mw = wid % MWV, pg = wid / MWV;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int tiles = tiles_x * tiles_y;
+  // XCD-aware order: the hardware deals consecutive block ids round-robin over the 8 XCDs, so
+  // block b runs on XCD b % 8; give each XCD a contiguous run of items instead.  An item is
+  // (tile, output-channel block nb) with nb fastest, so the COUT / BM blocks of one tile run
+  // together on one XCD and read its input halo once from HBM (the rest from that XCD's L2), and
+  // vertically adjacent tiles (which share halo rows) meet in the same L2
+  constexpr int NB = COUT / BM;
+  const int G = gridDim.x, xq = G >> 3, xr = G & 7, xb = blockIdx.x & 7;
+  const int bid = xb * xq + min(xb, xr) + (blockIdx.x >> 3);
+  const int tile = bid / NB, nb = bid - tile * NB;
+  const int n = tile / tiles;
+  const int t = tile - n * tiles;
+  const int ty0 = (t / tiles_x) * TY, tx0 = (t % tiles_x) * TX;
+  // in_up: the source pixel of (gy, gx) is (gy / 2, gx / 2) of the half-size input (nearest 2x
+  // upsampling folded into the halo DMA; the L2 serves each source line to four output pixels)
+  const int iu = ep.in_up, Wi = W >> iu;
+  const uint4* inb = in + (long long)n * (H >> iu) * Wi * QI;
+
+  // DMA sources: weights (lane-constant swizzle), halo chunk offsets (slab-independent)
+  const int fW = (lane & ~3) | ((lane & 3) ^ ((lane >> 4) & 3));
+  int inOff[JI];
+#pragma unroll
+  for (int jj = 0; jj < JI; ++jj) {
+    const int si = (wid + NWV * jj) * 64 + lane;
+    const int hp = si >> 2, cq = si & 3;
+    const int hy = hp / HX, hx = hp - (hp / HX) * HX;
+    const int gy = ty0 + hy - HALO, gx = tx0 + hx - HALO;
+    inOff[jj] = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+                    ? ((gy >> iu) * Wi + (gx >> iu)) * QI + (cq ^ swz4(hp)) : -1;
+  }
+  auto issue = [&](int ch, int buf) {
+    const uint4* wsl = wpk + (long long)(nb * NCH + ch) * SW;
+    uint4* dst = smem + buf * SB;
+#pragma unroll
+    for (int jj = 0; jj < JW; ++jj) {
+      const int j = wid + NWV * jj;
+      if (j < NWW)
+        __builtin_amdgcn_global_load_lds((glb_void_t*)(wsl + j * 64 + fW), (lds_void_t*)(dst + j * 64), 16, 0, 0);
+    }
+#pragma unroll
+    for (int jj = 0; jj < JI; ++jj) {
+      const int j = wid + NWV * jj;
+      if (j < NWIN) {
+        const uint4* src = inOff[jj] >= 0 ? inb + inOff[jj] + ch * 4 : &g_x3_zero16;
+        __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(dst + SW + j * 64), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x16 acc0[WM][WN], acc1[WM][WN];
+#pragma unroll
+  for (int m = 0; m < WM; ++m)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc0[m][j][r] = 0.0f;
+        acc1[m][j][r] = 0.0f;
+      }
+
+  const int nsub = max(0, min(WN, NS - pg * WN));
+  int aS[WM];
+#pragma unroll
+  for (int m = 0; m < WM; ++m) {
+    const int r = (mw * WM + m) * 32 + l32;
+    aS[m] = r * 4 + (h ^ swz4(r));
+  }
+  int hp0[WN];
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int px = min((pg * WN + j) * 32 + l32, P - 1);
+    hp0[j] = (px / TX) * HX + (px % TX);
+  }
+
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int ch = 0; ch < NCH; ++ch) {
+    if (ch + 1 < NCH) issue(ch + 1, (ch + 1) & 1);
+    const uint4* sb = smem + (ch & 1) * SB;
+    auto mma = [&](auto cnt) {
+      constexpr int C = decltype(cnt)::value;
+      if constexpr (C > 0) {
+        auto tapbody = [&](int tap) {
+          const int ky = tap / KS, kx = tap - KS * (tap / KS);
+          f16x8 ah[WM], al[WM];
+#pragma unroll
+          for (int m = 0; m < WM; ++m) {
+            ah[m] = __builtin_bit_cast(f16x8, sb[aS[m] + tap * BM * 4]);
+            al[m] = __builtin_bit_cast(f16x8, sb[(aS[m] ^ 2) + tap * BM * 4]);
+          }
+#pragma unroll
+          for (int j = 0; j < C; ++j) {
+            const int hp = hp0[j] + ky * HX + kx;
+            const int bs = SW + hp * 4 + (h ^ swz4(hp));
+            const f16x8 bh = __builtin_bit_cast(f16x8, sb[bs]);
+            const f16x8 bl = __builtin_bit_cast(f16x8, sb[bs ^ 2]);
+#pragma unroll
+            for (int m = 0; m < WM; ++m) {
+              acc0[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh, acc0[m][j], 0, 0, 0);
+              acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bl, acc1[m][j], 0, 0, 0);
+              acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bh, acc1[m][j], 0, 0, 0);
+            }
+          }
+        };
+        // single-fragment waves: all taps unrolled, the next tap's reads scheduled under this
+        // tap's MFMAs; larger wave tiles keep one tap per iteration (register budget)
+        if constexpr (WM * WN == 1) {
+#pragma unroll
+          for (int tap = 0; tap < T; ++tap) tapbody(tap);
+        } else {
+#pragma unroll 1
+          for (int tap = 0; tap < T; ++tap) tapbody(tap);
+        }
+      }
+    };
+    if constexpr (WN == 1) {
+      if (nsub == 1) mma(std::integral_constant<int, 1>{});
+    } else if constexpr (WN == 2) {
+      if (nsub == 2) mma(std::integral_constant<int, 2>{});
+      else if (nsub == 1) mma(std::integral_constant<int, 1>{});
+    } else {
+      static_assert(WN <= 2, "WN");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue on the fp32 values ----
+#pragma unroll
+  for (int m = 0; m < WM; ++m)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc0[m][j][r] += acc1[m][j][r] * kLoInv;  // exact product, one rounding
+
+  x3_epilogue<COUT, BM, TY, TX, WM, WN>(acc0, ep, smem, n, nb, ty0, tx0, H, W, mw, pg, nsub);
+}
+
+// The 224^2 level's 32 -> 32 convolutions as a persistent grid: both slabs of the weights
+// (36 KiB) are loaded into LDS once per block, and each block walks a run of 8 x 32 tiles loading
+// only the tile's halo (both slabs, 43.5 KiB: one wait per tile instead of a weight + halo DMA per
+// slab); the halo buffer then stages the tile's epilogue.  80 KiB per block, two per CU.  The
+// tiles of one XCD form a contiguous range that its blocks walk in step, so vertically adjacent
+// tiles (which share halo rows) are in flight together in that XCD's L2.  Per output pixel the
+// sums are formed in k_conv_x3's slab / tap / MFMA order: bit-identical results.
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, int N, int H,
+                   int W, int tiles_x, int tiles_y) {
+  constexpr int NWV = 8, BM = 32, T = 9, TY = 8, TX = 32, HX = TX + 2, NPIX = (TY + 2) * HX;
+  constexpr int NCH = 2, QI = 8;
+  constexpr int SW = T * BM * 4;                   // one slab's weights, 16-byte slots
+  constexpr int SI = (NPIX * 4 + 63) / 64 * 64;    // one slab of the halo
+  constexpr int NWW = NCH * SW / 64, NWIN = SI / 64;
+  constexpr int JW = (NWW + NWV - 1) / NWV, JI = (NWIN + NWV - 1) / NWV;
+  static_assert(TY * TX * (BM / 4) <= NCH * SI, "the epilogue stages in the halo buffer");
+  static_assert((NCH * SW + NCH * SI) * 16 <= 81920, "two blocks per CU");
+  __shared__ uint4 smem[NCH * SW + NCH * SI];
+  uint4* sx = smem + NCH * SW;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int tiles = tiles_x * tiles_y, total = N * tiles;
+  const int G = gridDim.x, xb = blockIdx.x & 7, ng = G < 8 ? G : 8;
+  const int lo = (int)((long long)total * xb / ng), hi = (int)((long long)total * (xb + 1) / ng);
+  const int nbx = (G - xb + 7) >> 3;  // blocks on this XCD
+  const int fW = (lane & ~3) | ((lane & 3) ^ ((lane >> 4) & 3));
+#pragma unroll
+  for (int jj = 0; jj < JW; ++jj) {
+    const int j = wid + NWV * jj;
+    if (j < NWW)
+      __builtin_amdgcn_global_load_lds((glb_void_t*)(wpk + j * 64 + fW), (lds_void_t*)(smem + j * 64), 16, 0, 0);
+  }
+  const int aS = l32 * 4 + (h ^ swz4(l32));
+  const int px = wid * 32 + l32;
+  const int hp0 = (px / TX) * HX + (px % TX);
+  for (int t = lo + (blockIdx.x >> 3); t < hi; t += nbx) {
+    const int n = t / tiles, tt = t - n * tiles;
+    const int ty0 = (tt / tiles_x) * TY, tx0 = (tt % tiles_x) * TX;
+    const uint4* inb = in + (long long)n * H * W * QI;
+#pragma unroll
+    for (int jj = 0; jj < JI; ++jj) {
+      const int j = wid + NWV * jj;
+      if (j < NWIN) {
+        const int si = j * 64 + lane;
+        const int hp = si >> 2, cq = si & 3;
+        const int hy = hp / HX, hx = hp - (hp / HX) * HX;
+        const int gy = ty0 + hy - 1, gx = tx0 + hx - 1;
+        const int off = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+                            ? (gy * W + gx) * QI + (cq ^ swz4(hp)) : -1;
+#pragma unroll
+        for (int s = 0; s < NCH; ++s) {
+          const uint4* src = off >= 0 ? inb + off + s * 4 : &g_x3_zero16;
+          __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(sx + s * SI + j * 64), 16, 0, 0);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // opaque per tile: keeps the compiler from hoisting every tap's fragment addresses out of the
+    // tile loop (they would stay live across the epilogue: spills)
+    int hpb = hp0, aSb = aS;
+    asm volatile("" : "+v"(hpb), "+v"(aSb));
+    f32x16 acc0[1][1], acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      acc0[0][0][r] = 0.0f;
+      acc1[r] = 0.0f;
+    }
+#pragma unroll 1
+    for (int s = 0; s < NCH; ++s) {
+#pragma unroll
+      for (int tap = 0; tap < T; ++tap) {
+        const int ky = tap / 3, kx = tap % 3;
+        const uint4* swt = smem + s * SW + tap * BM * 4;
+        const f16x8 ah = __builtin_bit_cast(f16x8, swt[aSb]);
+        const f16x8 al = __builtin_bit_cast(f16x8, swt[aSb ^ 2]);
+        const int hp = hpb + ky * HX + kx;
+        const int bs = s * SI + hp * 4 + (h ^ swz4(hp));
+        const f16x8 bh = __builtin_bit_cast(f16x8, sx[bs]);
+        const f16x8 bl = __builtin_bit_cast(f16x8, sx[bs ^ 2]);
+        acc0[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc0[0][0], 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc1, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc1, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc0[0][0][r] += acc1[r] * kLoInv;  // exact product, one rounding
+    __syncthreads();  // every halo read done: the epilogue stages its tile over the halo
+    // per-tile copies of the epilogue's table pointers behind an opaque zero: without it the
+    // compiler hoists the lane's bias / scale / shift / head loads out of the tile loop and keeps
+    // them live across the MFMAs (spills)
+    X3Epi et = ep;
+    int zo = 0;
+    asm volatile("" : "+s"(zo));
+    et.bias = et.bias ? et.bias + zo : nullptr;
+    et.scale = et.scale ? et.scale + zo : nullptr;
+    et.shift = et.shift ? et.shift + zo : nullptr;
+    et.style = et.style ? et.style + zo : nullptr;
+    et.head_w = et.head_w ? et.head_w + zo : nullptr;
+    et.head_b = et.head_b ? et.head_b + zo : nullptr;
+    x3_epilogue<32, BM, TY, TX, 1, 1>(acc0, et, sx, n, 0, ty0, tx0, H, W, 0, wid, 1);
+    __syncthreads();  // staging reads done before the next tile's halo lands
+  }
+}
+
 struct X3Cfg {
   int bm, ty, tx;
 };
@@ -504,7 +628,19 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
 #define X3_1(CI, CO)                                                                     \
   if (ks == 1 && cin == CI && cout == CO)                                                \
     return x3_run<1, CI, CO, 32, 16, 16, 1, 1, 4>(ctx, in, wpk, ep, N, H, W);
-  // 224^2 level
+  // 224^2 level (32 -> 32 without in_up: the persistent weights-resident kernel unless
+  // CPX_X3_P32=0)
+  static const bool p32 = !getenv("CPX_X3_P32") || atoi(getenv("CPX_X3_P32")) != 0;
+  if (p32 && ks == 3 && cin == 32 && cout == 32 && variant == 0 && !ep.in_up) {
+    const int tx = cpx_div_up(W, 32), ty = cpx_div_up(H, 8);
+    const long long tiles = (long long)N * tx * ty;
+    CPX_REQUIRE(tiles < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv: too many tiles");
+    const int grid = (int)std::max(1LL, std::min(tiles, 2LL * ctx->n_cu));
+    hipLaunchKernelGGL(k_conv_x3_p32, dim3(grid), dim3(512), 0, ctx->stream, (const uint4*)in,
+                       (const uint4*)wpk, ep, N, H, W, tx, ty);
+    CPX_CHECK_LAUNCH("k_conv_x3_p32");
+    return CPX_OK;
+  }
   X3_3(32, 32, 0, 32, 8, 32, 1, 1, 4)
   X3_3(64, 32, 0, 32, 8, 32, 1, 1, 4)
   X3_3(32, 32, 1, 32, 16, 32, 1, 2, 2)
