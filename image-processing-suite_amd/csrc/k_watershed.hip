@@ -430,11 +430,22 @@ __device__ __forceinline__ void block_flush(const int* s_buf, int* s_cnt, int* s
 
 // one block per 32 x 32 tile (tiles without free pixels stored only their border ring: nothing
 // to label there)
+// In-tile chain resolution: pointer chains that stay inside the tile are followed in LDS (ten
+// doubling rounds cover any chain of the tile's 1024 pixels); only pixels whose chain leaves the
+// tile go to the global list, their pointer compressed to the chain's first pixel outside.  (Done
+// per pixel in the global rounds alone, nearly every free pixel went through 5-7 rounds of
+// scattered 4-byte gathers.)
+constexpr int kInTileRounds = 10;
+static_assert((1 << kInTileRounds) >= kT * kT, "doubling rounds cover a whole tile");
+
 __global__ __launch_bounds__(kJumpThreads) void k_ws_ptr_init(WsArgs a, int* __restrict__ cells,
                                                               int* __restrict__ cyto, int* __restrict__ ptr,
                                                               int* __restrict__ list, int* __restrict__ cnt) {
   __shared__ int s_buf[kT * kT];
+  __shared__ int s_lab[kT * kT];  // label (> 0), 0 = unresolved, -1 = no chain (not a free reached pixel)
+  __shared__ int s_tgt[kT * kT];  // FOV-global index of the pixel's current ancestor
   __shared__ int s_cnt, s_base;
+  constexpr int PER = kT * kT / kJumpThreads;
   // XCD-aware: each XCD labels a contiguous run of tiles (neighbour level reads stay in its L2)
   const int G = gridDim.x, xb = blockIdx.x & 7;
   const int t = xb * (G >> 3) + min(xb, G & 7) + (blockIdx.x >> 3);
@@ -442,15 +453,17 @@ __global__ __launch_bounds__(kJumpThreads) void k_ws_ptr_init(WsArgs a, int* __r
   const int per = a.nty * a.ntx;
   const int fov = t / per, tt = t - fov * per, ty = tt / a.ntx, tx = tt - ty * a.ntx;
   const long long hw = (long long)a.H * a.W;
+  const int y0 = ty * kT, x0 = tx * kT;
   if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
-  for (int k = 0; k < kT * kT / kJumpThreads; ++k) {
-    const int i = threadIdx.x + k * kJumpThreads, y = ty * kT + i / kT, x = tx * kT + i % kT;
-    bool app = false;
-    long long g = 0;
+  int lab[PER], tgt[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = threadIdx.x + k * kJumpThreads, y = y0 + i / kT, x = x0 + i % kT;
+    lab[k] = -1;
+    tgt[k] = 0;
     if (y < a.H && x < a.W) {
       const long long idx = (long long)y * a.W + x;
-      g = fov * hw + idx;
+      const long long g = fov * hw + idx;
       const unsigned long long v = a.Bg[g];
       if (v != kBlocked && !stored_marker(v)) {
         if (v >= kUnreached) {  // never flooded: left unlabelled, as skimage leaves it
@@ -464,13 +477,52 @@ __global__ __launch_bounds__(kJumpThreads) void k_ws_ptr_init(WsArgs a, int* __r
           if (x + 1 < a.W) S = min(S, level_of(a.Bg[g + 1]));
           if (y + 1 < a.H) S = min(S, level_of(a.Bg[g + a.W]));
           const long long tg = fov * hw + (long long)((v == key ? S : v) & (unsigned long long)kIdxMask);
-          const int l = stored_marker(a.Bg[tg]) ? a.nuc[tg] : 0;
-          cells[g] = l;
-          cyto[g] = l;
-          ptr[g] = (int)tg;
-          app = l == 0;
+          lab[k] = stored_marker(a.Bg[tg]) ? a.nuc[tg] : 0;
+          tgt[k] = (int)tg;
         }
       }
+    }
+    s_lab[i] = lab[k];
+    s_tgt[i] = tgt[k];
+  }
+  __syncthreads();
+  // local index of a FOV-global pixel index, -1 outside this tile
+  auto local = [&](int gi) -> int {
+    const long long li = (long long)gi - fov * hw;
+    const int y = (int)(li / a.W), x = (int)(li - (long long)y * a.W);
+    return (y >= y0 && y < y0 + kT && x >= x0 && x < x0 + kT) ? (y - y0) * kT + (x - x0) : -1;
+  };
+  for (int r = 0; r < kInTileRounds; ++r) {
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (lab[k] != 0) continue;
+      const int li = local(tgt[k]);
+      if (li < 0) continue;  // the chain has left the tile
+      const int l = s_lab[li];
+      if (l > 0) lab[k] = l;
+      else if (l == 0) tgt[k] = s_tgt[li];  // jump to the ancestor's ancestor
+      else continue;  // (an ancestor is always a free reached pixel or a marker)
+      any = true;
+    }
+    __syncthreads();  // every read of this round before the writes
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = threadIdx.x + k * kJumpThreads;
+      s_lab[i] = lab[k];
+      s_tgt[i] = tgt[k];
+    }
+    if (!__syncthreads_or(any)) break;
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = threadIdx.x + k * kJumpThreads, y = y0 + i / kT, x = x0 + i % kT;
+    const long long g = fov * hw + (long long)y * a.W + x;
+    const bool app = lab[k] == 0;
+    if (lab[k] >= 0) {
+      cells[g] = lab[k];
+      cyto[g] = lab[k];
+      if (app) ptr[g] = tgt[k];
     }
     block_append(app, (int)g, s_buf, &s_cnt);
   }
