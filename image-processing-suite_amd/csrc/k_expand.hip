@@ -128,19 +128,15 @@ __global__ __launch_bounds__(kT) void k_edt_rows(const int* __restrict__ nuc, in
   if (c >= W) return;
   for (int rr = 0; rr < nr; ++rr) {
     const int* sr = seg + rr * sw + threadIdx.x;
-    int best = 0x7fffffff, blab = 0;
+    // branch-free lexicographic min of (d^2, k) as one key (d^2 << 8) | k: a column without a
+    // feature has dr = kNone = -128, so its d^2 >= 16384 > D^2 (D <= 127) and it can only win
+    // when no candidate is within D, which the threshold below maps to label 0 anyway
+    unsigned best = 0xffffffffu;
     for (int k = 0; k <= 2 * D; ++k) {
-      const int v = sr[k];
-      const int dr = ft_dr(v);
-      if (dr == kNone) continue;
-      const int dc = k - D;
-      const int d2 = dr * dr + dc * dc;
-      if (d2 < best) {
-        best = d2;
-        blab = v >> 8;
-      }
+      const int dr = ft_dr(sr[k]), dc = k - D;
+      best = min(best, ((unsigned)(dr * dr + dc * dc) << 8) | (unsigned)k);
     }
-    const int lab = best <= D * D ? blab : 0;
+    const int lab = (int)(best >> 8) <= D * D ? sr[best & 0xffu] >> 8 : 0;
     const long long px = ((long long)fov * H + r0 + rr) * W + c;
     const int nv = nuc[px];
     if (cells) cells[px] = lab;

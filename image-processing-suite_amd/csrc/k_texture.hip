@@ -130,13 +130,14 @@ __device__ __forceinline__ void glcm_count(const unsigned char* __restrict__ cro
   // neighbouring pixels of a smooth crop would.  p and its (row, chunk column) advance
   // incrementally.
   const int mul = nc % 7919 ? 7919 : 7907;
-  int p = (int)(((long long)threadIdx.x * mul) % nc);
-  const int step = (int)(((long long)kTT * mul) % nc);
+  static_assert((long long)kTT * 7919 < (1ll << 32), "32-bit products");
+  unsigned p = (threadIdx.x * (unsigned)mul) % (unsigned)nc;
+  const unsigned step = ((unsigned)kTT * (unsigned)mul) % (unsigned)nc;
   const int sr = step / nch, sc = step - sr * nch;
   int r = p / nch, ci = p - r * nch;
   const int boff = dr * bwp + (dc < 0 ? -8 : 0);
   for (int q = threadIdx.x; q < nc; q += kTT) {
-    const unsigned char* pa = crop + 8 * p;
+    const unsigned char* pa = crop + 8 * (int)p;
     const uint2 A = *reinterpret_cast<const uint2*>(pa);
     unsigned int b0, b1;
     if constexpr (sh == 0) {
@@ -203,7 +204,7 @@ __device__ __forceinline__ void glcm_count(const unsigned char* __restrict__ cro
       ci -= nch;
       ++r;
     }
-    if (p >= nc) {
+    if (p >= (unsigned)nc) {
       p -= nc;
       r -= rend;
     }
@@ -211,25 +212,30 @@ __device__ __forceinline__ void glcm_count(const unsigned char* __restrict__ cro
 }
 
 // Scan + clear of one angle's table: ASM = sum c^2 (v_dot2_u32_u16 on the packed counters) and
-// the non-background pair count sum c; wave w owns rows w + 16k (k < 16), read four at a time so
-// the LDS latency overlaps, all-zero rows skipped by ballot.
+// the non-background pair count sum c.  Wave w owns the row pairs w + 16k (k < 8), one 16-byte
+// read per lane and pair (a wave-instruction covers two whole rows), all eight reads in flight
+// before the first use; all-zero row pairs are skipped by ballot and only non-zero lanes store
+// their zeros back.
 __device__ __forceinline__ void glcm_scan(unsigned int* tab, GlcmSums& S) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint2* rows = reinterpret_cast<uint2*>(tab) + wid * 64 + lane;
+  static_assert(kTabW == 8 * kNW * 64 * 4, "eight row pairs per wave");
+  uint4* rows = reinterpret_cast<uint4*>(tab) + wid * 64 + lane;
+  uint4 w[8];
 #pragma unroll
-  for (int k0 = 0; k0 < 16; k0 += 4) {
-    uint2 w[4];
+  for (int k = 0; k < 8; ++k) w[k] = rows[k * kNW * 64];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) w[k] = rows[(k0 + k) * kNW * 64];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (!__builtin_amdgcn_ballot_w64((w[k].x | w[k].y) != 0u)) continue;
-      rows[(k0 + k) * kNW * 64] = uint2{0u, 0u};
-      S.asq = dot2_u16(w[k].x, w[k].x, S.asq);
-      S.asq = dot2_u16(w[k].y, w[k].y, S.asq);
-      S.cnt = dot2_u16(w[k].x, 0x10001u, S.cnt);
-      S.cnt = dot2_u16(w[k].y, 0x10001u, S.cnt);
-    }
+  for (int k = 0; k < 8; ++k) {
+    const bool nz = (w[k].x | w[k].y | w[k].z | w[k].w) != 0u;
+    if (!__builtin_amdgcn_ballot_w64(nz)) continue;
+    if (nz) rows[k * kNW * 64] = uint4{0u, 0u, 0u, 0u};
+    S.asq = dot2_u16(w[k].x, w[k].x, S.asq);
+    S.asq = dot2_u16(w[k].y, w[k].y, S.asq);
+    S.asq = dot2_u16(w[k].z, w[k].z, S.asq);
+    S.asq = dot2_u16(w[k].w, w[k].w, S.asq);
+    S.cnt = dot2_u16(w[k].x, 0x10001u, S.cnt);
+    S.cnt = dot2_u16(w[k].y, 0x10001u, S.cnt);
+    S.cnt = dot2_u16(w[k].z, 0x10001u, S.cnt);
+    S.cnt = dot2_u16(w[k].w, 0x10001u, S.cnt);
   }
 }
 
