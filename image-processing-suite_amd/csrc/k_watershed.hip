@@ -444,6 +444,7 @@ __global__ __launch_bounds__(kJumpThreads) void k_ws_ptr_init(WsArgs a, int* __r
   __shared__ int s_buf[kT * kT];
   __shared__ int s_lab[kT * kT];  // label (> 0), 0 = unresolved, -1 = no chain (not a free reached pixel)
   __shared__ int s_tgt[kT * kT];  // FOV-global index of the pixel's current ancestor
+  __shared__ short s_loc[kT * kT];  // that ancestor's index in this tile, -1 outside it
   __shared__ int s_cnt, s_base;
   constexpr int PER = kT * kT / kJumpThreads;
   // XCD-aware: each XCD labels a contiguous run of tiles (neighbour level reads stay in its L2)
@@ -455,12 +456,13 @@ __global__ __launch_bounds__(kJumpThreads) void k_ws_ptr_init(WsArgs a, int* __r
   const long long hw = (long long)a.H * a.W;
   const int y0 = ty * kT, x0 = tx * kT;
   if (threadIdx.x == 0) s_cnt = 0;
-  int lab[PER], tgt[PER];
+  int lab[PER], tgt[PER], loc[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int i = threadIdx.x + k * kJumpThreads, y = y0 + i / kT, x = x0 + i % kT;
     lab[k] = -1;
     tgt[k] = 0;
+    loc[k] = -1;
     if (y < a.H && x < a.W) {
       const long long idx = (long long)y * a.W + x;
       const long long g = fov * hw + idx;
@@ -476,33 +478,33 @@ __global__ __launch_bounds__(kJumpThreads) void k_ws_ptr_init(WsArgs a, int* __r
           if (x > 0) S = min(S, level_of(a.Bg[g - 1]));
           if (x + 1 < a.W) S = min(S, level_of(a.Bg[g + 1]));
           if (y + 1 < a.H) S = min(S, level_of(a.Bg[g + a.W]));
-          const long long tg = fov * hw + (long long)((v == key ? S : v) & (unsigned long long)kIdxMask);
+          const int ti = (int)((v == key ? S : v) & (unsigned long long)kIdxMask);
+          const long long tg = fov * hw + ti;
           lab[k] = stored_marker(a.Bg[tg]) ? a.nuc[tg] : 0;
           tgt[k] = (int)tg;
+          const int ty_ = ti / a.W - y0, tx_ = ti - (ti / a.W) * a.W - x0;
+          loc[k] = (ty_ >= 0 && ty_ < kT && tx_ >= 0 && tx_ < kT) ? ty_ * kT + tx_ : -1;
         }
       }
     }
     s_lab[i] = lab[k];
     s_tgt[i] = tgt[k];
+    s_loc[i] = (short)loc[k];
   }
   __syncthreads();
-  // local index of a FOV-global pixel index, -1 outside this tile
-  auto local = [&](int gi) -> int {
-    const long long li = (long long)gi - fov * hw;
-    const int y = (int)(li / a.W), x = (int)(li - (long long)y * a.W);
-    return (y >= y0 && y < y0 + kT && x >= x0 && x < x0 + kT) ? (y - y0) * kT + (x - x0) : -1;
-  };
   for (int r = 0; r < kInTileRounds; ++r) {
     bool any = false;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       if (lab[k] != 0) continue;
-      const int li = local(tgt[k]);
+      const int li = loc[k];
       if (li < 0) continue;  // the chain has left the tile
       const int l = s_lab[li];
       if (l > 0) lab[k] = l;
-      else if (l == 0) tgt[k] = s_tgt[li];  // jump to the ancestor's ancestor
-      else continue;  // (an ancestor is always a free reached pixel or a marker)
+      else if (l == 0) {  // jump to the ancestor's ancestor
+        tgt[k] = s_tgt[li];
+        loc[k] = s_loc[li];
+      } else continue;  // (an ancestor is always a free reached pixel or a marker)
       any = true;
     }
     __syncthreads();  // every read of this round before the writes
@@ -511,6 +513,7 @@ __global__ __launch_bounds__(kJumpThreads) void k_ws_ptr_init(WsArgs a, int* __r
       const int i = threadIdx.x + k * kJumpThreads;
       s_lab[i] = lab[k];
       s_tgt[i] = tgt[k];
+      s_loc[i] = (short)loc[k];
     }
     if (!__syncthreads_or(any)) break;
   }
