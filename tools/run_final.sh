@@ -1,0 +1,10 @@
+# Round-end rehearsal on the GPU box: smoke(), the whole -m gpu suite, the default bench line.
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/final
+mkdir -p $O
+cd $R
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gputests.log 2>&1
+timeout -k 10 420 python -u bench.py > $O/bench.log 2>&1
+echo done
