@@ -148,9 +148,17 @@ class FusedCPnetX3:
         self.head_w = dv(net.output[-1].weight.reshape(net.output[-1].out_channels, -1))
         self.head_b = dv(net.output[-1].bias)
         self.nout = net.output[-1].out_channels
+        # per network image (tile): non-zero once one of its activations left the fp16 range;
+        # sized and cleared by every forward (the clear is part of a captured graph)
         self.ovf = torch.zeros(1, dtype=torch.int32, device=td)
 
     # -- libcpx passes ----------------------------------------------------------------------------
+    def _ovf_p(self, N):
+        """The per-image overflow flags, at least N of them (a pass called on its own)."""
+        if self.ovf.numel() < N:
+            self.ovf = torch.zeros(N, dtype=torch.int32, device=self.td)
+        return _p(self.ovf)
+
     def _empty(self, N, H, W, C):
         return torch.empty((N, H, W, C), dtype=torch.int32, device=self.td)  # split: 4 B per channel
 
@@ -170,7 +178,7 @@ class FusedCPnetX3:
             self.dev.h, ks, self.variant, _p(x), int(in_up), N, H, W, cin, cout, _p(pk), _p(bias), _p(res), int(res_up),
             st, st_stride, _p(scale), _p(shift), int(relu), _p(yo), _p(zo), int(z_up),
             _p(self.head_w) if head else None, _p(self.head_b) if head else None, self.nout if head else 0,
-            _p(ho), _p(self.ovf)), "cpx_cpnet_x3_conv")
+            _p(ho), self._ovf_p(N)), "cpx_cpnet_x3_conv")
         return (ho,) if head else (yo, zo)
 
     def _proj(self, x, blk):
@@ -182,7 +190,7 @@ class FusedCPnetX3:
         zo = self._empty(N, H // 2, W // 2, C)
         scale, shift = bn
         check(self.lib.cpx_cpnet_x3_pool(self.dev.h, _p(x), _p(scale), _p(shift), 1, N, H // 2, W // 2, C,
-                                         _p(xo), _p(zo), _p(self.ovf)), "cpx_cpnet_x3_pool")
+                                         _p(xo), _p(zo), self._ovf_p(N)), "cpx_cpnet_x3_pool")
         return xo, zo
 
     def _stem(self, x, d):
@@ -192,7 +200,7 @@ class FusedCPnetX3:
         (s0, h0), (s1, h1) = d["bn"][0], d["bn"][1]
         check(self.lib.cpx_cpnet_x3_stem(self.dev.h, _p(x), N, H, W, _p(s0), _p(h0), _p(d["stem_w"]),
                                          _p(d["b"][0]), _p(s1), _p(h1), _p(d["stem_wp"]), _p(p), _p(z),
-                                         _p(self.ovf)), "cpx_cpnet_x3_stem")
+                                         self._ovf_p(N)), "cpx_cpnet_x3_stem")
         return p, z
 
     def _style(self, x):
@@ -208,6 +216,9 @@ class FusedCPnetX3:
         """x: fp32 [N, by, bx, 2] NHWC (CPX_TILE_F32_NHWC tiles) -> fp32 [N, by, bx, nout] NHWC."""
         self.dev._bind_stream()
         assert x.dtype == torch.float32 and x.is_contiguous() and x.shape[-1] == 2
+        if self.ovf.numel() != x.shape[0]:
+            self.ovf = torch.zeros(x.shape[0], dtype=torch.int32, device=self.td)
+        self.ovf.zero_()
         xd = []
         zu = None
         nd = len(self.down)

@@ -48,7 +48,8 @@ def main(argv=None):
         os.remove(f)
     pkg_root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     # fresh shared batch counters for this run (cpx.plate.WorkQueue): ranks claim batches
-    qdir = os.path.join(pa.out, f".cpx_queue_{os.getpid()}_{time.time_ns()}")
+    token = f"{os.getpid()}_{time.time_ns()}"
+    qdir = os.path.join(pa.out, f".cpx_queue_{token}")
     os.makedirs(qdir)
     procs = []
     for r in range(n):
@@ -56,7 +57,7 @@ def main(argv=None):
         env.pop("MASTER_ADDR", None)  # no process group: the launcher merges
         env["PYTHONPATH"] = pkg_root + os.pathsep + env.get("PYTHONPATH", "")
         cmd = [sys.executable, "-m", "cpx.plate", *rest, "--rank", str(r), "--world", str(n),
-               "--device", "0", "--no-merge", "--queue", qdir]
+               "--device", "0", "--no-merge", "--queue", qdir, "--queue-token", token]
         procs.append(subprocess.Popen(cmd, env=env))
     rcs = [p.wait() for p in procs]
     shutil.rmtree(qdir, ignore_errors=True)

@@ -78,20 +78,39 @@ class FovResults:
     objects: dict                    # set -> list of structured arrays (per FOV)
     feats: dict                      # set -> list of float64 [n_objects, F]
     seg_stats: np.ndarray
-    failed: np.ndarray | None = None  # [B] bool: the FOV's Cells watershed did not converge within
-                                      # ws_rounds; its object tables are emptied (the reference's
-                                      # per-site 'empty' result, Cellpose_GPU_s3fs.py:225-232)
+    failed: np.ndarray | None = None  # [B] bool: the FOV's Cells watershed did not converge even
+                                      # after the re-runs with more rounds; its object tables are
+                                      # emptied (the reference's per-site 'empty' result,
+                                      # Cellpose_GPU_s3fs.py:225-232)
+    recovered: np.ndarray | None = None  # [B] int: 0, or how the FOV was re-run on its own
+                                         # (RECOVER_FP32: a split-fp16 activation overflowed, so its
+                                         # CPnet ran in fp32; RECOVER_WS: its watershed needed more
+                                         # rounds; both bits possible)
+
+
+RECOVER_FP32 = 1
+RECOVER_WS = 2
+WS_RETRIES = 3  # re-runs of a non-converged watershed, each with twice the rounds of the last
 
 
 class FovPipeline:
     _copy_streams: dict = {}
 
-    def __init__(self, dev: Device, cfg: PipelineConfig, illum: np.ndarray | None):
+    def __init__(self, dev: Device, cfg: PipelineConfig, illum, recovery: bool = True):
         self.dev, self.cfg = dev, cfg
         B, C, H, W = cfg.batch, cfg.C, cfg.H, cfg.W
         td = dev.torch_device
-        self.raw = torch.empty((B * C, H, W), dtype=torch.int16, device=td)  # uint16 bits
-        self.illum = None if illum is None else torch.from_numpy(np.ascontiguousarray(illum)).to(td)
+        # the host loader's staging planes (uint16 bits): one buffer per result slot, so a step's
+        # planes stay intact until its fetch() (which may re-run single FOVs from them); self.raw
+        # is always the buffer the next run() reads
+        self._raw_bufs = [torch.empty((B * C, H, W), dtype=torch.int16, device=td)]
+        self.raw = self._raw_bufs[0]
+        if illum is None or isinstance(illum, torch.Tensor):
+            self.illum = None if illum is None else illum.to(td)
+        else:
+            self.illum = torch.from_numpy(np.ascontiguousarray(illum)).to(td)
+        self._recovery = recovery  # False for the single-FOV pipelines that do the re-runs
+        self._rec_pipes = {}
         self.corr = torch.empty((B, C, H, W), dtype=torch.float32, device=td)
         self.stats = dev.empty_bytes(64 * B * C)
         ML = cfg.max_objects
@@ -110,15 +129,15 @@ class FovPipeline:
                 "objects": {s: dev.empty_bytes(56 * B * ML) for s in OBJECT_SETS},
                 "feats": {s: torch.zeros((B, ML, self.F), dtype=torch.float64, device=td) for s in OBJECT_SETS},
                 "seg_stats": torch.empty_like(self.seg.stats),
-                "cpnet_ovf": torch.zeros(1, dtype=torch.int32, device=td),
-                "event": None})
+                "cpnet_ovf": torch.zeros(max(1, B * self.seg.geom.n_tiles), dtype=torch.int32, device=td),
+                "raw": None, "event": None})
         self._host = {
             "qc": torch.empty(24 * B * C, dtype=torch.uint8, pin_memory=True),
             "hdr": {s: torch.empty(16 * B, dtype=torch.uint8, pin_memory=True) for s in OBJECT_SETS},
             "objects": {s: torch.empty(56 * B * ML, dtype=torch.uint8, pin_memory=True) for s in OBJECT_SETS},
             "feats": {s: torch.empty(B * ML * self.F, dtype=torch.float64, pin_memory=True) for s in OBJECT_SETS},
             "seg_stats": torch.empty(self.seg.stats.shape, dtype=self.seg.stats.dtype, pin_memory=True),
-            "cpnet_ovf": torch.zeros(1, dtype=torch.int32, pin_memory=True)}
+            "cpnet_ovf": torch.zeros(max(1, B * self.seg.geom.n_tiles), dtype=torch.int32, pin_memory=True)}
         # one result-copy stream per device, shared by its pipelines: a process has only
         # GPU_MAX_HW_QUEUES (4) hardware queues, and streams beyond that share one, which
         # serialises two pipelines' kernels behind each other
@@ -199,6 +218,7 @@ class FovPipeline:
         stream = torch.cuda.current_stream(self.dev.torch_device)
         # (a slot's previous fetch() returned only after its copies completed)
         self._use_slot(k)
+        sl["raw"] = self.raw
         self.stage_illum_qc()
         self.stage_segment()
         self.stage_objects()
@@ -208,6 +228,11 @@ class FovPipeline:
             sl["cpnet_ovf"].copy_(ovf)
         sl["event"] = torch.cuda.Event()
         sl["event"].record(stream)
+        if raw is None:  # the loader fills the next slot's own staging buffer
+            nk = self._step % len(self._slots)
+            while len(self._raw_bufs) <= nk:
+                self._raw_bufs.append(torch.empty_like(self._raw_bufs[0]))
+            self.raw = self._raw_bufs[nk]
         return k
 
     def fetch(self, slot: int | None = None) -> FovResults:
@@ -246,21 +271,66 @@ class FovPipeline:
             feats[s] = [f[b, : n_b[b]].copy() for b in range(B)]
             objs[s] = [o[b, : n_b[b]].copy() for b in range(B)]
         seg_stats = hb["seg_stats"].numpy().view(SEG_STATS_DTYPE).copy()
-        if int(hb["cpnet_ovf"][0]) != 0:
-            raise RuntimeError("CPnet (f16x3): an activation left the fp16 range (|a| >= 65504); "
-                               "run this plate with cpnet_precision='fp32'")
+        nt = self.seg.geom.n_tiles
+        ovf = hb["cpnet_ovf"][:B * nt].numpy().reshape(B, nt).any(axis=1)
         failed = np.zeros(B, dtype=bool)
         if self.cfg.cells == "watershed":
             failed = seg_stats["cells_status"].ravel()[:B] < 0
-            if failed.any():
-                # per-site failure, not a failed batch: those FOVs get no object rows, every other
-                # FOV of the batch is kept (the reference logs a site's error and moves on)
-                log.error("cpx_watershed_cells: no convergence within ws_rounds %s for FOV(s) %s of the batch; "
-                          "recorded as empty sites", self.cfg.ws_rounds, np.nonzero(failed)[0].tolist())
+        res = FovResults(qc=qc, hdr=hdrs, objects=objs, feats=feats, seg_stats=seg_stats, failed=failed,
+                         recovered=np.zeros(B, dtype=np.int32))
+        if self._recovery and (ovf.any() or failed.any()):
+            self._recover(sl["raw"], res, ovf, failed)
+        if res.failed.any():
+            # per-site failure, not a failed batch: those FOVs get no object rows, every other
+            # FOV of the batch is kept (the reference logs a site's error and moves on)
+            log.error("cpx_watershed_cells: no convergence within %s rounds for FOV(s) %s of the batch; "
+                      "recorded as empty sites", self.cfg.ws_rounds, np.nonzero(res.failed)[0].tolist())
+            for s in OBJECT_SETS:
+                for b in np.nonzero(res.failed)[0]:
+                    res.objects[s][b] = res.objects[s][b][:0]
+                    res.feats[s][b] = res.feats[s][b][:0]
+                    res.hdr[s][b]["n_objects"] = 0
+                    res.hdr[s][b]["n_kept"] = 0
+        return res
+
+    # ---- per-FOV recovery (Cellpose_GPU_s3fs.py:142-147: a site that fails is retried, not
+    # dropped) ----------------------------------------------------------------------------------
+    def _recovery_pipe(self, precision: str, ws_rounds: tuple) -> "FovPipeline":
+        key = (precision, tuple(ws_rounds))
+        if key not in self._rec_pipes:
+            cfg = dataclasses.replace(self.cfg, batch=1, cpnet_precision=precision, ws_rounds=tuple(ws_rounds),
+                                      slots=1, crops=False)
+            self._rec_pipes[key] = FovPipeline(Device(self.dev.index), cfg, self.illum, recovery=False)
+        return self._rec_pipes[key]
+
+    def _recover(self, raw: torch.Tensor, res: FovResults, ovf: np.ndarray, failed: np.ndarray):
+        """Re-run single FOVs of a fetched step from its planes (`raw`, kept per slot) and splice
+        their results into `res`: a FOV whose split-fp16 CPnet overflowed runs its CPnet in fp32
+        (the reference's own arithmetic; the split format holds |a| < 65504 only), a FOV whose
+        Cells watershed did not converge runs again with twice the rounds, up to WS_RETRIES
+        times.  Runs on the device's copy stream, after the step's event."""
+        C = self.cfg.C
+        with torch.cuda.stream(self._copy_stream):
+            for b in np.nonzero(ovf | failed)[0]:
+                precision = "fp32" if ovf[b] else self.cfg.cpnet_precision
+                rounds = tuple(self.cfg.ws_rounds)
+                flag = RECOVER_FP32 if ovf[b] else 0
+                if failed[b] and not ovf[b]:
+                    rounds, flag = (2 * rounds[0], 2 * rounds[1]), flag | RECOVER_WS
+                for t in range(WS_RETRIES + 1):
+                    rp = self._recovery_pipe(precision, rounds)
+                    rp.raw.copy_(raw[b * C:(b + 1) * C])
+                    r1 = rp.fetch(rp.run())
+                    if not r1.failed[0] or t == WS_RETRIES:
+                        break
+                    rounds, flag = (2 * rounds[0], 2 * rounds[1]), flag | RECOVER_WS
+                log.warning("FOV %d of the batch re-run on its own (%s, watershed rounds %s): %s", b,
+                            "CPnet fp32 after a split-fp16 overflow" if ovf[b] else "more watershed rounds",
+                            rounds, "converged" if not r1.failed[0] else "watershed still not converged")
                 for s in OBJECT_SETS:
-                    for b in np.nonzero(failed)[0]:
-                        objs[s][b] = objs[s][b][:0]
-                        feats[s][b] = feats[s][b][:0]
-                        hdrs[s][b]["n_objects"] = 0
-                        hdrs[s][b]["n_kept"] = 0
-        return FovResults(qc=qc, hdr=hdrs, objects=objs, feats=feats, seg_stats=seg_stats, failed=failed)
+                    res.hdr[s][b] = r1.hdr[s][0]
+                    res.objects[s][b] = r1.objects[s][0]
+                    res.feats[s][b] = r1.feats[s][0]
+                res.seg_stats[b] = r1.seg_stats[0]
+                res.failed[b] = bool(r1.failed[0])
+                res.recovered[b] = flag

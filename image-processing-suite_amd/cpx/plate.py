@@ -66,6 +66,13 @@ def parse_args(argv=None):
     ap.add_argument("--queue", default=None,
                     help="with --world > 1: directory of the shared per-job batch counters (dynamic work "
                          "queue across the ranks; cpx.launch creates a fresh one); default: static well shards")
+    ap.add_argument("--queue-token", default=os.environ.get("CPX_QUEUE_TOKEN"),
+                    help="run identifier stored with the --queue counters: a counter left by another run "
+                         "(another token) starts over instead of reading as exhausted (cpx.launch sets one)")
+    ap.add_argument("--cpnet-precision", choices=("f16x3", "bf16", "fp32"), default="f16x3",
+                    help="CPnet arithmetic (PipelineConfig.cpnet_precision): f16x3 = split-fp16 MFMA kernels "
+                         "at the fp32 network's accuracy (default; a FOV whose activations leave the fp16 "
+                         "range is re-run in fp32), fp32 = the eager PyTorch module, bf16 = native bf16")
     ap.add_argument("--no-merge", action="store_true",
                     help="with --world > 1: leave the parts for cpx.launch / merge_parts")
     ap.add_argument("--ws-rounds", type=int, nargs=2, default=None, metavar=("RELAX", "LABEL"),
@@ -92,20 +99,28 @@ class WorkQueue:
     draw sites from one shared queue, Cellpose_GPU_s3fs.py:269-300).  The merged tables do not
     depend on which rank measured a site (merge_parts sorts the rows)."""
 
-    def __init__(self, qdir: str, key: str):
+    def __init__(self, qdir: str, key: str, token: str | None = None):
         os.makedirs(qdir, exist_ok=True)
         self.path = os.path.join(qdir, f"{key}.ctr")
+        self.token = token or "-"
+        if any(c.isspace() for c in self.token):
+            raise ValueError("WorkQueue token must not contain whitespace")
 
     def take(self) -> int:
+        """Claim the next batch index.  The counter file holds "<token> <next>"; a counter written
+        under another token (a reused --queue directory) restarts at 0 for this run."""
         import fcntl
         fd = os.open(self.path, os.O_RDWR | os.O_CREAT, 0o644)
         try:
             fcntl.flock(fd, fcntl.LOCK_EX)
-            raw = os.read(fd, 32)
-            k = int(raw) if raw.strip() else 0
+            raw = os.read(fd, 256).decode().split()
+            k = int(raw[1]) if len(raw) == 2 and raw[0] == self.token else 0
+            if raw and k == 0:
+                log.warning("%s: counter of another run (%s) found; restarting it for token %s",
+                            self.path, " ".join(raw), self.token)
             os.lseek(fd, 0, os.SEEK_SET)
             os.ftruncate(fd, 0)
-            os.write(fd, str(k + 1).encode())
+            os.write(fd, f"{self.token} {k + 1}".encode())
             return k
         finally:
             os.close(fd)  # releases the lock
@@ -116,12 +131,17 @@ def batch_source(table, a, job_index: int):
     WorkQueue (--queue, world > 1) or this rank's static well shard (shard_rows)."""
     B = max(1, a.batch)
     if a.queue and a.world > 1:
-        q = WorkQueue(a.queue, f"job{job_index:04d}")
+        q = WorkQueue(a.queue, f"job{job_index:04d}", getattr(a, "queue_token", None))
         nb = (len(table) + B - 1) // B
+        first = True
         while True:
             k = q.take()
             if k >= nb:
+                if first and nb and not getattr(a, "queue_token", None):
+                    log.error("%s: the job's counter is already exhausted on this rank's first claim (%d >= %d "
+                              "batches): a --queue directory reused without --queue-token?", q.path, k, nb)
                 return
+            first = False
             yield list(range(k * B, min(len(table), (k + 1) * B)))
     else:
         mine = shard_rows(table, a.rank, a.world)
@@ -293,7 +313,8 @@ def _run_sites(a, table, source, chans, state, out, status):
             cand = os.path.join(os.path.dirname(__file__), "weights", "cpnet_nuclei_synth.pt")
             weights = cand if os.path.exists(cand) else None
         B = max(1, a.batch)
-        cfg = PipelineConfig(H=H, W=W, C=C, batch=B, channels=tuple(chans), weights=weights)
+        cfg = PipelineConfig(H=H, W=W, C=C, batch=B, channels=tuple(chans), weights=weights,
+                             cpnet_precision=getattr(a, "cpnet_precision", "f16x3"))
         if a.ws_rounds:
             cfg.ws_rounds = tuple(a.ws_rounds)
         illum = _illum(a.illum_path, chans, H, W)

@@ -141,11 +141,14 @@ class Segmenter:
         self.layout = {"bf16": 1, "fp32": 0, "f16x3": 2}[precision]
         self.fnet = None
         if precision == "f16x3":
+            # the native kernels hold their own split, packed weights: the module stays on the
+            # host (it is never run in this mode)
             self.fnet = FusedCPnetX3(self.net, dev)
-        self.net = self.net.to(td)
-        if precision == "bf16" and fused:
-            self.fnet = FusedCPnet(self.net, dev)
-        self.net = self.net.to(memory_format=torch.channels_last, dtype=net_dtype)
+        else:
+            self.net = self.net.to(td)
+            if precision == "bf16" and fused:
+                self.fnet = FusedCPnet(self.net, dev)
+            self.net = self.net.to(memory_format=torch.channels_last, dtype=net_dtype)
         nt = batch * g.n_tiles
         if self.layout == 2:
             self.tiles = torch.empty((nt, g.by, g.bx, NET_CHANNELS), dtype=torch.float32, device=td)

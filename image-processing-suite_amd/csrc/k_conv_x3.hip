@@ -7,7 +7,8 @@
 // and lo = f16((a - hi) * 2^11); a is read back as hi + lo * 2^-11 (one rounding), within
 // 2^-22 |a| (below f16's normal range: 2^-35 absolute).  Activation tensors are NHWC with the
 // channels in slabs of 16: per pixel and slab, 16 hi halves then 16 lo halves (64 bytes), i.e.
-// 4 bytes per channel like fp32.  |a| >= 65504 does not fit: producers raise *ovf.
+// 4 bytes per channel like fp32.  |a| >= 65504 does not fit: producers raise ovf[n] for the
+// image n (network tile) whose activation it was, so the host can re-run only those FOVs.
 // Products.  With weights split the same way (host, once), a product w x = wh xh + wh xl' 2^-11
 // + wl' xh 2^-11 + O(2^-22 w x): per 16 input channels three v_mfma_f32_32x32x16_f16,
 //   acc0 += Wh Xh,   acc1 += Wh Xl' + Wl' Xh,   result = acc0 + acc1 * 2^-11,
@@ -55,16 +56,19 @@ __device__ __forceinline__ int swzq(int row) {
   else return 0;
 }
 
-// 4 fp32 -> (hi, lo) 8-byte pieces; *bad |= not representable
+// 4 fp32 -> (hi, lo) 8-byte pieces; bad |= not representable.  A value outside the fp16 range
+// is stored saturated (+-65504, NaN -> -65504): the image is flagged and re-run in fp32 by the
+// host, and no inf / NaN reaches the kernels after the network (flows stay finite)
 __device__ __forceinline__ void split4(float a, float b, float c, float d, uint2& hi, uint2& lo, bool& bad) {
   const float v[4] = {a, b, c, d};
   f16x4 h, l;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const _Float16 t = (_Float16)v[k];
-    h[k] = t;
-    l[k] = (_Float16)((v[k] - (float)t) * kLoScale);
     bad |= !(fabsf(v[k]) < 65504.0f);
+    const float vc = fminf(fmaxf(v[k], -65504.0f), 65504.0f);
+    const _Float16 t = (_Float16)vc;
+    h[k] = t;
+    l[k] = (_Float16)((vc - (float)t) * kLoScale);
   }
   hi = __builtin_bit_cast(uint2, h);
   lo = __builtin_bit_cast(uint2, l);
@@ -210,7 +214,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
   };
   auto flag = [&]() {
     if (ep.ovf && __ballot(bad)) {
-      if (lane == 0) atomicOr(ep.ovf, 1);
+      if (lane == 0) atomicOr(ep.ovf + n, 1);
     }
   };
   if (ep.y) {
@@ -756,7 +760,7 @@ __global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem_x3(
       p_out[g] = so[1][p * 8 + (k ^ (p & 7))];
     }
   }
-  if (ovf && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
+  if (ovf && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(ovf + n, 1);
 }
 
 // 2x2/2 max-pool of split [N][2Hh][2Ww][Cn] -> x_out (the maximum's own hi/lo pair, exact) and
@@ -817,8 +821,9 @@ __global__ __launch_bounds__(256) void k_cpnet_pool_x3(const uint4* __restrict__
       zo[pix * Q + q] = hi;
       zo[pix * Q + q + 2] = lo;
     }
+    if (bad && ovf) atomicOr(ovf + n, 1);  // rare: one atomic per offending element
+    bad = false;
   }
-  if (ovf && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
 }
 
 // style vector (CPnet.forward: avg_pool2d over the deepest feature map, L2-normalised) and the

@@ -441,7 +441,8 @@ int cpx_cpnet_stem(cpx_ctx* ctx, const void* x, int N, int H, int W, const float
  * host as [cout/bm][cin/16][ky][kx][bm][hi|lo][16] f16 (bm from cpx_cpnet_x3_cfg).  Every
  * product is formed as wh*xh + (wh*xl + wl*xh) * 2^-11 in fp32 (three v_mfma_f32_32x32x16_f16
  * per 16 channels), ~2^-22 relative per operand: the fp32 network to its rounding noise.
- * *ovf (device int, optional) is OR-ed with 1 when a stored activation is not below 65504.
+ * ovf (device int [N], optional): ovf[n] is OR-ed with 1 when an activation of image n that is
+ * not below 65504 in magnitude would be stored (the caller re-runs those images in fp32).
  * cpx_cpnet_x3_conv: ks = 3 (pad 1) or 1 (the block projections); the epilogue of
  * cpx_cpnet_conv3x3 (bias, res [split, res_up], y_out, style [N][style_stride], scale/shift,
  * relu, z_out [z_up]) or, for the last 3x3 convolution (cout 32), the output head:

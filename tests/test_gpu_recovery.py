@@ -1,0 +1,131 @@
+"""Per-FOV recovery instead of whole-batch failures (the reference retries a failing site,
+Cellpose_GPU_s3fs.py:142-147, and otherwise records it as an empty site, :225-232):
+
+  * a FOV whose split-fp16 (f16x3) CPnet activations leave the fp16 range is re-run on its own
+    with the fp32 network: its tables equal an fp32 pipeline's; the other FOVs of the batch keep
+    their f16x3 results; the overflow flags are cleared by every forward, so the next batch on the
+    same pipeline (and its captured HIP graph) runs normally;
+  * a FOV whose Cells watershed does not converge within ws_rounds is re-run with twice the
+    rounds until it does: its tables equal a run with enough rounds from the start;
+  * both through cpx.plate: a plate run with too few watershed rounds writes the same CSVs as a
+    default run.
+"""
+import dataclasses
+import filecmp
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WEIGHTS = os.path.join(REPO, "image-processing-suite_amd", "cpx", "weights", "cpnet_nuclei_synth.pt")
+SETS = ("Nuclei", "Cells", "Cytoplasm")
+
+
+def _cfg(**kw):
+    from cpx.pipeline import PipelineConfig
+    return PipelineConfig(H=2080, W=2080, C=5, batch=2, weights=WEIGHTS if os.path.exists(WEIGHTS) else None, **kw)
+
+
+@pytest.fixture(scope="module")
+def batch(dev):
+    from cpx import shard
+    from cpx.synth import synth_fovs, synth_illum
+    illum = synth_illum(5, 2080, 2080, seed=1)
+    raw = synth_fovs(2, 5, 2080, 2080, dev.torch_device, seed=shard.fov_seed(shard.plate_fovs(n_wells=384)[5]))
+    return illum, raw
+
+
+def _same_tables(a, b, fa, fb, exact=True):
+    """FOV fa of results a vs FOV fb of results b: same objects (labels, areas, boxes) and
+    features (bit-identical, or within rtol 1e-5 for two different fp32 networks)."""
+    for s in SETS:
+        oa, ob = a.objects[s][fa], b.objects[s][fb]
+        assert len(oa) == len(ob), s
+        np.testing.assert_array_equal(oa["label"], ob["label"])
+        if exact:
+            np.testing.assert_array_equal(oa, ob)
+            np.testing.assert_array_equal(a.feats[s][fa], b.feats[s][fb])
+        else:  # two fp32 networks: a few objects may carry rounding-noise boundary pixels
+            fa_, fb_ = a.feats[s][fa], b.feats[s][fb]
+            bad = ~np.isclose(fa_, fb_, rtol=1e-5, atol=1e-9).all(axis=1)
+            assert bad.sum() <= 4, (s, int(bad.sum()))
+
+
+def test_overflow_fov_rerun_in_fp32_and_flags_cleared(dev, batch):
+    from cpx.pipeline import RECOVER_FP32, FovPipeline
+    illum, raw = batch
+    pipe = FovPipeline(dev, _cfg(), illum)
+    base = pipe.fetch(pipe.run(raw))
+    assert not base.recovered.any() and not base.failed.any()
+    # one FOV flagged (as the kernels flag an overflowing network tile): only it is re-run, in fp32
+    sl = pipe._slots[pipe.run(raw)]
+    nt = pipe.seg.geom.n_tiles
+    sl["cpnet_ovf"][nt + 3:nt + 4].fill_(1)
+    torch.cuda.synchronize()
+    res = pipe.fetch()
+    assert res.recovered.tolist() == [0, RECOVER_FP32]
+    _same_tables(res, base, 0, 0)
+    ref = FovPipeline(dev, dataclasses.replace(_cfg(cpnet_precision="fp32"), batch=1), illum, recovery=False)
+    r32 = [ref.fetch(ref.run(raw[b * 5:(b + 1) * 5])) for b in range(2)]
+    _same_tables(res, r32[1], 1, 0, exact=False)
+    # a genuine overflow: the f16x3 network's stem weights scaled up, every tile overflows, every
+    # FOV is re-run in fp32; restoring them, the next batch runs on f16x3 again (flags cleared)
+    stem = pipe.seg.fnet.down[0]["stem_w"]
+    keep = stem.clone()
+    stem.mul_(1e7)
+    res = pipe.fetch(pipe.run(raw))
+    assert res.recovered.tolist() == [RECOVER_FP32, RECOVER_FP32]
+    for b in range(2):
+        _same_tables(res, r32[b], b, 0, exact=False)
+    stem.copy_(keep)
+    res = pipe.fetch(pipe.run(raw))
+    assert not res.recovered.any()
+    for b in range(2):
+        _same_tables(res, base, b, b)
+
+
+def test_watershed_nonconvergence_rerun_with_more_rounds(dev, batch):
+    from cpx.pipeline import RECOVER_WS, FovPipeline
+    illum, raw = batch
+    full = FovPipeline(dev, _cfg(), illum)
+    base = full.fetch(full.run(raw))
+    short = FovPipeline(dev, _cfg(ws_rounds=(1, 1)), illum)
+    res = short.fetch(short.run(raw))
+    assert (res.recovered == RECOVER_WS).all(), res.recovered
+    assert not res.failed.any()
+    for b in range(2):
+        _same_tables(res, base, b, b)
+
+
+def test_plate_with_too_few_watershed_rounds_matches_default(tmp_path, dev, caplog):
+    from cpx import plate, tiffio
+    from cpx.csvout import OBJECT_TABLES
+    from cpx.synth import synth_fovs
+    n, C, H, W = 4, 2, 384, 416
+    chans = ["DNA", "AGP"]
+    raw = synth_fovs(n, C, H, W, dev.torch_device, seed=21).cpu().numpy().view(np.uint16)
+    imgdir = tmp_path / "images"
+    imgdir.mkdir()
+    rows = []
+    for f in range(n):
+        row = {"Metadata_Plate": "P05", "Metadata_Well": f"E{f + 1:02d}", "Metadata_Site": 1, "Metadata_Timepoint": 6}
+        for c, ch in enumerate(chans):
+            tiffio.imwrite(str(imgdir / f"f{f}c{c}.tiff"), raw[f * C + c])
+            row[f"FileName_{ch}"] = f"f{f}c{c}.tiff"
+        rows.append(row)
+    pd.DataFrame(rows).to_csv(tmp_path / "ld.csv", index=False)
+    common = ["--load-data", str(tmp_path / "ld.csv"), "--data-path", str(imgdir), "--channels", *chans,
+              "--batch", "2", "--threads", "2", "--pipes", "1"]
+    d1 = plate.run(common + ["--out", str(tmp_path / "default")])
+    with caplog.at_level("WARNING", logger="cpx.pipeline"):
+        d2 = plate.run(common + ["--out", str(tmp_path / "short"), "--ws-rounds", "1", "1"])
+    assert "re-run on its own" in caplog.text  # the short rounds did fail and were recovered
+    for name in ("Image", *OBJECT_TABLES, "site_status"):
+        assert filecmp.cmp(os.path.join(d1, f"{name}.csv"), os.path.join(d2, f"{name}.csv"), shallow=False), name
+    st = pd.read_csv(os.path.join(d2, "site_status.csv"))
+    assert (st.status == "success").all()

@@ -160,3 +160,21 @@ def test_work_queue_claims_every_batch_once(tmp_path):
     flat = sorted((b for c in claimed for b in c), key=lambda b: b[0])
     assert flat == [list(range(4 * k, min(4 * n - 1, 4 * k + 4))) for k in range(n)]
     assert len(claimed[2]) < len(claimed[0]) + len(claimed[1])
+
+
+def test_work_queue_reused_directory(tmp_path, caplog):
+    """A --queue directory left by an earlier run: with a new --queue-token (cpx.launch passes
+    one) the stale counter restarts and every batch is claimed; without a token the exhausted
+    counter is reported instead of silently yielding nothing."""
+    table = pd.DataFrame({"x": range(10)})
+    q = str(tmp_path / "q")
+    old = argparse.Namespace(queue=q, world=2, rank=0, batch=4, queue_token="run1")
+    assert [r for r in plate.batch_source(table, old, 0)] == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9]]
+    new = argparse.Namespace(queue=q, world=2, rank=0, batch=4, queue_token="run2")
+    assert [r for r in plate.batch_source(table, new, 0)] == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9]]
+    bare = argparse.Namespace(queue=q, world=2, rank=0, batch=4, queue_token=None)
+    with open(os.path.join(q, "job0000.ctr"), "w") as f:
+        f.write("- 3")  # an exhausted counter of an earlier token-less run
+    with caplog.at_level("ERROR", logger="cpx.plate"):
+        assert list(plate.batch_source(table, bare, 0)) == []
+    assert "already exhausted" in caplog.text

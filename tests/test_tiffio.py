@@ -52,3 +52,51 @@ def test_read_into_matches_imread(tmp_path):
     np.testing.assert_array_equal(of, f)
     with pytest.raises(ValueError):
         tiffio.read_into(str(p), np.zeros((300, 256), np.uint16))
+
+
+def test_read_into_fallback_paths(tmp_path):
+    """read_into's imread-and-cast fallback: an 8-bit plane, a big-endian 16-bit plane and an
+    LZW-compressed 16-bit plane (written by Pillow) land in a uint16 staging buffer exactly as
+    imread(...).astype(np.uint16)."""
+    import struct
+    from PIL import Image
+    rng = np.random.default_rng(8)
+    a8 = rng.integers(0, 256, (33, 47), dtype=np.uint8)
+    tiffio.imwrite(str(tmp_path / "u8.tiff"), a8)
+    out = np.full((33, 47), 9, np.uint16)
+    tiffio.read_into(str(tmp_path / "u8.tiff"), out)
+    np.testing.assert_array_equal(out, tiffio.imread(str(tmp_path / "u8.tiff")).astype(np.uint16))
+    np.testing.assert_array_equal(out, a8.astype(np.uint16))
+    # big-endian: the little-endian file with its header and sample bytes swapped
+    a16 = rng.integers(0, 65536, (21, 30), dtype=np.uint16)
+    le = tiffio.imwrite_bytes(a16)
+    ifd = struct.unpack("<I", le[4:8])[0]
+    n = struct.unpack("<H", le[ifd:ifd + 2])[0]
+    be = bytearray(b"MM" + struct.pack(">H", 42) + struct.pack(">I", ifd))
+    be += le[8:ifd] + struct.pack(">H", n)
+    img_off = None
+    for i in range(n):
+        e = ifd + 2 + 12 * i
+        tag, typ, cnt = struct.unpack("<HHI", le[e:e + 8])
+        if typ == 3 and cnt == 1:
+            val = struct.unpack("<H", le[e + 8:e + 10])[0]
+            be += struct.pack(">HHIHH", tag, typ, cnt, val, 0)
+        else:
+            val = struct.unpack("<I", le[e + 8:e + 12])[0]
+            be += struct.pack(">HHII", tag, typ, cnt, val)
+            if tag == 273:
+                img_off = val
+            if typ == 5:  # rationals live in the data area: swap them there too
+                be_data = struct.pack(">II", *struct.unpack("<II", le[val:val + 8]))
+                le = le[:val] + be_data + le[val + 8:]
+    be += le[ifd + 2 + 12 * n:img_off]
+    be += a16.astype(">u2").tobytes()
+    (tmp_path / "be.tiff").write_bytes(bytes(be))
+    out = np.zeros((21, 30), np.uint16)
+    tiffio.read_into(str(tmp_path / "be.tiff"), out)
+    np.testing.assert_array_equal(out, a16)
+    # LZW-compressed 16-bit (Pillow/libtiff)
+    Image.fromarray(a16).save(str(tmp_path / "lzw.tiff"), compression="tiff_lzw")
+    out = np.zeros((21, 30), np.uint16)
+    tiffio.read_into(str(tmp_path / "lzw.tiff"), out)
+    np.testing.assert_array_equal(out, a16)
