@@ -51,6 +51,10 @@ def parse():
                     help="PCIe-inclusive variant (not the headline): the synthetic batches live in "
                          "pinned host memory and every step copies its planes to the GPU inside the "
                          "timed region (on the pipeline's stream, so the other pipeline overlaps it)")
+    ap.add_argument("--scheduler", choices=("queue", "static"), default="queue",
+                    help="N > 1: 'queue' (default, the product's scheduler: every rank claims the next batch "
+                         "of the job's steps x N batches from one shared counter, cpx.plate.WorkQueue, as "
+                         "cpx.launch ranks do) or 'static' (each rank runs exactly --steps batches)")
     ap.add_argument("--zstack", type=int, default=0,
                     help="configs[4] variant: Z planes per channel, z-max projected on the GPU "
                          "inside every step (default size 2048); not the headline workload")
@@ -118,21 +122,23 @@ def main():
         for q in pipes:
             q.raw = torch.empty_like(pool[0], device=td)
 
-    def run_step(i):
-        """Enqueue step i on pipeline i % P (its stream); returns (pipeline, result slot)."""
+    def run_step(i, k=None):
+        """Enqueue this rank's step i (input batch k, default i) on pipeline i % P (its
+        stream); returns (pipeline, result slot)."""
         q = pipes[i % len(pipes)]
+        i_in = i if k is None else k
         with torch.cuda.stream(streams[i % len(pipes)]):
             if Z > 1:  # a5: z-max projection into the pipeline's raw planes, then the hot path
-                src = pool[i % a.pool]
+                src = pool[i_in % a.pool]
                 if a.host_inputs:
                     src = src.to(td, non_blocking=True)
                 q.dev.zmax(src, q.raw)
                 slot = q.run()
             elif a.host_inputs:  # H2D of the step's planes, then the hot path on the same stream
-                q.raw.copy_(pool[i % a.pool], non_blocking=True)
+                q.raw.copy_(pool[i_in % a.pool], non_blocking=True)
                 slot = q.run()
             else:
-                slot = q.run(pool[i % a.pool])
+                slot = q.run(pool[i_in % a.pool])
         return q, slot
     torch.cuda.synchronize()
 
@@ -140,34 +146,55 @@ def main():
         if world > 1:
             dist.barrier()
 
-    def run_steps(n, record=None):
-        """n steps with every step's results fetched to the host.  Up to P + 1 steps are
+    def run_steps(batches, record=None):
+        """One step per batch index of `batches` (an iterable: a range, or the claims from the
+        shared work queue), every step's results fetched to the host.  Up to P + 1 steps are
         enqueued ahead of the oldest unfetched one; a fetch waits for its own step only and
-        copies on a side stream, so the GPU never idles on the host."""
+        copies on a side stream, so the GPU never idles on the host.  Returns the step count."""
         pend = []
+        done = 0
 
         def fetch_oldest():
             q, slot = pend.pop(0)
             res = q.fetch(slot)
             if record is not None:
                 record.append([int(res.hdr[s]["n_objects"].sum()) for s in ("Nuclei", "Cells", "Cytoplasm")])
-        for i in range(n):
-            pend.append(run_step(i))
+        for k in batches:
+            pend.append(run_step(done, k))
+            done += 1
             if len(pend) > len(pipes):
                 fetch_oldest()
         while pend:
             fetch_oldest()
+        return done
+
+    queue = None
+    if world > 1 and a.scheduler == "queue":
+        # the product's multi-GPU scheduler (cpx.launch -> cpx.plate.WorkQueue): one shared counter
+        # over the job's steps x N batches, each rank claiming the next one when it can take it
+        import tempfile
+        from cpx.plate import WorkQueue
+        qd = [tempfile.mkdtemp(prefix="cpx_benchq_") if rank == 0 else None]
+        dist.broadcast_object_list(qd, src=0)
+        queue = WorkQueue(qd[0], "bench", token=os.path.basename(qd[0]))  # the same token on every rank
+
+    def claims(total):
+        while True:
+            k = queue.take()
+            if k >= total:
+                return
+            yield k
 
     n_obj = []
-    run_steps(a.warmup)
+    run_steps(range(a.warmup))
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run_steps(a.steps, n_obj)
+    n_done = run_steps(claims(a.steps * world) if queue is not None else range(a.steps), n_obj)
     torch.cuda.synchronize()
     barrier()
     dt = shard.max_over_ranks(time.perf_counter() - t0)
-    total_fovs = shard.sum_over_ranks(a.steps * B)
+    total_fovs = shard.sum_over_ranks(n_done * B)
     value = total_fovs / dt
 
     # ---- instrumented steps (outside the timed region): per-stage device time by HIP events on
@@ -306,6 +333,9 @@ def main():
                    "cellpose_model": cfg.model, "diameter": cfg.diameter,
                    "cpnet_weights": os.path.basename(weights) if weights else "seeded-random-init",
                    "tiles_per_fov": n_tiles, "parallelism": f"fov-sharded x{world}",
+                   "scheduler": ("shared work queue (cpx.plate.WorkQueue)" if queue is not None
+                                 else "static per-rank steps"),
+                   "steps_this_rank": n_done,
                    "batches_in_flight_per_gpu": len(pipes)},
         "objects_per_fov": ([round(x / (B * world) * world, 1) for x in np.mean(np.array(n_obj), axis=0)]
                             if n_obj else None),
@@ -320,6 +350,10 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
+        barrier()
+        if queue is not None and rank == 0:
+            import shutil
+            shutil.rmtree(os.path.dirname(queue.path), ignore_errors=True)
         dist.destroy_process_group()
 
 

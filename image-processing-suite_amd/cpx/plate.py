@@ -330,11 +330,18 @@ def _run_sites(a, table, source, chans, state, out, status):
     B, H, W = state["B"], state["H"], state["W"]
     n_pipes = len(pipes)
 
+    # where the time goes (tools/plate_bench.py): host seconds the main thread waited for the
+    # decode threads / for fetch (GPU + D2H), decode-thread seconds, table assembly seconds, and
+    # GPU milliseconds of the uploads and of the pipeline steps (HIP events on the stream)
+    tm = {"decode_wait_s": 0.0, "decode_thread_s": 0.0, "fetch_wait_s": 0.0, "tables_s": 0.0,
+          "h2d_gpu_ms": 0.0, "pipeline_gpu_ms": 0.0}
+
     def read_fov(paths, dst):
         """Decode the site's C planes straight into dst [C][H][W] (a slice of the pinned staging
         buffer); False when any of them cannot be read (missing, undecodable, other shape): the
         reference's producer then sends (site_id, None) and the consumer records the site as
         {'status': 'empty', 'n_cells': 0} (Cellpose_GPU_s3fs.py:76-87, 123-136)."""
+        t0 = time.perf_counter()
         try:
             for c, p in enumerate(paths):
                 tiffio.read_into(p, dst[c])
@@ -343,6 +350,8 @@ def _run_sites(a, table, source, chans, state, out, status):
             log.error("failed on site %s: %s", paths, e)
             dst[...] = 0
             return False
+        finally:
+            tm["decode_thread_s"] += time.perf_counter() - t0
 
     batches = [first]  # row positions per batch, grown as batches are claimed
     inflight = []  # (batch index, pipeline, slot, upload event, empty flags)
@@ -383,33 +392,47 @@ def _run_sites(a, table, source, chans, state, out, status):
         hn[len(idx):] = 0
         return [pool.submit(read_fov, site_files(r), hn[k]) for k, r in enumerate(idx)]
 
+    def retire():
+        obi, q, sl, evs, em = inflight.pop(0)
+        t0 = time.perf_counter()
+        res = q.fetch(sl)
+        t1 = time.perf_counter()
+        record(obi, res, em)
+        tm["fetch_wait_s"] += t1 - t0
+        tm["tables_s"] += time.perf_counter() - t1
+        tm["h2d_gpu_ms"] += evs[0].elapsed_time(evs[1])
+        tm["pipeline_gpu_ms"] += evs[1].elapsed_time(evs[2])
+
     with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, a.threads)) as pool:
         pending = decode(0, pool)
         bi = 0
         while bi < len(batches):
+            t0 = time.perf_counter()
             empty = [not f.result() for f in pending]
+            tm["decode_wait_s"] += time.perf_counter() - t0
             p_i = bi % n_pipes
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             with torch.cuda.stream(streams[p_i]):
+                evs[0].record(streams[p_i])
                 pipes[p_i].raw.copy_(hosts[p_i], non_blocking=True)
-                up = torch.cuda.Event()
-                up.record(streams[p_i])
-                uploads[p_i] = up
+                evs[1].record(streams[p_i])
+                uploads[p_i] = evs[1]
                 slot = pipes[p_i].run()
-            inflight.append((bi, pipes[p_i], slot, up, empty))
+                evs[2].record(streams[p_i])
+            inflight.append((bi, pipes[p_i], slot, evs, empty))
             nxt = next(source, None)  # claim and decode the next batch while this one runs
             if nxt is not None:
                 batches.append(nxt)
                 pending = decode(bi + 1, pool)
             if len(inflight) > n_pipes:   # results in batch order, one step behind the GPU
-                obi, q, sl, _, em = inflight.pop(0)
-                record(obi, q.fetch(sl), em)
+                retire()
             bi += 1
         while inflight:
-            obi, q, sl, _, em = inflight.pop(0)
-            record(obi, q.fetch(sl), em)
+            retire()
     secs = time.perf_counter() - t_start
     nsites = sum(len(b) for b in batches)
-    state["timing"] = {"seconds": secs, "threads": a.threads, "batch": B, "pipes": n_pipes}
+    state["timing"] = {"seconds": secs, "threads": a.threads, "batch": B, "pipes": n_pipes,
+                       **{k: round(v, 3) for k, v in tm.items()}}
     log.info("%d sites in %.2f s: %.1f FOV/s (decode threads %d, batch %d, pipelines %d)",
              nsites, secs, nsites / max(secs, 1e-9), a.threads, B, n_pipes)
     return nsites

@@ -74,7 +74,13 @@ def main():
                           "pipelines": t["pipes"], "tiff_GB": round(tif_bytes / 1e9, 3),
                           "tiff_decode_GBs": round(tif_bytes / 1e9 / t["seconds"], 2),
                           "cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
-                          "generation_s": round(gen_s, 1)}), flush=True)
+                          "generation_s": round(gen_s, 1),
+                          # where the time goes (cpx.plate._run_sites): main-thread waits on the TIFF
+                          # decode threads and on fetch (GPU + D2H), the decode threads' own seconds,
+                          # table assembly, and the GPU time of the uploads and of the pipeline steps
+                          "split": {k: t[k] for k in ("decode_wait_s", "decode_thread_s", "fetch_wait_s",
+                                                      "tables_s", "h2d_gpu_ms", "pipeline_gpu_ms")}}),
+              flush=True)
     finally:
         shutil.rmtree(root, ignore_errors=True)
 
