@@ -133,6 +133,8 @@ SIGNATURES = {
     "cpx_cpnet_x3_cfg": (_I, [_I, _I, _I, _I, _P]),
     "cpx_cpnet_x3_conv": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _I, _P, _P, _I,
                                _P, _P, _I, _P, _P, _I, _P, _P]),
+    "cpx_cpnet_x3_conv_proj": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P, _I, _P, _P, _I,
+                                    _P, _P, _I, _P]),
     "cpx_cpnet_x3_stem": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cpx_cpnet_x3_pool": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cpx_cpnet_x3_style": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _I, _P]),

@@ -24,6 +24,9 @@ from ._lib import check
 from .cpnet import CPnet
 
 X3_VARIANT = int(os.environ.get("CPX_X3_VARIANT", "0"))
+# fold each down block's (and the deepest up block's) 1x1 residual projection into the block's
+# second 3x3 convolution (cpx_cpnet_x3_conv_proj); CPX_X3_FOLD=0 keeps the separate 1x1 pass
+X3_FOLD = os.environ.get("CPX_X3_FOLD", "1") != "0"
 
 
 def split_f16(w: np.ndarray):
@@ -102,21 +105,30 @@ class FusedCPnetX3:
         def dv(t):
             return t.detach().float().contiguous().to(td)
 
-        def conv_pack(w, ks):
+        def conv_pack(w, ks, cfg_cin=None):
+            """pack for the tile configuration of a ks x ks conv of cfg_cin (default: w's own
+            input channels) -> w's output channels"""
             cout, cin = w.shape[0], w.shape[1]
             bm = ct.c_int()
-            check(self.lib.cpx_cpnet_x3_cfg(ks, cin, cout, self.variant, ct.byref(bm)), "cpx_cpnet_x3_cfg")
+            check(self.lib.cpx_cpnet_x3_cfg(ks, cin if cfg_cin is None else cfg_cin, cout, self.variant,
+                                            ct.byref(bm)), "cpx_cpnet_x3_cfg")
             return torch.from_numpy(pack_conv(w.detach().float().numpy(), bm.value)).to(td)
+
+        # the folded projections exist for variant 0's tile configurations
+        self.fold = X3_FOLD and self.variant == 0
 
         self.down = []
         for blk in net.down:
             wp, bp = _fold_proj(blk.proj)
             bns = [_bn_affine(blk.conv[t][0]) for t in range(4)]
             b = [blk.conv[t][-1].bias.detach().float() for t in range(4)]
+            cout_b = blk.conv[0][-1].out_channels
             d = dict(bn=[(dv(s), dv(h)) for s, h in bns], b=[dv(x) for x in b], b1p=dv(b[1] + bp),
                      pk=[None if t == 0 and blk is net.down[0] else conv_pack(blk.conv[t][-1].weight, 3)
                          for t in range(4)],
-                     wp=None if blk is net.down[0] else conv_pack(wp, 1), cout=blk.conv[0][-1].out_channels)
+                     wp=None if blk is net.down[0] else conv_pack(wp, 1), cout=cout_b,
+                     # the projection packed as extra one-tap slabs of the block's second conv
+                     wpf=None if blk is net.down[0] or not self.fold else conv_pack(wp, 3, cfg_cin=cout_b))
             if blk is net.down[0]:
                 d["stem_w"] = dv(blk.conv[0][-1].weight.reshape(32, 18))
                 d["stem_wp"] = dv(wp.reshape(32, 2))
@@ -141,9 +153,13 @@ class FusedCPnetX3:
             convs = [blk.conv0, blk.conv1.conv, blk.conv2.conv, blk.conv3.conv]
             bns = [_bn_affine(c[0]) for c in convs]
             b = [c[-1].bias.detach().float() for c in convs]
+            cout_b = convs[0][-1].out_channels
             self.up.append(dict(bn=[(dv(s), dv(h)) for s, h in bns], b=[dv(x) for x in b], b1p=dv(b[1] + bp),
                                 pk=[conv_pack(c[-1].weight, 3) for c in convs], wp=conv_pack(wp, 1),
-                                cout=convs[0][-1].out_channels))
+                                cout=cout_b,
+                                # the deepest up block reads its projection input at full size:
+                                # folded like the down blocks' (the others read it upsampled)
+                                wpf=conv_pack(wp, 3, cfg_cin=cout_b) if self.fold and blk is net.up[-1] else None))
         self.bn_out = tuple(dv(x) for x in _bn_affine(net.output[0]))
         self.head_w = dv(net.output[-1].weight.reshape(net.output[-1].out_channels, -1))
         self.head_b = dv(net.output[-1].bias)
@@ -180,6 +196,18 @@ class FusedCPnetX3:
             _p(self.head_w) if head else None, _p(self.head_b) if head else None, self.nout if head else 0,
             _p(ho), self._ovf_p(N)), "cpx_cpnet_x3_conv")
         return (ho,) if head else (yo, zo)
+
+    def _conv_proj(self, x, pk, cout, bias, x2, pk2, style=None, bn=None, y=True):
+        """3x3 conv of x + the folded 1x1 projection of x2 (cpx_cpnet_x3_conv_proj)."""
+        N, H, W, cin = x.shape
+        yo = self._empty(N, H, W, cout) if y else None
+        zo = self._empty(N, H, W, cout)
+        scale, shift = bn if bn is not None else (None, None)
+        st, st_stride = (None, 0) if style is None else style
+        check(self.lib.cpx_cpnet_x3_conv_proj(
+            self.dev.h, self.variant, _p(x), N, H, W, cin, cout, _p(pk), _p(x2), x2.shape[-1], _p(pk2), _p(bias),
+            st, st_stride, _p(scale), _p(shift), 1, _p(yo), _p(zo), 0, self._ovf_p(N)), "cpx_cpnet_x3_conv_proj")
+        return yo, zo
 
     def _proj(self, x, blk):
         return self._conv(x, blk["wp"], blk["cout"], None, ks=1, relu=False, y=True, z=False)[0]
@@ -225,11 +253,15 @@ class FusedCPnetX3:
         for n, d in enumerate(self.down):
             if n == 0:
                 p, z = self._stem(x, d)
+                x1, z = self._conv(z, d["pk"][1], d["cout"], d["b1p"], res=p, bn=d["bn"][2], y=True)
             else:
                 xin, z0 = self._pool(xd[-1], d["bn"][0])
-                p = self._proj(xin, d)
                 _, z = self._conv(z0, d["pk"][0], d["cout"], d["b"][0], bn=d["bn"][1])
-            x1, z = self._conv(z, d["pk"][1], d["cout"], d["b1p"], res=p, bn=d["bn"][2], y=True)
+                if d["wpf"] is not None:
+                    x1, z = self._conv_proj(z, d["pk"][1], d["cout"], d["b1p"], xin, d["wpf"], bn=d["bn"][2])
+                else:
+                    p = self._proj(xin, d)
+                    x1, z = self._conv(z, d["pk"][1], d["cout"], d["b1p"], res=p, bn=d["bn"][2], y=True)
             _, z = self._conv(z, d["pk"][2], d["cout"], d["b"][2], bn=d["bn"][3])
             if n < nd - 1:
                 xo, _ = self._conv(z, d["pk"][3], d["cout"], d["b"][3], res=x1, y=True, z=False)
@@ -243,13 +275,17 @@ class FusedCPnetX3:
             u = self.up[n]
             so = self.style_off[n]
             sty = [(ct.c_void_p(S.data_ptr() + 4 * o), J) for o in so]
-            p = self._proj(x_small, u)
+            p = None if u["wpf"] is not None else self._proj(x_small, u)
             # below the deepest level the block input is nn.Upsample(x_small): z0 (its
             # BatchNorm+ReLU, pointwise) stays at the small size and is read upsampled
             _, z = self._conv(z0, u["pk"][0], u["cout"], u["b"][0], res=xd[n], style=sty[0], bn=u["bn"][1],
                               in_up=(n < len(self.up) - 1))
-            x1, z = self._conv(z, u["pk"][1], u["cout"], u["b1p"], res=p, res_up=(n < len(self.up) - 1),
-                               style=sty[1], bn=u["bn"][2], y=True)
+            if p is None:
+                x1, z = self._conv_proj(z, u["pk"][1], u["cout"], u["b1p"], x_small, u["wpf"], style=sty[1],
+                                        bn=u["bn"][2])
+            else:
+                x1, z = self._conv(z, u["pk"][1], u["cout"], u["b1p"], res=p, res_up=(n < len(self.up) - 1),
+                                   style=sty[1], bn=u["bn"][2], y=True)
             _, z = self._conv(z, u["pk"][2], u["cout"], u["b"][2], style=sty[2], bn=u["bn"][3])
             if n > 0:
                 x_small, z0 = self._conv(z, u["pk"][3], u["cout"], u["b"][3], res=x1, bn=self.up[n - 1]["bn"][0],

@@ -109,6 +109,11 @@ struct X3Epi {
   int n_head;
   int* ovf;
   int in_up;  // the input is the (H/2) x (W/2) tensor read 2x nearest-upsampled
+  // block projection folded into the convolution (k_conv_x3 with CIN2 > 0): after the 3x3 slabs
+  // of `in`, CIN2 / 16 one-tap slabs of in2 [N][H][W][CIN2] (split) with weights wpk2
+  // [COUT/BM][CIN2/16][BM][hi|lo][16] accumulate conv1x1(in2, wp) into the same sums
+  const uint4* in2;
+  const uint4* wpk2;
 };
 
 // Epilogue of a 3x3 / 1x1 convolution tile on its fp32 values (acc0 = the joined sums): bias,
@@ -318,7 +323,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
   flag();
 }
 
-template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE>
+template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, int CIN2 = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, int N, int H,
                int W, int tiles_x, int tiles_y) {
@@ -327,6 +332,9 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   constexpr int MWV = BM / (32 * WM), PW = NWV / MWV;
   constexpr int HY = TY + KS - 1, HX = TX + KS - 1, NPIX = HY * HX;
   constexpr int NCH = CIN / 16;
+  constexpr int NCH2 = CIN2 / 16, QI2 = CIN2 / 4;     // folded projection slabs (one tap each)
+  constexpr int NW2 = BM * 4 / 64;                    // their weight DMA rows
+  static_assert(CIN2 == 0 || (KS == 3 && CIN2 % 16 == 0), "projection slabs fold into a 3x3 conv");
   constexpr int P = TY * TX, NS = (P + 31) / 32;
   constexpr int SW = T * BM * 4;                      // 16-byte slots [tap][BM][4 chunks]
   constexpr int SI = (NPIX * 4 + 63) / 64 * 64;       // [halo pixel][4 chunks]
@@ -365,33 +373,53 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   const int iu = ep.in_up, Wi = W >> iu;
   const uint4* inb = in + (long long)n * (H >> iu) * Wi * QI;
 
-  // DMA sources: weights (lane-constant swizzle), halo chunk offsets (slab-independent)
+  // DMA sources: weights (lane-constant swizzle), halo pixel + chunk (slab-independent)
   const int fW = (lane & ~3) | ((lane & 3) ^ ((lane >> 4) & 3));
-  int inOff[JI];
+  int inPC[JI];  // source pixel * 4 + swizzled chunk, -1 outside the image
 #pragma unroll
   for (int jj = 0; jj < JI; ++jj) {
     const int si = (wid + NWV * jj) * 64 + lane;
     const int hp = si >> 2, cq = si & 3;
     const int hy = hp / HX, hx = hp - (hp / HX) * HX;
     const int gy = ty0 + hy - HALO, gx = tx0 + hx - HALO;
-    inOff[jj] = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-                    ? ((gy >> iu) * Wi + (gx >> iu)) * QI + (cq ^ swz4(hp)) : -1;
+    inPC[jj] = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+                   ? ((gy >> iu) * Wi + (gx >> iu)) * 4 + (cq ^ swz4(hp)) : -1;
   }
+  const uint4* inb2 = CIN2 ? ep.in2 + (long long)n * H * W * QI2 : nullptr;
+  // slab ch < NCH: the 3x3 weights and the halo of `in`; ch >= NCH: a projection slab (one tap
+  // of weights, the halo of in2 — only its centre is read)
   auto issue = [&](int ch, int buf) {
-    const uint4* wsl = wpk + (long long)(nb * NCH + ch) * SW;
     uint4* dst = smem + buf * SB;
+    if (CIN2 == 0 || ch < NCH) {
+      const uint4* wsl = wpk + (long long)(nb * NCH + ch) * SW;
 #pragma unroll
-    for (int jj = 0; jj < JW; ++jj) {
-      const int j = wid + NWV * jj;
-      if (j < NWW)
-        __builtin_amdgcn_global_load_lds((glb_void_t*)(wsl + j * 64 + fW), (lds_void_t*)(dst + j * 64), 16, 0, 0);
-    }
+      for (int jj = 0; jj < JW; ++jj) {
+        const int j = wid + NWV * jj;
+        if (j < NWW)
+          __builtin_amdgcn_global_load_lds((glb_void_t*)(wsl + j * 64 + fW), (lds_void_t*)(dst + j * 64), 16, 0, 0);
+      }
 #pragma unroll
-    for (int jj = 0; jj < JI; ++jj) {
-      const int j = wid + NWV * jj;
-      if (j < NWIN) {
-        const uint4* src = inOff[jj] >= 0 ? inb + inOff[jj] + ch * 4 : &g_x3_zero16;
-        __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(dst + SW + j * 64), 16, 0, 0);
+      for (int jj = 0; jj < JI; ++jj) {
+        const int j = wid + NWV * jj;
+        if (j < NWIN) {
+          const uint4* src = inPC[jj] >= 0 ? inb + (long long)(inPC[jj] >> 2) * QI + (inPC[jj] & 3) + ch * 4
+                                           : &g_x3_zero16;
+          __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(dst + SW + j * 64), 16, 0, 0);
+        }
+      }
+    } else {
+      const int c2 = ch - NCH;
+      const uint4* wsl = ep.wpk2 + (long long)(nb * NCH2 + c2) * (BM * 4);
+      if (wid < NW2)
+        __builtin_amdgcn_global_load_lds((glb_void_t*)(wsl + wid * 64 + fW), (lds_void_t*)(dst + wid * 64), 16, 0, 0);
+#pragma unroll
+      for (int jj = 0; jj < JI; ++jj) {
+        const int j = wid + NWV * jj;
+        if (j < NWIN) {
+          const uint4* src = inPC[jj] >= 0 ? inb2 + (long long)(inPC[jj] >> 2) * QI2 + (inPC[jj] & 3) + c2 * 4
+                                           : &g_x3_zero16;
+          __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(dst + SW + j * 64), 16, 0, 0);
+        }
       }
     }
   };
@@ -424,53 +452,64 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int ch = 0; ch < NCH; ++ch) {
-    if (ch + 1 < NCH) issue(ch + 1, (ch + 1) & 1);
-    const uint4* sb = smem + (ch & 1) * SB;
-    auto mma = [&](auto cnt) {
-      constexpr int C = decltype(cnt)::value;
-      if constexpr (C > 0) {
-        auto tapbody = [&](int tap) {
-          const int ky = tap / KS, kx = tap - KS * (tap / KS);
-          f16x8 ah[WM], al[WM];
+  constexpr int NCHT = NCH + NCH2;
+  // weights of tap `tw` against the halo at (ky, kx) of slab buffer sb, over C subtiles
+  auto tapbody = [&](auto cnt, const uint4* sb, int tw, int ky, int kx) {
+    constexpr int C = decltype(cnt)::value;
+    f16x8 ah[WM], al[WM];
 #pragma unroll
-          for (int m = 0; m < WM; ++m) {
-            ah[m] = __builtin_bit_cast(f16x8, sb[aS[m] + tap * BM * 4]);
-            al[m] = __builtin_bit_cast(f16x8, sb[(aS[m] ^ 2) + tap * BM * 4]);
-          }
+    for (int m = 0; m < WM; ++m) {
+      ah[m] = __builtin_bit_cast(f16x8, sb[aS[m] + tw * BM * 4]);
+      al[m] = __builtin_bit_cast(f16x8, sb[(aS[m] ^ 2) + tw * BM * 4]);
+    }
 #pragma unroll
-          for (int j = 0; j < C; ++j) {
-            const int hp = hp0[j] + ky * HX + kx;
-            const int bs = SW + hp * 4 + (h ^ swz4(hp));
-            const f16x8 bh = __builtin_bit_cast(f16x8, sb[bs]);
-            const f16x8 bl = __builtin_bit_cast(f16x8, sb[bs ^ 2]);
+    for (int j = 0; j < C; ++j) {
+      const int hp = hp0[j] + ky * HX + kx;
+      const int bs = SW + hp * 4 + (h ^ swz4(hp));
+      const f16x8 bh = __builtin_bit_cast(f16x8, sb[bs]);
+      const f16x8 bl = __builtin_bit_cast(f16x8, sb[bs ^ 2]);
 #pragma unroll
-            for (int m = 0; m < WM; ++m) {
-              acc0[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh, acc0[m][j], 0, 0, 0);
-              acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bl, acc1[m][j], 0, 0, 0);
-              acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bh, acc1[m][j], 0, 0, 0);
-            }
-          }
-        };
-        // single-fragment waves: all taps unrolled, the next tap's reads scheduled under this
-        // tap's MFMAs; larger wave tiles keep one tap per iteration (register budget)
-        if constexpr (WM * WN == 1) {
-#pragma unroll
-          for (int tap = 0; tap < T; ++tap) tapbody(tap);
-        } else {
-#pragma unroll 1
-          for (int tap = 0; tap < T; ++tap) tapbody(tap);
-        }
+      for (int m = 0; m < WM; ++m) {
+        acc0[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh, acc0[m][j], 0, 0, 0);
+        acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bl, acc1[m][j], 0, 0, 0);
+        acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bh, acc1[m][j], 0, 0, 0);
       }
-    };
+    }
+  };
+  // the wave's subtile count as a compile-time constant
+  auto per_nsub = [&](auto body) {
     if constexpr (WN == 1) {
-      if (nsub == 1) mma(std::integral_constant<int, 1>{});
+      if (nsub == 1) body(std::integral_constant<int, 1>{});
     } else if constexpr (WN == 2) {
-      if (nsub == 2) mma(std::integral_constant<int, 2>{});
-      else if (nsub == 1) mma(std::integral_constant<int, 1>{});
+      if (nsub == 2) body(std::integral_constant<int, 2>{});
+      else if (nsub == 1) body(std::integral_constant<int, 1>{});
     } else {
       static_assert(WN <= 2, "WN");
     }
+  };
+  for (int ch = 0; ch < NCH; ++ch) {
+    if (ch + 1 < NCHT) issue(ch + 1, (ch + 1) & 1);
+    const uint4* sb = smem + (ch & 1) * SB;
+    per_nsub([&](auto cnt) {
+      if constexpr (WM * WN == 1) {
+        // single-fragment waves: all taps unrolled, the next tap's reads scheduled under this
+        // tap's MFMAs; larger wave tiles keep one tap per iteration (register budget)
+#pragma unroll
+        for (int tap = 0; tap < T; ++tap) tapbody(cnt, sb, tap, tap / KS, tap % KS);
+      } else {
+#pragma unroll 1
+        for (int tap = 0; tap < T; ++tap) tapbody(cnt, sb, tap, tap / KS, tap % KS);
+      }
+    });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // folded projection: one centre tap per slab of in2 (weight slot 0)
+#pragma unroll 1
+  for (int ch = NCH; ch < NCHT; ++ch) {
+    if (ch + 1 < NCHT) issue(ch + 1, (ch + 1) & 1);
+    const uint4* sb = smem + (ch & 1) * SB;
+    per_nsub([&](auto cnt) { tapbody(cnt, sb, 0, HALO, HALO); });
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -613,15 +652,33 @@ bool x3_cfg(int ks, int cin, int cout, int variant, X3Cfg* c) {
   return true;
 }
 
-template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE>
+template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, int CIN2 = 0>
 int x3_run(cpx_ctx* ctx, const void* in, const void* wpk, const X3Epi& ep, int N, int H, int W) {
   const int tx = cpx_div_up(W, TX), ty = cpx_div_up(H, TY);
   const long long blocks = (long long)N * tx * ty * (COUT / BM);  // (tile, output-channel block) items
   CPX_REQUIRE(blocks < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv: too many tiles");
-  hipLaunchKernelGGL((k_conv_x3<KS, CIN, COUT, BM, TY, TX, WM, WN, WPE>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((k_conv_x3<KS, CIN, COUT, BM, TY, TX, WM, WN, WPE, CIN2>), dim3((unsigned)blocks),
                      dim3(512), 0, ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N, H, W, tx, ty);
   CPX_CHECK_LAUNCH("k_conv_x3");
   return CPX_OK;
+}
+
+// 3x3 convolution + folded block projection (cin2 > 0): the instances the CPnet schedule uses
+// (each down block's second convolution, whose residual is the projection of the pooled block
+// input, and the deepest up block's, at the same resolution); tile configurations as x3_cfg
+int x3_launch_proj(cpx_ctx* ctx, int cin, int cout, int cin2, int variant, const void* in, const void* wpk,
+                   const X3Epi& ep, int N, int H, int W) {
+#define X3_P(CI, CO, C2, V, BM_, TY_, TX_, WM_, WN_, WPE_)                                \
+  if (cin == CI && cout == CO && cin2 == C2 && variant == V)                               \
+    return x3_run<3, CI, CO, BM_, TY_, TX_, WM_, WN_, WPE_, C2>(ctx, in, wpk, ep, N, H, W);
+  X3_P(64, 64, 32, 0, 32, 16, 16, 1, 1, 4)
+  X3_P(128, 128, 64, 0, 32, 8, 28, 1, 1, 4)
+  X3_P(256, 256, 128, 0, 32, 8, 28, 1, 1, 4)
+  X3_P(256, 256, 256, 0, 32, 8, 28, 1, 1, 4)
+#undef X3_P
+  cpx_set_error("cpx_cpnet_x3_conv_proj: no instance for %d -> %d channels + projection of %d (variant %d)",
+                cin, cout, cin2, variant);
+  return CPX_ERR_SHAPE;
 }
 
 int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* in, const void* wpk,
@@ -899,8 +956,28 @@ extern "C" int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* 
               CPX_ERR_ARG, "cpx_cpnet_x3_conv: head needs a 3x3 conv with cout 32, no z_out, 1..4 outputs");
   CPX_REQUIRE(!z_up || z_out, CPX_ERR_ARG, "cpx_cpnet_x3_conv: z_up without z_out");
   X3Epi ep{bias, (const uint4*)res, style, scale, shift, (uint4*)y_out, (uint4*)z_out, res_up, relu,
-           z_up, style_stride, head_w, head_b, head_out, n_head, ovf, in_up};
+           z_up, style_stride, head_w, head_b, head_out, n_head, ovf, in_up, nullptr, nullptr};
   return x3_launch(ctx, ks, cin, cout, variant, in, wpk, ep, N, H, W);
+}
+
+extern "C" int cpx_cpnet_x3_conv_proj(cpx_ctx* ctx, int variant, const void* in, int N, int H, int W,
+                                      int cin, int cout, const void* wpk, const void* in2, int cin2,
+                                      const void* wpk2, const float* bias, const float* style,
+                                      int style_stride, const float* scale, const float* shift, int relu,
+                                      void* y_out, void* z_out, int z_up, int* ovf) {
+  CPX_REQUIRE(ctx && in && wpk && in2 && wpk2 && (y_out || z_out), CPX_ERR_ARG,
+              "cpx_cpnet_x3_conv_proj: null argument");
+  CPX_REQUIRE(N > 0 && H > 0 && W > 0 && cin2 > 0 && cin2 % 16 == 0, CPX_ERR_ARG, "cpx_cpnet_x3_conv_proj: bad sizes");
+  CPX_REQUIRE(!(scale == nullptr) == !(shift == nullptr), CPX_ERR_ARG,
+              "cpx_cpnet_x3_conv_proj: scale and shift go together");
+  CPX_REQUIRE(((uintptr_t)in | (uintptr_t)wpk | (uintptr_t)in2 | (uintptr_t)wpk2 | (uintptr_t)y_out |
+               (uintptr_t)z_out) % 16 == 0, CPX_ERR_ARG, "cpx_cpnet_x3_conv_proj: misaligned buffers");
+  CPX_REQUIRE(!style || (style_stride >= cout && style_stride % 4 == 0 && ((uintptr_t)style % 16) == 0),
+              CPX_ERR_ARG, "cpx_cpnet_x3_conv_proj: style needs a 16-byte aligned [N][stride >= cout] table");
+  CPX_REQUIRE(!z_up || z_out, CPX_ERR_ARG, "cpx_cpnet_x3_conv_proj: z_up without z_out");
+  X3Epi ep{bias, nullptr, style, scale, shift, (uint4*)y_out, (uint4*)z_out, 0, relu, z_up, style_stride,
+           nullptr, nullptr, nullptr, 0, ovf, 0, (const uint4*)in2, (const uint4*)wpk2};
+  return x3_launch_proj(ctx, cin, cout, cin2, variant, in, wpk, ep, N, H, W);
 }
 
 extern "C" int cpx_cpnet_x3_stem(cpx_ctx* ctx, const float* x, int N, int H, int W,

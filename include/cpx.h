@@ -456,6 +456,15 @@ int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* in, int in_
                       const float* shift, int relu, void* y_out, void* z_out, int z_up,
                       const float* head_w, const float* head_b, int n_head, float* head_out,
                       int* ovf);
+/* 3x3 convolution (pad 1) with its block's residual projection folded in: the sums are
+ * conv3x3(in, wpk) + conv1x1(in2, wpk2) with in2 [N][H][W][cin2] split (the block input the
+ * 1x1 projection reads; wpk2 packed like a 1x1 conv with the 3x3's bm), then the epilogue of
+ * cpx_cpnet_x3_conv without a residual tensor (bias = conv bias + projection bias).  Replaces a
+ * cpx_cpnet_x3_conv(ks = 1) pass + the residual read of the 3x3 convolution.                 */
+int cpx_cpnet_x3_conv_proj(cpx_ctx* ctx, int variant, const void* in, int N, int H, int W, int cin,
+                           int cout, const void* wpk, const void* in2, int cin2, const void* wpk2,
+                           const float* bias, const float* style, int style_stride, const float* scale,
+                           const float* shift, int relu, void* y_out, void* z_out, int z_up, int* ovf);
 /* stem on the fp32 network input x [N][H][W][2] (CPX_TILE_F32_NHWC tiles): z0 = relu(scale0 x
  * + shift0), z_out = relu(scale1 (conv3x3(z0, w0) + bias0) + shift1), p_out = conv1x1(x, wp),
  * fp32 arithmetic, split stores (32 channels).                                               */

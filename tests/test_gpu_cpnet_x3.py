@@ -131,6 +131,55 @@ def test_x3_conv_epilogue_vs_fp64(dev, ks, cin, cout, H, W, variant):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cin,cin2,H,W,with_style", [(64, 32, 20, 18, False), (128, 64, 30, 29, False),
+                                                     (256, 128, 14, 14, False), (256, 256, 16, 12, True)])
+def test_x3_conv_proj_vs_fp64(dev, cin, cin2, H, W, with_style):
+    """cpx_cpnet_x3_conv_proj: a 3x3 convolution with the block's 1x1 projection folded in as
+    extra one-tap slabs (every down block's second convolution and the deepest up block's) vs
+    fp64 conv3x3(x) + conv1x1(x2) + bias (+ style), BatchNorm, ReLU on the same split operands."""
+    lib, td = dev.lib, dev.torch_device
+    rng = np.random.default_rng(cin + cin2)
+    N, cout = 2, cin
+    bm = ct.c_int()
+    assert lib.cpx_cpnet_x3_cfg(3, cin, cout, 0, ct.byref(bm)) == 0
+    x = rng.standard_normal((N, H, W, cin)).astype(np.float32)
+    x2 = rng.standard_normal((N, H, W, cin2)).astype(np.float32)
+    w = (rng.standard_normal((cout, cin, 3, 3)) * (2.0 / (cin * 9)) ** 0.5).astype(np.float32)
+    wp = (rng.standard_normal((cout, cin2, 1, 1)) * (2.0 / cin2) ** 0.5).astype(np.float32)
+    bias = (0.1 * rng.standard_normal(cout)).astype(np.float32)
+    style = (0.3 * rng.standard_normal((N, cout + 8))).astype(np.float32)
+    scale = (1 + 0.2 * rng.standard_normal(cout)).astype(np.float32)
+    shift = (0.1 * rng.standard_normal(cout)).astype(np.float32)
+    pk, pk2 = (torch.from_numpy(pack_conv(a, bm.value)).to(td) for a in (w, wp))
+    xd, x2d = _dev_split(x, td), _dev_split(x2, td)
+    yd = torch.empty((N, H, W, cout), dtype=torch.int32, device=td)
+    zd = torch.empty((N, H, W, cout), dtype=torch.int32, device=td)
+    bd, sd, scd, shd = (torch.from_numpy(a).to(td) for a in (bias, style, scale, shift))
+    ovf = torch.zeros(N, dtype=torch.int32, device=td)
+    P = lambda t: ct.c_void_p(t.data_ptr())  # noqa: E731
+    rc = lib.cpx_cpnet_x3_conv_proj(dev.h, 0, P(xd), N, H, W, cin, cout, P(pk), P(x2d), cin2, P(pk2), P(bd),
+                                    P(sd) if with_style else None, cout + 8 if with_style else 0, P(scd), P(shd), 1,
+                                    P(yd), P(zd), 0, P(ovf))
+    assert rc == 0, lib.cpx_last_error()
+    torch.cuda.synchronize()
+    w64, wp64 = (torch.from_numpy(from_split(to_split(a.transpose(0, 2, 3, 1))).astype(np.float64)).permute(0, 3, 1, 2)
+                 for a in (w, wp))
+    x64, x264 = _ref(x).permute(0, 3, 1, 2), _ref(x2).permute(0, 3, 1, 2)
+    t = F.conv2d(x64, w64, padding=1) + F.conv2d(x264, wp64) + torch.from_numpy(bias.astype(np.float64))[None, :, None, None]
+    mag = F.conv2d(x64.abs(), w64.abs(), padding=1) + F.conv2d(x264.abs(), wp64.abs())
+    u = t + (torch.from_numpy(style[:, :cout].astype(np.float64))[:, :, None, None] if with_style else 0)
+    z = torch.relu(torch.from_numpy(scale.astype(np.float64))[None, :, None, None] * u +
+                   torch.from_numpy(shift.astype(np.float64))[None, :, None, None])
+    tol_t = 1e-6 * (mag + 1.0) + 2.0 ** -21 * t.abs()
+    y_got = torch.from_numpy(_host_split(yd)).permute(0, 3, 1, 2).double()
+    assert ((y_got - t).abs() <= tol_t).all(), float((y_got - t).abs().max())
+    z_got = torch.from_numpy(_host_split(zd)).permute(0, 3, 1, 2).double()
+    tol = tol_t * np.abs(scale).max() + 2.0 ** -21 * z.abs()
+    assert ((z_got - z).abs() <= tol).all(), float((z_got - z).abs().max())
+    assert int(ovf.sum()) == 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cin,cout,variant", [(64, 32, 0), (128, 64, 0), (256, 128, 0), (64, 32, 1), (128, 64, 1),
                                               (256, 128, 1)])
 def test_x3_conv_in_up(dev, cin, cout, variant):

@@ -26,6 +26,10 @@ WEIGHTS = os.path.join(REPO, "image-processing-suite_amd", "cpx", "weights", "cp
 SETS = ("Nuclei", "Cells", "Cytoplasm")
 
 
+def _say(*a):
+    print("[recovery]", *a, flush=True)  # progress (the fp32 module's first MIOpen kernels build slowly)
+
+
 def _cfg(**kw):
     from cpx.pipeline import PipelineConfig
     return PipelineConfig(H=2080, W=2080, C=5, batch=2, weights=WEIGHTS if os.path.exists(WEIGHTS) else None, **kw)
@@ -61,6 +65,7 @@ def test_overflow_fov_rerun_in_fp32_and_flags_cleared(dev, batch):
     illum, raw = batch
     pipe = FovPipeline(dev, _cfg(), illum)
     base = pipe.fetch(pipe.run(raw))
+    _say("f16x3 batch done")
     assert not base.recovered.any() and not base.failed.any()
     # one FOV flagged (as the kernels flag an overflowing network tile): only it is re-run, in fp32
     sl = pipe._slots[pipe.run(raw)]
@@ -68,10 +73,12 @@ def test_overflow_fov_rerun_in_fp32_and_flags_cleared(dev, batch):
     sl["cpnet_ovf"][nt + 3:nt + 4].fill_(1)
     torch.cuda.synchronize()
     res = pipe.fetch()
+    _say("flagged FOV re-run in fp32")
     assert res.recovered.tolist() == [0, RECOVER_FP32]
     _same_tables(res, base, 0, 0)
     ref = FovPipeline(dev, dataclasses.replace(_cfg(cpnet_precision="fp32"), batch=1), illum, recovery=False)
     r32 = [ref.fetch(ref.run(raw[b * 5:(b + 1) * 5])) for b in range(2)]
+    _say("fp32 reference pipeline done")
     _same_tables(res, r32[1], 1, 0, exact=False)
     # a genuine overflow: the f16x3 network's stem weights scaled up, every tile overflows, every
     # FOV is re-run in fp32; restoring them, the next batch runs on f16x3 again (flags cleared)
@@ -79,6 +86,7 @@ def test_overflow_fov_rerun_in_fp32_and_flags_cleared(dev, batch):
     keep = stem.clone()
     stem.mul_(1e7)
     res = pipe.fetch(pipe.run(raw))
+    _say("overflowing batch recovered")
     assert res.recovered.tolist() == [RECOVER_FP32, RECOVER_FP32]
     for b in range(2):
         _same_tables(res, r32[b], b, 0, exact=False)
@@ -94,8 +102,10 @@ def test_watershed_nonconvergence_rerun_with_more_rounds(dev, batch):
     illum, raw = batch
     full = FovPipeline(dev, _cfg(), illum)
     base = full.fetch(full.run(raw))
+    _say("default watershed rounds done")
     short = FovPipeline(dev, _cfg(ws_rounds=(1, 1)), illum)
     res = short.fetch(short.run(raw))
+    _say("short watershed rounds recovered:", res.recovered.tolist())
     assert (res.recovered == RECOVER_WS).all(), res.recovered
     assert not res.failed.any()
     for b in range(2):
@@ -122,6 +132,7 @@ def test_plate_with_too_few_watershed_rounds_matches_default(tmp_path, dev, capl
     common = ["--load-data", str(tmp_path / "ld.csv"), "--data-path", str(imgdir), "--channels", *chans,
               "--batch", "2", "--threads", "2", "--pipes", "1"]
     d1 = plate.run(common + ["--out", str(tmp_path / "default")])
+    _say("plate default done")
     with caplog.at_level("WARNING", logger="cpx.pipeline"):
         d2 = plate.run(common + ["--out", str(tmp_path / "short"), "--ws-rounds", "1", "1"])
     assert "re-run on its own" in caplog.text  # the short rounds did fail and were recovered
