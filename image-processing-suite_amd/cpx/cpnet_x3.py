@@ -291,4 +291,8 @@ class FusedCPnetX3:
                 x_small, z0 = self._conv(z, u["pk"][3], u["cout"], u["b"][3], res=x1, bn=self.up[n - 1]["bn"][0],
                                          y=True)
             else:
-                return self._conv(z, u["pk"][3], u["cout"], u["b"][3], res=x1, bn=self.bn_out, head=True)[0]
+                out = self._conv(z, u["pk"][3], u["cout"], u["b"][3], res=x1, bn=self.bn_out, head=True)[0]
+                N, H, W, nout = out.shape
+                check(self.lib.cpx_cpnet_x3_mask_overflow(self.dev.h, _p(out), N, H, W, nout, _p(self.ovf)),
+                      "cpx_cpnet_x3_mask_overflow")
+                return out

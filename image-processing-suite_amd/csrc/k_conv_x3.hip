@@ -925,7 +925,30 @@ __global__ __launch_bounds__(256) void k_cpnet_style_x3(const uint4* __restrict_
   }
 }
 
+// Network output of an image whose split activations overflowed (ovf[n] != 0): the values are
+// garbage (saturated), so they are replaced by "no cell anywhere" (flows 0, cell probability
+// -1 < the 0.0 threshold) before the post-processing sees them; the host re-runs that FOV with
+// the fp32 network.  One block per (image, chunk of pixels); unflagged images return at once.
+__global__ __launch_bounds__(256) void k_cpnet_x3_mask_overflow(float* __restrict__ out, long long P, int nout,
+                                                                const int* __restrict__ ovf) {
+  const int n = blockIdx.y;
+  if (ovf[n] == 0) return;
+  float* o = out + (long long)n * P * nout;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < P; i += (long long)gridDim.x * 256)
+    for (int q = 0; q < nout; ++q) o[i * nout + q] = q == nout - 1 ? -1.0f : 0.0f;
+}
+
 }  // namespace
+
+extern "C" int cpx_cpnet_x3_mask_overflow(cpx_ctx* ctx, float* out, int N, int H, int W, int nout, const int* ovf) {
+  CPX_REQUIRE(ctx && out && ovf, CPX_ERR_ARG, "cpx_cpnet_x3_mask_overflow: null argument");
+  CPX_REQUIRE(N > 0 && N < 65536 && H > 0 && W > 0 && nout > 0, CPX_ERR_ARG, "cpx_cpnet_x3_mask_overflow: bad sizes");
+  const long long P = (long long)H * W;
+  const unsigned gx = (unsigned)std::min<long long>((P + 255) / 256, 64);
+  hipLaunchKernelGGL(k_cpnet_x3_mask_overflow, dim3(gx, (unsigned)N), dim3(256), 0, ctx->stream, out, P, nout, ovf);
+  CPX_CHECK_LAUNCH("k_cpnet_x3_mask_overflow");
+  return CPX_OK;
+}
 
 extern "C" int cpx_cpnet_x3_cfg(int ks, int cin, int cout, int variant, int* bm) {
   X3Cfg c;

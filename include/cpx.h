@@ -474,6 +474,10 @@ int cpx_cpnet_x3_stem(cpx_ctx* ctx, const float* x, int N, int H, int W, const f
 /* 2x2/2 max-pool of split [N][2Hh][2Ww][Cn] -> x_out (exact) and z_out = relu?(scale x + shift). */
 int cpx_cpnet_x3_pool(cpx_ctx* ctx, const void* in, const float* scale, const float* shift,
                       int relu, int N, int Hh, int Ww, int Cn, void* x_out, void* z_out, int* ovf);
+/* head_out [N][H][W][nout] fp32 of every image n with ovf[n] != 0 := flows 0, last channel
+ * (cell probability) -1: an image whose activations overflowed yields no masks (its FOV is
+ * re-run in fp32 by the host) instead of post-processing saturated values.                    */
+int cpx_cpnet_x3_mask_overflow(cpx_ctx* ctx, float* out, int N, int H, int W, int nout, const int* ovf);
 /* style vector of split x [N][H][W][C] (mean over pixels, L2-normalised; CPnet.forward) and the
  * up path's Linear layers: out [N][J] = lin_b + lin_w [J][C] . style.                          */
 int cpx_cpnet_x3_style(cpx_ctx* ctx, const void* x, int N, int H, int W, int C, const float* lin_w,
