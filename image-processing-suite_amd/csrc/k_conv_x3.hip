@@ -114,6 +114,22 @@ struct X3Epi {
   // [COUT/BM][CIN2/16][BM][hi|lo][16] accumulate conv1x1(in2, wp) into the same sums
   const uint4* in2;
   const uint4* wpk2;
+  // stem fused into the first convolution (k_conv_x3_p32<true>): the residual is the block
+  // projection conv1x1(stem_x, stem_wp) of the fp32 network input, formed here (split-rounded as
+  // the stem kernel stored it) instead of read
+  const float* stem_x;
+  const float* stem_wp;
+};
+
+// the stem's own parameters (k_cpnet_stem_x3), for the first convolution's halo
+struct X3Stem {
+  const float* x;  // fp32 network input [N][H][W][2]
+  const float* scale0;
+  const float* shift0;
+  const float* w0;  // [32][2][3][3]
+  const float* bias0;
+  const float* scale1;
+  const float* shift1;
 };
 
 // Epilogue of a 3x3 / 1x1 convolution tile on its fp32 values (acc0 = the joined sums): bias,
@@ -158,7 +174,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
         }
       }
   }
-  if (ep.res) {
+  if (ep.res || ep.stem_x) {
 #pragma unroll
     for (int r = 0; r < OUT_R; ++r) {
       const int i = threadIdx.x + r * NT;
@@ -167,9 +183,22 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
         const int gy = ty0 + px / TX, gx = tx0 + px % TX;
         uint4 v = {0u, 0u, 0u, 0u};
         if (gy < H && gx < W) {
-          const long long rp = ep.res_up ? ((long long)n * (H >> 1) + (gy >> 1)) * (W >> 1) + (gx >> 1)
-                                         : ((long long)n * H + gy) * W + gx;
-          v = ep.res[rp * QC + nb * QB + k];
+          if (ep.stem_x) {
+            // chunk k of the pixel: slab k >> 2, channels (k & 1) * 8 + 0..7, hi (k & 2 == 0) or lo
+            const float2 xv = *reinterpret_cast<const float2*>(ep.stem_x + (((long long)n * H + gy) * W + gx) * 2);
+            const int c0 = nb * BM + (k >> 2) * 16 + (k & 1) * 8;
+            float pf[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              pf[e] = __builtin_fmaf(ep.stem_wp[(c0 + e) * 2], xv.x, ep.stem_wp[(c0 + e) * 2 + 1] * xv.y);
+            uint4 ph, pl;
+            split8(pf, ph, pl, bad);
+            v = (k & 2) ? pl : ph;
+          } else {
+            const long long rp = ep.res_up ? ((long long)n * (H >> 1) + (gy >> 1)) * (W >> 1) + (gx >> 1)
+                                           : ((long long)n * H + gy) * W + gx;
+            v = ep.res[rp * QC + nb * QB + k];
+          }
         }
         smem[px * QB + (k ^ swzq<QB>(px))] = v;
       }
@@ -532,9 +561,13 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
 // tiles of one XCD form a contiguous range that its blocks walk in step, so vertically adjacent
 // tiles (which share halo rows) are in flight together in that XCD's L2.  Per output pixel the
 // sums are formed in k_conv_x3's slab / tap / MFMA order: bit-identical results.
+// STEM: the convolution's input is the stem's output z, computed here on the tile's halo from the
+// fp32 network input (k_cpnet_stem_x3's arithmetic, bit-identical) instead of read: the stem
+// kernel's z and p tensors (256 B per pixel written, then read back) are never stored.
+template <bool STEM>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
-void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, int N, int H,
-                   int W, int tiles_x, int tiles_y) {
+void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, X3Stem st, int N,
+                   int H, int W, int tiles_x, int tiles_y) {
   constexpr int NWV = 8, BM = 32, T = 9, TY = 8, TX = 32, HX = TX + 2, NPIX = (TY + 2) * HX;
   constexpr int NCH = 2, QI = 8;
   constexpr int SW = T * BM * 4;                   // one slab's weights, 16-byte slots
@@ -564,26 +597,71 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
   for (int t = lo + (blockIdx.x >> 3); t < hi; t += nbx) {
     const int n = t / tiles, tt = t - n * tiles;
     const int ty0 = (tt / tiles_x) * TY, tx0 = (tt % tiles_x) * TX;
-    const uint4* inb = in + (long long)n * H * W * QI;
+    if constexpr (STEM) {
+      // the stem on the halo: task (8-channel group g, halo pixel), 384 task slots per group (six
+      // waves: g is wave-uniform, so the weights come through the scalar cache)
+      bool bad = false;
+      const float* xb = st.x + (long long)n * H * W * 2;
+      for (int t = threadIdx.x; t < 4 * 384; t += 512) {
+        const int g = t / 384, hp = t - g * 384;
+        if (hp < NPIX) {
+          const int hy = hp / HX, hx = hp - (hp / HX) * HX;
+          const int gy = ty0 + hy - 1, gx = tx0 + hx - 1;
+          uint4 zh = {0u, 0u, 0u, 0u}, zl = {0u, 0u, 0u, 0u};
+          if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W) {
+            float inp[18];
 #pragma unroll
-    for (int jj = 0; jj < JI; ++jj) {
-      const int j = wid + NWV * jj;
-      if (j < NWIN) {
-        const int si = j * 64 + lane;
-        const int hp = si >> 2, cq = si & 3;
-        const int hy = hp / HX, hx = hp - (hp / HX) * HX;
-        const int gy = ty0 + hy - 1, gx = tx0 + hx - 1;
-        const int off = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-                            ? (gy * W + gx) * QI + (cq ^ swz4(hp)) : -1;
+            for (int k = 0; k < 9; ++k) {
+              const int yy = gy + k / 3 - 1, xx = gx + k % 3 - 1;
+              float a = 0.0f, b = 0.0f;
+              if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
+                const float2 v = *reinterpret_cast<const float2*>(xb + ((long long)yy * W + xx) * 2);
+                a = fmaxf(st.scale0[0] * v.x + st.shift0[0], 0.0f);
+                b = fmaxf(st.scale0[1] * v.y + st.shift0[1], 0.0f);
+              }
+              inp[k] = a;
+              inp[9 + k] = b;
+            }
+            float zf[8];
 #pragma unroll
-        for (int s = 0; s < NCH; ++s) {
-          const uint4* src = off >= 0 ? inb + off + s * 4 : &g_x3_zero16;
-          __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(sx + s * SI + j * 64), 16, 0, 0);
+            for (int e = 0; e < 8; ++e) {
+              const int co = g * 8 + e;
+              float acc = 0.0f;
+#pragma unroll
+              for (int k = 0; k < 18; ++k) acc = __builtin_fmaf(st.w0[co * 18 + k], inp[k], acc);
+              zf[e] = fmaxf(__builtin_fmaf(st.scale1[co], acc + st.bias0[co], st.shift1[co]), 0.0f);
+            }
+            split8(zf, zh, zl, bad);
+          }
+          const int sl = g >> 1, c = g & 1;
+          sx[sl * SI + hp * 4 + (c ^ swz4(hp))] = zh;
+          sx[sl * SI + hp * 4 + ((c + 2) ^ swz4(hp))] = zl;
         }
       }
+      if (ep.ovf && __ballot(bad) && lane == 0) atomicOr(ep.ovf + n, 1);
+      __syncthreads();
+    } else {
+      const uint4* inb = in + (long long)n * H * W * QI;
+#pragma unroll
+      for (int jj = 0; jj < JI; ++jj) {
+        const int j = wid + NWV * jj;
+        if (j < NWIN) {
+          const int si = j * 64 + lane;
+          const int hp = si >> 2, cq = si & 3;
+          const int hy = hp / HX, hx = hp - (hp / HX) * HX;
+          const int gy = ty0 + hy - 1, gx = tx0 + hx - 1;
+          const int off = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+                              ? (gy * W + gx) * QI + (cq ^ swz4(hp)) : -1;
+#pragma unroll
+          for (int s = 0; s < NCH; ++s) {
+            const uint4* src = off >= 0 ? inb + off + s * 4 : &g_x3_zero16;
+            __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(sx + s * SI + j * 64), 16, 0, 0);
+          }
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
     // opaque per tile: keeps the compiler from hoisting every tap's fragment addresses out of the
     // tile loop (they would stay live across the epilogue: spills)
     int hpb = hp0, aSb = aS;
@@ -626,6 +704,7 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
     et.style = et.style ? et.style + zo : nullptr;
     et.head_w = et.head_w ? et.head_w + zo : nullptr;
     et.head_b = et.head_b ? et.head_b + zo : nullptr;
+    et.stem_wp = et.stem_wp ? et.stem_wp + zo : nullptr;
     x3_epilogue<32, BM, TY, TX, 1, 1>(acc0, et, sx, n, 0, ty0, tx0, H, W, 0, wid, 1);
     __syncthreads();  // staging reads done before the next tile's halo lands
   }
@@ -697,8 +776,8 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
     const long long tiles = (long long)N * tx * ty;
     CPX_REQUIRE(tiles < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv: too many tiles");
     const int grid = (int)std::max(1LL, std::min(tiles, 2LL * ctx->n_cu));
-    hipLaunchKernelGGL(k_conv_x3_p32, dim3(grid), dim3(512), 0, ctx->stream, (const uint4*)in,
-                       (const uint4*)wpk, ep, N, H, W, tx, ty);
+    hipLaunchKernelGGL(k_conv_x3_p32<false>, dim3(grid), dim3(512), 0, ctx->stream, (const uint4*)in,
+                       (const uint4*)wpk, ep, X3Stem{}, N, H, W, tx, ty);
     CPX_CHECK_LAUNCH("k_conv_x3_p32");
     return CPX_OK;
   }
@@ -979,7 +1058,7 @@ extern "C" int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* 
               CPX_ERR_ARG, "cpx_cpnet_x3_conv: head needs a 3x3 conv with cout 32, no z_out, 1..4 outputs");
   CPX_REQUIRE(!z_up || z_out, CPX_ERR_ARG, "cpx_cpnet_x3_conv: z_up without z_out");
   X3Epi ep{bias, (const uint4*)res, style, scale, shift, (uint4*)y_out, (uint4*)z_out, res_up, relu,
-           z_up, style_stride, head_w, head_b, head_out, n_head, ovf, in_up, nullptr, nullptr};
+           z_up, style_stride, head_w, head_b, head_out, n_head, ovf, in_up, nullptr, nullptr, nullptr, nullptr};
   return x3_launch(ctx, ks, cin, cout, variant, in, wpk, ep, N, H, W);
 }
 
@@ -999,7 +1078,7 @@ extern "C" int cpx_cpnet_x3_conv_proj(cpx_ctx* ctx, int variant, const void* in,
               CPX_ERR_ARG, "cpx_cpnet_x3_conv_proj: style needs a 16-byte aligned [N][stride >= cout] table");
   CPX_REQUIRE(!z_up || z_out, CPX_ERR_ARG, "cpx_cpnet_x3_conv_proj: z_up without z_out");
   X3Epi ep{bias, nullptr, style, scale, shift, (uint4*)y_out, (uint4*)z_out, 0, relu, z_up, style_stride,
-           nullptr, nullptr, nullptr, 0, ovf, 0, (const uint4*)in2, (const uint4*)wpk2};
+           nullptr, nullptr, nullptr, 0, ovf, 0, (const uint4*)in2, (const uint4*)wpk2, nullptr, nullptr};
   return x3_launch_proj(ctx, cin, cout, cin2, variant, in, wpk, ep, N, H, W);
 }
 
@@ -1019,6 +1098,31 @@ extern "C" int cpx_cpnet_x3_stem(cpx_ctx* ctx, const float* x, int N, int H, int
                      W, scale0, shift0, w0, bias0, scale1, shift1, wp, (uint4*)p_out, (uint4*)z_out, tx,
                      ty, ovf);
   CPX_CHECK_LAUNCH("k_cpnet_stem_x3");
+  return CPX_OK;
+}
+
+extern "C" int cpx_cpnet_x3_conv_stem(cpx_ctx* ctx, const float* x, int N, int H, int W, const float* scale0,
+                                      const float* shift0, const float* w0, const float* bias0,
+                                      const float* scale1, const float* shift1, const float* wp,
+                                      const void* wpk, const float* bias, const float* scale, const float* shift,
+                                      void* y_out, void* z_out, int* ovf) {
+  CPX_REQUIRE(ctx && x && scale0 && shift0 && w0 && bias0 && scale1 && shift1 && wp && wpk && (y_out || z_out),
+              CPX_ERR_ARG, "cpx_cpnet_x3_conv_stem: null argument");
+  CPX_REQUIRE(N > 0 && H > 0 && W > 0, CPX_ERR_ARG, "cpx_cpnet_x3_conv_stem: bad sizes");
+  CPX_REQUIRE(!(scale == nullptr) == !(shift == nullptr), CPX_ERR_ARG,
+              "cpx_cpnet_x3_conv_stem: scale and shift go together");
+  CPX_REQUIRE(((uintptr_t)x % 8) == 0 && ((uintptr_t)wpk | (uintptr_t)y_out | (uintptr_t)z_out) % 16 == 0,
+              CPX_ERR_ARG, "cpx_cpnet_x3_conv_stem: misaligned buffers");
+  X3Epi ep{bias, nullptr, nullptr, scale, shift, (uint4*)y_out, (uint4*)z_out, 0, 1, 0, 0, nullptr, nullptr,
+           nullptr, 0, ovf, 0, nullptr, nullptr, x, wp};
+  const X3Stem st{x, scale0, shift0, w0, bias0, scale1, shift1};
+  const int tx = cpx_div_up(W, 32), ty = cpx_div_up(H, 8);
+  const long long tiles = (long long)N * tx * ty;
+  CPX_REQUIRE(tiles < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv_stem: too many tiles");
+  const int grid = (int)std::max(1LL, std::min(tiles, 2LL * ctx->n_cu));
+  hipLaunchKernelGGL(k_conv_x3_p32<true>, dim3(grid), dim3(512), 0, ctx->stream, nullptr, (const uint4*)wpk, ep,
+                     st, N, H, W, tx, ty);
+  CPX_CHECK_LAUNCH("k_conv_x3_p32<stem>");
   return CPX_OK;
 }
 

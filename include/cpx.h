@@ -471,6 +471,16 @@ int cpx_cpnet_x3_conv_proj(cpx_ctx* ctx, int variant, const void* in, int N, int
 int cpx_cpnet_x3_stem(cpx_ctx* ctx, const float* x, int N, int H, int W, const float* scale0,
                       const float* shift0, const float* w0, const float* bias0, const float* scale1,
                       const float* shift1, const float* wp, void* p_out, void* z_out, int* ovf);
+/* the stem fused into the first 32 -> 32 convolution (the first down block's conv1): with the
+ * stem's parameters (as cpx_cpnet_x3_stem) and that convolution's packed weights wpk, bias
+ * (conv bias + projection bias), scale / shift (BatchNorm + ReLU of the next input): y_out =
+ * conv3x3(stem z, wpk) + bias + conv1x1(x, wp), z_out = relu(scale y_out + shift), both split;
+ * the stem's z and p tensors are formed on each tile's halo and never stored.  Bit-identical to
+ * cpx_cpnet_x3_stem followed by cpx_cpnet_x3_conv(res = p).                                   */
+int cpx_cpnet_x3_conv_stem(cpx_ctx* ctx, const float* x, int N, int H, int W, const float* scale0,
+                           const float* shift0, const float* w0, const float* bias0, const float* scale1,
+                           const float* shift1, const float* wp, const void* wpk, const float* bias,
+                           const float* scale, const float* shift, void* y_out, void* z_out, int* ovf);
 /* 2x2/2 max-pool of split [N][2Hh][2Ww][Cn] -> x_out (exact) and z_out = relu?(scale x + shift). */
 int cpx_cpnet_x3_pool(cpx_ctx* ctx, const void* in, const float* scale, const float* shift,
                       int relu, int N, int Hh, int Ww, int Cn, void* x_out, void* z_out, int* ovf);
