@@ -1,16 +1,21 @@
-"""CPnet — the Cellpose (<= v3) residual U-Net, run with PyTorch-ROCm (MIOpen/MFMA convs).
+"""CPnet — the Cellpose (<= v3) residual U-Net: the architecture, its weights and the fp32 module.
 
-This is the only PyTorch compute in the pipeline (north_star: "PyTorch-ROCm only for the
-Cellpose U-Net forward").  Architecture restated from Cellpose's resnet_torch.CPnet (the model
-behind ``models.CellposeModel(model_type='nuclei')``, Cellpose_GPU_s3fs.py:28,108):
-nbase = [2, 32, 64, 128, 256], 3x3 convs, 4 BN-ReLU-conv per residual block (down path with
-1x1 projection), global style vector (mean-pool + L2-normalise) added through Linear layers in
-the up path, nearest x2 upsampling, 1x1 output head -> (dy, dx, cellprob).
+Architecture restated from Cellpose's resnet_torch.CPnet (the model behind
+``models.CellposeModel(model_type='nuclei')``, Cellpose_GPU_s3fs.py:28,108): nbase = [2, 32, 64,
+128, 256], 3x3 convs, 4 BN-ReLU-conv per residual block (down path with 1x1 projection), global
+style vector (mean-pool + L2-normalise) added through Linear layers in the up path, nearest x2
+upsampling, 1x1 output head -> (dy, dx, cellprob).
+
+This module is the network's definition, not the product forward: the pipeline runs it on
+libcpx's native split-fp16 MFMA kernels at the fp32 network's accuracy (cpx.cpnet_x3, the
+default "f16x3" precision); the eager fp32 module here is the named "fp32" variant (and the
+per-FOV re-run when a split-fp16 activation overflows), the CPU reference of the tests and the
+CPU baseline's network; the bf16 kernels (cpx.cpnet_fused) are a named variant off every default.
 
 Weights: Cellpose's pretrained weights are a network fetch (unavailable offline), so the model is
-built with a seeded random initialisation of this architecture (bench contract) or loaded from a
-local state_dict.  Eval-mode BatchNorm is an affine per channel; the forward is run in bf16
-channels_last (MFMA) inside a captured HIP graph for fixed batch shapes.
+built with a seeded random initialisation of this architecture or loaded from a local state_dict
+(the bench uses cpx/weights/cpnet_nuclei_synth.pt, trained on the synthetic plates).  Eval-mode
+BatchNorm is an affine per channel.
 """
 from __future__ import annotations
 
