@@ -47,6 +47,32 @@ __device__ uint4 g_x3_zero16 = {0u, 0u, 0u, 0u};
 
 __device__ __forceinline__ int swz4(int row) { return (row >> 2) & 3; }
 
+// Bank-conflict-free halo fragment reads.  A ds_read_b128 serves its 64 lanes in four groups of
+// 16 ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32); a group is conflict-free when its
+// 16 chunks fall in 16 distinct 16-byte bank quads, i.e. the pairs (halo pixel mod 4, stored chunk
+// slot) are distinct.  With the chunk slot c ^ swz4(hp) that holds for 16 consecutive halo pixels,
+// but a 32-pixel subtile of a 16- or 28-wide tile crosses a row inside a group (2-way conflicts on
+// every B read: SQ_LDS_BANK_CONFLICT ~ 1/3 of the LDS cycles at 112^2 and below).  Fixes, checked
+// exhaustively for every subtile, tap and lane group:
+//  * TX = 16: subtile pixel of lane l32 permuted so that each group reads one row's 16 pixels
+//    (the accumulator columns follow the same map, so only the pixel bookkeeping changes);
+//  * TX = 28 (3x3): halo rows at a 32-pixel pitch with chunk slot c ^ ((hp >> 2) + 3 hy) & 3.
+template <int TX>
+__device__ __forceinline__ int lane_px(int l32) {
+  if constexpr (TX == 16) {
+    return l32 < 4 ? l32 : l32 < 12 ? 12 + l32 : l32 < 16 ? l32 - 8 : l32 < 20 ? l32 + 8 : l32 < 28 ? l32 - 12 : l32;
+  } else {
+    return l32;
+  }
+}
+template <int KS, int TX>
+struct HaloGeom {
+  static constexpr bool kPitch = KS == 3 && TX == 28;
+  static constexpr int HX = TX + KS - 1;              // halo row length
+  static constexpr int HXP = kPitch ? 32 : HX;         // LDS row pitch (pixels)
+  __device__ static __forceinline__ int swz(int hp, int hy) { return kPitch ? ((hp >> 2) + 3 * hy) & 3 : (hp >> 2) & 3; }
+};
+
 // output-tile chunk swizzle (Q chunks per pixel row)
 template <int Q>
 __device__ __forceinline__ int swzq(int row) {
@@ -121,16 +147,6 @@ struct X3Epi {
   const float* stem_wp;
 };
 
-// the stem's own parameters (k_cpnet_stem_x3), for the first convolution's halo
-struct X3Stem {
-  const float* x;  // fp32 network input [N][H][W][2]
-  const float* scale0;
-  const float* shift0;
-  const float* w0;  // [32][2][3][3]
-  const float* bias0;
-  const float* scale1;
-  const float* shift1;
-};
 
 // Epilogue of a 3x3 / 1x1 convolution tile on its fp32 values (acc0 = the joined sums): bias,
 // residual, residual-stream store, style, eval BatchNorm, ReLU, next-input store or output head.
@@ -206,7 +222,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < WN; ++j) {
-      const int px = min((pg * WN + j) * 32 + l32, P - 1);
+      const int px = min((pg * WN + j) * 32 + lane_px<TX>(l32), P - 1);
 #pragma unroll
       for (int m = 0; m < WM; ++m)
 #pragma unroll
@@ -222,7 +238,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
   auto stage = [&]() {
 #pragma unroll
     for (int j = 0; j < WN; ++j) {
-      const int px = (pg * WN + j) * 32 + l32;
+      const int px = (pg * WN + j) * 32 + lane_px<TX>(l32);
       if (j < nsub && px < P) {
 #pragma unroll
         for (int m = 0; m < WM; ++m)
@@ -317,7 +333,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
           }
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] += __shfl_xor(o[q], 32, 64);
-        const int px = (pg * WN + j) * 32 + l32;
+        const int px = (pg * WN + j) * 32 + lane_px<TX>(l32);
         const long long gp = gpix(px);
         if (h == 0 && j < nsub && gp >= 0) {
 #pragma unroll
@@ -359,7 +375,8 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   constexpr int NT = 512, NWV = NT / 64;
   constexpr int T = KS * KS, HALO = KS / 2;
   constexpr int MWV = BM / (32 * WM), PW = NWV / MWV;
-  constexpr int HY = TY + KS - 1, HX = TX + KS - 1, NPIX = HY * HX;
+  using HG = HaloGeom<KS, TX>;
+  constexpr int HY = TY + KS - 1, HX = HG::HX, HXP = HG::HXP, NPIX = HY * HXP;
   constexpr int NCH = CIN / 16;
   constexpr int NCH2 = CIN2 / 16, QI2 = CIN2 / 4;     // folded projection slabs (one tap each)
   constexpr int NW2 = BM * 4 / 64;                    // their weight DMA rows
@@ -409,10 +426,10 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   for (int jj = 0; jj < JI; ++jj) {
     const int si = (wid + NWV * jj) * 64 + lane;
     const int hp = si >> 2, cq = si & 3;
-    const int hy = hp / HX, hx = hp - (hp / HX) * HX;
+    const int hy = hp / HXP, hx = hp - (hp / HXP) * HXP;
     const int gy = ty0 + hy - HALO, gx = tx0 + hx - HALO;
-    inPC[jj] = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-                   ? ((gy >> iu) * Wi + (gx >> iu)) * 4 + (cq ^ swz4(hp)) : -1;
+    inPC[jj] = (hp < NPIX && hx < HX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+                   ? ((gy >> iu) * Wi + (gx >> iu)) * 4 + (cq ^ HG::swz(hp, hy)) : -1;
   }
   const uint4* inb2 = CIN2 ? ep.in2 + (long long)n * H * W * QI2 : nullptr;
   // slab ch < NCH: the 3x3 weights and the halo of `in`; ch >= NCH: a projection slab (one tap
@@ -471,11 +488,12 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
     const int r = (mw * WM + m) * 32 + l32;
     aS[m] = r * 4 + (h ^ swz4(r));
   }
-  int hp0[WN];
+  int hp0[WN], hy0[WN];
 #pragma unroll
   for (int j = 0; j < WN; ++j) {
-    const int px = min((pg * WN + j) * 32 + l32, P - 1);
-    hp0[j] = (px / TX) * HX + (px % TX);
+    const int px = min((pg * WN + j) * 32 + lane_px<TX>(l32), P - 1);
+    hy0[j] = px / TX;
+    hp0[j] = hy0[j] * HXP + (px % TX);
   }
 
   issue(0, 0);
@@ -493,8 +511,8 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
     }
 #pragma unroll
     for (int j = 0; j < C; ++j) {
-      const int hp = hp0[j] + ky * HX + kx;
-      const int bs = SW + hp * 4 + (h ^ swz4(hp));
+      const int hp = hp0[j] + ky * HXP + kx;
+      const int bs = SW + hp * 4 + (h ^ HG::swz(hp, hy0[j] + ky));
       const f16x8 bh = __builtin_bit_cast(f16x8, sb[bs]);
       const f16x8 bl = __builtin_bit_cast(f16x8, sb[bs ^ 2]);
 #pragma unroll
@@ -561,13 +579,9 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
 // tiles of one XCD form a contiguous range that its blocks walk in step, so vertically adjacent
 // tiles (which share halo rows) are in flight together in that XCD's L2.  Per output pixel the
 // sums are formed in k_conv_x3's slab / tap / MFMA order: bit-identical results.
-// STEM: the convolution's input is the stem's output z, computed here on the tile's halo from the
-// fp32 network input (k_cpnet_stem_x3's arithmetic, bit-identical) instead of read: the stem
-// kernel's z and p tensors (256 B per pixel written, then read back) are never stored.
-template <bool STEM>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
-void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, X3Stem st, int N,
-                   int H, int W, int tiles_x, int tiles_y) {
+void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, int N, int H,
+                   int W, int tiles_x, int tiles_y) {
   constexpr int NWV = 8, BM = 32, T = 9, TY = 8, TX = 32, HX = TX + 2, NPIX = (TY + 2) * HX;
   constexpr int NCH = 2, QI = 8;
   constexpr int SW = T * BM * 4;                   // one slab's weights, 16-byte slots
@@ -597,50 +611,6 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
   for (int t = lo + (blockIdx.x >> 3); t < hi; t += nbx) {
     const int n = t / tiles, tt = t - n * tiles;
     const int ty0 = (tt / tiles_x) * TY, tx0 = (tt % tiles_x) * TX;
-    if constexpr (STEM) {
-      // the stem on the halo: task (8-channel group g, halo pixel), 384 task slots per group (six
-      // waves: g is wave-uniform, so the weights come through the scalar cache)
-      bool bad = false;
-      const float* xb = st.x + (long long)n * H * W * 2;
-      for (int t = threadIdx.x; t < 4 * 384; t += 512) {
-        const int g = t / 384, hp = t - g * 384;
-        if (hp < NPIX) {
-          const int hy = hp / HX, hx = hp - (hp / HX) * HX;
-          const int gy = ty0 + hy - 1, gx = tx0 + hx - 1;
-          uint4 zh = {0u, 0u, 0u, 0u}, zl = {0u, 0u, 0u, 0u};
-          if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W) {
-            float inp[18];
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-              const int yy = gy + k / 3 - 1, xx = gx + k % 3 - 1;
-              float a = 0.0f, b = 0.0f;
-              if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
-                const float2 v = *reinterpret_cast<const float2*>(xb + ((long long)yy * W + xx) * 2);
-                a = fmaxf(st.scale0[0] * v.x + st.shift0[0], 0.0f);
-                b = fmaxf(st.scale0[1] * v.y + st.shift0[1], 0.0f);
-              }
-              inp[k] = a;
-              inp[9 + k] = b;
-            }
-            float zf[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const int co = g * 8 + e;
-              float acc = 0.0f;
-#pragma unroll
-              for (int k = 0; k < 18; ++k) acc = __builtin_fmaf(st.w0[co * 18 + k], inp[k], acc);
-              zf[e] = fmaxf(__builtin_fmaf(st.scale1[co], acc + st.bias0[co], st.shift1[co]), 0.0f);
-            }
-            split8(zf, zh, zl, bad);
-          }
-          const int sl = g >> 1, c = g & 1;
-          sx[sl * SI + hp * 4 + (c ^ swz4(hp))] = zh;
-          sx[sl * SI + hp * 4 + ((c + 2) ^ swz4(hp))] = zl;
-        }
-      }
-      if (ep.ovf && __ballot(bad) && lane == 0) atomicOr(ep.ovf + n, 1);
-      __syncthreads();
-    } else {
       const uint4* inb = in + (long long)n * H * W * QI;
 #pragma unroll
       for (int jj = 0; jj < JI; ++jj) {
@@ -661,7 +631,6 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-    }
     // opaque per tile: keeps the compiler from hoisting every tap's fragment addresses out of the
     // tile loop (they would stay live across the epilogue: spills)
     int hpb = hp0, aSb = aS;
@@ -776,8 +745,8 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
     const long long tiles = (long long)N * tx * ty;
     CPX_REQUIRE(tiles < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv: too many tiles");
     const int grid = (int)std::max(1LL, std::min(tiles, 2LL * ctx->n_cu));
-    hipLaunchKernelGGL(k_conv_x3_p32<false>, dim3(grid), dim3(512), 0, ctx->stream, (const uint4*)in,
-                       (const uint4*)wpk, ep, X3Stem{}, N, H, W, tx, ty);
+    hipLaunchKernelGGL(k_conv_x3_p32, dim3(grid), dim3(512), 0, ctx->stream, (const uint4*)in,
+                       (const uint4*)wpk, ep, N, H, W, tx, ty);
     CPX_CHECK_LAUNCH("k_conv_x3_p32");
     return CPX_OK;
   }
@@ -870,7 +839,7 @@ __global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem_x3(
 #pragma unroll
         for (int k = 0; k < 18; ++k) acc = __builtin_fmaf(w0[co * 18 + k], in[k], acc);
         zf[e] = fmaxf(__builtin_fmaf(scale1[co], acc + bias0[co], shift1[co]), 0.0f);
-        pf[e] = __builtin_fmaf(wp[co * 2], xv.x, wp[co * 2 + 1] * xv.y);
+        pf[e] = p_out ? __builtin_fmaf(wp[co * 2], xv.x, wp[co * 2 + 1] * xv.y) : 0.0f;
       }
       uint4 hi, lo;
       const int base = (q >> 1) * 4 + (q & 1);
@@ -878,9 +847,11 @@ __global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem_x3(
       split8(zf, hi, lo, bad);
       so[0][px * 8 + (base ^ (px & 7))] = hi;
       so[0][px * 8 + ((base + 2) ^ (px & 7))] = lo;
-      split8(pf, hi, lo, bad);
-      so[1][px * 8 + (base ^ (px & 7))] = hi;
-      so[1][px * 8 + ((base + 2) ^ (px & 7))] = lo;
+      if (p_out) {
+        split8(pf, hi, lo, bad);
+        so[1][px * 8 + (base ^ (px & 7))] = hi;
+        so[1][px * 8 + ((base + 2) ^ (px & 7))] = lo;
+      }
     }
   }
   __syncthreads();
@@ -893,7 +864,7 @@ __global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem_x3(
     if (py < H && pxg < W) {
       const long long g = (((long long)n * H + py) * W + pxg) * 8 + k;
       z_out[g] = so[0][p * 8 + (k ^ (p & 7))];
-      p_out[g] = so[1][p * 8 + (k ^ (p & 7))];
+      if (p_out) p_out[g] = so[1][p * 8 + (k ^ (p & 7))];
     }
   }
   if (ovf && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(ovf + n, 1);
@@ -1086,7 +1057,7 @@ extern "C" int cpx_cpnet_x3_stem(cpx_ctx* ctx, const float* x, int N, int H, int
                                  const float* scale0, const float* shift0, const float* w0,
                                  const float* bias0, const float* scale1, const float* shift1,
                                  const float* wp, void* p_out, void* z_out, int* ovf) {
-  CPX_REQUIRE(ctx && x && scale0 && shift0 && w0 && bias0 && scale1 && shift1 && wp && p_out && z_out,
+  CPX_REQUIRE(ctx && x && scale0 && shift0 && w0 && bias0 && scale1 && shift1 && (wp || !p_out) && z_out,
               CPX_ERR_ARG, "cpx_cpnet_x3_stem: null argument");
   CPX_REQUIRE(N > 0 && H > 0 && W > 0, CPX_ERR_ARG, "cpx_cpnet_x3_stem: bad sizes");
   CPX_REQUIRE(((uintptr_t)x % 8) == 0 && ((uintptr_t)p_out | (uintptr_t)z_out) % 16 == 0,
@@ -1101,28 +1072,24 @@ extern "C" int cpx_cpnet_x3_stem(cpx_ctx* ctx, const float* x, int N, int H, int
   return CPX_OK;
 }
 
-extern "C" int cpx_cpnet_x3_conv_stem(cpx_ctx* ctx, const float* x, int N, int H, int W, const float* scale0,
-                                      const float* shift0, const float* w0, const float* bias0,
-                                      const float* scale1, const float* shift1, const float* wp,
-                                      const void* wpk, const float* bias, const float* scale, const float* shift,
-                                      void* y_out, void* z_out, int* ovf) {
-  CPX_REQUIRE(ctx && x && scale0 && shift0 && w0 && bias0 && scale1 && shift1 && wp && wpk && (y_out || z_out),
-              CPX_ERR_ARG, "cpx_cpnet_x3_conv_stem: null argument");
+extern "C" int cpx_cpnet_x3_conv_stem(cpx_ctx* ctx, const float* x, int N, int H, int W, const void* z,
+                                      const float* wp, const void* wpk, const float* bias, const float* scale,
+                                      const float* shift, void* y_out, void* z_out, int* ovf) {
+  CPX_REQUIRE(ctx && x && z && wp && wpk && (y_out || z_out), CPX_ERR_ARG, "cpx_cpnet_x3_conv_stem: null argument");
   CPX_REQUIRE(N > 0 && H > 0 && W > 0, CPX_ERR_ARG, "cpx_cpnet_x3_conv_stem: bad sizes");
   CPX_REQUIRE(!(scale == nullptr) == !(shift == nullptr), CPX_ERR_ARG,
               "cpx_cpnet_x3_conv_stem: scale and shift go together");
-  CPX_REQUIRE(((uintptr_t)x % 8) == 0 && ((uintptr_t)wpk | (uintptr_t)y_out | (uintptr_t)z_out) % 16 == 0,
+  CPX_REQUIRE(((uintptr_t)x % 8) == 0 && ((uintptr_t)z | (uintptr_t)wpk | (uintptr_t)y_out | (uintptr_t)z_out) % 16 == 0,
               CPX_ERR_ARG, "cpx_cpnet_x3_conv_stem: misaligned buffers");
   X3Epi ep{bias, nullptr, nullptr, scale, shift, (uint4*)y_out, (uint4*)z_out, 0, 1, 0, 0, nullptr, nullptr,
            nullptr, 0, ovf, 0, nullptr, nullptr, x, wp};
-  const X3Stem st{x, scale0, shift0, w0, bias0, scale1, shift1};
   const int tx = cpx_div_up(W, 32), ty = cpx_div_up(H, 8);
   const long long tiles = (long long)N * tx * ty;
   CPX_REQUIRE(tiles < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv_stem: too many tiles");
   const int grid = (int)std::max(1LL, std::min(tiles, 2LL * ctx->n_cu));
-  hipLaunchKernelGGL(k_conv_x3_p32<true>, dim3(grid), dim3(512), 0, ctx->stream, nullptr, (const uint4*)wpk, ep,
-                     st, N, H, W, tx, ty);
-  CPX_CHECK_LAUNCH("k_conv_x3_p32<stem>");
+  hipLaunchKernelGGL(k_conv_x3_p32, dim3(grid), dim3(512), 0, ctx->stream, (const uint4*)z, (const uint4*)wpk, ep, N,
+                     H, W, tx, ty);
+  CPX_CHECK_LAUNCH("k_conv_x3_p32");
   return CPX_OK;
 }
 

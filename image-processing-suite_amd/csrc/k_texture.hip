@@ -14,8 +14,6 @@
 //    diagonal-major u16 table, one scan per angle for ASM / the pair count.
 #include "cpx_internal.h"
 #include <math.h>
-#include <stdlib.h>
-#include <type_traits>
 
 namespace {
 
@@ -60,15 +58,6 @@ __device__ __forceinline__ int quantize(float v, bool in, float mn, float rng, b
 __host__ __device__ __forceinline__ int crop_stride(int bw) { return (bw + 7) & ~7; }
 __host__ __device__ __forceinline__ long long crop_bytes(int bh, int bw) {
   return ((long long)bh * crop_stride(bw) + kSlack + 15) / 16 * 16;
-}
-
-// small-item GLCM path (k_tex_glcm_small)
-constexpr int kTS = 256;                 // threads per small-item block
-constexpr int kSmallNB = 4096;           // bbox pixels of a small item (>= its pairs per angle)
-constexpr int kHashBits = 13, kHashN = 1 << kHashBits;  // 8192 slots, 32 KiB
-constexpr int kCropS = 4608;             // crop bytes held in LDS
-__device__ __forceinline__ bool glcm_is_small(int bh, int bw) {
-  return bh * bw <= kSmallNB && crop_bytes(bh, bw) <= kCropS;
 }
 
 // GLCM of one (object, channel) item: skimage graycomatrix offsets (dr, dc) for angles
@@ -392,7 +381,7 @@ __device__ __forceinline__ GlcmItem glcm_item(int code, int C, int max_label,
                                               const cpx_object* objects,
                                               const long long* crop_off,
                                               const unsigned char* scratch,
-                                              long long scratch_per_fov, int skip_small) {
+                                              long long scratch_per_fov) {
   GlcmItem g{0, 0, 0, 0, 0, 0, 0, nullptr};
   if (code < 0) return g;
   const int fov = code >> 20, item = code & 0xfffff;
@@ -405,7 +394,6 @@ __device__ __forceinline__ GlcmItem glcm_item(int code, int C, int max_label,
   g.bw = o.bbox[3] - o.bbox[1];
   const int nb = g.bh * g.bw;
   if (off < 0 || nb > 65535) return g;  // u16 counters / u32 sums: fallback kernel
-  if (skip_small && glcm_is_small(g.bh, g.bw)) return g;  // k_tex_glcm_small measures it
   g.nb = nb;
   g.bytes = (int)crop_bytes(g.bh, g.bw);
   g.src = scratch + (long long)fov * scratch_per_fov + off + (long long)g.ch * g.bytes;
@@ -441,7 +429,7 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
                                                  const unsigned char* __restrict__ scratch,
                                                  long long scratch_per_fov,
                                                  int* __restrict__ glcm_next,
-                                                 unsigned long long* __restrict__ glcm_raw, int skip_small) {
+                                                 unsigned long long* __restrict__ glcm_raw) {
   // LDS: table at offset 0 (static, so the atomics' addresses need no base), then the
   // 64 sink words, the reduction totals, the queue codes and the crop
   __shared__ __attribute__((aligned(16))) unsigned int lds[40 * 1024];  // all 160 KiB, static
@@ -464,7 +452,7 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
   // L2 while the current item runs its four angles (the crop was written by k_obj_stage, possibly
   // on another XCD, so a cold load is HBM/MALL latency); thread 0 grabs the item after that one
   // from the queue during the current item, so the atomic's latency is hidden too.
-  GlcmItem cur = glcm_item(s_code[0], C, max_label, objects, crop_off, scratch, scratch_per_fov, skip_small);
+  GlcmItem cur = glcm_item(s_code[0], C, max_label, objects, crop_off, scratch, scratch_per_fov);
   unsigned int touched = glcm_touch(cur), sink_word = 0u;
   int ahead = -2;  // -2: nothing grabbed yet
   for (int par = 1; s_code[par ^ 1] >= 0; par ^= 1) {
@@ -484,7 +472,7 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
     if (threadIdx.x == 0 && ahead != -2) s_code[par] = ahead;
     __syncthreads();
     const GlcmItem it = cur;
-    cur = glcm_item(s_code[par], C, max_label, objects, crop_off, scratch, scratch_per_fov, skip_small);
+    cur = glcm_item(s_code[par], C, max_label, objects, crop_off, scratch, scratch_per_fov);
     touched = glcm_touch(cur);
     if (threadIdx.x == 0) ahead = s_code[par] >= 0 ? glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next) : -1;
     if (it.nb <= 0) continue;
@@ -510,222 +498,6 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
   if (C < 0 && sink_word + touched == 0x9e3779b9u) glcm_raw[0] = 0ull;
 }
 
-// ---------------------------------------------------------------------------------------------
-// Small items (bbox <= kSmallNB pixels, crop <= kCropS bytes: the common case): GLCM in a hashed
-// pair table, four items per CU.  Only ASM needs per-pair counts, and an item with T <= 4096
-// pairs per angle has at most T distinct pair keys, so a 8192-slot open-addressing table (32 KiB,
-// load <= 1/2) replaces k_tex_glcm's dense 64K-counter table (128 KiB: one item per CU, and a
-// 128 KiB scan per angle).  A 256-thread block per item stream: crop (<= 4 KiB) and table in
-// LDS, four blocks per CU.  Per angle: the count phase of k_tex_glcm (same chunks, same byte-SIMD
-// pair sums, same homogeneity lookups) with each non-background pair key (i << 8 | j) added to its
-// slot (entry = key << 16 | count; linear probing from a multiplicative hash; an empty slot is
-// claimed by compare-and-swap), then a 32 KiB scan for sum c^2 / sum c that also clears.  Every
-// total is the same integer k_tex_glcm forms, so k_glcm_props gives bit-identical features.
-
-__device__ __forceinline__ void hash_add(unsigned int* tab, unsigned int key) {
-  if (key == 0u) return;  // background (0, 0) and masked slots: counted from the totals
-  unsigned int h = (key * 0x9E3779B1u) >> (32 - kHashBits);
-  const unsigned int mine = (key << 16) | 1u;
-  while (true) {
-    const unsigned int e = tab[h];
-    if ((e >> 16) == key) {
-      atomicAdd(&tab[h], 1u);
-      return;
-    }
-    if (e == 0u) {
-      const unsigned int old = atomicCAS(&tab[h], 0u, mine);
-      if (old == 0u) return;
-      if ((old >> 16) == key) {
-        atomicAdd(&tab[h], 1u);
-        return;
-      }
-    }
-    h = (h + 1u) & (kHashN - 1);
-  }
-}
-
-template <int ANG>
-__device__ __forceinline__ void glcm_count_small(const unsigned char* __restrict__ crop, unsigned int* tab,
-                                                 const unsigned long long* hom, GlcmSums& S, int bh, int bw) {
-  constexpr int dr = ANG == 0 ? 0 : ANG == 2 ? 3 : 2;
-  constexpr int dc = ANG == 0 ? 3 : ANG == 1 ? 2 : ANG == 2 ? 0 : -2;
-  constexpr int sh = dc >= 0 ? dc : dc + 8;
-  const int bwp = crop_stride(bw), nch = bwp >> 3;
-  const int rend = bh - dr;
-  const int cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
-  if (rend <= 0 || cend <= cbeg) return;
-  const int nc = rend * nch;
-  // scattered visiting order as k_tex_glcm (lanes of one atomic rarely share a slot)
-  const int mul = nc % 7919 ? 7919 : 7907;
-  unsigned p = (threadIdx.x * (unsigned)mul) % (unsigned)nc;
-  const unsigned step = ((unsigned)kTS * (unsigned)mul) % (unsigned)nc;
-  const int sr = step / nch, sc = step - sr * nch;
-  int r = p / nch, ci = p - r * nch;
-  const int boff = dr * bwp + (dc < 0 ? -8 : 0);
-  for (int q = threadIdx.x; q < nc; q += kTS) {
-    const unsigned char* pa = crop + 8 * (int)p;
-    const uint2 A = *reinterpret_cast<const uint2*>(pa);
-    unsigned int b0, b1;
-    if constexpr (sh == 0) {
-      const uint2 Bw = *reinterpret_cast<const uint2*>(pa + boff);
-      b0 = Bw.x;
-      b1 = Bw.y;
-    } else {
-      const uint2 L = *reinterpret_cast<const uint2*>(pa + boff);
-      const uint2 R = *reinterpret_cast<const uint2*>(pa + boff + 8);
-      if constexpr (sh < 4) {
-        b0 = __builtin_amdgcn_alignbyte(L.y, L.x, sh);
-        b1 = __builtin_amdgcn_alignbyte(R.x, L.y, sh);
-      } else {
-        b0 = __builtin_amdgcn_alignbyte(R.x, L.y, sh - 4);
-        b1 = __builtin_amdgcn_alignbyte(R.y, R.x, sh - 4);
-      }
-    }
-    const int c0 = 8 * ci;
-    const int hi = min(cend - c0, 8), lo = max(cbeg - c0, 0);
-    unsigned long long m = hi >= 8 ? ~0ull : (hi <= 0 ? 0ull : (1ull << (8 * hi)) - 1ull);
-    m &= ~0ull << (8 * lo);
-    const unsigned int m0 = (unsigned int)m, m1 = (unsigned int)(m >> 32);
-    const unsigned int a0 = A.x & m0, a1 = A.y & m1;
-    b0 &= m0;
-    b1 &= m1;
-    S.sisj = __builtin_amdgcn_sad_u8(a0, 0u, S.sisj);
-    S.sisj = __builtin_amdgcn_sad_u8(a1, 0u, S.sisj);
-    S.sisj += __builtin_amdgcn_sad_u8(b1, 0u, __builtin_amdgcn_sad_u8(b0, 0u, 0u)) << 16;
-    S.dis = __builtin_amdgcn_sad_u8(a0, b0, S.dis);
-    S.dis = __builtin_amdgcn_sad_u8(a1, b1, S.dis);
-    S.sii = __builtin_amdgcn_udot4(a0, a0, S.sii, false);
-    S.sii = __builtin_amdgcn_udot4(a1, a1, S.sii, false);
-    S.sjj = __builtin_amdgcn_udot4(b0, b0, S.sjj, false);
-    S.sjj = __builtin_amdgcn_udot4(b1, b1, S.sjj, false);
-    S.sij = __builtin_amdgcn_udot4(a0, b0, S.sij, false);
-    S.sij = __builtin_amdgcn_udot4(a1, b1, S.sij, false);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const unsigned int ia = (a0 >> (8 * u)) & 255u, ib = (b0 >> (8 * u)) & 255u;
-      const unsigned int ja = (a1 >> (8 * u)) & 255u, jb = (b1 >> (8 * u)) & 255u;
-      S.hom += hom[ia > ib ? ia - ib : ib - ia];
-      S.hom += hom[ja > jb ? ja - jb : jb - ja];
-      hash_add(tab, (ia << 8) | ib);
-      hash_add(tab, (ja << 8) | jb);
-    }
-    p += step;
-    r += sr;
-    ci += sc;
-    if (ci >= nch) {
-      ci -= nch;
-      ++r;
-    }
-    if (p >= (unsigned)nc) {
-      p -= nc;
-      r -= rend;
-    }
-  }
-}
-
-// sum c^2 and sum c over the occupied slots, clearing them (32 slots per thread)
-__device__ __forceinline__ void glcm_scan_small(unsigned int* tab, GlcmSums& S) {
-  uint4* t4 = reinterpret_cast<uint4*>(tab);
-#pragma unroll 2
-  for (int k = 0; k < kHashN / 4 / kTS; ++k) {
-    uint4 w[1] = {t4[threadIdx.x + k * kTS]};
-    const unsigned int e[4] = {w[0].x, w[0].y, w[0].z, w[0].w};
-    bool nz = false;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const unsigned int c = e[u] & 0xffffu;
-      S.asq += c * c;
-      S.cnt += c;
-      nz |= e[u] != 0u;
-    }
-    if (nz) t4[threadIdx.x + k * kTS] = uint4{0u, 0u, 0u, 0u};
-  }
-}
-
-// u64 sum over a wave (butterfly shuffles)
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-__global__ __launch_bounds__(kTS) __attribute__((amdgpu_waves_per_eu(4))) void k_tex_glcm_small(int C, int max_label,
-                                                        const cpx_object* __restrict__ objects,
-                                                        const cpx_fov_objects* __restrict__ hdr,
-                                                        const long long* __restrict__ crop_off,
-                                                        const unsigned char* __restrict__ scratch,
-                                                        long long scratch_per_fov, int* __restrict__ next,
-                                                        unsigned long long* __restrict__ glcm_raw) {
-  __shared__ __attribute__((aligned(16))) unsigned int tab[kHashN];
-  __shared__ __attribute__((aligned(16))) unsigned char crop[kCropS];
-  __shared__ unsigned long long s_hom[256];
-  __shared__ unsigned long long s_red[4][4 * kRedW];
-  __shared__ int s_code;
-  const int B = gridDim.y, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int q_fov = blockIdx.y, q_visited = 0;
-  for (int x = threadIdx.x; x < kHashN; x += kTS) tab[x] = 0u;
-  for (int x = threadIdx.x; x < 256; x += kTS) s_hom[x] = kHom.m[x];
-  while (true) {
-    if (threadIdx.x == 0) {
-      int code = -1;
-      while (q_visited < B) {  // this block's FOV queue first, then the others (k_tex_glcm's order)
-        const int n_items = hdr[q_fov].n_objects * C;
-        const int v = atomicAdd(&next[q_fov], 1);
-        if (v < n_items) {
-          code = (q_fov << 20) | v;
-          break;
-        }
-        ++q_visited;
-        q_fov = q_fov + 1 == B ? 0 : q_fov + 1;
-      }
-      s_code = code;
-    }
-    __syncthreads();
-    const int code = s_code;
-    if (code < 0) break;
-    const int fov = code >> 20, item = code & 0xfffff;
-    const int k = item / C, ch = item - k * C;
-    const long long ok = (long long)fov * max_label + k;
-    const long long off = crop_off[ok];
-    const cpx_object o = objects[ok];
-    const int bh = o.bbox[2] - o.bbox[0], bw = o.bbox[3] - o.bbox[1];
-    if (off < 0 || !glcm_is_small(bh, bw)) {  // k_tex_glcm (or the fallback kernel) measures it
-      __syncthreads();                        // s_code read by all before thread 0 rewrites it
-      continue;
-    }
-    const int bytes = (int)crop_bytes(bh, bw);
-    const uint4* src = reinterpret_cast<const uint4*>(scratch + (long long)fov * scratch_per_fov + off +
-                                                      (long long)ch * bytes);
-    for (int x = threadIdx.x; x < bytes / 16; x += kTS) reinterpret_cast<uint4*>(crop)[x] = src[x];
-    __syncthreads();
-    // per angle: count, scan (+ clear), the wave totals to LDS (one GlcmSums live at a time)
-    auto angle = [&](auto ac) {
-      constexpr int a = decltype(ac)::value;
-      GlcmSums g = {};
-      glcm_count_small<a>(crop, tab, s_hom, g, bh, bw);
-      __syncthreads();
-      glcm_scan_small(tab, g);
-      const unsigned long long v[kRedW] = {g.sisj & 0xffffu, g.sisj >> 16, g.sii, g.sjj, g.sij, g.dis, g.asq, g.cnt,
-                                           g.hom & 0xffffffffull, g.hom >> 32};
-#pragma unroll
-      for (int t = 0; t < kRedW; ++t) {
-        const unsigned long long x = wave_sum_u64(v[t]);
-        if (lane == 0) s_red[wid][a * kRedW + t] = x;
-      }
-      __syncthreads();
-    };
-    angle(std::integral_constant<int, 0>{});
-    angle(std::integral_constant<int, 1>{});
-    angle(std::integral_constant<int, 2>{});
-    angle(std::integral_constant<int, 3>{});
-    if (threadIdx.x < 4 * kRedW) {
-      const unsigned long long x = s_red[0][threadIdx.x] + s_red[1][threadIdx.x] + s_red[2][threadIdx.x] +
-                                   s_red[3][threadIdx.x];
-      glcm_raw[(ok * C + ch) * (4 * kRedW) + threadIdx.x] = x;
-    }
-    __syncthreads();
-  }
-}
-
 // crop slots: per FOV exclusive scan of C * bbox area; objects beyond the scratch capacity or
 // with bbox > 65535 px get -1 (fallback kernel).
 __global__ __launch_bounds__(1024) void k_crop_offsets(int C, int max_label,
@@ -735,10 +507,9 @@ __global__ __launch_bounds__(1024) void k_crop_offsets(int C, int max_label,
                                                       int* __restrict__ glcm_next, cpx_fallback_lists fb) {
   const int fov = blockIdx.x;
   const int n = hdr[fov].n_objects;
-  if (threadIdx.x == 0) {  // this FOV's work queues: k_tex_glcm [0, B), k_obj_stage [B, 2B),
-    glcm_next[fov] = 0;     // k_tex_glcm_small [2B, 3B)
+  if (threadIdx.x == 0) {  // this FOV's work queues: k_tex_glcm [0, B), k_obj_stage [B, 2B)
+    glcm_next[fov] = 0;
     glcm_next[gridDim.x + fov] = 0;
-    glcm_next[2 * gridDim.x + fov] = 0;
   }
   __shared__ long long wsum[16];
   __shared__ long long base;
@@ -1223,7 +994,7 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   // + one GLCM and one k_obj_stage work-queue counter per FOV (zeroed by k_crop_offsets) + the
   // fallback lists
   // + the AreaShape raw sums [B][max_label][kShapeRaw]
-  const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + sizeof(int) * (size_t)B * 5 +
+  const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + sizeof(int) * (size_t)B * 4 +
                              sizeof(int) * 2 * (size_t)B * max_label + 255) / 256) * 256;
   const size_t raw_bytes = ((sizeof(long long) * kShapeRaw * (size_t)B * max_label + 255) / 256) * 256;
   // + the GLCM integer totals [B][max_label][C][4 angles][kRedW] for k_glcm_props
@@ -1234,8 +1005,8 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   CPX_REQUIRE(B < 2048 && (long long)max_label * C < (1 << 20), CPX_ERR_SHAPE,
               "GLCM queue codes hold fov < 2048 and items < 2^20");
   long long* crop_off = (long long*)ws;
-  int* glcm_next = (int*)(crop_off + (size_t)B * max_label);  // + k_obj_stage's at B, small GLCM's at 2B
-  fb->n_shape = glcm_next + 3 * B;
+  int* glcm_next = (int*)(crop_off + (size_t)B * max_label);  // + k_obj_stage's queues at B
+  fb->n_shape = glcm_next + 2 * B;
   fb->n_tex = fb->n_shape + B;
   fb->shape = fb->n_tex + B;
   fb->tex = fb->shape + (size_t)B * max_label;
@@ -1255,20 +1026,10 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
   hipLaunchKernelGGL(k_shape_props, dim3(cpx_div_up(max_label, 256), B), dim3(256), 0, ctx->stream,
                      max_label, F, objects_dev, hdr_dev, (const long long*)raws, feats_dev);
   CPX_CHECK_LAUNCH("k_shape_props");
-  // small items (the common case) four per CU in hashed tables, then the rest one per CU in the
-  // dense table (CPX_GLCM_SMALL=0: every item in the dense table)
-  const bool small = !getenv("CPX_GLCM_SMALL") || atoi(getenv("CPX_GLCM_SMALL")) != 0;
-  if (small) {
-    const int per_fov_s = std::max(1, std::min(max_label * C, (4 * ctx->n_cu + B - 1) / B));
-    hipLaunchKernelGGL(k_tex_glcm_small, dim3(per_fov_s, B), dim3(kTS), 0, ctx->stream, C, max_label,
-                       objects_dev, hdr_dev, (const long long*)crop_off, (const unsigned char*)scratch, per_fov,
-                       glcm_next + 2 * B, glcm_raw);
-    CPX_CHECK_LAUNCH("k_tex_glcm_small");
-  }
   const int per_fov_t = std::max(1, std::min(max_label * C, (ctx->n_cu + B - 1) / B));
   hipLaunchKernelGGL(k_tex_glcm, dim3(per_fov_t, B), dim3(kTT), 0, ctx->stream, C, max_label,
                      F, objects_dev, hdr_dev, (const long long*)crop_off,
-                     (const unsigned char*)scratch, per_fov, glcm_next, glcm_raw, (int)small);
+                     (const unsigned char*)scratch, per_fov, glcm_next, glcm_raw);
   CPX_CHECK_LAUNCH("k_tex_glcm");
   hipLaunchKernelGGL(k_glcm_props, dim3(cpx_div_up(max_label * C * 4, 256), B), dim3(256), 0, ctx->stream,
                      C, max_label, F, objects_dev, hdr_dev, (const long long*)crop_off,

@@ -287,17 +287,3 @@ def test_features_bit_reproducible(dev):
     b = _features(dev, lab, planes)
     np.testing.assert_array_equal(a, b)
 
-
-def test_glcm_small_items_equal_dense_table(dev, monkeypatch):
-    """The hashed small-item GLCM (k_tex_glcm_small: bbox <= 4096 px, four items per CU) and the
-    dense 64K-counter table (k_tex_glcm, CPX_GLCM_SMALL=0) form the same integer totals: every
-    feature bit-identical, on objects from a few pixels to beyond the small-item limit."""
-    H, W, C = 600, 640, 3
-    lab = sg.labels(83, H, W, n=70, rmin=2, rmax=70, skip_every=0)
-    planes = np.stack([sg.plane(830 + c, H, W, n_blobs=40).astype(np.float32) /
-                       sg.illum(840 + c, H, W) for c in range(C)]).astype(np.float32)
-    small = _features(dev, lab, planes)
-    monkeypatch.setenv("CPX_GLCM_SMALL", "0")
-    dense = _features(dev, lab, planes)
-    np.testing.assert_array_equal(small, dense)
-    assert np.count_nonzero(small) > 0.5 * small.size
