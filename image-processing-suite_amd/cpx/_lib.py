@@ -135,7 +135,6 @@ SIGNATURES = {
                                _P, _P, _I, _P, _P, _I, _P, _P]),
     "cpx_cpnet_x3_conv_proj": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P, _I, _P, _P, _I,
                                     _P, _P, _I, _P]),
-    "cpx_cpnet_x3_conv_stem": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cpx_cpnet_x3_mask_overflow": (_I, [_P, _P, _I, _I, _I, _I, _P]),
     "cpx_cpnet_x3_stem": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cpx_cpnet_x3_pool": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),

@@ -27,10 +27,6 @@ X3_VARIANT = int(os.environ.get("CPX_X3_VARIANT", "0"))
 # fold each down block's (and the deepest up block's) 1x1 residual projection into the block's
 # second 3x3 convolution (cpx_cpnet_x3_conv_proj); CPX_X3_FOLD=0 keeps the separate 1x1 pass
 X3_FOLD = os.environ.get("CPX_X3_FOLD", "1") != "0"
-# the first down block's residual (the projection of the network input) formed in its second
-# convolution's epilogue instead of stored by the stem and read back (cpx_cpnet_x3_conv_stem;
-# CPX_X3_STEM=0: the stem's p tensor, bit-identical)
-X3_STEM = os.environ.get("CPX_X3_STEM", "1") != "0"
 
 
 def split_f16(w: np.ndarray):
@@ -235,23 +231,6 @@ class FusedCPnetX3:
                                          self._ovf_p(N)), "cpx_cpnet_x3_stem")
         return p, z
 
-    def _conv_stem(self, x, d):
-        """The stem (z only) and the first down block's second convolution, whose residual (the
-        block projection of x) is formed in its epilogue: (x1, z)."""
-        N, H, W, _ = x.shape
-        z0 = self._empty(N, H, W, 32)
-        (s0, h0), (s1, h1) = d["bn"][0], d["bn"][1]
-        check(self.lib.cpx_cpnet_x3_stem(self.dev.h, _p(x), N, H, W, _p(s0), _p(h0), _p(d["stem_w"]),
-                                         _p(d["b"][0]), _p(s1), _p(h1), None, None, _p(z0), self._ovf_p(N)),
-              "cpx_cpnet_x3_stem")
-        y = self._empty(N, H, W, 32)
-        z = self._empty(N, H, W, 32)
-        s2, h2 = d["bn"][2]
-        check(self.lib.cpx_cpnet_x3_conv_stem(self.dev.h, _p(x), N, H, W, _p(z0), _p(d["stem_wp"]), _p(d["pk"][1]),
-                                              _p(d["b1p"]), _p(s2), _p(h2), _p(y), _p(z), self._ovf_p(N)),
-              "cpx_cpnet_x3_conv_stem")
-        return y, z
-
     def _style(self, x):
         N, H, W, C = x.shape
         S = torch.empty((N, self.J), dtype=torch.float32, device=self.td)
@@ -272,9 +251,7 @@ class FusedCPnetX3:
         zu = None
         nd = len(self.down)
         for n, d in enumerate(self.down):
-            if n == 0 and X3_STEM and self.variant == 0 and d["cout"] == 32:
-                x1, z = self._conv_stem(x, d)
-            elif n == 0:
+            if n == 0:
                 p, z = self._stem(x, d)
                 x1, z = self._conv(z, d["pk"][1], d["cout"], d["b1p"], res=p, bn=d["bn"][2], y=True)
             else:

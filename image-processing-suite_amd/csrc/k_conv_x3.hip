@@ -47,32 +47,6 @@ __device__ uint4 g_x3_zero16 = {0u, 0u, 0u, 0u};
 
 __device__ __forceinline__ int swz4(int row) { return (row >> 2) & 3; }
 
-// Bank-conflict-free halo fragment reads.  A ds_read_b128 serves its 64 lanes in four groups of
-// 16 ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32); a group is conflict-free when its
-// 16 chunks fall in 16 distinct 16-byte bank quads, i.e. the pairs (halo pixel mod 4, stored chunk
-// slot) are distinct.  With the chunk slot c ^ swz4(hp) that holds for 16 consecutive halo pixels,
-// but a 32-pixel subtile of a 16- or 28-wide tile crosses a row inside a group (2-way conflicts on
-// every B read: SQ_LDS_BANK_CONFLICT ~ 1/3 of the LDS cycles at 112^2 and below).  Fixes, checked
-// exhaustively for every subtile, tap and lane group:
-//  * TX = 16: subtile pixel of lane l32 permuted so that each group reads one row's 16 pixels
-//    (the accumulator columns follow the same map, so only the pixel bookkeeping changes);
-//  * TX = 28 (3x3): halo rows at a 32-pixel pitch with chunk slot c ^ ((hp >> 2) + 3 hy) & 3.
-template <int TX>
-__device__ __forceinline__ int lane_px(int l32) {
-  if constexpr (TX == 16) {
-    return l32 < 4 ? l32 : l32 < 12 ? 12 + l32 : l32 < 16 ? l32 - 8 : l32 < 20 ? l32 + 8 : l32 < 28 ? l32 - 12 : l32;
-  } else {
-    return l32;
-  }
-}
-template <int KS, int TX>
-struct HaloGeom {
-  static constexpr bool kPitch = KS == 3 && TX == 28;
-  static constexpr int HX = TX + KS - 1;              // halo row length
-  static constexpr int HXP = kPitch ? 32 : HX;         // LDS row pitch (pixels)
-  __device__ static __forceinline__ int swz(int hp, int hy) { return kPitch ? ((hp >> 2) + 3 * hy) & 3 : (hp >> 2) & 3; }
-};
-
 // output-tile chunk swizzle (Q chunks per pixel row)
 template <int Q>
 __device__ __forceinline__ int swzq(int row) {
@@ -140,13 +114,7 @@ struct X3Epi {
   // [COUT/BM][CIN2/16][BM][hi|lo][16] accumulate conv1x1(in2, wp) into the same sums
   const uint4* in2;
   const uint4* wpk2;
-  // stem fused into the first convolution (k_conv_x3_p32<true>): the residual is the block
-  // projection conv1x1(stem_x, stem_wp) of the fp32 network input, formed here (split-rounded as
-  // the stem kernel stored it) instead of read
-  const float* stem_x;
-  const float* stem_wp;
 };
-
 
 // Epilogue of a 3x3 / 1x1 convolution tile on its fp32 values (acc0 = the joined sums): bias,
 // residual, residual-stream store, style, eval BatchNorm, ReLU, next-input store or output head.
@@ -190,7 +158,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
         }
       }
   }
-  if (ep.res || ep.stem_x) {
+  if (ep.res) {
 #pragma unroll
     for (int r = 0; r < OUT_R; ++r) {
       const int i = threadIdx.x + r * NT;
@@ -199,22 +167,9 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
         const int gy = ty0 + px / TX, gx = tx0 + px % TX;
         uint4 v = {0u, 0u, 0u, 0u};
         if (gy < H && gx < W) {
-          if (ep.stem_x) {
-            // chunk k of the pixel: slab k >> 2, channels (k & 1) * 8 + 0..7, hi (k & 2 == 0) or lo
-            const float2 xv = *reinterpret_cast<const float2*>(ep.stem_x + (((long long)n * H + gy) * W + gx) * 2);
-            const int c0 = nb * BM + (k >> 2) * 16 + (k & 1) * 8;
-            float pf[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              pf[e] = __builtin_fmaf(ep.stem_wp[(c0 + e) * 2], xv.x, ep.stem_wp[(c0 + e) * 2 + 1] * xv.y);
-            uint4 ph, pl;
-            split8(pf, ph, pl, bad);
-            v = (k & 2) ? pl : ph;
-          } else {
-            const long long rp = ep.res_up ? ((long long)n * (H >> 1) + (gy >> 1)) * (W >> 1) + (gx >> 1)
-                                           : ((long long)n * H + gy) * W + gx;
-            v = ep.res[rp * QC + nb * QB + k];
-          }
+          const long long rp = ep.res_up ? ((long long)n * (H >> 1) + (gy >> 1)) * (W >> 1) + (gx >> 1)
+                                         : ((long long)n * H + gy) * W + gx;
+          v = ep.res[rp * QC + nb * QB + k];
         }
         smem[px * QB + (k ^ swzq<QB>(px))] = v;
       }
@@ -222,7 +177,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < WN; ++j) {
-      const int px = min((pg * WN + j) * 32 + lane_px<TX>(l32), P - 1);
+      const int px = min((pg * WN + j) * 32 + l32, P - 1);
 #pragma unroll
       for (int m = 0; m < WM; ++m)
 #pragma unroll
@@ -238,7 +193,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
   auto stage = [&]() {
 #pragma unroll
     for (int j = 0; j < WN; ++j) {
-      const int px = (pg * WN + j) * 32 + lane_px<TX>(l32);
+      const int px = (pg * WN + j) * 32 + l32;
       if (j < nsub && px < P) {
 #pragma unroll
         for (int m = 0; m < WM; ++m)
@@ -333,7 +288,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
           }
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] += __shfl_xor(o[q], 32, 64);
-        const int px = (pg * WN + j) * 32 + lane_px<TX>(l32);
+        const int px = (pg * WN + j) * 32 + l32;
         const long long gp = gpix(px);
         if (h == 0 && j < nsub && gp >= 0) {
 #pragma unroll
@@ -375,8 +330,7 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   constexpr int NT = 512, NWV = NT / 64;
   constexpr int T = KS * KS, HALO = KS / 2;
   constexpr int MWV = BM / (32 * WM), PW = NWV / MWV;
-  using HG = HaloGeom<KS, TX>;
-  constexpr int HY = TY + KS - 1, HX = HG::HX, HXP = HG::HXP, NPIX = HY * HXP;
+  constexpr int HY = TY + KS - 1, HX = TX + KS - 1, NPIX = HY * HX;
   constexpr int NCH = CIN / 16;
   constexpr int NCH2 = CIN2 / 16, QI2 = CIN2 / 4;     // folded projection slabs (one tap each)
   constexpr int NW2 = BM * 4 / 64;                    // their weight DMA rows
@@ -426,10 +380,10 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   for (int jj = 0; jj < JI; ++jj) {
     const int si = (wid + NWV * jj) * 64 + lane;
     const int hp = si >> 2, cq = si & 3;
-    const int hy = hp / HXP, hx = hp - (hp / HXP) * HXP;
+    const int hy = hp / HX, hx = hp - (hp / HX) * HX;
     const int gy = ty0 + hy - HALO, gx = tx0 + hx - HALO;
-    inPC[jj] = (hp < NPIX && hx < HX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-                   ? ((gy >> iu) * Wi + (gx >> iu)) * 4 + (cq ^ HG::swz(hp, hy)) : -1;
+    inPC[jj] = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+                   ? ((gy >> iu) * Wi + (gx >> iu)) * 4 + (cq ^ swz4(hp)) : -1;
   }
   const uint4* inb2 = CIN2 ? ep.in2 + (long long)n * H * W * QI2 : nullptr;
   // slab ch < NCH: the 3x3 weights and the halo of `in`; ch >= NCH: a projection slab (one tap
@@ -488,12 +442,11 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
     const int r = (mw * WM + m) * 32 + l32;
     aS[m] = r * 4 + (h ^ swz4(r));
   }
-  int hp0[WN], hy0[WN];
+  int hp0[WN];
 #pragma unroll
   for (int j = 0; j < WN; ++j) {
-    const int px = min((pg * WN + j) * 32 + lane_px<TX>(l32), P - 1);
-    hy0[j] = px / TX;
-    hp0[j] = hy0[j] * HXP + (px % TX);
+    const int px = min((pg * WN + j) * 32 + l32, P - 1);
+    hp0[j] = (px / TX) * HX + (px % TX);
   }
 
   issue(0, 0);
@@ -511,8 +464,8 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
     }
 #pragma unroll
     for (int j = 0; j < C; ++j) {
-      const int hp = hp0[j] + ky * HXP + kx;
-      const int bs = SW + hp * 4 + (h ^ HG::swz(hp, hy0[j] + ky));
+      const int hp = hp0[j] + ky * HX + kx;
+      const int bs = SW + hp * 4 + (h ^ swz4(hp));
       const f16x8 bh = __builtin_bit_cast(f16x8, sb[bs]);
       const f16x8 bl = __builtin_bit_cast(f16x8, sb[bs ^ 2]);
 #pragma unroll
@@ -611,26 +564,26 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
   for (int t = lo + (blockIdx.x >> 3); t < hi; t += nbx) {
     const int n = t / tiles, tt = t - n * tiles;
     const int ty0 = (tt / tiles_x) * TY, tx0 = (tt % tiles_x) * TX;
-      const uint4* inb = in + (long long)n * H * W * QI;
+    const uint4* inb = in + (long long)n * H * W * QI;
 #pragma unroll
-      for (int jj = 0; jj < JI; ++jj) {
-        const int j = wid + NWV * jj;
-        if (j < NWIN) {
-          const int si = j * 64 + lane;
-          const int hp = si >> 2, cq = si & 3;
-          const int hy = hp / HX, hx = hp - (hp / HX) * HX;
-          const int gy = ty0 + hy - 1, gx = tx0 + hx - 1;
-          const int off = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-                              ? (gy * W + gx) * QI + (cq ^ swz4(hp)) : -1;
+    for (int jj = 0; jj < JI; ++jj) {
+      const int j = wid + NWV * jj;
+      if (j < NWIN) {
+        const int si = j * 64 + lane;
+        const int hp = si >> 2, cq = si & 3;
+        const int hy = hp / HX, hx = hp - (hp / HX) * HX;
+        const int gy = ty0 + hy - 1, gx = tx0 + hx - 1;
+        const int off = (hp < NPIX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+                            ? (gy * W + gx) * QI + (cq ^ swz4(hp)) : -1;
 #pragma unroll
-          for (int s = 0; s < NCH; ++s) {
-            const uint4* src = off >= 0 ? inb + off + s * 4 : &g_x3_zero16;
-            __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(sx + s * SI + j * 64), 16, 0, 0);
-          }
+        for (int s = 0; s < NCH; ++s) {
+          const uint4* src = off >= 0 ? inb + off + s * 4 : &g_x3_zero16;
+          __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(sx + s * SI + j * 64), 16, 0, 0);
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     // opaque per tile: keeps the compiler from hoisting every tap's fragment addresses out of the
     // tile loop (they would stay live across the epilogue: spills)
     int hpb = hp0, aSb = aS;
@@ -673,7 +626,6 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
     et.style = et.style ? et.style + zo : nullptr;
     et.head_w = et.head_w ? et.head_w + zo : nullptr;
     et.head_b = et.head_b ? et.head_b + zo : nullptr;
-    et.stem_wp = et.stem_wp ? et.stem_wp + zo : nullptr;
     x3_epilogue<32, BM, TY, TX, 1, 1>(acc0, et, sx, n, 0, ty0, tx0, H, W, 0, wid, 1);
     __syncthreads();  // staging reads done before the next tile's halo lands
   }
@@ -839,7 +791,7 @@ __global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem_x3(
 #pragma unroll
         for (int k = 0; k < 18; ++k) acc = __builtin_fmaf(w0[co * 18 + k], in[k], acc);
         zf[e] = fmaxf(__builtin_fmaf(scale1[co], acc + bias0[co], shift1[co]), 0.0f);
-        pf[e] = p_out ? __builtin_fmaf(wp[co * 2], xv.x, wp[co * 2 + 1] * xv.y) : 0.0f;
+        pf[e] = __builtin_fmaf(wp[co * 2], xv.x, wp[co * 2 + 1] * xv.y);
       }
       uint4 hi, lo;
       const int base = (q >> 1) * 4 + (q & 1);
@@ -847,11 +799,9 @@ __global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem_x3(
       split8(zf, hi, lo, bad);
       so[0][px * 8 + (base ^ (px & 7))] = hi;
       so[0][px * 8 + ((base + 2) ^ (px & 7))] = lo;
-      if (p_out) {
-        split8(pf, hi, lo, bad);
-        so[1][px * 8 + (base ^ (px & 7))] = hi;
-        so[1][px * 8 + ((base + 2) ^ (px & 7))] = lo;
-      }
+      split8(pf, hi, lo, bad);
+      so[1][px * 8 + (base ^ (px & 7))] = hi;
+      so[1][px * 8 + ((base + 2) ^ (px & 7))] = lo;
     }
   }
   __syncthreads();
@@ -864,7 +814,7 @@ __global__ __launch_bounds__(kSTY * kSTX) void k_cpnet_stem_x3(
     if (py < H && pxg < W) {
       const long long g = (((long long)n * H + py) * W + pxg) * 8 + k;
       z_out[g] = so[0][p * 8 + (k ^ (p & 7))];
-      if (p_out) p_out[g] = so[1][p * 8 + (k ^ (p & 7))];
+      p_out[g] = so[1][p * 8 + (k ^ (p & 7))];
     }
   }
   if (ovf && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(ovf + n, 1);
@@ -1029,7 +979,7 @@ extern "C" int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* 
               CPX_ERR_ARG, "cpx_cpnet_x3_conv: head needs a 3x3 conv with cout 32, no z_out, 1..4 outputs");
   CPX_REQUIRE(!z_up || z_out, CPX_ERR_ARG, "cpx_cpnet_x3_conv: z_up without z_out");
   X3Epi ep{bias, (const uint4*)res, style, scale, shift, (uint4*)y_out, (uint4*)z_out, res_up, relu,
-           z_up, style_stride, head_w, head_b, head_out, n_head, ovf, in_up, nullptr, nullptr, nullptr, nullptr};
+           z_up, style_stride, head_w, head_b, head_out, n_head, ovf, in_up, nullptr, nullptr};
   return x3_launch(ctx, ks, cin, cout, variant, in, wpk, ep, N, H, W);
 }
 
@@ -1049,7 +999,7 @@ extern "C" int cpx_cpnet_x3_conv_proj(cpx_ctx* ctx, int variant, const void* in,
               CPX_ERR_ARG, "cpx_cpnet_x3_conv_proj: style needs a 16-byte aligned [N][stride >= cout] table");
   CPX_REQUIRE(!z_up || z_out, CPX_ERR_ARG, "cpx_cpnet_x3_conv_proj: z_up without z_out");
   X3Epi ep{bias, nullptr, style, scale, shift, (uint4*)y_out, (uint4*)z_out, 0, relu, z_up, style_stride,
-           nullptr, nullptr, nullptr, 0, ovf, 0, (const uint4*)in2, (const uint4*)wpk2, nullptr, nullptr};
+           nullptr, nullptr, nullptr, 0, ovf, 0, (const uint4*)in2, (const uint4*)wpk2};
   return x3_launch_proj(ctx, cin, cout, cin2, variant, in, wpk, ep, N, H, W);
 }
 
@@ -1057,7 +1007,7 @@ extern "C" int cpx_cpnet_x3_stem(cpx_ctx* ctx, const float* x, int N, int H, int
                                  const float* scale0, const float* shift0, const float* w0,
                                  const float* bias0, const float* scale1, const float* shift1,
                                  const float* wp, void* p_out, void* z_out, int* ovf) {
-  CPX_REQUIRE(ctx && x && scale0 && shift0 && w0 && bias0 && scale1 && shift1 && (wp || !p_out) && z_out,
+  CPX_REQUIRE(ctx && x && scale0 && shift0 && w0 && bias0 && scale1 && shift1 && wp && p_out && z_out,
               CPX_ERR_ARG, "cpx_cpnet_x3_stem: null argument");
   CPX_REQUIRE(N > 0 && H > 0 && W > 0, CPX_ERR_ARG, "cpx_cpnet_x3_stem: bad sizes");
   CPX_REQUIRE(((uintptr_t)x % 8) == 0 && ((uintptr_t)p_out | (uintptr_t)z_out) % 16 == 0,
@@ -1069,27 +1019,6 @@ extern "C" int cpx_cpnet_x3_stem(cpx_ctx* ctx, const float* x, int N, int H, int
                      W, scale0, shift0, w0, bias0, scale1, shift1, wp, (uint4*)p_out, (uint4*)z_out, tx,
                      ty, ovf);
   CPX_CHECK_LAUNCH("k_cpnet_stem_x3");
-  return CPX_OK;
-}
-
-extern "C" int cpx_cpnet_x3_conv_stem(cpx_ctx* ctx, const float* x, int N, int H, int W, const void* z,
-                                      const float* wp, const void* wpk, const float* bias, const float* scale,
-                                      const float* shift, void* y_out, void* z_out, int* ovf) {
-  CPX_REQUIRE(ctx && x && z && wp && wpk && (y_out || z_out), CPX_ERR_ARG, "cpx_cpnet_x3_conv_stem: null argument");
-  CPX_REQUIRE(N > 0 && H > 0 && W > 0, CPX_ERR_ARG, "cpx_cpnet_x3_conv_stem: bad sizes");
-  CPX_REQUIRE(!(scale == nullptr) == !(shift == nullptr), CPX_ERR_ARG,
-              "cpx_cpnet_x3_conv_stem: scale and shift go together");
-  CPX_REQUIRE(((uintptr_t)x % 8) == 0 && ((uintptr_t)z | (uintptr_t)wpk | (uintptr_t)y_out | (uintptr_t)z_out) % 16 == 0,
-              CPX_ERR_ARG, "cpx_cpnet_x3_conv_stem: misaligned buffers");
-  X3Epi ep{bias, nullptr, nullptr, scale, shift, (uint4*)y_out, (uint4*)z_out, 0, 1, 0, 0, nullptr, nullptr,
-           nullptr, 0, ovf, 0, nullptr, nullptr, x, wp};
-  const int tx = cpx_div_up(W, 32), ty = cpx_div_up(H, 8);
-  const long long tiles = (long long)N * tx * ty;
-  CPX_REQUIRE(tiles < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv_stem: too many tiles");
-  const int grid = (int)std::max(1LL, std::min(tiles, 2LL * ctx->n_cu));
-  hipLaunchKernelGGL(k_conv_x3_p32, dim3(grid), dim3(512), 0, ctx->stream, (const uint4*)z, (const uint4*)wpk, ep, N,
-                     H, W, tx, ty);
-  CPX_CHECK_LAUNCH("k_conv_x3_p32");
   return CPX_OK;
 }
 

@@ -466,20 +466,11 @@ int cpx_cpnet_x3_conv_proj(cpx_ctx* ctx, int variant, const void* in, int N, int
                            const float* bias, const float* style, int style_stride, const float* scale,
                            const float* shift, int relu, void* y_out, void* z_out, int z_up, int* ovf);
 /* stem on the fp32 network input x [N][H][W][2] (CPX_TILE_F32_NHWC tiles): z0 = relu(scale0 x
- * + shift0), z_out = relu(scale1 (conv3x3(z0, w0) + bias0) + shift1), p_out = conv1x1(x, wp)
- * (optional: NULL skips it), fp32 arithmetic, split stores (32 channels).                     */
+ * + shift0), z_out = relu(scale1 (conv3x3(z0, w0) + bias0) + shift1), p_out = conv1x1(x, wp),
+ * fp32 arithmetic, split stores (32 channels).                                               */
 int cpx_cpnet_x3_stem(cpx_ctx* ctx, const float* x, int N, int H, int W, const float* scale0,
                       const float* shift0, const float* w0, const float* bias0, const float* scale1,
                       const float* shift1, const float* wp, void* p_out, void* z_out, int* ovf);
-/* the first down block's second convolution (32 -> 32, after the stem) with its residual — the
- * block projection conv1x1(x, wp) of the fp32 network input x [N][H][W][2] — formed in the
- * epilogue from x (split-rounded as cpx_cpnet_x3_stem stores it) instead of read: y_out =
- * conv3x3(z, wpk) + bias + conv1x1(x, wp), z_out = relu(scale y_out + shift), both split.  With
- * cpx_cpnet_x3_stem(p_out = NULL) it replaces the stem's p tensor (written, then read back).
- * Bit-identical to cpx_cpnet_x3_stem + cpx_cpnet_x3_conv(res = p).                            */
-int cpx_cpnet_x3_conv_stem(cpx_ctx* ctx, const float* x, int N, int H, int W, const void* z, const float* wp,
-                           const void* wpk, const float* bias, const float* scale, const float* shift,
-                           void* y_out, void* z_out, int* ovf);
 /* 2x2/2 max-pool of split [N][2Hh][2Ww][Cn] -> x_out (exact) and z_out = relu?(scale x + shift). */
 int cpx_cpnet_x3_pool(cpx_ctx* ctx, const void* in, const float* scale, const float* shift,
                       int relu, int N, int Hh, int Ww, int Cn, void* x_out, void* z_out, int* ovf);
