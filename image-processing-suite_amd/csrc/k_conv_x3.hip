@@ -122,7 +122,11 @@ struct X3Epi {
 // subtile (j >= nsub) only move data.
 template <int COUT, int BM, int TY, int TX, int WM, int WN>
 __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi& ep, uint4* smem, int n,
-                                            int nb, int ty0, int tx0, int H, int W, int mw, int pg, int nsub) {
+                                            int nb, int ty0, int tx0, int H, int W, int mw, int pg, int nsub,
+                                            int tid = -1) {
+  // tid: threadIdx.x, or a per-tile opaque copy of it from a persistent caller (the staging
+  // offsets derived from it are then recomputed per tile instead of hoisted and spilled)
+  if (tid < 0) tid = threadIdx.x;
   constexpr int NT = 512;
   constexpr int P = TY * TX;
   constexpr int QB = BM / 4;
@@ -161,7 +165,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
   if (ep.res) {
 #pragma unroll
     for (int r = 0; r < OUT_R; ++r) {
-      const int i = threadIdx.x + r * NT;
+      const int i = tid + r * NT;
       if (i < P * QB) {
         const int px = i / QB, k = i - px * QB;
         const int gy = ty0 + px / TX, gx = tx0 + px % TX;
@@ -211,7 +215,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
   auto drain = [&](uint4* dst) {
 #pragma unroll
     for (int r = 0; r < OUT_R; ++r) {
-      const int i = threadIdx.x + r * NT;
+      const int i = tid + r * NT;
       const int px = i / QB, k = i - px * QB;
       const long long gp = gpix(px);
       if (i < P * QB && gp >= 0) dst[gp * QC + nb * QB + k] = smem[px * QB + (k ^ swzq<QB>(px))];
@@ -308,7 +312,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
     const long long W2 = 2LL * W;
 #pragma unroll
     for (int r = 0; r < 4 * OUT_R; ++r) {
-      const int i = threadIdx.x + r * NT;
+      const int i = tid + r * NT;
       if (i >= 4 * P * QB) continue;
       const int k = i % QB;
       const int d = i / QB;
@@ -487,8 +491,14 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
       static_assert(WN <= 2, "WN");
     }
   };
+  // CPX_X3_DIAG (development timing builds, tools/build_variants.sh; wrong results by
+  // construction): 1 = no slab DMA after the first (compute + barriers only), 2 = that and no
+  // per-slab barrier, 3 = no epilogue, 4 = 2 and 3 (the MFMA + fragment-read loop alone)
+#ifndef CPX_X3_DIAG
+#define CPX_X3_DIAG 0
+#endif
   for (int ch = 0; ch < NCH; ++ch) {
-    if (ch + 1 < NCHT) issue(ch + 1, (ch + 1) & 1);
+    if (CPX_X3_DIAG != 1 && CPX_X3_DIAG != 2 && CPX_X3_DIAG != 4 && ch + 1 < NCHT) issue(ch + 1, (ch + 1) & 1);
     const uint4* sb = smem + (ch & 1) * SB;
     per_nsub([&](auto cnt) {
       if constexpr (WM * WN == 1) {
@@ -502,7 +512,7 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
       }
     });
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (CPX_X3_DIAG != 2 && CPX_X3_DIAG != 4) __syncthreads();
   }
   // folded projection: one centre tap per slab of in2 (weight slot 0)
 #pragma unroll 1
@@ -522,6 +532,17 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc0[m][j][r] += acc1[m][j][r] * kLoInv;  // exact product, one rounding
 
+  if (CPX_X3_DIAG == 3 || CPX_X3_DIAG == 4) {  // keep the sums alive without the epilogue
+    float t = 0.0f;
+#pragma unroll
+    for (int m = 0; m < WM; ++m)
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += acc0[m][j][r];
+    if (t == 1.2345e-30f && ep.ovf) atomicOr(ep.ovf, 2);
+    return;
+  }
   x3_epilogue<COUT, BM, TY, TX, WM, WN>(acc0, ep, smem, n, nb, ty0, tx0, H, W, mw, pg, nsub);
 }
 
@@ -626,7 +647,9 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
     et.style = et.style ? et.style + zo : nullptr;
     et.head_w = et.head_w ? et.head_w + zo : nullptr;
     et.head_b = et.head_b ? et.head_b + zo : nullptr;
-    x3_epilogue<32, BM, TY, TX, 1, 1>(acc0, et, sx, n, 0, ty0, tx0, H, W, 0, wid, 1);
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    x3_epilogue<32, BM, TY, TX, 1, 1>(acc0, et, sx, n, 0, ty0, tx0, H, W, 0, wid, 1, tid);
     __syncthreads();  // staging reads done before the next tile's halo lands
   }
 }
