@@ -9,6 +9,7 @@
 // [Ly+40][Lx+40] -> net-resolution labels [Ly][Lx] -> full-resolution labels int32 [H][W].
 // Every reduction is integer (exact) or fixed-order, so masks are bit-reproducible.
 #include "cpx_internal.h"
+#include <stdlib.h>
 #include <limits.h>
 #include <math.h>
 #include <stdio.h>
@@ -2097,7 +2098,12 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   const size_t sz_cnt = al(sizeof(int) * (size_t)B * (kMaxSeeds + 1));
   const size_t sz_act = al(sizeof(int) * B * n);
   const size_t sz_small = al(sizeof(int) * (size_t)B);
-  const int rounds = 24 + cpx_div_up(std::max(0, niter - 384), 128) + 2;
+  // follow rounds: K = k0 steps while most pixels still move (until step sw), then k1 for the
+  // long tail; CPX_FOLLOW_K0 / _SWITCH / _K1 override the defaults 16 / 384 / 128 (A/B runs)
+  static const int k0 = std::max(1, getenv("CPX_FOLLOW_K0") ? atoi(getenv("CPX_FOLLOW_K0")) : 16);
+  static const int sw = std::max(0, getenv("CPX_FOLLOW_SWITCH") ? atoi(getenv("CPX_FOLLOW_SWITCH")) : 384);
+  static const int k1 = std::max(1, getenv("CPX_FOLLOW_K1") ? atoi(getenv("CPX_FOLLOW_K1")) : 128);
+  const int rounds = cpx_div_up(sw, k0) + cpx_div_up(std::max(0, niter - sw), k1) + 2;
   const size_t sz_fcnt = al(sizeof(int) * (size_t)B * (rounds + 1));
   const size_t sz_items = al((size_t)16 * B * n);
   const size_t sz_tiles = al(sizeof(int) * (size_t)B * ntile);
@@ -2142,12 +2148,11 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   else
     hipLaunchKernelGGL(k_dyn_prep<false>, gprep, dim3(kT), 0, ctx->stream, yf_dev, Ly, Lx, Dy, Dx,
                        tabs.uy, tabs.ux, d);
-  // follow rounds: K = 16 steps while most pixels still move, then 128 for the long tail
   const int fblk = std::max(1, std::min(cpx_div_up(n, kT), (16 * ctx->n_cu + B - 1) / B));
   {
     int step = 0, r = 0;
     do {  // at least one round: with niter = 0 it only records the start positions
-      const int K = step < 384 ? 16 : 128;
+      const int K = step < sw ? k0 : k1;
       const FollowItem* in = (const FollowItem*)(r & 1 ? d.fitems1 : d.fitems0);
       FollowItem* out = (FollowItem*)(r & 1 ? d.fitems0 : d.fitems1);
       hipLaunchKernelGGL(k_dyn_follow, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step,
