@@ -120,13 +120,19 @@ struct X3Epi {
 // residual, residual-stream store, style, eval BatchNorm, ReLU, next-input store or output head.
 // Every thread of the block takes part (the output tile is staged through smem); waves without a
 // subtile (j >= nsub) only move data.
+// res_lds (optional): the residual tile already in LDS in the staging layout (k_conv_x3 DMAs it
+// into its free slab buffer during the last slab); y is then staged in `smem` and z in the
+// residual's buffer (y-less calls: z in `smem`), which needs two block barriers instead of six and
+// no global-load wait.
 template <int COUT, int BM, int TY, int TX, int WM, int WN>
 __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi& ep, uint4* smem, int n,
                                             int nb, int ty0, int tx0, int H, int W, int mw, int pg, int nsub,
-                                            int tid = -1) {
+                                            int tid = -1, uint4* res_lds = nullptr) {
   // tid: threadIdx.x, or a per-tile opaque copy of it from a persistent caller (the staging
   // offsets derived from it are then recomputed per tile instead of hoisted and spilled)
   if (tid < 0) tid = threadIdx.x;
+  uint4* const ybuf = smem;
+  uint4* const zbuf = (res_lds && ep.y) ? res_lds : smem;
   constexpr int NT = 512;
   constexpr int P = TY * TX;
   constexpr int QB = BM / 4;
@@ -142,9 +148,9 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
   };
   // lane's channel group (m, g): channels cb(m) + 8 g + {0..3} of the block, slab (m', g >> 1)
   auto slice = [&](int m) { return mw * WM + m; };
-  auto piece = [&](int px, int m, int g, int lo) -> uint2* {
+  auto piece = [&](const uint4* buf, int px, int m, int g, int lo) -> uint2* {
     const int q = (slice(m) * 2 + (g >> 1)) * 4 + 2 * lo + (g & 1);
-    return reinterpret_cast<uint2*>(smem + px * QB + (q ^ swzq<QB>(px))) + h;
+    return reinterpret_cast<uint2*>(const_cast<uint4*>(buf) + px * QB + (q ^ swzq<QB>(px))) + h;
   };
   auto chan = [&](int m, int g) { return nb * BM + slice(m) * 32 + 8 * g + 4 * h; };
   if (ep.bias) {
@@ -163,22 +169,25 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
       }
   }
   if (ep.res) {
+    const uint4* rbuf = res_lds ? res_lds : smem;
+    if (!res_lds) {
 #pragma unroll
-    for (int r = 0; r < OUT_R; ++r) {
-      const int i = tid + r * NT;
-      if (i < P * QB) {
-        const int px = i / QB, k = i - px * QB;
-        const int gy = ty0 + px / TX, gx = tx0 + px % TX;
-        uint4 v = {0u, 0u, 0u, 0u};
-        if (gy < H && gx < W) {
-          const long long rp = ep.res_up ? ((long long)n * (H >> 1) + (gy >> 1)) * (W >> 1) + (gx >> 1)
-                                         : ((long long)n * H + gy) * W + gx;
-          v = ep.res[rp * QC + nb * QB + k];
+      for (int r = 0; r < OUT_R; ++r) {
+        const int i = tid + r * NT;
+        if (i < P * QB) {
+          const int px = i / QB, k = i - px * QB;
+          const int gy = ty0 + px / TX, gx = tx0 + px % TX;
+          uint4 v = {0u, 0u, 0u, 0u};
+          if (gy < H && gx < W) {
+            const long long rp = ep.res_up ? ((long long)n * (H >> 1) + (gy >> 1)) * (W >> 1) + (gx >> 1)
+                                           : ((long long)n * H + gy) * W + gx;
+            v = ep.res[rp * QC + nb * QB + k];
+          }
+          smem[px * QB + (k ^ swzq<QB>(px))] = v;
         }
-        smem[px * QB + (k ^ swzq<QB>(px))] = v;
       }
+      __syncthreads();
     }
-    __syncthreads();
 #pragma unroll
     for (int j = 0; j < WN; ++j) {
       const int px = min((pg * WN + j) * 32 + l32, P - 1);
@@ -187,14 +196,14 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           float rv[4];
-          join4(*piece(px, m, g, 0), *piece(px, m, g, 1), rv);
+          join4(*piece(rbuf, px, m, g, 0), *piece(rbuf, px, m, g, 1), rv);
 #pragma unroll
           for (int k = 0; k < 4; ++k) acc0[m][j][4 * g + k] += rv[k];
         }
     }
-    __syncthreads();
+    if (!res_lds) __syncthreads();  // (res_lds: y is staged in the other buffer, z after y's barrier)
   }
-  auto stage = [&]() {
+  auto stage = [&](uint4* buf) {
 #pragma unroll
     for (int j = 0; j < WN; ++j) {
       const int px = (pg * WN + j) * 32 + l32;
@@ -206,19 +215,19 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
             uint2 hi, lo;
             split4(acc0[m][j][4 * g], acc0[m][j][4 * g + 1], acc0[m][j][4 * g + 2], acc0[m][j][4 * g + 3],
                    hi, lo, bad);
-            *piece(px, m, g, 0) = hi;
-            *piece(px, m, g, 1) = lo;
+            *piece(buf, px, m, g, 0) = hi;
+            *piece(buf, px, m, g, 1) = lo;
           }
       }
     }
   };
-  auto drain = [&](uint4* dst) {
+  auto drain = [&](const uint4* buf, uint4* dst) {
 #pragma unroll
     for (int r = 0; r < OUT_R; ++r) {
       const int i = tid + r * NT;
       const int px = i / QB, k = i - px * QB;
       const long long gp = gpix(px);
-      if (i < P * QB && gp >= 0) dst[gp * QC + nb * QB + k] = smem[px * QB + (k ^ swzq<QB>(px))];
+      if (i < P * QB && gp >= 0) dst[gp * QC + nb * QB + k] = buf[px * QB + (k ^ swzq<QB>(px))];
     }
   };
   auto flag = [&]() {
@@ -227,10 +236,10 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
     }
   };
   if (ep.y) {
-    stage();
+    stage(ybuf);
     __syncthreads();
-    drain(ep.y);
-    __syncthreads();
+    drain(ybuf, ep.y);
+    if (zbuf == ybuf) __syncthreads();  // z is staged over y's tile
   }
   if (!ep.z && !ep.head) {
     flag();
@@ -304,10 +313,10 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
       return;
     }
   }
-  stage();
+  stage(zbuf);
   __syncthreads();
   if (!ep.z_up) {
-    drain(ep.z);
+    drain(zbuf, ep.z);
   } else {
     const long long W2 = 2LL * W;
 #pragma unroll
@@ -321,7 +330,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
       const int gy = ty0 + (dy >> 1), gx = tx0 + (dx >> 1);
       if (gy >= H || gx >= W) continue;
       const long long dp = ((long long)n * 2 * H + 2LL * ty0 + dy) * W2 + 2LL * tx0 + dx;
-      ep.z[dp * QC + nb * QB + k] = smem[px * QB + (k ^ swzq<QB>(px))];
+      ep.z[dp * QC + nb * QB + k] = zbuf[px * QB + (k ^ swzq<QB>(px))];
     }
   }
   flag();
@@ -390,6 +399,31 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
                    ? ((gy >> iu) * Wi + (gx >> iu)) * 4 + (cq ^ swz4(hp)) : -1;
   }
   const uint4* inb2 = CIN2 ? ep.in2 + (long long)n * H * W * QI2 : nullptr;
+  // the residual tile, DMA'd during the last slab into the slab buffer that slab does not use, in
+  // the epilogue's staging layout (chunk k of pixel px at px * QB + (k ^ swzq(px)))
+  constexpr int NCHT_ = NCH + NCH2;
+  constexpr bool kResPre = P * QB <= SB;
+  uint4* const bufO = smem + ((NCHT_ - 1) & 1) * SB;  // the last slab's buffer
+  uint4* const bufR = smem + (NCHT_ & 1) * SB;        // free during the last slab
+  auto issue_res = [&]() {
+    constexpr int NRR = (P * QB + 63) / 64, JR = (NRR + NWV - 1) / NWV;
+#pragma unroll
+    for (int jj = 0; jj < JR; ++jj) {
+      const int j = wid + NWV * jj;
+      if (j < NRR) {
+        const int sl = j * 64 + lane;
+        const int px = sl / QB, kk = (sl - (sl / QB) * QB) ^ swzq<QB>(px);
+        const int gy = ty0 + px / TX, gx = tx0 + px % TX;
+        const uint4* src = &g_x3_zero16;
+        if (sl < P * QB && gy < H && gx < W) {
+          const long long rp = ep.res_up ? ((long long)n * (H >> 1) + (gy >> 1)) * (W >> 1) + (gx >> 1)
+                                         : ((long long)n * H + gy) * W + gx;
+          src = ep.res + rp * QC + nb * QB + kk;
+        }
+        __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(bufR + j * 64), 16, 0, 0);
+      }
+    }
+  };
   // slab ch < NCH: the 3x3 weights and the halo of `in`; ch >= NCH: a projection slab (one tap
   // of weights, the halo of in2 — only its centre is read)
   auto issue = [&](int ch, int buf) {
@@ -499,6 +533,7 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
 #endif
   for (int ch = 0; ch < NCH; ++ch) {
     if (CPX_X3_DIAG != 1 && CPX_X3_DIAG != 2 && CPX_X3_DIAG != 4 && ch + 1 < NCHT) issue(ch + 1, (ch + 1) & 1);
+    if (kResPre && ch + 1 == NCHT && ep.res) issue_res();
     const uint4* sb = smem + (ch & 1) * SB;
     per_nsub([&](auto cnt) {
       if constexpr (WM * WN == 1) {
@@ -518,6 +553,7 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
 #pragma unroll 1
   for (int ch = NCH; ch < NCHT; ++ch) {
     if (ch + 1 < NCHT) issue(ch + 1, (ch + 1) & 1);
+    if (kResPre && ch + 1 == NCHT && ep.res) issue_res();
     const uint4* sb = smem + (ch & 1) * SB;
     per_nsub([&](auto cnt) { tapbody(cnt, sb, 0, HALO, HALO); });
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -543,7 +579,11 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
     if (t == 1.2345e-30f && ep.ovf) atomicOr(ep.ovf, 2);
     return;
   }
-  x3_epilogue<COUT, BM, TY, TX, WM, WN>(acc0, ep, smem, n, nb, ty0, tx0, H, W, mw, pg, nsub);
+  if constexpr (kResPre)
+    x3_epilogue<COUT, BM, TY, TX, WM, WN>(acc0, ep, bufO, n, nb, ty0, tx0, H, W, mw, pg, nsub, -1,
+                                          ep.res ? bufR : nullptr);
+  else
+    x3_epilogue<COUT, BM, TY, TX, WM, WN>(acc0, ep, smem, n, nb, ty0, tx0, H, W, mw, pg, nsub);
 }
 
 // The 224^2 level's 32 -> 32 convolutions as a persistent grid: both slabs of the weights
