@@ -715,13 +715,20 @@ bool x3_cfg(int ks, int cin, int cout, int variant, X3Cfg* c) {
   return true;
 }
 
+// development knob (A/B runs): CPX_X3_LDS_PAD bytes of unused dynamic LDS per convolution block,
+// which lowers the convolutions' residency per CU and leaves room for the other pipeline's kernels
+static size_t x3_lds_pad() {
+  static const size_t pad = getenv("CPX_X3_LDS_PAD") ? (size_t)atol(getenv("CPX_X3_LDS_PAD")) : 0;
+  return pad;
+}
+
 template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, int CIN2 = 0>
 int x3_run(cpx_ctx* ctx, const void* in, const void* wpk, const X3Epi& ep, int N, int H, int W) {
   const int tx = cpx_div_up(W, TX), ty = cpx_div_up(H, TY);
   const long long blocks = (long long)N * tx * ty * (COUT / BM);  // (tile, output-channel block) items
   CPX_REQUIRE(blocks < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv: too many tiles");
   hipLaunchKernelGGL((k_conv_x3<KS, CIN, COUT, BM, TY, TX, WM, WN, WPE, CIN2>), dim3((unsigned)blocks),
-                     dim3(512), 0, ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N, H, W, tx, ty);
+                     dim3(512), x3_lds_pad(), ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N, H, W, tx, ty);
   CPX_CHECK_LAUNCH("k_conv_x3");
   return CPX_OK;
 }
