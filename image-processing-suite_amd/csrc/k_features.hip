@@ -511,7 +511,11 @@ int launch_fallbacks(cpx_ctx* ctx, hipStream_t stream, const cpx_fallback_lists&
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  const int per_fov = std::max(1, std::min(max_label * C * CPX_N_ANGLES, (ctx->n_cu + B - 1) / B));
+  // blocks per FOV: enough for two listed objects' C x 4 items at once (the bench plate lists
+  // ~2 objects per 48 FOVs, each a serial chain of items on the old n_cu / B blocks per FOV:
+  // 0.85 ms per object set, gpurun_out/r04k); a block without an item exits at once
+  const int per_fov = std::max(1, std::min(max_label * C * CPX_N_ANGLES,
+                                           std::max((ctx->n_cu + B - 1) / B, 2 * C * CPX_N_ANGLES)));
   hipLaunchKernelGGL(k_intensity_texture, dim3(per_fov, B), dim3(kTexThreads), lds, stream,
                      (const int*)a.labels_dev, a.corr_dev, C, H, W, max_label, F, a.objects_dev,
                      (const int*)fb.tex, (const int*)fb.n_tex, a.feats_dev);

@@ -43,6 +43,11 @@ def main():
         print(f"{s}: objects/FOV min {n.min()} mean {n.mean():.1f} max {n.max()}; bbox px "
               f"p10 {np.percentile(areas, 10):.0f} p50 {np.percentile(areas, 50):.0f} "
               f"p90 {np.percentile(areas, 90):.0f} max {areas.max()}; > 12288: {(areas > 12288).mean():.2f}")
+        # the fallback kernels' share: bbox > 65535 px (texture) or a membership mask over 4096 words
+        fb = [int(((o["bbox"][:, 2] - o["bbox"][:, 0]) * (o["bbox"][:, 3] - o["bbox"][:, 1]) > 65535).sum() +
+                  ((o["bbox"][:, 2] - o["bbox"][:, 0] + 4) * ((o["bbox"][:, 3] - o["bbox"][:, 1] + 35) // 32)
+                   > 4096).sum()) for o in res.objects[s]]
+        print(f"{s}: fallback objects per FOV {fb}")
     try:
         prof = dev.lib.cpx_debug_glcm_prof
         prof.argtypes = [ct.c_void_p, ct.c_int]
