@@ -132,6 +132,12 @@ struct cpx_fallback_lists {
 // Fallback launcher cpx_features_fast calls on its stream once the lists exist.
 typedef int (*cpx_fallback_fn)(cpx_ctx* ctx, hipStream_t stream, const cpx_fallback_lists& fb,
                                void* arg);
+// register-resident fp32 flow-error screening (k_flowerr_reg.hip): flags the masks it decides in
+// bad[] (and lists the undecided ones in und) before the LDS screening kernels of cpx_seg_masks;
+// uses the queue counters ctr[0 .. 2] (zeroed by the caller)
+int cpx_flow_error_reg_launch(int n_cu, hipStream_t stream, const int* m0, const float2* dpf, int Dy, int Dx,
+                              int B, int ML, const cpx_object* obj, const int* off, int* ctr, double thr,
+                              unsigned char* bad, int* und);
 int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B, int C,
                       int H, int W, int max_label, int F, const cpx_object* objects_dev,
                       const cpx_fov_objects* hdr_dev, double* feats_dev, cpx_fallback_lists* fb,

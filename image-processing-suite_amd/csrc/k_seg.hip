@@ -926,6 +926,8 @@ __global__ __launch_bounds__(THREADS, WPE) void k_flow_error_lds(  // WPE waves 
     // block-uniform: objects of the smaller variant or of k_flow_error_big are skipped
     if (!fe_fits(bh, bw, THREADS, U, CELLS)) continue;
     if (lo_threads > 0 && fe_fits(bh, bw, lo_threads, lo_units, lo_cells)) continue;
+    // screening: masks k_flow_error_reg already decided (or deferred) carry their flag
+    if (kScreen && !list && bad[(long long)fov * (max_label + 1) + L] != 0) continue;
     // rows per unit: the one-block-per-CU variant (latency-bound: one mask at a time) takes the
     // fewest (<= kFeKS) that keep the units within the block, so a mask spreads over more lanes
     // with shorter per-iteration chains; the multi-block variants keep kFeKS (throughput-bound:
@@ -2189,7 +2191,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   const size_t sz_l2i = al(sizeof(int) * (size_t)B * (ML + 1));
   const size_t sz_abs = al(sizeof(int) * (size_t)B * ML);
   const size_t sz_nl = sz_abs;
-  const size_t sz_off = al(sizeof(int) * (size_t)(B + 1 + 8));  // prefix + 8 queue counters
+  const size_t sz_off = al(sizeof(int) * (size_t)(B + 1 + 11));  // prefix + 11 queue counters
   const size_t sz_und = al(sizeof(int) * ((size_t)B * ML + 1));  // screening: undecided masks
   const size_t gscr_per = (size_t)2 * (Dy + 2) * (Dx + 2);  // doubles per FOV (oversize masks)
   const size_t sz_gscr = al(sizeof(double) * B * gscr_per);
@@ -2210,7 +2212,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
     rc = cpx_objects(ctx, d.m0, B, Dy, Dx, ML, 0, lst, obj, hdr);
     if (rc) return rc;
     CPX_CHECK_HIP(hipMemsetAsync(bad, 0, sz_bad, ctx->stream));
-    CPX_CHECK_HIP(hipMemsetAsync(off + B + 1, 0, 8 * sizeof(int), ctx->stream));
+    CPX_CHECK_HIP(hipMemsetAsync(off + B + 1, 0, 11 * sizeof(int), ctx->stream));
     CPX_CHECK_HIP(hipMemsetAsync(und, 0, sizeof(int), ctx->stream));
     hipLaunchKernelGGL(k_obj_prefix, dim3(1), dim3(64), 0, ctx->stream, B,
                        (const cpx_fov_objects*)hdr, off);
@@ -2224,6 +2226,14 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
                      ctx->stream, (const int*)d.m0, (const float2*)d.dpf, Dy, Dx, B, ML,             \
                      (const cpx_object*)obj, (const int*)off, off + B + (CTR), LT, LU, LC, flow_threshold, \
                      bad, (const int*)nullptr, und)
+      // masks whose shorter side fits 48 / 96 register rows (and the longer one 126 lanes' columns)
+      // first, in VGPRs (k_flow_error_reg); the LDS kernels skip the masks those flagged
+      static const bool reg = !getenv("CPX_FE_NOREG");
+      if (reg) {
+        rc = cpx_flow_error_reg_launch(ctx->n_cu, ctx->stream, d.m0, (const float2*)d.dpf, Dy, Dx, B, ML,
+                                       obj, off, off + B + 9, flow_threshold, bad, und);
+        if (rc) return rc;
+      }
       // six waves per SIMD for the small and mid classes; the large class as 512 threads with two
       // units each (the same masks as the fp64 1024 x 1 kernel), two 79 KiB blocks per CU
       FE_SCREEN(kFeSmallThreads, kFeSmallCells, kFeU, 6, 6, 6, 0, 0, 0);
