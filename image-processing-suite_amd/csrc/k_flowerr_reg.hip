@@ -11,9 +11,6 @@
 #include <math.h>
 #include <stdlib.h>
 
-#ifndef CPX_FE_REG1_STAGE
-#define CPX_FE_REG1_STAGE 0  // development bisection builds: 1 claim, 2 + setup, 3 + sweeps
-#endif
 
 #pragma clang fp contract(off)
 
@@ -367,9 +364,6 @@ __global__ __launch_bounds__(64, 2) void k_flow_error_reg1(
     const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
     bool tr = false;
     if (fe_reg_class(bh, bw, tr) != 1) continue;  // wave-uniform
-#if CPX_FE_REG1_STAGE == 1
-    continue;
-#endif
     const int SR = __builtin_amdgcn_readfirstlane(tr ? bw : bh), SC = tr ? bh : bw;  // storage rows / columns
     const int* lab = m0 + (long long)fov * n + (long long)r0 * Dx + c0;
     hcol[lane] = 0;
@@ -420,10 +414,6 @@ __global__ __launch_bounds__(64, 2) void k_flow_error_reg1(
     const int jc = __builtin_amdgcn_readfirstlane((tr ? xm : ym) - 1), cgc = tr ? ym : xm;
     float cadd = lane == cgc - 1 ? 1.f : 0.f;
     const int niter = 2 * ((bw - 1) + (bh - 1));
-#if CPX_FE_REG1_STAGE == 2
-    if (lane == 0 && niter == -12345) bad[0] = (unsigned char)(ym2 + xm2 + jc + (int)cadd);
-    continue;
-#endif
     if (niter > 0) fe_row_op<0, RW>(T, jc, cadd);  // the first iteration's T[centre] += 1
     // ---- the sweeps (rows in groups of 8; rows past SR have Wt = 0 and stay 0)
     for (int it = 0; it < niter; ++it) {
@@ -445,15 +435,6 @@ __global__ __launch_bounds__(64, 2) void k_flow_error_reg1(
       }
       if (it + 1 < niter) fe_row_op<0, RW>(T, jc, cadd);  // the next sweep's T[centre] += 1
     }
-#if CPX_FE_REG1_STAGE == 3
-    {
-      float acc = 0.f;
-#pragma unroll
-      for (int k = 0; k < RW; ++k) acc += T[k];
-      if (lane == 0 && acc == -1.f) bad[0] = 0;
-      continue;
-    }
-#endif
     // ---- gradients, normalisation, error vs dP/5 (k_flow_error_lds's screening arithmetic); one
     // row per iteration from T[0] / Wt[0], the arrays shifted down by one row after it
     const float2* F = dpf + (long long)fov * n;
@@ -505,19 +486,6 @@ __global__ __launch_bounds__(64, 2) void k_flow_error_reg1(
     e0 = wave_sum(e0);
     e1 = wave_sum(e1);
     eb = wave_sum(eb);
-#if CPX_FE_REG1_STAGE == 4
-    if (lane == 0 && e0 + e1 + eb == -1.0) bad[0] = 0;
-    continue;
-#endif
-#if CPX_FE_REG1_STAGE == 5
-    if (lane == 0) {
-      const double err = 0.0 + e0 / (double)o.area + e1 / (double)o.area;
-      const double bnd = eb / (double)o.area + 1e-9 * (1.0 + err);
-      const unsigned char v = err - thr > bnd ? 1 : thr - err > bnd ? 2 : 3;
-      if (v != 3) bad[(long long)fov * (max_label + 1) + L] = v;
-    }
-    continue;
-#endif
     if (lane == 0) {
       const double err = 0.0 + e0 / (double)o.area + e1 / (double)o.area;
       const double bnd = eb / (double)o.area + 1e-9 * (1.0 + err);
