@@ -259,11 +259,15 @@ __global__ __launch_bounds__(64 * NW, 2) void k_flow_error_reg(
     // one row per iteration from T[0] / Wt[0], the arrays shifted down by one row after it (the
     // heavy fp64 body is emitted once; static register indices only)
     fe_v2 tu = up, dnx = nrow == RW ? dn : fe_v2{0.f, 0.f};
+    // eight rows per iteration from T[0 .. 8] / Wt[0 .. 7], the arrays shifted down by eight rows
+    // after it (static register indices only); the row below the slab enters at the first shift
 #pragma unroll 1
-    for (int j = 0; j < nrow; ++j) {
-      const int gr = 1 + wv * RS + j;
-      const fe_v2 tc = T[0], wc2 = Wt[0];
-      const fe_v2 td = RW > 1 ? T[1] : dnx;
+    for (int j0 = 0; j0 < nrow; j0 += 8) {
+#pragma unroll
+     for (int jj = 0; jj < 8; ++jj) {
+      const int gr = 1 + wv * RS + j0 + jj;
+      const fe_v2 tc = T[jj], wc2 = Wt[jj];
+      const fe_v2 td = T[jj + 1];
       // storage horizontal neighbours of columns a (2l) and b (2l + 1)
       const float la = dpp_from_left(tc.y), ra = tc.y, lb = tc.x, rb = dpp_from_right(tc.x);
 #pragma unroll
@@ -297,13 +301,12 @@ __global__ __launch_bounds__(64 * NW, 2) void k_flow_error_reg(
         }
       }
       tu = tc;
+     }
 #pragma unroll
-      for (int k = 0; k + 1 < RW; ++k) {
-        T[k] = T[k + 1];
-        Wt[k] = Wt[k + 1];
+      for (int k = 0; k < RW; ++k) {
+        T[k] = k + 8 < RW ? T[k + 8] : k + 8 == RW ? dnx : fe_v2{0.f, 0.f};
+        Wt[k] = k + 8 < RW ? Wt[k + 8] : fe_v2{0.f, 0.f};
       }
-      T[RW - 1] = dnx;
-      Wt[RW - 1] = fe_v2{0.f, 0.f};
       dnx = fe_v2{0.f, 0.f};
     }
     e0 = wave_sum(e0);
@@ -417,19 +420,25 @@ __global__ __launch_bounds__(64, 2) void k_flow_error_reg1(
     if (niter > 0) fe_row_op<0, RW>(T, jc, cadd);  // the first iteration's T[centre] += 1
     // ---- the sweeps (rows in groups of 8; rows past SR have Wt = 0 and stay 0)
     for (int it = 0; it < niter; ++it) {
-      float po = 0.f;
+      float po = 0.f;  // the old value of the row above the group
 #pragma unroll
       for (int g = 0; g < RW / 8; ++g) {
         if (8 * g < SR) {
+          // the group's vertical sums from the old rows, then the horizontal sums, then the
+          // stores: eight rows between a sum and its DPP reads (no hazard wait states)
+          float v[8];
 #pragma unroll
           for (int jj = 0; jj < 8; ++jj) {
             const int j = 8 * g + jj;
-            const float cur = T[j];
+            const float up = jj ? T[j - 1] : po;
             const float nx = j + 1 < RW ? T[j + 1] : 0.f;
-            const float v = (po + cur) + nx;
-            const float h = (dpp_from_left(v) + v) + dpp_from_right(v);
-            po = cur;
-            T[j] = h * Wt[j];
+            v[jj] = (up + T[j]) + nx;
+          }
+          po = T[8 * g + 7];
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            const int j = 8 * g + jj;
+            T[j] = ((dpp_from_left(v[jj]) + v[jj]) + dpp_from_right(v[jj])) * Wt[j];
           }
         }
       }
@@ -443,45 +452,53 @@ __global__ __launch_bounds__(64, 2) void k_flow_error_reg1(
     const double alpha = 4.0 * (double)niter * 0x1p-126;
     double e0 = 0.0, e1 = 0.0, eb = 0.0;
     float tu = 0.f;
+    // eight rows per iteration from T[0 .. 8] / Wt[0 .. 7], the arrays shifted down by eight rows
+    // after it (static register indices only; nine moves per row instead of eighty)
 #pragma unroll 1
-    for (int j = 0; j < SR; ++j) {
-      const float tc = T[0], w = Wt[0], td = T[1];
-      const float sl = dpp_from_left(tc), sr = dpp_from_right(tc);
-      if (w != 0.f) {
-        const int gr = j + 1;
-        // original orientation: down / up / right / left
-        const double tdn = (double)(tr ? sr : td), tup = (double)(tr ? sl : tu);
-        const double trt = (double)(tr ? td : sr), tlf = (double)(tr ? tu : sl);
-        const int Y = tr ? gc : gr, X = tr ? gr : gc;
-        const double dy = tdn - tup;
-        const double dx = trt - tlf;
-        const double g = sqrt(dy * dy + dx * dx);
-        const double nrm = 1e-20 + g;
-        const double my = dy / nrm, mx = dx / nrm;
-        const float2 f = F[(long long)(r0 + Y - 1) * Dx + c0 + X - 1];
-        const double fy = (double)(f.x / 5.0f), fx = (double)(f.y / 5.0f);
-        const double ty = my - fy;
-        const double tx = mx - fx;
-        e0 += ty * ty;
-        e1 += tx * tx;
-        const double Dy_ = rho * (tdn + tup) + 2.0 * alpha, Dx_ = rho * (trt + tlf) + 2.0 * alpha;
-        const double D = sqrt(Dy_ * Dy_ + Dx_ * Dx_) * (1.0 + 1e-9);
-        const double ff = sqrt(fy * fy + fx * fx);
-        if (g > 3.0 * D && g > 1e-12) {
-          const double ep = 2.0 * D / g + 1e-7;
-          eb += ep * (2.0 * sqrt(ty * ty + tx * tx) + ep);
-        } else {
-          eb += (1.0 + ff) * (1.0 + ff);
-        }
-      }
-      tu = tc;
+    for (int j0 = 0; j0 < SR; j0 += 8) {
 #pragma unroll
-      for (int k = 0; k + 1 < RW; ++k) {
-        T[k] = T[k + 1];
-        Wt[k] = Wt[k + 1];
+      for (int jj = 0; jj < 8; ++jj) {
+        const float tc = T[jj], w = Wt[jj], td = T[jj + 1];
+        const float sl = dpp_from_left(tc), sr = dpp_from_right(tc);
+        if (w != 0.f) {
+          const int gr = j0 + jj + 1;
+          // original orientation: down / up / right / left
+          const double tdn = (double)(tr ? sr : td), tup = (double)(tr ? sl : tu);
+          const double trt = (double)(tr ? td : sr), tlf = (double)(tr ? tu : sl);
+          const int Y = tr ? gc : gr, X = tr ? gr : gc;
+          const double dy = tdn - tup;
+          const double dx = trt - tlf;
+          const double g = sqrt(dy * dy + dx * dx);
+          const double nrm = 1e-20 + g;
+          const double my = dy / nrm, mx = dx / nrm;
+          const float2 f = F[(long long)(r0 + Y - 1) * Dx + c0 + X - 1];
+          const double fy = (double)(f.x / 5.0f), fx = (double)(f.y / 5.0f);
+          const double ty = my - fy;
+          const double tx = mx - fx;
+          e0 += ty * ty;
+          e1 += tx * tx;
+          const double Dy_ = rho * (tdn + tup) + 2.0 * alpha, Dx_ = rho * (trt + tlf) + 2.0 * alpha;
+          const double D = sqrt(Dy_ * Dy_ + Dx_ * Dx_) * (1.0 + 1e-9);
+          const double ff = sqrt(fy * fy + fx * fx);
+          if (g > 3.0 * D && g > 1e-12) {
+            const double ep = 2.0 * D / g + 1e-7;
+            eb += ep * (2.0 * sqrt(ty * ty + tx * tx) + ep);
+          } else {
+            eb += (1.0 + ff) * (1.0 + ff);
+          }
+        }
+        tu = tc;
       }
-      T[RW - 1] = 0.f;
-      Wt[RW - 1] = 0.f;
+#pragma unroll
+      for (int k = 0; k + 8 < RW; ++k) {
+        T[k] = T[k + 8];
+        Wt[k] = Wt[k + 8];
+      }
+#pragma unroll
+      for (int k = RW - 8; k < RW; ++k) {
+        T[k] = 0.f;
+        Wt[k] = 0.f;
+      }
     }
     e0 = wave_sum(e0);
     e1 = wave_sum(e1);
