@@ -71,6 +71,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # development rehearsal of the multi-rank path on a one-GPU box: every rank on this device
+    if os.environ.get("CPX_BENCH_DEVICE"):
+        local = int(os.environ["CPX_BENCH_DEVICE"])
     # the CPU baseline's worker processes fork from a server started before this process
     # touches the GPU (no fork or exec of a GPU-initialised process)
     cpu_ctx = _cpu_pool_context() if (rank == 0 and world == 1 and not a.no_cpu_baseline) else None
