@@ -337,7 +337,8 @@ __global__ __launch_bounds__(kT) void k_dyn_prep(const float* __restrict__ yf, i
     if (q >= n) break;
     float v[3];
     if (RESAMPLE) {
-      const int y = (int)(q / Dx), x = (int)(q - (long long)y * Dx);
+      const int qi = (int)q;  // n < 2^29 (cpx_seg_masks): 32-bit division
+      const int y = qi / Dx, x = qi - y * Dx;
       const int y0 = uy.i0[y], y1 = uy.i1[y], x0 = ux.i0[x], x1 = ux.i1[x];
       const float wy = uy.w[y], wx = ux.w[x];
 #pragma unroll
@@ -517,7 +518,8 @@ __global__ __launch_bounds__(kT) void k_hist_init(int Dy, int Dx, DynBufs d) {
   const long long nh = (long long)Dyh * Dxh;
   const long long b = (long long)blockIdx.x * kT + threadIdx.x;
   if (b >= nh) return;
-  const int y = (int)(b / Dxh) - kRpad, x = (int)(b % Dxh) - kRpad;
+  const int bi = (int)b;  // nh < 2^31 (cpx_seg_masks): 32-bit division
+  const int y = bi / Dxh - kRpad, x = bi - (bi / Dxh) * Dxh - kRpad;
   int v = 0;
   if (y >= 0 && y < Dy && x >= 0 && x < Dx) v = d.mov[(long long)fov * Dy * Dx + (long long)y * Dx + x] ? 0 : 1;
   d.h[(long long)fov * nh + b] = v;
