@@ -39,20 +39,27 @@ __device__ __forceinline__ float dpp_from_right(float v) {  // lane l gets lane 
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
-// first index i < len (<= 128) with h[0] + ... + h[i] > k: one wave, two entries per lane
+// first index i < len (<= 192) with h[0] + ... + h[i] > k: one wave, three consecutive entries
+// per lane
 __device__ __forceinline__ int fe_hist_rank(const int* h, int len, long long k) {
   const int lane = threadIdx.x & 63;
-  const int a = 2 * lane < len ? h[2 * lane] : 0, b = 2 * lane + 1 < len ? h[2 * lane + 1] : 0;
-  int s = a + b;
+  int e[3], s = 0;
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    e[u] = 3 * lane + u < len ? h[3 * lane + u] : 0;
+    s += e[u];
+  }
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const int y = __shfl_up(s, d, 64);
     if (lane >= d) s += y;
   }
-  const int ex = s - a - b;
-  const unsigned long long ba = __ballot((long long)(ex + a) > k), bb = __ballot((long long)s > k);
-  const int la = ba ? __ffsll((long long)ba) - 1 : 64, lb = bb ? __ffsll((long long)bb) - 1 : 64;
-  return la == lb ? 2 * lb : 2 * lb + 1;
+  // the first lane whose inclusive total exceeds k holds the index; inside it, the first entry
+  const unsigned long long bb = __ballot((long long)s > k);
+  const int lb = bb ? __ffsll((long long)bb) - 1 : 63;
+  const long long c0 = (long long)__shfl(s - e[1] - e[2], lb, 64);  // through entry 3 lb
+  const long long c1 = c0 + __shfl(e[1], lb, 64);                    // through entry 3 lb + 1
+  return c0 > k ? 3 * lb : c1 > k ? 3 * lb + 1 : 3 * lb + 2;
 }
 
 constexpr int kFeRegRows = 40;  // register rows per wave (T + Wt: 4 VGPRs per row)
@@ -123,7 +130,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_flow_error_reg(
     const int r0 = o.bbox[0], c0 = o.bbox[1];
     const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
     bool tr = false;
-    if (fe_reg_class(bh, bw, tr) != NW) continue;  // block-uniform (class 2: NW = 2, class 3: NW = 3)
+    if (fe_reg_class(bh, bw, tr) != NW) continue;  // block-uniform (class c: NW = c waves)
     const int SR = tr ? bw : bh, SC = tr ? bh : bw;  // storage rows / columns
     // rows per wave (the slabs split the mask evenly); this wave's rows 1 + wv RS .. wv RS + nrow
     const int RS = (SR + NW - 1) / NW;

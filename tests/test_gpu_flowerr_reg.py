@@ -3,10 +3,12 @@ class and orientation, against the Cellpose restatement (oracle/seg_oracle.py).
 
 fe_reg_class sends a mask to the one-column kernel (both sides <= 64, or one side <= 64 and the
 other <= 80: stored transposed when its rows are the longer side), to the column-pair kernels
-(columns <= 128 with rows <= 80 / 120) or leaves it to the LDS kernels.  The masks here are sheared
+(columns <= 128 with rows <= 80 / 120) or leaves it to the LDS kernels (a fourth class, four
+waves of column pairs for rows <= 160, measured slower than the LDS kernel it relieved and was
+dropped; its 153 x 106 shapes stay here as LDS-path cases).  The masks here are sheared
 ellipses drawn at network resolution with semi-axes chosen so that, at full resolution (x 100/17),
 their bboxes land in each class in both orientations (about 40 x 60 / 60 x 40, 70 x 59, 100 x 70 /
-70 x 100, 118 x 94 and 150 x 140 px); each object's flows are scaled so that its flow error falls
+70 x 100, 118 x 94, 153 x 106 / 106 x 153 and 141 x 141 px); each object's flows are scaled so that its flow error falls
 on either side of the 0.4 threshold.  The labels must be bit-identical to the oracle's, i.e. every
 mask's keep / remove decision equals the fp64 reference's.
 """
@@ -20,7 +22,7 @@ from test_gpu_seg import _gpu_masks
 pytestmark = pytest.mark.gpu
 
 # (ry, rx) at network resolution -> full-resolution bbox ~ (2 ry, 2 rx) x 100 / 17
-SHAPES = [(3, 5), (5, 3), (6, 5), (5, 6), (8, 6), (6, 8), (10, 8), (8, 10), (12, 12), (2, 2)]
+SHAPES = [(3, 5), (5, 3), (6, 5), (5, 6), (8, 6), (6, 8), (10, 8), (8, 10), (13, 9), (9, 13), (12, 12), (2, 2)]
 
 
 def _labels(Ly, Lx, seed):
@@ -73,9 +75,10 @@ def test_register_classes_decide_like_fp64(dev, seed):
     c1 = (mx <= 64) | ((mn <= 64) & (mx <= 80))
     c2 = ~c1 & (mx <= 128) & (mn <= 80)
     c3 = ~c1 & ~c2 & (mx <= 128) & (mn <= 120)
-    print("masks per class (1, 2, 3, LDS):", int(c1.sum()), int(c2.sum()), int(c3.sum()),
-          int((~c1 & ~c2 & ~c3).sum()), "removed:", int(st[0]["n_bad_flow"]))
+    c4 = ~c1 & ~c2 & ~c3 & (mx <= 160) & (mn <= 128)  # LDS kernels (elongated large masks)
+    print("masks per class (1, 2, 3, 4, LDS):", int(c1.sum()), int(c2.sum()), int(c3.sum()), int(c4.sum()),
+          int((~c1 & ~c2 & ~c3 & ~c4).sum()), "removed:", int(st[0]["n_bad_flow"]))
     assert c1[bh > bw].any() and c1[bh < bw].any()
     assert c2[bh > bw].any() and c2[bh < bw].any()
-    assert c3.any()
+    assert c3.any() and c4[bh > bw].any() and c4[bh < bw].any()
     assert st[0]["n_bad_flow"] >= 2 and ref.max() < pre.max()
