@@ -294,7 +294,10 @@ def run(argv=None):
             res = pipe.fetch(slot)
             kept = [0 if fovs[k] is None else int(res.hdr["Nuclei"][k]["n_kept"]) for k in range(len(chunk))]
             kept += [0] * (B - len(chunk))
-            feats = emb.embed(pipe.crops8, kept, C)
+            own = res.crops8 or {}  # FOVs re-run on their own carry their own crops
+            feats = emb.embed(pipe.crops8, [0 if k in own else n for k, n in enumerate(kept)], C)
+            for k, c8 in own.items():
+                feats[k] = emb.embed(c8, [kept[k]], C)[0] if kept[k] else None
             for k, (idx, _) in enumerate(chunk):
                 if fovs[k] is None or kept[k] == 0 or feats[k] is None:
                     results[idx] = {"status": "empty", "n_cells": 0}

@@ -85,16 +85,32 @@ class FovResults:
     recovered: np.ndarray | None = None  # [B] int: 0, or how the FOV was re-run on its own
                                          # (RECOVER_FP32: a split-fp16 activation overflowed, so its
                                          # CPnet ran in fp32; RECOVER_WS: its watershed needed more
-                                         # rounds; both bits possible)
+                                         # rounds; RECOVER_CAPACITY: it has more seeds / objects
+                                         # than max_objects, so it ran with larger tables; bits
+                                         # combine)
+    crops8: dict | None = None           # FOV -> device uint8 [1][ML'][C][box][box]: the a7 crops
+                                         # of a re-run FOV (cfg.crops), replacing its batch slot
 
 
 RECOVER_FP32 = 1
 RECOVER_WS = 2
-WS_RETRIES = 3  # re-runs of a non-converged watershed, each with twice the rounds of the last
+RECOVER_CAPACITY = 4
+WS_RETRIES = 4   # at most this many re-runs of a FOV whose watershed did not converge, with 2x,
+                 # 4x, 8x, 16x the configured rounds
+REC_CACHE = 4    # single-FOV recovery pipelines kept per process (shared by every pipeline)
+
+
+def _sync_after(stream):
+    """Wait for the work enqueued on `stream` so far (not for what other threads of the host
+    loop enqueue on it later, e.g. the next batch's upload)."""
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    ev.synchronize()
 
 
 class FovPipeline:
     _copy_streams: dict = {}
+    _rec_cache: dict = {}  # (device, precision, max_objects, crops, config) -> single-FOV pipeline
 
     def __init__(self, dev: Device, cfg: PipelineConfig, illum, recovery: bool = True):
         self.dev, self.cfg = dev, cfg
@@ -110,7 +126,7 @@ class FovPipeline:
         else:
             self.illum = torch.from_numpy(np.ascontiguousarray(illum)).to(td)
         self._recovery = recovery  # False for the single-FOV pipelines that do the re-runs
-        self._rec_pipes = {}
+        self.ws_rounds = tuple(cfg.ws_rounds)  # per run (a recovery re-run raises them)
         self.corr = torch.empty((B, C, H, W), dtype=torch.float32, device=td)
         self.stats = dev.empty_bytes(64 * B * C)
         ML = cfg.max_objects
@@ -145,6 +161,7 @@ class FovPipeline:
         if key not in FovPipeline._copy_streams:
             FovPipeline._copy_streams[key] = torch.cuda.Stream(device=td)
         self._copy_stream = FovPipeline._copy_streams[key]
+        self.copy_stream = self._copy_stream  # also the host loaders' upload stream (cpx.plate)
         self._step = 0
         self._use_slot(0)
         self.crops = None
@@ -183,7 +200,7 @@ class FovPipeline:
             st = self.seg.stats  # cpx_seg_stats [B] (32 bytes): cells_status is int32 field 6
             check(self.dev.lib.cpx_watershed_cells(
                 self.dev.h, _ptr(self.labels["Nuclei"]), _ptr(self.corr), B, cfg.C, ch,
-                H, W, cfg.cell_expand, cfg.ws_rounds[0], cfg.ws_rounds[1], _ptr(self.labels["Cells"]),
+                H, W, cfg.cell_expand, self.ws_rounds[0], self.ws_rounds[1], _ptr(self.labels["Cells"]),
                 _ptr(self.labels["Cytoplasm"]), st.data_ptr() + 6 * 4, 8),
                 "cpx_watershed_cells")
         elif cfg.cells == "expand":
@@ -239,7 +256,7 @@ class FovPipeline:
         """Copy one slot's results to the host (default: the last run) and return them.  Waits
         only for that slot's step (its recorded event), with the copies on the device's copy stream, so a
         step enqueued after it keeps the GPU busy meanwhile."""
-        from .segment import SEG_STATS_DTYPE
+        from .segment import SEG_ERR_INTERNAL, SEG_OVF_SEEDS, SEG_STATS_DTYPE
         k = self.cur if slot is None else slot
         sl, hb = self._slots[k], self._host
         B, ML, F = self.cfg.batch, self.cfg.max_objects, self.F
@@ -251,35 +268,48 @@ class FovPipeline:
             hb["cpnet_ovf"].copy_(sl["cpnet_ovf"], non_blocking=True)
             for s in OBJECT_SETS:
                 hb["hdr"][s].copy_(sl["hdr"][s], non_blocking=True)
-        cs.synchronize()
+        _sync_after(cs)
         hdrs = {s: as_numpy(hb["hdr"][s], "hdr").copy() for s in OBJECT_SETS}
         qc = as_numpy(hb["qc"], "qc").copy()
-        nmax = {s: max(int(hdrs[s]["n_objects"].max()) if B else 0, 1) for s in OBJECT_SETS}
+        seg_stats = hb["seg_stats"].numpy().view(SEG_STATS_DTYPE).copy()
+        sovf = seg_stats["overflow"].ravel()[:B]
+        if (sovf & SEG_ERR_INTERNAL).any():
+            raise RuntimeError("cpx_seg_masks: a flow-error work loop reached its claim bound "
+                               "(CPX_SEG_ERR_INTERNAL): the batch's masks are invalid")
+        nmax = {s: min(ML, max(int(hdrs[s]["n_objects"].max()) if B else 0, 1)) for s in OBJECT_SETS}
         with torch.cuda.stream(cs):
             for s in OBJECT_SETS:
                 n = nmax[s]
                 hb["feats"][s][:B * n * F].view(B, n, F).copy_(sl["feats"][s][:, :n], non_blocking=True)
                 hb["objects"][s][:B * n * 56].view(B, n * 56).copy_(
                     sl["objects"][s].view(B, ML * 56)[:, :n * 56], non_blocking=True)
-        cs.synchronize()
+        _sync_after(cs)
         objs, feats = {}, {}
         for s in OBJECT_SETS:
-            n_b = hdrs[s]["n_objects"].astype(int)
+            n_b = np.minimum(hdrs[s]["n_objects"].astype(int), ML)
             n = nmax[s]
             f = hb["feats"][s][:B * n * F].view(B, n, F).numpy()
             o = as_numpy(hb["objects"][s][:B * n * 56], "object").reshape(B, n)
             feats[s] = [f[b, : n_b[b]].copy() for b in range(B)]
             objs[s] = [o[b, : n_b[b]].copy() for b in range(B)]
-        seg_stats = hb["seg_stats"].numpy().view(SEG_STATS_DTYPE).copy()
         nt = self.seg.geom.n_tiles
         ovf = hb["cpnet_ovf"][:B * nt].numpy().reshape(B, nt).any(axis=1)
         failed = np.zeros(B, dtype=bool)
         if self.cfg.cells == "watershed":
             failed = seg_stats["cells_status"].ravel()[:B] < 0
+        # capacity: a FOV with more seeds than max_objects (its masks were truncated), or a label
+        # table that dropped labels above max_objects, needs larger tables (reference: no limit,
+        # Cellpose_GPU_s3fs.py:143-170); masks <= seeds, so n_seeds_found tables are enough
+        need = np.where(sovf & SEG_OVF_SEEDS, seg_stats["n_seeds_found"].ravel()[:B], 0)
+        for s in OBJECT_SETS:
+            need = np.maximum(need, np.where(hdrs[s]["overflow"] != 0, hdrs[s]["max_label"], 0))
         res = FovResults(qc=qc, hdr=hdrs, objects=objs, feats=feats, seg_stats=seg_stats, failed=failed,
                          recovered=np.zeros(B, dtype=np.int32))
-        if self._recovery and (ovf.any() or failed.any()):
-            self._recover(sl["raw"], res, ovf, failed)
+        if self._recovery and (ovf.any() or failed.any() or (need > ML).any()):
+            self._recover(sl["raw"], res, ovf, failed, need)
+        elif (need > ML).any():
+            raise RuntimeError(f"FOV(s) {np.nonzero(need > ML)[0].tolist()} need {int(need.max())} object "
+                               f"slots, max_objects is {ML} (recovery disabled)")
         if res.failed.any():
             # per-site failure, not a failed batch: those FOVs get no object rows, every other
             # FOV of the batch is kept (the reference logs a site's error and moves on)
@@ -295,37 +325,58 @@ class FovPipeline:
 
     # ---- per-FOV recovery (Cellpose_GPU_s3fs.py:142-147: a site that fails is retried, not
     # dropped) ----------------------------------------------------------------------------------
-    def _recovery_pipe(self, precision: str, ws_rounds: tuple) -> "FovPipeline":
-        key = (precision, tuple(ws_rounds))
-        if key not in self._rec_pipes:
-            cfg = dataclasses.replace(self.cfg, batch=1, cpnet_precision=precision, ws_rounds=tuple(ws_rounds),
-                                      slots=1, crops=False)
-            self._rec_pipes[key] = FovPipeline(Device(self.dev.index), cfg, self.illum, recovery=False)
-        return self._rec_pipes[key]
+    def _recovery_pipe(self, precision: str, max_objects: int) -> "FovPipeline":
+        """A single-FOV pipeline for re-runs, shared by every pipeline of the process (one per
+        (device, precision, max_objects, ...), at most REC_CACHE kept: the oldest is dropped)."""
+        cfg = dataclasses.replace(self.cfg, batch=1, cpnet_precision=precision, max_objects=max_objects,
+                                  slots=1, crops_f32=False)
+        key = (self.dev.index, repr(cfg))
+        cache = FovPipeline._rec_cache
+        if key in cache:
+            cache[key] = cache.pop(key)  # most recently used last
+        else:
+            while len(cache) >= REC_CACHE:
+                cache.pop(next(iter(cache)))
+            cache[key] = FovPipeline(Device(self.dev.index), cfg, self.illum, recovery=False)
+        return cache[key]
 
-    def _recover(self, raw: torch.Tensor, res: FovResults, ovf: np.ndarray, failed: np.ndarray):
+    def _recover(self, raw: torch.Tensor, res: FovResults, ovf: np.ndarray, failed: np.ndarray,
+                 need: np.ndarray):
         """Re-run single FOVs of a fetched step from its planes (`raw`, kept per slot) and splice
         their results into `res`: a FOV whose split-fp16 CPnet overflowed runs its CPnet in fp32
-        (the reference's own arithmetic; the split format holds |a| < 65504 only), a FOV whose
-        Cells watershed did not converge runs again with twice the rounds, up to WS_RETRIES
-        times.  Runs on the device's copy stream, after the step's event."""
-        C = self.cfg.C
+        (the reference's own arithmetic; the split format holds |a| < 65504 only); a FOV with more
+        seeds or labels than max_objects runs with tables of the next power of two that holds
+        them; a FOV whose Cells watershed did not converge runs again with twice the rounds, at
+        most WS_RETRIES times.  The re-runs are synchronous on the device's copy stream (after the
+        step's event): the host thread that called fetch() waits for them (about one single-FOV
+        pipeline each), and so do result copies of the other pipelines queued behind them; the
+        other pipelines' kernels keep running on their own streams."""
+        C, ML = self.cfg.C, self.cfg.max_objects
         with torch.cuda.stream(self._copy_stream):
-            for b in np.nonzero(ovf | failed)[0]:
+            for b in np.nonzero(ovf | failed | (need > ML))[0]:
                 precision = "fp32" if ovf[b] else self.cfg.cpnet_precision
-                rounds = tuple(self.cfg.ws_rounds)
                 flag = RECOVER_FP32 if ovf[b] else 0
-                if failed[b] and not ovf[b]:
-                    rounds, flag = (2 * rounds[0], 2 * rounds[1]), flag | RECOVER_WS
-                for t in range(WS_RETRIES + 1):
-                    rp = self._recovery_pipe(precision, rounds)
+                ml = ML
+                if need[b] > ML:
+                    ml = max(2 * ML, 1 << int(need[b] - 1).bit_length())
+                    flag |= RECOVER_CAPACITY
+                # a FOV re-run only for its watershed starts at twice the rounds; every re-run
+                # that still does not converge doubles them again, up to 2^WS_RETRIES x
+                rounds, doublings = tuple(self.cfg.ws_rounds), 0
+                if failed[b] and flag == 0:
+                    rounds, flag, doublings = (2 * rounds[0], 2 * rounds[1]), RECOVER_WS, 1
+                while True:
+                    rp = self._recovery_pipe(precision, ml)
+                    rp.ws_rounds = rounds
                     rp.raw.copy_(raw[b * C:(b + 1) * C])
                     r1 = rp.fetch(rp.run())
-                    if not r1.failed[0] or t == WS_RETRIES:
+                    if not r1.failed[0] or doublings >= WS_RETRIES:
                         break
-                    rounds, flag = (2 * rounds[0], 2 * rounds[1]), flag | RECOVER_WS
-                log.warning("FOV %d of the batch re-run on its own (%s, watershed rounds %s): %s", b,
-                            "CPnet fp32 after a split-fp16 overflow" if ovf[b] else "more watershed rounds",
+                    rounds, flag, doublings = (2 * rounds[0], 2 * rounds[1]), flag | RECOVER_WS, doublings + 1
+                log.warning("FOV %d of the batch re-run on its own (%s; watershed rounds %s): %s", b,
+                            ", ".join(w for f, w in ((RECOVER_FP32, "CPnet fp32 after a split-fp16 overflow"),
+                                                     (RECOVER_CAPACITY, f"max_objects {ml}"),
+                                                     (RECOVER_WS, "more watershed rounds")) if flag & f) or "rerun",
                             rounds, "converged" if not r1.failed[0] else "watershed still not converged")
                 for s in OBJECT_SETS:
                     res.hdr[s][b] = r1.hdr[s][0]
@@ -334,3 +385,7 @@ class FovPipeline:
                 res.seg_stats[b] = r1.seg_stats[0]
                 res.failed[b] = bool(r1.failed[0])
                 res.recovered[b] = flag
+                if self.cfg.crops:
+                    if res.crops8 is None:
+                        res.crops8 = {}
+                    res.crops8[int(b)] = rp.crops8.clone()

@@ -401,7 +401,7 @@ def _run_sites(a, table, source, chans, state, out, status):
         tm["fetch_wait_s"] += t1 - t0
         tm["tables_s"] += time.perf_counter() - t1
         tm["h2d_gpu_ms"] += evs[0].elapsed_time(evs[1])
-        tm["pipeline_gpu_ms"] += evs[1].elapsed_time(evs[2])
+        tm["pipeline_gpu_ms"] += evs[2].elapsed_time(evs[3])
 
     with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, a.threads)) as pool:
         pending = decode(0, pool)
@@ -411,14 +411,23 @@ def _run_sites(a, table, source, chans, state, out, status):
             empty = [not f.result() for f in pending]
             tm["decode_wait_s"] += time.perf_counter() - t0
             p_i = bi % n_pipes
-            evs = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-            with torch.cuda.stream(streams[p_i]):
-                evs[0].record(streams[p_i])
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            # the upload runs on the device's copy stream (the pipelines' shared result-copy
+            # stream: no extra hardware queue), so it overlaps this pipeline's previous batch and
+            # the other pipelines' kernels; the pipeline's stream waits for it.  pipes[p_i].raw
+            # is the staging buffer of the pipeline's next result slot, whose previous batch was
+            # fetched (retired) before this one was claimed
+            cs = pipes[p_i].copy_stream
+            with torch.cuda.stream(cs):
+                evs[0].record(cs)
                 pipes[p_i].raw.copy_(hosts[p_i], non_blocking=True)
-                evs[1].record(streams[p_i])
-                uploads[p_i] = evs[1]
-                slot = pipes[p_i].run()
+                evs[1].record(cs)
+            uploads[p_i] = evs[1]
+            streams[p_i].wait_event(evs[1])
+            with torch.cuda.stream(streams[p_i]):
                 evs[2].record(streams[p_i])
+                slot = pipes[p_i].run()
+                evs[3].record(streams[p_i])
             inflight.append((bi, pipes[p_i], slot, evs, empty))
             nxt = next(source, None)  # claim and decode the next batch while this one runs
             if nxt is not None:

@@ -57,7 +57,9 @@ class SegGeom(ct.Structure):
 
 
 SEG_STATS_DTYPE = np.dtype([("n_moving", "i4"), ("n_seeds", "i4"), ("n_masks", "i4"),
-                            ("n_bad_flow", "i4"), ("n_final", "i4"), ("overflow", "i4"), ("cells_status", "i4"), ("_pad", "i4")])
+                            ("n_bad_flow", "i4"), ("n_final", "i4"), ("overflow", "i4"), ("cells_status", "i4"), ("n_seeds_found", "i4")])
+SEG_OVF_SEEDS = 1        # cpx.h CPX_SEG_OVF_SEEDS: more seeds than max_objects (re-run with more)
+SEG_ERR_INTERNAL = 8     # cpx.h CPX_SEG_ERR_INTERNAL: a flow-error work loop hit its claim bound
 
 
 def _pad_amounts(L: int, div: int = 16, extra: int = 1):
@@ -209,7 +211,8 @@ class Segmenter:
         self.graph.replay()
 
     def cpnet_overflow(self) -> torch.Tensor | None:
-        """Device int32 [1], non-zero once a split-fp16 activation left the fp16 range (f16x3)."""
+        """Device int32 [B * n_tiles]: per network tile, non-zero once a split-fp16 activation of that
+        tile left the fp16 range (f16x3); cleared by every forward."""
         return self.fnet.ovf if self.layout == 2 else None
 
     # -- pipeline ----------------------------------------------------------------------------

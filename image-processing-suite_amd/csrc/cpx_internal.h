@@ -114,6 +114,13 @@ __device__ __forceinline__ T wave_max(T v) {
   return v;
 }
 
+// Work-claim bound of the flow-error kernels: a block claims at most total + 1 items from a
+// queue counter that only grows, so a loop past that is broken (e.g. a shared item re-read
+// instead of re-claimed, as once happened in a one-wave block) — it ORs kClaimBroken into its
+// counter (which also drains the other blocks) and exits; cpx_seg_masks reports it as
+// CPX_SEG_ERR_INTERNAL in every FOV's stats instead of a kernel that never ends.
+constexpr int kClaimBroken = 1 << 30;
+
 // Objects handled by the LDS fast paths in k_texture.hip; the rest go to the k_features.hip
 // fallback kernels (the two predicates must agree between the translation units).
 constexpr int kFastShapeWords = 4096;  // 32 KiB of LDS for both masks: 5 blocks per CU (watershed

@@ -336,7 +336,7 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
   flag();
 }
 
-template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, int CIN2 = 0>
+template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, int CIN2 = 0, int NBUF = 2>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, int N, int H,
                int W, int tiles_x, int tiles_y) {
@@ -361,9 +361,13 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   static_assert(CIN % 16 == 0 && COUT % BM == 0 && BM % (32 * WM) == 0 && NWV % MWV == 0, "shape");
   static_assert(PW * WN >= NS, "every subtile needs a wave");
   static_assert(SW % 64 == 0, "weight DMA rows");
-  static_assert(P * QB <= 2 * SB, "output tile must fit the staging LDS");
-  static_assert(2 * SB * 16 <= 163840, "LDS");
-  __shared__ uint4 smem[2 * SB];
+  // NBUF 2: slab c + 1 streams into the second buffer under slab c's MFMAs; NBUF 1: one slab
+  // buffer (half the LDS per block, so more blocks per CU cover each other's DMA waits)
+  static_assert(NBUF == 1 || NBUF == 2, "slab buffers");
+  constexpr int SMEM = NBUF == 2 ? 2 * SB : (P * QB > SB ? P * QB : SB);
+  static_assert(P * QB <= SMEM, "output tile must fit the staging LDS");
+  static_assert(SMEM * 16 <= 163840, "LDS");
+  __shared__ uint4 smem[SMEM];
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int mw = wid % MWV, pg = wid / MWV;
@@ -402,9 +406,9 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   // the residual tile, DMA'd during the last slab into the slab buffer that slab does not use, in
   // the epilogue's staging layout (chunk k of pixel px at px * QB + (k ^ swzq(px)))
   constexpr int NCHT_ = NCH + NCH2;
-  constexpr bool kResPre = P * QB <= SB;
-  uint4* const bufO = smem + ((NCHT_ - 1) & 1) * SB;  // the last slab's buffer
-  uint4* const bufR = smem + (NCHT_ & 1) * SB;        // free during the last slab
+  constexpr bool kResPre = NBUF == 2 && P * QB <= SB;
+  uint4* const bufO = smem + (NBUF == 2 ? ((NCHT_ - 1) & 1) * SB : 0);  // the last slab's buffer
+  uint4* const bufR = smem + (NBUF == 2 ? (NCHT_ & 1) * SB : 0);        // free during the last slab
   auto issue_res = [&]() {
     constexpr int NRR = (P * QB + 63) / 64, JR = (NRR + NWV - 1) / NWV;
 #pragma unroll
@@ -532,9 +536,10 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
 #define CPX_X3_DIAG 0
 #endif
   for (int ch = 0; ch < NCH; ++ch) {
-    if (CPX_X3_DIAG != 1 && CPX_X3_DIAG != 2 && CPX_X3_DIAG != 4 && ch + 1 < NCHT) issue(ch + 1, (ch + 1) & 1);
+    if (NBUF == 2 && CPX_X3_DIAG != 1 && CPX_X3_DIAG != 2 && CPX_X3_DIAG != 4 && ch + 1 < NCHT)
+      issue(ch + 1, (ch + 1) & 1);
     if (kResPre && ch + 1 == NCHT && ep.res) issue_res();
-    const uint4* sb = smem + (ch & 1) * SB;
+    const uint4* sb = smem + (NBUF == 2 ? (ch & 1) * SB : 0);
     per_nsub([&](auto cnt) {
       if constexpr (WM * WN == 1) {
         // single-fragment waves: all taps unrolled, the next tap's reads scheduled under this
@@ -546,16 +551,24 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
         for (int tap = 0; tap < T; ++tap) tapbody(cnt, sb, tap, tap / KS, tap % KS);
       }
     });
+    if (NBUF == 1) {  // every wave is done with the buffer before the next slab lands in it
+      __syncthreads();
+      if (ch + 1 < NCHT) issue(ch + 1, 0);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (CPX_X3_DIAG != 2 && CPX_X3_DIAG != 4) __syncthreads();
   }
   // folded projection: one centre tap per slab of in2 (weight slot 0)
 #pragma unroll 1
   for (int ch = NCH; ch < NCHT; ++ch) {
-    if (ch + 1 < NCHT) issue(ch + 1, (ch + 1) & 1);
+    if (NBUF == 2 && ch + 1 < NCHT) issue(ch + 1, (ch + 1) & 1);
     if (kResPre && ch + 1 == NCHT && ep.res) issue_res();
-    const uint4* sb = smem + (ch & 1) * SB;
+    const uint4* sb = smem + (NBUF == 2 ? (ch & 1) * SB : 0);
     per_nsub([&](auto cnt) { tapbody(cnt, sb, 0, HALO, HALO); });
+    if (NBUF == 1) {
+      __syncthreads();
+      if (ch + 1 < NCHT) issue(ch + 1, 0);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -709,9 +722,10 @@ bool x3_cfg(int ks, int cin, int cout, int variant, X3Cfg* c) {
     return true;
   }
   if (ks != 3) return false;
+  // variant 2 (development): BM 32, two subtiles per wave, one slab buffer (k_conv_x3 NBUF 1)
   if (cout == 32) *c = variant == 1 ? X3Cfg{32, 16, 32} : X3Cfg{32, 8, 32};
-  else if (cout == 64) *c = variant == 1 ? X3Cfg{64, 16, 16} : X3Cfg{32, 16, 16};
-  else *c = variant == 1 ? X3Cfg{64, 14, 28} : X3Cfg{32, 8, 28};
+  else if (cout == 64) *c = variant == 1 ? X3Cfg{64, 16, 16} : variant == 2 ? X3Cfg{32, 16, 32} : X3Cfg{32, 16, 16};
+  else *c = variant == 1 ? X3Cfg{64, 14, 28} : variant == 2 ? X3Cfg{32, 16, 28} : X3Cfg{32, 8, 28};
   return true;
 }
 
@@ -722,12 +736,12 @@ static size_t x3_lds_pad() {
   return pad;
 }
 
-template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, int CIN2 = 0>
+template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, int CIN2 = 0, int NBUF = 2>
 int x3_run(cpx_ctx* ctx, const void* in, const void* wpk, const X3Epi& ep, int N, int H, int W) {
   const int tx = cpx_div_up(W, TX), ty = cpx_div_up(H, TY);
   const long long blocks = (long long)N * tx * ty * (COUT / BM);  // (tile, output-channel block) items
   CPX_REQUIRE(blocks < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv: too many tiles");
-  hipLaunchKernelGGL((k_conv_x3<KS, CIN, COUT, BM, TY, TX, WM, WN, WPE, CIN2>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((k_conv_x3<KS, CIN, COUT, BM, TY, TX, WM, WN, WPE, CIN2, NBUF>), dim3((unsigned)blocks),
                      dim3(512), x3_lds_pad(), ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N, H, W, tx, ty);
   CPX_CHECK_LAUNCH("k_conv_x3");
   return CPX_OK;
@@ -745,6 +759,14 @@ int x3_launch_proj(cpx_ctx* ctx, int cin, int cout, int cin2, int variant, const
   X3_P(128, 128, 64, 0, 32, 8, 28, 1, 1, 4)
   X3_P(256, 256, 128, 0, 32, 8, 28, 1, 1, 4)
   X3_P(256, 256, 256, 0, 32, 8, 28, 1, 1, 4)
+#define X3_P1(CI, CO, C2, V, BM_, TY_, TX_, WM_, WN_, WPE_)                               \
+  if (cin == CI && cout == CO && cin2 == C2 && variant == V)                               \
+    return x3_run<3, CI, CO, BM_, TY_, TX_, WM_, WN_, WPE_, C2, 1>(ctx, in, wpk, ep, N, H, W);
+  X3_P1(64, 64, 32, 2, 32, 16, 32, 1, 2, 4)
+  X3_P1(128, 128, 64, 2, 32, 16, 28, 1, 2, 4)
+  X3_P1(256, 256, 128, 2, 32, 16, 28, 1, 2, 4)
+  X3_P1(256, 256, 256, 2, 32, 16, 28, 1, 2, 4)
+#undef X3_P1
 #undef X3_P
   cpx_set_error("cpx_cpnet_x3_conv_proj: no instance for %d -> %d channels + projection of %d (variant %d)",
                 cin, cout, cin2, variant);
@@ -761,6 +783,7 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
     return x3_run<1, CI, CO, 32, 16, 16, 1, 1, 4>(ctx, in, wpk, ep, N, H, W);
   // 224^2 level (32 -> 32 without in_up: the persistent weights-resident kernel unless
   // CPX_X3_P32=0)
+  if (variant == 2 && cout == 32) variant = 0;  // (the 224^2 level keeps variant 0's kernels)
   static const bool p32 = !getenv("CPX_X3_P32") || atoi(getenv("CPX_X3_P32")) != 0;
   if (p32 && ks == 3 && cin == 32 && cout == 32 && variant == 0 && !ep.in_up) {
     const int tx = cpx_div_up(W, 32), ty = cpx_div_up(H, 8);
@@ -772,6 +795,18 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
     CPX_CHECK_LAUNCH("k_conv_x3_p32");
     return CPX_OK;
   }
+#define X3_3B(CI, CO, V, BM_, TY_, TX_, WM_, WN_, WPE_)                                  \
+  if (ks == 3 && cin == CI && cout == CO && variant == V)                                \
+    return x3_run<3, CI, CO, BM_, TY_, TX_, WM_, WN_, WPE_, 0, 1>(ctx, in, wpk, ep, N, H, W);
+  X3_3B(32, 64, 2, 32, 16, 32, 1, 2, 4)
+  X3_3B(64, 64, 2, 32, 16, 32, 1, 2, 4)
+  X3_3B(128, 64, 2, 32, 16, 32, 1, 2, 4)
+  X3_3B(64, 128, 2, 32, 16, 28, 1, 2, 4)
+  X3_3B(128, 128, 2, 32, 16, 28, 1, 2, 4)
+  X3_3B(256, 128, 2, 32, 16, 28, 1, 2, 4)
+  X3_3B(128, 256, 2, 32, 16, 28, 1, 2, 4)
+  X3_3B(256, 256, 2, 32, 16, 28, 1, 2, 4)
+#undef X3_3B
   X3_3(32, 32, 0, 32, 8, 32, 1, 1, 4)
   X3_3(64, 32, 0, 32, 8, 32, 1, 1, 4)
   X3_3(32, 32, 1, 32, 16, 32, 1, 2, 2)

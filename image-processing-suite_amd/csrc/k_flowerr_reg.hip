@@ -4,7 +4,7 @@
 // screening pass (k_seg.hip, k_flow_error_lds<..., float>) decides a mask's flag in fp32 only where
 // a certified bound puts its error clearly on one side of the threshold and defers the rest to the
 // fp64 kernels.  The kernels here run the same screening with the grid in VGPRs instead of LDS for
-// masks up to 128 x 160 px; they are launched first, and the LDS screening kernels skip every mask
+// masks up to 128 x 120 px (fe_reg_class); they are launched first, and the LDS screening kernels skip every mask
 // whose flag they set.  Compiled with -fno-slp-vectorize: pairing rows into packed adds would
 // separate the DPP neighbour reads from the adds they fold into.
 #include "cpx_internal.h"
@@ -88,8 +88,9 @@ __device__ __forceinline__ void fe_row_op(V* T, int jc, V& v) {
 // Which register kernel takes a mask, and its storage orientation (tr: storage rows = original
 // columns).  Class 1 (k_flow_error_reg1): one column per lane, the mask's columns <= 64 lanes and
 // its rows <= kFeReg1Rows registers, rows = the shorter side when both fit.  Class 2
-// (k_flow_error_reg, two columns per lane): columns <= 128, rows <= 2 x kFeRegRows, rows = the
-// shorter side.  Class 0: the LDS kernels.
+// (k_flow_error_reg, two columns per lane over two waves): columns <= 128, rows <= 2 x kFeRegRows
+// (80); class 3 the same over three waves, rows <= 3 x kFeRegRows (120); rows = the shorter side.
+// Class 0: the LDS kernels.
 constexpr int kFeReg1Rows = 80;
 __device__ __forceinline__ int fe_reg_class(int bh, int bw, bool& tr) {
   const int mn = min(bh, bw), mx = max(bh, bw);
@@ -116,7 +117,11 @@ __global__ __launch_bounds__(64 * NW, 2) void k_flow_error_reg(
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const long long n = (long long)Dy * Dx;
   const int total = off[B];
-  while (true) {
+  for (int claims = 0;; ++claims) {
+    if (claims > total) {  // broken claim (cpx_internal.h kClaimBroken)
+      if (tid == 0) atomicOr(ctr, kClaimBroken);
+      break;
+    }
     if (tid == 0) sitem = atomicAdd(ctr, 1);
     __syncthreads();
     const int item = __builtin_amdgcn_readfirstlane(sitem);  // uniform control flow from here
@@ -358,7 +363,11 @@ __global__ __launch_bounds__(64, 2) void k_flow_error_reg1(
   const int lane = threadIdx.x;
   const long long n = (long long)Dy * Dx;
   const int total = off[B];
-  while (true) {
+  for (int claims = 0;; ++claims) {
+    if (claims > total) {  // broken claim (cpx_internal.h kClaimBroken); claims is wave-uniform
+      if (lane == 0) atomicOr(ctr, kClaimBroken);
+      break;
+    }
     // the claim without a divergent branch (every lane adds, only lane 0 adds 1; its old value,
     // read into an SGPR, is the item): the item loop's control flow stays wave-uniform — with a
     // lane-0 branch and a one-wave block (whose barriers are no-ops) the compiler re-read the

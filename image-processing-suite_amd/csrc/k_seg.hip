@@ -22,7 +22,6 @@ namespace {
 
 constexpr int kT = 256;
 constexpr int kRpad = 20;
-constexpr int kMaxSeeds = 32768;
 
 __device__ __forceinline__ unsigned int f2key(float f) {
   unsigned int u = __float_as_uint(f);
@@ -300,12 +299,14 @@ struct DynBufs {
   unsigned int* M;       // [B][nh] seed-expansion label map
   unsigned char* sflag;  // [B][nh] seed flags
   int* m0;               // [B][n] get_masks labels (the caller's labels buffer at full res)
-  int* seeds;            // [B][kMaxSeeds] seed pixels (padded grid), row-major
-  int* cnt;              // [B][kMaxSeeds + 1] pixels per seed label
-  int* first;            // [B][kMaxSeeds + 1] first pixel (raster order) per seed label
-  int* newlab;           // [B][kMaxSeeds + 1] renumbered label (0: removed)
+  int ms;                // seed capacity per FOV (= max_objects: masks <= seeds, so every mask fits
+                         // the object tables; more seeds set CPX_SEG_OVF_SEEDS)
+  int* seeds;            // [B][ms] seed pixels (padded grid), row-major
+  int* cnt;              // [B][ms + 1] pixels per seed label
+  int* first;            // [B][ms + 1] first pixel (raster order) per seed label
+  int* newlab;           // [B][ms + 1] renumbered label (0: removed)
   unsigned char* mark;   // [B][n] first-occurrence pixels of the kept labels
-  int* marklist;         // [B][kMaxSeeds] marked pixels in raster order
+  int* marklist;         // [B][ms] marked pixels in raster order
   int* act;              // [B][n] moving pixels (first n_moving entries per FOV, any order)
   void* fitems0;         // [B][n] FollowItem ping
   void* fitems1;         // [B][n] FollowItem pong
@@ -704,7 +705,7 @@ __global__ __launch_bounds__(kT) void k_seed_expand(int Dyh, int Dxh, DynBufs d)
   for (int kb = blockIdx.x * (kT / 64); kb < ns; kb += gridDim.x * (kT / 64)) {  // block-uniform
   const int k = kb + wid;
   const bool active = k < ns;
-  const int s = active ? d.seeds[(long long)fov * kMaxSeeds + k] : 0;
+  const int s = active ? d.seeds[(long long)fov * d.ms + k] : 0;
   const int sy = s / Dxh, sx = s - sy * Dxh;
   const int* h = d.h + (long long)fov * nh;
   bool good[3];
@@ -774,8 +775,8 @@ __global__ __launch_bounds__(kT) void k_assign(int Dy, int Dx, DynBufs d) {
     const int l0 = __shfl(l, leader);
     const unsigned long long m = __ballot(l == l0);
     if (lane == leader) {
-      atomicAdd(&d.cnt[(long long)fov * (kMaxSeeds + 1) + l0], __popcll(m));
-      atomicMin(&d.first[(long long)fov * (kMaxSeeds + 1) + l0], q);  // lowest lane = first pixel
+      atomicAdd(&d.cnt[(long long)fov * (d.ms + 1) + l0], __popcll(m));
+      atomicMin(&d.first[(long long)fov * (d.ms + 1) + l0], q);  // lowest lane = first pixel
     }
     pend &= ~m;
   }
@@ -786,7 +787,7 @@ __global__ __launch_bounds__(kT) void k_relabel_mark(int Dy, int Dx, DynBufs d) 
   const int fov = blockIdx.y;
   const int l = blockIdx.x * kT + threadIdx.x + 1;
   if (l > d.st[fov].n_seeds) return;
-  const long long o = (long long)fov * (kMaxSeeds + 1) + l;
+  const long long o = (long long)fov * (d.ms + 1) + l;
   const int c = d.cnt[o];
   const double big = (double)Dy * (double)Dx * 0.4;
   if (c > 0 && !((double)c > big)) d.mark[(long long)fov * Dy * Dx + d.first[o]] = 1;
@@ -795,12 +796,12 @@ __global__ __launch_bounds__(kT) void k_relabel_mark(int Dy, int Dx, DynBufs d) 
 // the j-th marked pixel (raster order) carries the label that becomes j + 1
 __global__ __launch_bounds__(kT) void k_relabel_apply(int Dy, int Dx, DynBufs d) {
   const int fov = blockIdx.y;
-  const int n_masks = min(d.totals[fov], kMaxSeeds);
+  const int n_masks = min(d.totals[fov], d.ms);
   const long long n = (long long)Dy * Dx;
   for (int j = blockIdx.x * kT + threadIdx.x; j < n_masks; j += gridDim.x * kT) {
-    const int pix = d.marklist[(long long)fov * kMaxSeeds + j];
+    const int pix = d.marklist[(long long)fov * d.ms + j];
     d.mark[(long long)fov * n + pix] = 0;
-    d.newlab[(long long)fov * (kMaxSeeds + 1) + d.m0[(long long)fov * n + pix]] = j + 1;
+    d.newlab[(long long)fov * (d.ms + 1) + d.m0[(long long)fov * n + pix]] = j + 1;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) d.st[fov].n_masks = n_masks;
 }
@@ -812,7 +813,7 @@ __global__ __launch_bounds__(kT) void k_apply_newlab(int Dy, int Dx, DynBufs d) 
   if (q >= n) return;
   int* m = d.m0 + (long long)fov * n + q;
   const int l = *m;
-  *m = l ? d.newlab[(long long)fov * (kMaxSeeds + 1) + l] : 0;  // big masks map to 0
+  *m = l ? d.newlab[(long long)fov * (d.ms + 1) + l] : 0;  // big masks map to 0
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -906,7 +907,11 @@ __global__ __launch_bounds__(THREADS, WPE) void k_flow_error_lds(  // WPE waves 
   const long long n = (long long)Dy * Dx;
   const int total = list ? list[0] : off[B];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  while (true) {
+  for (int claims = 0;; ++claims) {
+    if (claims > total) {  // broken claim (cpx_internal.h kClaimBroken)
+      if (tid == 0) atomicOr(ctr, kClaimBroken);
+      break;
+    }
     if (tid == 0) sitem = atomicAdd(ctr, 1);
     __syncthreads();
     const int item = sitem;
@@ -1190,7 +1195,11 @@ __global__ __launch_bounds__(THREADS, 1) void k_flow_error_cmp(
   const int total = off[B];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const double2 z2 = {0.0, 0.0};
-  while (true) {
+  for (int claims = 0;; ++claims) {
+    if (claims > total) {  // broken claim (cpx_internal.h kClaimBroken)
+      if (tid == 0) atomicOr(ctr, kClaimBroken);
+      break;
+    }
     if (tid == 0) sitem = atomicAdd(ctr, 1);
     __syncthreads();
     const int item = sitem;
@@ -1443,7 +1452,11 @@ __global__ __launch_bounds__(kBigThreads) void k_flow_error_big(
   const int total = off[B];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   double* T0 = gscratch + (long long)blockIdx.x * slice;
-  while (true) {
+  for (int claims = 0;; ++claims) {
+    if (claims > total) {  // broken claim (cpx_internal.h kClaimBroken)
+      if (tid == 0) atomicOr(ctr, kClaimBroken);
+      break;
+    }
     if (tid == 0) sitem = atomicAdd(ctr, 1);
     __syncthreads();
     const int item = sitem;
@@ -1717,8 +1730,10 @@ __global__ __launch_bounds__(kT) void k_apply_bad(long long n, int max_label,
 }
 
 __global__ void k_count_bad(int max_label, const unsigned char* __restrict__ bad,
-                            cpx_seg_stats* __restrict__ st) {
+                            const int* __restrict__ ctrs, int nctr, cpx_seg_stats* __restrict__ st) {
   const int fov = blockIdx.x;
+  if (threadIdx.x < nctr && (ctrs[threadIdx.x] & kClaimBroken))
+    atomicOr(&st[fov].overflow, CPX_SEG_ERR_INTERNAL);
   int c = 0;
   for (int l = threadIdx.x; l <= max_label; l += blockDim.x) c += bad[(long long)fov * (max_label + 1) + l] == 1;
   c = wave_sum(c);
@@ -1754,29 +1769,43 @@ __global__ __launch_bounds__(kT) void k_lab2idx(int max_label, const cpx_object*
   lab2idx[(long long)fov * (max_label + 1) + objects[(long long)fov * max_label + k].label] = k;
 }
 
-__global__ __launch_bounds__(kFillThreads) void k_fill_holes(
-    const int* __restrict__ labels, int H, int W, int max_label, int min_size,
-    const cpx_object* __restrict__ objects, const cpx_fov_objects* __restrict__ hdr,
-    const int* __restrict__ lab2idx, int* __restrict__ fillidx, int* __restrict__ absorber,
-    cpx_seg_stats* __restrict__ st) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned int* own = reinterpret_cast<unsigned int*>(smem);
-  unsigned int* reach = own + kFillMaxWords;
-  const int fov = blockIdx.y;
-  const int nobj = hdr[fov].n_objects;
-  for (int k = blockIdx.x; k < nobj; k += gridDim.x) {
-  const cpx_object o = objects[(long long)fov * max_label + k];
-  if (o.area < min_size) continue;
+// Closure of the reached set x within one 32-pixel word over the free pixels f (x a subset of f):
+// an addition carries each reached bit up to the top of its run of free bits, the bit-reversed
+// addition down to its bottom, so a flood crosses any horizontal run in one step (only the turns
+// and the vertical moves cost iterations; the fixed point is the same as one pixel per step).
+__device__ __forceinline__ unsigned int fill_hrun(unsigned int x, unsigned int f) {
+  const unsigned int up = (((f + x) ^ f) | x) & f;
+  const unsigned int rf = __builtin_bitreverse32(f), rx = __builtin_bitreverse32(x);
+  const unsigned int dn = __builtin_bitreverse32((((rf + rx) ^ rf) | rx) & rf);
+  return up | dn;
+}
+
+// One mask k of a FOV: own / reach are its bbox bitmasks (nw words, LDS or global scratch);
+// the non-object pixels reached from the bbox border (4-connectivity) are flooded, the rest are
+// holes: they record the filling mask and the masks they absorb.  Block-uniform.
+// G: the bitmasks are in global scratch — words are loaded and stored at agent scope (L2) and
+// a device fence precedes each barrier, so no wave reads a neighbour word from a stale L1 line
+template <bool G>
+__device__ __forceinline__ unsigned int fill_ld(const unsigned int* p) {
+  if constexpr (G) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool G>
+__device__ __forceinline__ void fill_st(unsigned int* p, unsigned int v) {
+  if constexpr (G) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+template <bool G>
+__device__ __forceinline__ void fill_one(const int* __restrict__ lab, int W, int max_label, int k,
+                                         const cpx_object& o, unsigned int* own, unsigned int* reach,
+                                         const int* __restrict__ l2i, int* __restrict__ fillidx,
+                                         int* __restrict__ absorber) {
   const int r0 = o.bbox[0], c0 = o.bbox[1];
   const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
   const int wpr = (bw + 31) / 32;
   const int nw = wpr * bh;
-  if (nw > kFillMaxWords) {
-    if (threadIdx.x == 0) atomicMax(&st[fov].overflow, 2);
-    continue;
-  }
-  const int* lab = labels + (long long)fov * H * W;
-  for (int w = threadIdx.x; w < nw; w += kFillThreads) {
+  for (int w = threadIdx.x; w < nw; w += blockDim.x) {
     const int r = w / wpr, cw = w - r * wpr;
     unsigned int bits = 0, rb = 0;
     for (int b = 0; b < 32; ++b) {
@@ -1787,50 +1816,94 @@ __global__ __launch_bounds__(kFillThreads) void k_fill_holes(
       const bool border = (r == 0 || r == bh - 1 || c == 0 || c == bw - 1);
       rb |= (unsigned int)(border && !in) << b;
     }
-    own[w] = bits;
-    reach[w] = rb;
+    fill_st<G>(own + w, bits);
+    fill_st<G>(reach + w, rb);
   }
+  if (G) __threadfence();
   __syncthreads();
-  // flood the non-object cells from the bbox border (4-connectivity), in place until stable
+  // flood in place until stable (a stale neighbour read only delays a change to a later
+  // iteration: every change forces another one, so the loop ends at the unique fixed point)
   for (int iter = 0; iter < bh * bw + 1; ++iter) {
     int ch = 0;
-    for (int w = threadIdx.x; w < nw; w += kFillThreads) {
+    for (int w = threadIdx.x; w < nw; w += blockDim.x) {
       const int r = w / wpr, cw = w - r * wpr;
       const unsigned int valid = (cw == wpr - 1 && (bw & 31)) ? ((1u << (bw & 31)) - 1u) : 0xffffffffu;
-      const unsigned int freeb = ~own[w] & valid;
-      const unsigned int cur = reach[w];
+      const unsigned int freeb = ~fill_ld<G>(own + w) & valid;
+      const unsigned int cur = fill_ld<G>(reach + w);
       unsigned int nb = (cur << 1) | (cur >> 1);
-      if (cw > 0) nb |= reach[w - 1] >> 31;
-      if (cw < wpr - 1) nb |= reach[w + 1] << 31;
-      if (r > 0) nb |= reach[w - wpr];
-      if (r < bh - 1) nb |= reach[w + wpr];
-      const unsigned int nxt = cur | (nb & freeb);
+      if (cw > 0) nb |= fill_ld<G>(reach + w - 1) >> 31;
+      if (cw < wpr - 1) nb |= fill_ld<G>(reach + w + 1) << 31;
+      if (r > 0) nb |= fill_ld<G>(reach + w - wpr);
+      if (r < bh - 1) nb |= fill_ld<G>(reach + w + wpr);
+      const unsigned int nxt = fill_hrun(cur | (nb & freeb), freeb);
       if (nxt != cur) {
-        reach[w] = nxt;
+        fill_st<G>(reach + w, nxt);
         ch = 1;
       }
     }
+    if (G) __threadfence();
     // one barrier that also returns the block-wide decision: a flag reset by thread 0 at the
     // top of the next iteration could be read as 0 by a wave still leaving this one (which then
     // broke out early: an incomplete flood, barriers out of step)
     if (!__syncthreads_or(ch)) break;
   }
   // holes: free and unreached; mark fill owner and absorbed objects
-  for (int w = threadIdx.x; w < nw; w += kFillThreads) {
+  for (int w = threadIdx.x; w < nw; w += blockDim.x) {
     const int r = w / wpr, cw = w - r * wpr;
     const unsigned int valid = (cw == wpr - 1 && (bw & 31)) ? ((1u << (bw & 31)) - 1u) : 0xffffffffu;
-    unsigned int hole = ~own[w] & ~reach[w] & valid;
+    unsigned int hole = ~fill_ld<G>(own + w) & ~fill_ld<G>(reach + w) & valid;
     while (hole) {
       const int b = __ffs(hole) - 1;
       hole &= hole - 1;
       const long long gi = (long long)(r0 + r) * W + c0 + cw * 32 + b;
-      atomicMax(&fillidx[(long long)fov * H * W + gi], k + 1);
+      atomicMax(&fillidx[gi], k + 1);
       const int l2 = lab[gi];
-      if (l2 > 0 && l2 <= max_label) atomicMin(&absorber[(long long)fov * max_label + lab2idx[(long long)fov * (max_label + 1) + l2]], k);
+      if (l2 > 0 && l2 <= max_label) atomicMin(&absorber[l2i[l2]], k);
     }
   }
   __syncthreads();
-  }  // object loop
+}
+
+__device__ __forceinline__ int fill_words(const cpx_object& o) {
+  return ((o.bbox[3] - o.bbox[1] + 31) / 32) * (o.bbox[2] - o.bbox[0]);
+}
+
+// masks whose bbox bitmasks fit the LDS (bbox <= 262144 px): several blocks per FOV
+__global__ __launch_bounds__(kFillThreads) void k_fill_holes(
+    const int* __restrict__ labels, int H, int W, int max_label, int min_size,
+    const cpx_object* __restrict__ objects, const cpx_fov_objects* __restrict__ hdr,
+    const int* __restrict__ lab2idx, int* __restrict__ fillidx, int* __restrict__ absorber) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned int* own = reinterpret_cast<unsigned int*>(smem);
+  const int fov = blockIdx.y;
+  const int nobj = hdr[fov].n_objects;
+  for (int k = blockIdx.x; k < nobj; k += gridDim.x) {
+    const cpx_object o = objects[(long long)fov * max_label + k];
+    if (o.area < min_size || fill_words(o) > kFillMaxWords) continue;
+    fill_one<false>(labels + (long long)fov * H * W, W, max_label, k, o, own, own + kFillMaxWords,
+             lab2idx + (long long)fov * (max_label + 1), fillidx + (long long)fov * H * W,
+             absorber + (long long)fov * max_label);
+  }
+}
+
+// the larger masks (the reference has no size limit): one block per FOV, bitmasks in a global
+// scratch of 2 x ceil(W / 32) x H words per FOV (L2-resident: <= 1.1 MB at 2080^2)
+__global__ __launch_bounds__(1024) void k_fill_holes_big(
+    const int* __restrict__ labels, int H, int W, int max_label, int min_size,
+    const cpx_object* __restrict__ objects, const cpx_fov_objects* __restrict__ hdr,
+    const int* __restrict__ lab2idx, int* __restrict__ fillidx, int* __restrict__ absorber,
+    unsigned int* __restrict__ scratch) {
+  const int fov = blockIdx.x;
+  const int nobj = hdr[fov].n_objects;
+  const long long per = (long long)((W + 31) / 32) * H;
+  unsigned int* own = scratch + (long long)fov * 2 * per;
+  for (int k = 0; k < nobj; ++k) {
+    const cpx_object o = objects[(long long)fov * max_label + k];
+    if (o.area < min_size || fill_words(o) <= kFillMaxWords) continue;
+    fill_one<true>(labels + (long long)fov * H * W, W, max_label, k, o, own, own + per,
+             lab2idx + (long long)fov * (max_label + 1), fillidx + (long long)fov * H * W,
+             absorber + (long long)fov * max_label);
+  }
 }
 
 // one block per FOV: kept flags + sequential new labels
@@ -2058,12 +2131,13 @@ static int ordered_compact(cpx_ctx* ctx, const unsigned char* flags, long long n
   return CPX_OK;
 }
 
-__global__ void k_seed_count(int B, const int* __restrict__ totals, cpx_seg_stats* __restrict__ st) {
+__global__ void k_seed_count(int B, int ms, const int* __restrict__ totals, cpx_seg_stats* __restrict__ st) {
   const int fov = blockIdx.x * blockDim.x + threadIdx.x;
   if (fov >= B) return;
   const int t = totals[fov];
-  st[fov].n_seeds = min(t, kMaxSeeds);
-  if (t > kMaxSeeds) st[fov].overflow = 1;
+  st[fov].n_seeds = min(t, ms);
+  st[fov].n_seeds_found = t;
+  if (t > ms) atomicOr(&st[fov].overflow, CPX_SEG_OVF_SEEDS);
 }
 
 constexpr int kFeSmallThreads = 256, kFeSmallCells = 5000;    // 40 KiB: 4 blocks per CU
@@ -2098,8 +2172,12 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   const size_t sz_b = al((size_t)B * n);
   const size_t sz_h = al(sizeof(int) * B * nh), sz_hb = al((size_t)B * nh);
   const size_t sz_m0 = resample ? 0 : al(sizeof(int) * B * n);
-  const size_t sz_seeds = al(sizeof(int) * (size_t)B * kMaxSeeds);
-  const size_t sz_cnt = al(sizeof(int) * (size_t)B * (kMaxSeeds + 1));
+  // seeds beyond max_objects cannot all become objects of the caller's tables: the first
+  // max_objects (raster order) are expanded, CPX_SEG_OVF_SEEDS is set and n_seeds_found tells
+  // the caller the capacity a re-run needs (masks <= seeds, so the tables below never overflow)
+  const int ms = max_objects;
+  const size_t sz_seeds = al(sizeof(int) * (size_t)B * ms);
+  const size_t sz_cnt = al(sizeof(int) * (size_t)B * (ms + 1));
   const size_t sz_act = al(sizeof(int) * B * n);
   const size_t sz_small = al(sizeof(int) * (size_t)B);
   // follow rounds: K = k0 steps while most pixels still move (until step sw), then k1 for the
@@ -2137,6 +2215,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   d.totals = (int*)w; w += sz_small;
   d.tiles = (int*)w; w += sz_tiles;
   d.st = stats_dev;
+  d.ms = ms;
   CPX_CHECK_HIP(hipMemsetAsync(stats_dev, 0, sizeof(cpx_seg_stats) * B, ctx->stream));
   CPX_CHECK_HIP(hipMemsetAsync(d.M, 0, sz_h, ctx->stream));
   CPX_CHECK_HIP(hipMemsetAsync(d.mark, 0, sz_b, ctx->stream));
@@ -2170,16 +2249,16 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   hipLaunchKernelGGL(k_hist_moving, gp, dim3(kT), 0, ctx->stream, Dy, Dx, d);
   hipLaunchKernelGGL(k_seed_flags, gh, dim3(kT), 0, ctx->stream, Dyh, Dxh, d);
   CPX_CHECK_LAUNCH("cpx_seg_masks follow");
-  rc = ordered_compact(ctx, d.sflag, nh, B, d.tiles, d.totals, kMaxSeeds, d.seeds, kMaxSeeds);
+  rc = ordered_compact(ctx, d.sflag, nh, B, d.tiles, d.totals, ms, d.seeds, ms);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_seed_count, dim3(cpx_div_up(B, 256)), dim3(256), 0, ctx->stream, B,
+  hipLaunchKernelGGL(k_seed_count, dim3(cpx_div_up(B, 256)), dim3(256), 0, ctx->stream, B, ms,
                      (const int*)d.totals, stats_dev);
   hipLaunchKernelGGL(k_seed_expand, dim3(std::max(1, (4 * ctx->n_cu + B - 1) / B), B), dim3(kT), 0,
                      ctx->stream, Dyh, Dxh, d);
   hipLaunchKernelGGL(k_assign, gp, dim3(kT), 0, ctx->stream, Dy, Dx, d);
-  hipLaunchKernelGGL(k_relabel_mark, dim3(cpx_div_up(kMaxSeeds, kT), B), dim3(kT), 0, ctx->stream, Dy, Dx, d);
+  hipLaunchKernelGGL(k_relabel_mark, dim3(cpx_div_up(ms, kT), B), dim3(kT), 0, ctx->stream, Dy, Dx, d);
   CPX_CHECK_LAUNCH("cpx_seg_masks seeds");
-  rc = ordered_compact(ctx, d.mark, n, B, d.tiles, d.totals, kMaxSeeds, d.marklist, kMaxSeeds);
+  rc = ordered_compact(ctx, d.mark, n, B, d.tiles, d.totals, ms, d.marklist, ms);
   if (rc) return rc;
   hipLaunchKernelGGL(k_relabel_apply, dim3(4, B), dim3(kT), 0, ctx->stream, Dy, Dx, d);
   hipLaunchKernelGGL(k_apply_newlab, gp, dim3(kT), 0, ctx->stream, Dy, Dx, d);
@@ -2228,7 +2307,8 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
                      ctx->stream, (const int*)d.m0, (const float2*)d.dpf, Dy, Dx, B, ML,             \
                      (const cpx_object*)obj, (const int*)off, off + B + (CTR), LT, LU, LC, flow_threshold, \
                      bad, (const int*)nullptr, und)
-      // masks whose shorter side fits 48 / 96 register rows (and the longer one 126 lanes' columns)
+      // masks of fe_reg_class 1-3 (k_flowerr_reg.hip: up to 64 x 80 one column per lane, 128 x 80 /
+      // 128 x 120 in column pairs over two / three waves)
       // first, in VGPRs (k_flow_error_reg); the LDS kernels skip the masks those flagged
       static const bool reg = !getenv("CPX_FE_NOREG");
       if (reg) {
@@ -2282,7 +2362,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
     hipLaunchKernelGGL(k_apply_bad, gp, dim3(kT), 0, ctx->stream, n, ML,
                        (const unsigned char*)bad, d.m0);
     hipLaunchKernelGGL(k_count_bad, dim3(B), dim3(256), 0, ctx->stream, ML,
-                       (const unsigned char*)bad, stats_dev);
+                       (const unsigned char*)bad, (const int*)(off + B + 1), 11, stats_dev);
     CPX_CHECK_LAUNCH("cpx_seg_masks flow error");
   }
   if (!resample) {
@@ -2294,8 +2374,12 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   rc = cpx_objects(ctx, labels_dev, B, H, W, ML, 0, lst, obj, hdr);
   if (rc) return rc;
   const long long N = (long long)H * W;
-  int* fillidx = (int*)cpx_ws(ctx, WS_SEG_FILL, sizeof(int) * (size_t)B * N);
-  if (!fillidx) return CPX_ERR_OOM;
+  const size_t sz_fill = al(sizeof(int) * (size_t)B * N);
+  const size_t sz_fscr = al(sizeof(unsigned int) * 2 * (size_t)B * ((W + 31) / 32) * H);
+  unsigned char* fw = (unsigned char*)cpx_ws(ctx, WS_SEG_FILL, sz_fill + sz_fscr);
+  if (!fw) return CPX_ERR_OOM;
+  int* fillidx = (int*)fw;
+  unsigned int* fscr = (unsigned int*)(fw + sz_fill);
   CPX_CHECK_HIP(hipMemsetAsync(fillidx, 0, sizeof(int) * (size_t)B * N, ctx->stream));
   CPX_CHECK_HIP(hipMemsetAsync(absorber, 0x7f, sz_abs, ctx->stream));
   CPX_CHECK_HIP(hipMemsetAsync(l2i, 0, sz_l2i, ctx->stream));
@@ -2311,7 +2395,10 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   hipLaunchKernelGGL(k_fill_holes, dim3(std::max(1, std::min(ML, (2 * ctx->n_cu + B - 1) / B)), B),
                      dim3(kFillThreads), flds, ctx->stream,
                      (const int*)labels_dev, H, W, ML, min_size, (const cpx_object*)obj,
-                     (const cpx_fov_objects*)hdr, (const int*)l2i, fillidx, absorber, stats_dev);
+                     (const cpx_fov_objects*)hdr, (const int*)l2i, fillidx, absorber);
+  hipLaunchKernelGGL(k_fill_holes_big, dim3(B), dim3(1024), 0, ctx->stream,
+                     (const int*)labels_dev, H, W, ML, min_size, (const cpx_object*)obj,
+                     (const cpx_fov_objects*)hdr, (const int*)l2i, fillidx, absorber, fscr);
   hipLaunchKernelGGL(k_fill_final, dim3(B), dim3(1024), 0, ctx->stream, ML, min_size,
                      (const cpx_object*)obj, (const cpx_fov_objects*)hdr, (const int*)absorber,
                      newlab, stats_dev);

@@ -320,10 +320,21 @@ typedef struct cpx_seg_stats {
   int32_t n_masks;    /* labels after get_masks (big masks removed, renumbered)               */
   int32_t n_bad_flow; /* masks removed by the flow-error test                                 */
   int32_t n_final;    /* labels after fill_holes_and_remove_small_masks                       */
-  int32_t overflow;   /* capacity exceeded (seeds or labels truncated)                        */
+  int32_t overflow;   /* CPX_SEG_OVF_* bits; 0 = the labels are complete                       */
   int32_t cells_status; /* written by cpx_watershed_cells when pointed here (else untouched)     */
-  int32_t _pad;
+  int32_t n_seeds_found; /* histogram maxima found (n_seeds is min(found, max_objects))          */
 } cpx_seg_stats;      /* 32 bytes */
+
+/* cpx_seg_stats.overflow bits.  The reference (Cellpose get_masks / fill_holes, regionprops,
+ * Cellpose_GPU_s3fs.py:143-170) has no capacity limit; libcpx's per-FOV tables hold max_objects:
+ *   CPX_SEG_OVF_SEEDS  more seeds than max_objects were found: only the first max_objects (raster
+ *                      order) were expanded, so masks are missing; re-run the FOV with
+ *                      max_objects >= n_seeds_found (masks <= seeds: that run cannot overflow).
+ *   CPX_SEG_ERR_INTERNAL a flow-error work loop reached its claim bound (cannot happen in a correct
+ *                      build; the labels are invalid and the host must raise).
+ * Fill-holes has no size limit (masks whose bbox exceeds the LDS bitmasks use global memory). */
+#define CPX_SEG_OVF_SEEDS 1
+#define CPX_SEG_ERR_INTERNAL 8
 
 #define CPX_TILE_F32_NCHW 0  /* tiles/net output as float32 [n][c][by][bx]                   */
 #define CPX_TILE_BF16_NHWC 1 /* tiles/net output as bfloat16 [n][by][bx][c] (channels_last)  */
@@ -349,7 +360,8 @@ int cpx_seg_average(cpx_ctx* ctx, const void* net_dev, int layout, int B, int no
  * (transforms.resize_image, cv2 INTER_LINEAR) and everything runs at full resolution, with
  * niter = uint32(200 / rescale) (1176 for nuclei at diameter 100; the host passes it).
  * resample = 0: dynamics at Ly x Lx, masks nearest-resized to H x W (Cellpose's resize=).
- * labels_dev int32 [B][H][W]; stats_dev cpx_seg_stats [B].  max_objects bounds labels per FOV.*/
+ * labels_dev int32 [B][H][W]; stats_dev cpx_seg_stats [B].  max_objects bounds the seeds and
+ * hence the labels per FOV (CPX_SEG_OVF_SEEDS when a FOV has more: re-run it with more).        */
 int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx_seg_geom* geom, int H,
                   int W, int niter, double flow_threshold, int min_size, int max_objects,
                   int resample, int32_t* labels_dev, cpx_seg_stats* stats_dev);

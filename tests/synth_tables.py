@@ -18,7 +18,7 @@ def plate_tables(n_wells: int = 24, sites: int = 2, objects: int = 20, n_feat: i
                  seed: int = 0, channels=("DNA", "ER", "RNA", "AGP", "Mito"), plate: str = "Plate_1",
                  time: str = "T1", nan_frac: float = 0.002):
     import pandas as pd
-    from .csvout import feature_names
+    from cpx.csvout import feature_names
     rng = np.random.default_rng(seed)
     cols = feature_names(channels) if n_feat is None else [f"Feature_{i:03d}" for i in range(n_feat)]
     F = len(cols)

@@ -92,7 +92,7 @@ def _synthetic_yf(Ly, Lx, seed, noise=0.05, rmin=3, rmax=10, n=18):
     return yf, lab
 
 
-def _gpu_masks(dev, yf, g, H, W, flow_threshold=0.4, min_size=15, resample=True, niter=None):
+def _gpu_masks(dev, yf, g, H, W, flow_threshold=0.4, min_size=15, resample=True, niter=None, max_objects=1024):
     B = yf.shape[0]
     if niter is None:
         niter = so.default_niter(resample=resample)
@@ -100,7 +100,7 @@ def _gpu_masks(dev, yf, g, H, W, flow_threshold=0.4, min_size=15, resample=True,
     labels = torch.empty((B, H, W), dtype=torch.int32, device=dev.torch_device)
     stats = torch.zeros(32 * B, dtype=torch.uint8, device=dev.torch_device)
     check(dev.lib.cpx_seg_masks(dev.h, _ptr(yft), B, _geom_ptr(g), H, W, niter, float(flow_threshold),
-                                min_size, 1024, int(resample), _ptr(labels), _ptr(stats)), "masks")
+                                min_size, max_objects, int(resample), _ptr(labels), _ptr(stats)), "masks")
     dev.sync()
     return labels.cpu().numpy(), stats.cpu().numpy().view(SEG_STATS_DTYPE)
 

@@ -22,7 +22,7 @@ pd = pytest.importorskip("pandas")
 
 
 def _plate(seed=3, n_wells=24, sites=3):
-    from cpx.synth_tables import plate_tables
+    from synth_tables import plate_tables
     # feature_names columns: CellProfiler-length headers (> 1 KiB), which the reference's
     # csv.Sniffer on the first 1024 characters needs to recognise the delimiter
     tb = plate_tables(n_wells=n_wells, sites=sites, objects=18, n_feat=None, seed=seed)

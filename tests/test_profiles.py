@@ -106,7 +106,7 @@ def test_oracle_feature_select_matches_pandas_restatement():
 
 
 def test_oracle_pipeline_runs(tmp_path):
-    from cpx.synth_tables import plate_tables
+    from synth_tables import plate_tables
     tb = plate_tables(n_wells=16, sites=2, objects=12, n_feat=10, seed=2)
     sel, avg, sims = po.pycyto_pertime(tb["Image"], tb["Nuclei"], tb["Cells"], tb["Cytoplasm"],
                                        "Plate_1", "T1", str(tmp_path / "sel.csv"))
@@ -124,7 +124,7 @@ def eng():
 
 @pytest.mark.gpu
 def test_gpu_group_mean_bit_exact(eng):
-    from cpx.synth_tables import plate_tables
+    from synth_tables import plate_tables
     tb = plate_tables(n_wells=40, sites=3, objects=30, n_feat=None, seed=7)
     nuc = tb["Nuclei"].merge(tb["Image"][po.IMAGE_META], on="ImageNumber")
     nuc.loc[5, "AreaShape_Area"] = np.inf
@@ -147,7 +147,7 @@ def test_gpu_object_means_without_merge(eng):
     """The merge-free path == merge(Image metadata) -> drop -> groupby mean, including a well
     whose images have no objects and a bool column."""
     from cpx.profiles import object_means_applies
-    from cpx.synth_tables import plate_tables
+    from synth_tables import plate_tables
     tb = plate_tables(n_wells=20, sites=2, objects=15, n_feat=12, seed=13)
     img, nuc = tb["Image"], tb["Nuclei"]
     nuc = nuc[~nuc.ImageNumber.isin([3, 4])].reset_index(drop=True)   # well 2 has no objects
@@ -241,7 +241,7 @@ def test_gpu_group_cosine(eng):
 def test_gpu_pertime_cli_matches_oracle(eng, tmp_path):
     """python -m cpx.profiles over a CSV tree == the oracle pipeline on the same tables."""
     from cpx.profiles import main
-    from cpx.synth_tables import plate_tables, write_tree
+    from synth_tables import plate_tables, write_tree
     tb = plate_tables(n_wells=32, sites=3, objects=25, n_feat=None, seed=12)
     write_tree(str(tmp_path / "in"), "Exp/Plate_1", "T1", tb)
     main(["--bucket_name", str(tmp_path / "in"), "--base_folder", "Exp/Plate_1", "--times", "T1",

@@ -33,6 +33,7 @@ def main():
     x = torch.rand(a.tiles, 224, 224, 2, device=td)
     lib = dev.lib
     real = lib.cpx_cpnet_x3_conv
+    ref_out = None
     for v in a.variants:
         f = FusedCPnetX3(net, dev, variant=v)
         rows = []
@@ -62,8 +63,12 @@ def main():
             return rc
 
         with torch.no_grad():
-            f(x)
+            out = f(x).clone()
             torch.cuda.synchronize()
+            if ref_out is None:
+                ref_out = out
+            same = bool(torch.equal(out, ref_out))
+            print(f"variant={v}: forward output bit-identical to variant {a.variants[0]}: {same}", flush=True)
             lib.cpx_cpnet_x3_conv = wrap
             f(x)
             lib.cpx_cpnet_x3_conv = real

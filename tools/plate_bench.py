@@ -4,7 +4,11 @@ threads, pinned upload, the GPU pipeline and the table assembly — timed from t
 the last recorded site.  A warm-up job (pipeline construction, graph capture) runs first; the
 timed job's FOV/s is printed as one JSON line.
 
-  python tools/plate_bench.py [--fovs 96] [--threads 16] [--batch 48] [--pipes 2]"""
+  python tools/plate_bench.py [--fovs 96] [--repeat 1] [--threads 16] [--batch 48] [--pipes 2]
+
+--repeat R lists the timed job's FOV files R times (R x --fovs LoadData rows, distinct
+ImageNumbers, every file decoded again each time): a steady-state run of many batches without
+R x the TIFFs on disk."""
 import argparse
 import json
 import os
@@ -21,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fovs", type=int, default=96)
     ap.add_argument("--warm", type=int, default=48)
+    ap.add_argument("--repeat", type=int, default=1)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--batch", type=int, default=48)
     ap.add_argument("--pipes", type=int, default=2)
@@ -58,6 +63,9 @@ def main():
                         tiffio.imwrite(os.path.join(img, name), raw[j * C + c])
                         row[f"FileName_{ch}"] = name
                     rows.append(row)
+            if job == "timed" and a.repeat > 1:
+                rows = [dict(r, Metadata_Well=wells[(i * n + f) % 384], Metadata_Site=1 + (i * n + f) // 384)
+                        for i in range(a.repeat) for f, r in enumerate(rows)]
             ld = os.path.join(root, f"ld_{job}.csv")
             pd.DataFrame(rows).to_csv(ld, index=False)
             lds.append(ld)
@@ -67,9 +75,10 @@ def main():
                    "--out", os.path.join(root, "out"), "--batch", str(a.batch), "--threads", str(a.threads),
                    "--pipes", str(a.pipes)])
         t = [x for x in plate.LAST_TIMING if x["job"] == "ld_timed.csv"][0]
-        tif_bytes = sum(os.path.getsize(os.path.join(img, f)) for f in os.listdir(img) if f.startswith("timed"))
+        tif_bytes = a.repeat * sum(os.path.getsize(os.path.join(img, f)) for f in os.listdir(img) if f.startswith("timed"))
         print(json.dumps({"metric": "I/O-inclusive FOV/s (cpx.plate on uncompressed TIFFs, local disk)",
                           "value": round(t["fovs"] / t["seconds"], 2), "unit": "FOV/s", "fovs": t["fovs"],
+                          "unique_fovs": a.fovs, "repeat": a.repeat,
                           "seconds": round(t["seconds"], 3), "decode_threads": t["threads"], "batch": t["batch"],
                           "pipelines": t["pipes"], "tiff_GB": round(tif_bytes / 1e9, 3),
                           "tiff_decode_GBs": round(tif_bytes / 1e9 / t["seconds"], 2),

@@ -20,11 +20,12 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "image-processing-suite_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from cpx.profiles import KEYS, IMAGE_META, ProfileEngine, profile_time  # noqa: E402
-from cpx.synth_tables import plate_tables  # noqa: E402
+from synth_tables import plate_tables  # noqa: E402
 
 
 def main():
