@@ -115,7 +115,7 @@ class FusedCPnetX3:
             return torch.from_numpy(pack_conv(w.detach().float().numpy(), bm.value)).to(td)
 
         # the folded projections exist for variant 0's tile configurations
-        self.fold = X3_FOLD and self.variant in (0, 2)
+        self.fold = X3_FOLD and self.variant in (0, 2, 3)
 
         self.down = []
         for blk in net.down:

@@ -110,6 +110,7 @@ def _sync_after(stream):
 
 class FovPipeline:
     _copy_streams: dict = {}
+    _upload_streams: dict = {}
     _rec_cache: dict = {}  # (device, precision, max_objects, crops, config) -> single-FOV pipeline
 
     def __init__(self, dev: Device, cfg: PipelineConfig, illum, recovery: bool = True):
@@ -161,7 +162,6 @@ class FovPipeline:
         if key not in FovPipeline._copy_streams:
             FovPipeline._copy_streams[key] = torch.cuda.Stream(device=td)
         self._copy_stream = FovPipeline._copy_streams[key]
-        self.copy_stream = self._copy_stream  # also the host loaders' upload stream (cpx.plate)
         self._step = 0
         self._use_slot(0)
         self.crops = None
@@ -170,6 +170,16 @@ class FovPipeline:
                           if cfg.crops_f32 else None)
             self.crops8 = torch.zeros((B, ML, C, cfg.box, cfg.box), dtype=torch.uint8, device=td)
         dev.reserve(B * C, H, W, B, ML)
+
+    @staticmethod
+    def upload_stream(device: torch.device) -> torch.cuda.Stream:
+        """One host-to-device upload stream per device (cpx.plate's staging uploads): with the
+        two pipeline streams and the result-copy stream that is four streams, one hardware queue
+        each (GPU_MAX_HW_QUEUES = 4), and a result fetch never queues behind an upload."""
+        key = torch.device(device).index
+        if key not in FovPipeline._upload_streams:
+            FovPipeline._upload_streams[key] = torch.cuda.Stream(device=device)
+        return FovPipeline._upload_streams[key]
 
     def _use_slot(self, k: int):
         sl = self._slots[k]
@@ -197,11 +207,11 @@ class FovPipeline:
         B, H, W = cfg.batch, cfg.H, cfg.W
         if cfg.cells == "watershed":
             ch = cfg.ws_channel()
-            st = self.seg.stats  # cpx_seg_stats [B] (32 bytes): cells_status is int32 field 6
+            st = self.seg.stats  # cpx_seg_stats [B] (48 bytes): cells_status is int32 field 6 of 12
             check(self.dev.lib.cpx_watershed_cells(
                 self.dev.h, _ptr(self.labels["Nuclei"]), _ptr(self.corr), B, cfg.C, ch,
                 H, W, cfg.cell_expand, self.ws_rounds[0], self.ws_rounds[1], _ptr(self.labels["Cells"]),
-                _ptr(self.labels["Cytoplasm"]), st.data_ptr() + 6 * 4, 8),
+                _ptr(self.labels["Cytoplasm"]), st.data_ptr() + 6 * 4, 12),
                 "cpx_watershed_cells")
         elif cfg.cells == "expand":
             check(self.dev.lib.cpx_expand_labels(self.dev.h, _ptr(self.labels["Nuclei"]), B, H, W,

@@ -412,12 +412,12 @@ def _run_sites(a, table, source, chans, state, out, status):
             tm["decode_wait_s"] += time.perf_counter() - t0
             p_i = bi % n_pipes
             evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-            # the upload runs on the device's copy stream (the pipelines' shared result-copy
-            # stream: no extra hardware queue), so it overlaps this pipeline's previous batch and
-            # the other pipelines' kernels; the pipeline's stream waits for it.  pipes[p_i].raw
+            # the upload runs on the device's upload stream, so it overlaps this pipeline's
+            # previous batch and the other pipelines' kernels, and the result fetches (on the copy
+            # stream) never wait behind it; the pipeline's stream waits for it.  pipes[p_i].raw
             # is the staging buffer of the pipeline's next result slot, whose previous batch was
             # fetched (retired) before this one was claimed
-            cs = pipes[p_i].copy_stream
+            cs = FovPipeline.upload_stream(torch.device("cuda", a.device))
             with torch.cuda.stream(cs):
                 evs[0].record(cs)
                 pipes[p_i].raw.copy_(hosts[p_i], non_blocking=True)

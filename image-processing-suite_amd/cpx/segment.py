@@ -57,7 +57,11 @@ class SegGeom(ct.Structure):
 
 
 SEG_STATS_DTYPE = np.dtype([("n_moving", "i4"), ("n_seeds", "i4"), ("n_masks", "i4"),
-                            ("n_bad_flow", "i4"), ("n_final", "i4"), ("overflow", "i4"), ("cells_status", "i4"), ("n_seeds_found", "i4")])
+                            ("n_bad_flow", "i4"), ("n_final", "i4"), ("overflow", "i4"), ("cells_status", "i4"), ("n_seeds_found", "i4"),
+                            ("n_fill_partial", "i4"), ("_reserved", "i4", (3,))])
+SEG_STATS_BYTES = 48
+assert SEG_STATS_DTYPE.itemsize == SEG_STATS_BYTES
+SEG_OVF_FILL_PARTIAL = 2  # cpx.h CPX_SEG_OVF_FILL_PARTIAL: a partly absorbed mask (fill approximation)
 SEG_OVF_SEEDS = 1        # cpx.h CPX_SEG_OVF_SEEDS: more seeds than max_objects (re-run with more)
 SEG_ERR_INTERNAL = 8     # cpx.h CPX_SEG_ERR_INTERNAL: a flow-error work loop hit its claim bound
 
@@ -164,7 +168,7 @@ class Segmenter:
         self.pct = torch.empty((batch, NET_CHANNELS, 2), dtype=torch.float64, device=td)
         self.taper = torch.from_numpy(taper_mask(g.by, g.bx)).to(td)
         self.yf = torch.empty((batch, 3, g.Ly, g.Lx), dtype=torch.float32, device=td)
-        self.stats = torch.zeros(batch * 32, dtype=torch.uint8, device=td)
+        self.stats = torch.zeros(batch * SEG_STATS_BYTES, dtype=torch.uint8, device=td)
         self.net_out = None
         self.graph = None
         self.use_graph = use_graph

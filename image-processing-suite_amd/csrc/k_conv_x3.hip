@@ -724,8 +724,11 @@ bool x3_cfg(int ks, int cin, int cout, int variant, X3Cfg* c) {
   if (ks != 3) return false;
   // variant 2 (development): BM 32, two subtiles per wave, one slab buffer (k_conv_x3 NBUF 1)
   if (cout == 32) *c = variant == 1 ? X3Cfg{32, 16, 32} : X3Cfg{32, 8, 32};
-  else if (cout == 64) *c = variant == 1 ? X3Cfg{64, 16, 16} : variant == 2 ? X3Cfg{32, 16, 32} : X3Cfg{32, 16, 16};
-  else *c = variant == 1 ? X3Cfg{64, 14, 28} : variant == 2 ? X3Cfg{32, 16, 28} : X3Cfg{32, 8, 28};
+  // variant 3 (development): BM 64, two channel slices per wave, one slab buffer
+  else if (cout == 64) *c = variant == 1 ? X3Cfg{64, 16, 16} : variant == 2 ? X3Cfg{32, 16, 32}
+                          : variant == 3 ? X3Cfg{64, 16, 16} : X3Cfg{32, 16, 16};
+  else *c = variant == 1 ? X3Cfg{64, 14, 28} : variant == 2 ? X3Cfg{32, 16, 28}
+          : variant == 3 ? X3Cfg{64, 8, 28} : X3Cfg{32, 8, 28};
   return true;
 }
 
@@ -766,6 +769,10 @@ int x3_launch_proj(cpx_ctx* ctx, int cin, int cout, int cin2, int variant, const
   X3_P1(128, 128, 64, 2, 32, 16, 28, 1, 2, 4)
   X3_P1(256, 256, 128, 2, 32, 16, 28, 1, 2, 4)
   X3_P1(256, 256, 256, 2, 32, 16, 28, 1, 2, 4)
+  X3_P1(64, 64, 32, 3, 64, 16, 16, 2, 1, 4)
+  X3_P1(128, 128, 64, 3, 64, 8, 28, 2, 1, 4)
+  X3_P1(256, 256, 128, 3, 64, 8, 28, 2, 1, 4)
+  X3_P1(256, 256, 256, 3, 64, 8, 28, 2, 1, 4)
 #undef X3_P1
 #undef X3_P
   cpx_set_error("cpx_cpnet_x3_conv_proj: no instance for %d -> %d channels + projection of %d (variant %d)",
@@ -783,7 +790,7 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
     return x3_run<1, CI, CO, 32, 16, 16, 1, 1, 4>(ctx, in, wpk, ep, N, H, W);
   // 224^2 level (32 -> 32 without in_up: the persistent weights-resident kernel unless
   // CPX_X3_P32=0)
-  if (variant == 2 && cout == 32) variant = 0;  // (the 224^2 level keeps variant 0's kernels)
+  if ((variant == 2 || variant == 3) && cout == 32) variant = 0;  // (224^2: variant 0's kernels)
   static const bool p32 = !getenv("CPX_X3_P32") || atoi(getenv("CPX_X3_P32")) != 0;
   if (p32 && ks == 3 && cin == 32 && cout == 32 && variant == 0 && !ep.in_up) {
     const int tx = cpx_div_up(W, 32), ty = cpx_div_up(H, 8);
@@ -806,6 +813,14 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
   X3_3B(256, 128, 2, 32, 16, 28, 1, 2, 4)
   X3_3B(128, 256, 2, 32, 16, 28, 1, 2, 4)
   X3_3B(256, 256, 2, 32, 16, 28, 1, 2, 4)
+  X3_3B(32, 64, 3, 64, 16, 16, 2, 1, 4)
+  X3_3B(64, 64, 3, 64, 16, 16, 2, 1, 4)
+  X3_3B(128, 64, 3, 64, 16, 16, 2, 1, 4)
+  X3_3B(64, 128, 3, 64, 8, 28, 2, 1, 4)
+  X3_3B(128, 128, 3, 64, 8, 28, 2, 1, 4)
+  X3_3B(256, 128, 3, 64, 8, 28, 2, 1, 4)
+  X3_3B(128, 256, 3, 64, 8, 28, 2, 1, 4)
+  X3_3B(256, 256, 3, 64, 8, 28, 2, 1, 4)
 #undef X3_3B
   X3_3(32, 32, 0, 32, 8, 32, 1, 1, 4)
   X3_3(64, 32, 0, 32, 8, 32, 1, 1, 4)

@@ -1945,13 +1945,26 @@ __global__ __launch_bounds__(1024) void k_fill_final(int max_label, int min_size
   if (threadIdx.x == 0) st[fov].n_final = base;
 }
 
+// Final labels: a pixel takes the new label of the last kept mask whose holes cover it (masks
+// fill in label order, the later fill wins), else its own mask's if kept.  A filler that is not
+// kept was itself inside an earlier mask's holes (absorbed), and so is everything its holes
+// cover: the chain filler -> absorber[filler] leads to the mask whose fill the reference leaves
+// there (tests/test_gpu_capacity.py: holes inside a mask inside a ring).  A pixel of an absorbed
+// mask that no kept fill covers (the mask was only partly inside the earlier holes — disconnected
+// or diagonal-touching masks) is 0 here, where the reference's sequential loop keeps the rest of
+// that mask if it still has min_size pixels: counted in n_fill_partial (CPX_SEG_OVF_FILL_PARTIAL).
 __global__ __launch_bounds__(kT) void k_fill_apply(int* __restrict__ labels, long long n, int max_label,
                                                    const int* __restrict__ lab2idx,
                                                    const int* __restrict__ fillidx,
-                                                   const int* __restrict__ newlab) {
+                                                   const int* __restrict__ newlab,
+                                                   const int* __restrict__ absorber,
+                                                   const cpx_object* __restrict__ objects, int min_size,
+                                                   cpx_seg_stats* __restrict__ st) {
   const int fov = blockIdx.y;
   const int* l2i = lab2idx + (long long)fov * (max_label + 1);
   const int* nl = newlab + (long long)fov * max_label;
+  const int* ab = absorber + (long long)fov * max_label;
+  int partial = 0;
   // four independent pixels per iteration: their dependent lookups (label -> index -> new
   // label) overlap instead of one chain of loads at a time
   const long long stride = (long long)gridDim.x * kT;
@@ -1970,7 +1983,12 @@ __global__ __launch_bounds__(kT) void k_fill_apply(int* __restrict__ labels, lon
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       cand[u] = (k[u] >= 0 && nl[k[u]]) ? k[u] + 1 : 0;
-      fk[u] = (f[u] && nl[f[u] - 1]) ? f[u] : 0;
+      int c = f[u];
+      while (c && !nl[c - 1]) {  // not kept: absorbed by an earlier mask (a shorter k each step)
+        const int a = ab[c - 1];
+        c = a < c - 1 ? a + 1 : 0;
+      }
+      fk[u] = c;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1978,7 +1996,14 @@ __global__ __launch_bounds__(kT) void k_fill_apply(int* __restrict__ labels, lon
       if (q >= n) continue;
       const int best = max(cand[u], fk[u]);
       labels[(long long)fov * n + q] = best ? nl[best - 1] : 0;
+      partial += !best && k[u] >= 0 && ab[k[u]] < k[u] &&
+                 objects[(long long)fov * max_label + k[u]].area >= min_size;
     }
+  }
+  partial = wave_sum(partial);
+  if ((threadIdx.x & 63) == 0 && partial) {
+    atomicAdd(&st[fov].n_fill_partial, partial);
+    atomicOr(&st[fov].overflow, CPX_SEG_OVF_FILL_PARTIAL);
   }
 }
 
@@ -2404,7 +2429,8 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
                      newlab, stats_dev);
   hipLaunchKernelGGL(k_fill_apply, dim3(std::max(1, std::min(cpx_div_up(N, kT), 4 * ctx->n_cu / B + 1)), B),
                      dim3(kT), 0, ctx->stream, labels_dev, N, ML, (const int*)l2i,
-                     (const int*)fillidx, (const int*)newlab);
+                     (const int*)fillidx, (const int*)newlab, (const int*)absorber,
+                     (const cpx_object*)obj, min_size, stats_dev);
   CPX_CHECK_LAUNCH("cpx_seg_masks fill holes");
   return CPX_OK;
 }

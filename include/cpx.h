@@ -323,17 +323,24 @@ typedef struct cpx_seg_stats {
   int32_t overflow;   /* CPX_SEG_OVF_* bits; 0 = the labels are complete                       */
   int32_t cells_status; /* written by cpx_watershed_cells when pointed here (else untouched)     */
   int32_t n_seeds_found; /* histogram maxima found (n_seeds is min(found, max_objects))          */
-} cpx_seg_stats;      /* 32 bytes */
+  int32_t n_fill_partial; /* pixels of CPX_SEG_OVF_FILL_PARTIAL masks (see below)                   */
+  int32_t _reserved[3];
+} cpx_seg_stats;      /* 48 bytes */
 
 /* cpx_seg_stats.overflow bits.  The reference (Cellpose get_masks / fill_holes, regionprops,
  * Cellpose_GPU_s3fs.py:143-170) has no capacity limit; libcpx's per-FOV tables hold max_objects:
  *   CPX_SEG_OVF_SEEDS  more seeds than max_objects were found: only the first max_objects (raster
  *                      order) were expanded, so masks are missing; re-run the FOV with
  *                      max_objects >= n_seeds_found (masks <= seeds: that run cannot overflow).
+ *   CPX_SEG_OVF_FILL_PARTIAL a mask lay partly (not wholly) inside an earlier mask's filled holes:
+ *                      the reference's sequential fill keeps the rest of it if it still has
+ *                      min_size pixels, libcpx's parallel fill removes it (n_fill_partial pixels;
+ *                      disconnected / diagonal-touching masks only).
  *   CPX_SEG_ERR_INTERNAL a flow-error work loop reached its claim bound (cannot happen in a correct
  *                      build; the labels are invalid and the host must raise).
  * Fill-holes has no size limit (masks whose bbox exceeds the LDS bitmasks use global memory). */
 #define CPX_SEG_OVF_SEEDS 1
+#define CPX_SEG_OVF_FILL_PARTIAL 2
 #define CPX_SEG_ERR_INTERNAL 8
 
 #define CPX_TILE_F32_NCHW 0  /* tiles/net output as float32 [n][c][by][bx]                   */

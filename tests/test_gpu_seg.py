@@ -98,7 +98,7 @@ def _gpu_masks(dev, yf, g, H, W, flow_threshold=0.4, min_size=15, resample=True,
         niter = so.default_niter(resample=resample)
     yft = torch.from_numpy(np.ascontiguousarray(yf)).to(dev.torch_device)
     labels = torch.empty((B, H, W), dtype=torch.int32, device=dev.torch_device)
-    stats = torch.zeros(32 * B, dtype=torch.uint8, device=dev.torch_device)
+    stats = torch.zeros(48 * B, dtype=torch.uint8, device=dev.torch_device)
     check(dev.lib.cpx_seg_masks(dev.h, _ptr(yft), B, _geom_ptr(g), H, W, niter, float(flow_threshold),
                                 min_size, max_objects, int(resample), _ptr(labels), _ptr(stats)), "masks")
     dev.sync()
