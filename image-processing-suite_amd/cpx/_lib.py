@@ -101,6 +101,7 @@ SIGNATURES = {
     "cpx_objects": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cpx_crops": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P]),
     "cpx_features": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "cpx_features_pair": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "cpx_expand_labels": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     "cpx_watershed_cells": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I]),
     "cpx_seg_percentiles": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
@@ -135,6 +136,7 @@ SIGNATURES = {
                                _P, _P, _I, _P, _P, _I, _P, _P]),
     "cpx_cpnet_x3_conv_proj": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P, _I, _P, _P, _I,
                                     _P, _P, _I, _P]),
+    "cpx_cpnet_x3_conv_pool": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cpx_cpnet_x3_mask_overflow": (_I, [_P, _P, _I, _I, _I, _I, _P]),
     "cpx_cpnet_x3_stem": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cpx_cpnet_x3_pool": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),

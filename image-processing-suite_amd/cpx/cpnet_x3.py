@@ -24,6 +24,15 @@ from ._lib import check
 from .cpnet import CPnet
 
 X3_VARIANT = int(os.environ.get("CPX_X3_VARIANT", "0"))
+# the convolutions that write only the next input z (no residual stream y) run as variant 3 at the
+# 112^2 and deeper levels (BM 64: two channel slices per wave, one slab buffer): 5-12 % faster
+# there, slower where the epilogue also stores y (tools/conv_bench_x3.py, gpurun_out/r05c);
+# bit-identical outputs.  CPX_X3_ZVARIANT=-1 keeps every convolution at X3_VARIANT
+X3_ZVARIANT = int(os.environ.get("CPX_X3_ZVARIANT", "3"))
+# each down block's last convolution also max-pools its output for the next block (the pooled
+# tensor and its BatchNorm+ReLU from the staged tile: no read of y back); CPX_X3_POOL_FUSE=0 keeps
+# the separate pool kernel
+X3_POOL_FUSE = os.environ.get("CPX_X3_POOL_FUSE", "1") != "0"
 # fold each down block's (and the deepest up block's) 1x1 residual projection into the block's
 # second 3x3 convolution (cpx_cpnet_x3_conv_proj); CPX_X3_FOLD=0 keeps the separate 1x1 pass
 X3_FOLD = os.environ.get("CPX_X3_FOLD", "1") != "0"
@@ -92,7 +101,7 @@ def _p(t):
 class FusedCPnetX3:
     """Native split-fp16 CPnet forward: __call__(x fp32 [N, by, bx, 2] NHWC) -> fp32 [N, by, bx, 3]."""
 
-    def __init__(self, net: CPnet, dev, variant: int | None = None):
+    def __init__(self, net: CPnet, dev, variant: int | None = None, zvariant: int | None = None):
         self.dev = dev
         self.lib = dev.lib
         self.variant = X3_VARIANT if variant is None else int(variant)
@@ -105,17 +114,27 @@ class FusedCPnetX3:
         def dv(t):
             return t.detach().float().contiguous().to(td)
 
-        def conv_pack(w, ks, cfg_cin=None):
+        def conv_pack(w, ks, cfg_cin=None, variant=None):
             """pack for the tile configuration of a ks x ks conv of cfg_cin (default: w's own
-            input channels) -> w's output channels"""
+            input channels) -> w's output channels, in `variant` (default self.variant)"""
             cout, cin = w.shape[0], w.shape[1]
             bm = ct.c_int()
-            check(self.lib.cpx_cpnet_x3_cfg(ks, cin if cfg_cin is None else cfg_cin, cout, self.variant,
+            check(self.lib.cpx_cpnet_x3_cfg(ks, cin if cfg_cin is None else cfg_cin, cout,
+                                            self.variant if variant is None else variant,
                                             ct.byref(bm)), "cpx_cpnet_x3_cfg")
             return torch.from_numpy(pack_conv(w.detach().float().numpy(), bm.value)).to(td)
 
+        # z-only convolutions (each block's conv0 and conv2) in X3_ZVARIANT when the default is 0
+        zvar = X3_ZVARIANT if zvariant is None else int(zvariant)
+        zv = zvar if (self.variant == 0 and zvar >= 0) else self.variant
+
+        def zconv(w):
+            """(packed weights, variant) of a z-only 3x3 convolution"""
+            v = zv if w.shape[0] >= 64 else self.variant  # the 224^2 level keeps its kernels
+            return (conv_pack(w, 3, variant=v), v)
+
         # the folded projections exist for variant 0's tile configurations
-        self.fold = X3_FOLD and self.variant in (0, 2, 3)
+        self.fold = X3_FOLD and self.variant != 1
 
         self.down = []
         for blk in net.down:
@@ -124,7 +143,8 @@ class FusedCPnetX3:
             b = [blk.conv[t][-1].bias.detach().float() for t in range(4)]
             cout_b = blk.conv[0][-1].out_channels
             d = dict(bn=[(dv(s), dv(h)) for s, h in bns], b=[dv(x) for x in b], b1p=dv(b[1] + bp),
-                     pk=[None if t == 0 and blk is net.down[0] else conv_pack(blk.conv[t][-1].weight, 3)
+                     pk=[None if t == 0 and blk is net.down[0] else
+                         (zconv(blk.conv[t][-1].weight) if t in (0, 2) else conv_pack(blk.conv[t][-1].weight, 3))
                          for t in range(4)],
                      wp=None if blk is net.down[0] else conv_pack(wp, 1), cout=cout_b,
                      # the projection packed as extra one-tap slabs of the block's second conv
@@ -155,7 +175,8 @@ class FusedCPnetX3:
             b = [c[-1].bias.detach().float() for c in convs]
             cout_b = convs[0][-1].out_channels
             self.up.append(dict(bn=[(dv(s), dv(h)) for s, h in bns], b=[dv(x) for x in b], b1p=dv(b[1] + bp),
-                                pk=[conv_pack(c[-1].weight, 3) for c in convs], wp=conv_pack(wp, 1),
+                                pk=[zconv(c[-1].weight) if t in (0, 2) else conv_pack(c[-1].weight, 3)
+                                    for t, c in enumerate(convs)], wp=conv_pack(wp, 1),
                                 cout=cout_b,
                                 # the deepest up block reads its projection input at full size:
                                 # folded like the down blocks' (the others read it upsampled)
@@ -180,6 +201,9 @@ class FusedCPnetX3:
 
     def _conv(self, x, pk, cout, bias, ks=3, res=None, res_up=False, style=None, bn=None, relu=True,
               y=False, z=True, z_up=False, head=False, in_up=False):
+        variant = self.variant
+        if isinstance(pk, tuple):  # (weights, variant) of a z-only convolution
+            pk, variant = pk
         N, H, W, cin = x.shape
         if in_up:  # x is read 2x nearest-upsampled: the output has twice its size
             H, W = 2 * H, 2 * W
@@ -191,7 +215,7 @@ class FusedCPnetX3:
         scale, shift = bn if bn is not None else (None, None)
         st, st_stride = (None, 0) if style is None else style
         check(self.lib.cpx_cpnet_x3_conv(
-            self.dev.h, ks, self.variant, _p(x), int(in_up), N, H, W, cin, cout, _p(pk), _p(bias), _p(res), int(res_up),
+            self.dev.h, ks, variant, _p(x), int(in_up), N, H, W, cin, cout, _p(pk), _p(bias), _p(res), int(res_up),
             st, st_stride, _p(scale), _p(shift), int(relu), _p(yo), _p(zo), int(z_up),
             _p(self.head_w) if head else None, _p(self.head_b) if head else None, self.nout if head else 0,
             _p(ho), self._ovf_p(N)), "cpx_cpnet_x3_conv")
@@ -208,6 +232,18 @@ class FusedCPnetX3:
             self.dev.h, self.variant, _p(x), N, H, W, cin, cout, _p(pk), _p(x2), x2.shape[-1], _p(pk2), _p(bias),
             st, st_stride, _p(scale), _p(shift), 1, _p(yo), _p(zo), 0, self._ovf_p(N)), "cpx_cpnet_x3_conv_proj")
         return yo, zo
+
+    def _conv_pool(self, x, pk, cout, bias, res, bn):
+        """A down block's last convolution (residual, y) with the next block's max-pool and its
+        BatchNorm+ReLU fused into the epilogue (cpx_cpnet_x3_conv_pool): (y, pooled, z)."""
+        N, H, W, cin = x.shape
+        yo = self._empty(N, H, W, cout)
+        xo = self._empty(N, H // 2, W // 2, cout)
+        zo = self._empty(N, H // 2, W // 2, cout)
+        check(self.lib.cpx_cpnet_x3_conv_pool(
+            self.dev.h, self.variant, _p(x), N, H, W, cin, cout, _p(pk), _p(bias), _p(res), _p(yo), _p(xo), _p(zo),
+            _p(bn[0]), _p(bn[1]), self._ovf_p(N)), "cpx_cpnet_x3_conv_pool")
+        return yo, xo, zo
 
     def _proj(self, x, blk):
         return self._conv(x, blk["wp"], blk["cout"], None, ks=1, relu=False, y=True, z=False)[0]
@@ -250,12 +286,13 @@ class FusedCPnetX3:
         xd = []
         zu = None
         nd = len(self.down)
+        pooled = None  # (xin, z0) of the next block from the fused pool
         for n, d in enumerate(self.down):
             if n == 0:
                 p, z = self._stem(x, d)
                 x1, z = self._conv(z, d["pk"][1], d["cout"], d["b1p"], res=p, bn=d["bn"][2], y=True)
             else:
-                xin, z0 = self._pool(xd[-1], d["bn"][0])
+                xin, z0 = pooled if pooled is not None else self._pool(xd[-1], d["bn"][0])
                 _, z = self._conv(z0, d["pk"][0], d["cout"], d["b"][0], bn=d["bn"][1])
                 if d["wpf"] is not None:
                     x1, z = self._conv_proj(z, d["pk"][1], d["cout"], d["b1p"], xin, d["wpf"], bn=d["bn"][2])
@@ -263,7 +300,10 @@ class FusedCPnetX3:
                     p = self._proj(xin, d)
                     x1, z = self._conv(z, d["pk"][1], d["cout"], d["b1p"], res=p, bn=d["bn"][2], y=True)
             _, z = self._conv(z, d["pk"][2], d["cout"], d["b"][2], bn=d["bn"][3])
-            if n < nd - 1:
+            if n < nd - 1 and X3_POOL_FUSE:
+                xo, xin_n, z0_n = self._conv_pool(z, d["pk"][3], d["cout"], d["b"][3], x1, self.down[n + 1]["bn"][0])
+                pooled = (xin_n, z0_n)
+            elif n < nd - 1:
                 xo, _ = self._conv(z, d["pk"][3], d["cout"], d["b"][3], res=x1, y=True, z=False)
             else:  # deepest level also feeds the first up block's BatchNorm+ReLU
                 xo, zu = self._conv(z, d["pk"][3], d["cout"], d["b"][3], res=x1, bn=self.up[-1]["bn"][0], y=True)

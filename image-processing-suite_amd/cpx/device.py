@@ -233,6 +233,14 @@ class Device:
         check(self.lib.cpx_features(self.h, _ptr(labels), _ptr(corr), B, C, H, W, max_label,
                                     _ptr(objects), _ptr(hdr), _ptr(feats)), "cpx_features")
 
+    def features_pair(self, cells, cyto, corr, C, max_label, cells_tab, cyto_tab):
+        """cpx_features of Cells and Cytoplasm in one call; *_tab = (objects, hdr, feats)."""
+        B, H, W = cells.shape
+        self._bind_stream()
+        check(self.lib.cpx_features_pair(self.h, _ptr(cells), _ptr(cyto), _ptr(corr), B, C, H, W, max_label,
+                                         *(_ptr(t) for t in cells_tab), *(_ptr(t) for t in cyto_tab)),
+              "cpx_features_pair")
+
 
 def n_features(C: int) -> int:
     return _lib.N_SHAPE + C * _lib.FEATURES_PER_CHANNEL

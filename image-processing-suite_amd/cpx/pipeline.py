@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import dataclasses
 import logging
+import os
 
 import numpy as np
 import torch
@@ -28,6 +29,8 @@ from .device import Device, as_numpy, n_features
 from .segment import CELLPOSE_MODEL, DIAMETER, Segmenter
 
 OBJECT_SETS = ("Nuclei", "Cells", "Cytoplasm")
+# Cells + Cytoplasm features in one libcpx call (CPX_PAIR_FEATURES=0: one call per set, A/B runs)
+PAIR_FEATURES = os.environ.get("CPX_PAIR_FEATURES", "1") != "0"
 log = logging.getLogger("cpx.pipeline")
 
 
@@ -221,12 +224,22 @@ class FovPipeline:
             raise ValueError(f"PipelineConfig.cells: {cfg.cells!r}")
 
     def stage_features(self):
-        """Object tables and shape / intensity / texture features of the three object sets."""
+        """Object tables and shape / intensity / texture features of the three object sets (Cells
+        and Cytoplasm measured together: cpx_features_pair stages a Cytoplasm object from its
+        cell's reads of the channels when the two share the bbox)."""
         cfg = self.cfg
         for s in OBJECT_SETS:
             self.dev.objects(self.labels[s], cfg.max_objects, cfg.box, self.lstats, self.objects[s], self.hdr[s])
-            self.dev.features(self.labels[s], self.corr, cfg.C, cfg.max_objects, self.objects[s],
-                              self.hdr[s], self.feats[s])
+        self.dev.features(self.labels["Nuclei"], self.corr, cfg.C, cfg.max_objects, self.objects["Nuclei"],
+                          self.hdr["Nuclei"], self.feats["Nuclei"])
+        if PAIR_FEATURES:
+            self.dev.features_pair(self.labels["Cells"], self.labels["Cytoplasm"], self.corr, cfg.C, cfg.max_objects,
+                                   (self.objects["Cells"], self.hdr["Cells"], self.feats["Cells"]),
+                                   (self.objects["Cytoplasm"], self.hdr["Cytoplasm"], self.feats["Cytoplasm"]))
+        else:
+            for s in ("Cells", "Cytoplasm"):
+                self.dev.features(self.labels[s], self.corr, cfg.C, cfg.max_objects, self.objects[s],
+                                  self.hdr[s], self.feats[s])
         if self.cfg.crops:
             self.dev.objects(self.labels["Nuclei"], cfg.max_objects, cfg.box, self.lstats,
                              self.objects["Nuclei"], self.hdr["Nuclei"])

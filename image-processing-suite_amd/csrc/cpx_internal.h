@@ -59,6 +59,7 @@ enum {
   WS_REBIN_TMP = 12, // re-binning horizontal-pass intermediate (16-bit)
   WS_EMBED = 13,     // embedding preprocessing coefficients + horizontal-pass intermediate
   WS_WATERSHED = 14, // Cells watershed flood levels + tile flags
+  WS_MISC2 = 15,     // the second object set's feature workspace (cpx_features_pair)
 };
 
 void cpx_set_error(const char* fmt, ...);
@@ -149,3 +150,10 @@ int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr
                       int H, int W, int max_label, int F, const cpx_object* objects_dev,
                       const cpx_fov_objects* hdr_dev, double* feats_dev, cpx_fallback_lists* fb,
                       cpx_fallback_fn fallback, void* fallback_arg);
+// Two object sets whose second set's objects lie inside the first's with the same labels (Cells,
+// Cytoplasm): the LDS fast paths of both (k_texture.hip); the caller launches both fallbacks.
+int cpx_features_pair_fast(cpx_ctx* ctx, const int32_t* labels_dev, const int32_t* tlabels_dev,
+                           const float* corr_dev, int B, int C, int H, int W, int max_label, int F,
+                           const cpx_object* objects_dev, const cpx_fov_objects* hdr_dev, double* feats_dev,
+                           const cpx_object* tobjects_dev, const cpx_fov_objects* thdr_dev, double* tfeats_dev,
+                           cpx_fallback_lists* fb, cpx_fallback_lists* tfb);

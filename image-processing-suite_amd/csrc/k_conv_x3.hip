@@ -114,6 +114,13 @@ struct X3Epi {
   // [COUT/BM][CIN2/16][BM][hi|lo][16] accumulate conv1x1(in2, wp) into the same sums
   const uint4* in2;
   const uint4* wpk2;
+  // 2x2/2 max-pool of the y tile (k_cpnet_pool_x3's arithmetic, fused into the epilogue of a down
+  // block's last convolution): pool_x [N][H/2][W/2][COUT] = the maximum's own hi/lo pair and
+  // pool_z = split(relu(pool_scale x + pool_shift)), the next block's input and its BatchNorm+ReLU
+  uint4* pool_x;
+  uint4* pool_z;
+  const float* pool_scale;
+  const float* pool_shift;
 };
 
 // Epilogue of a 3x3 / 1x1 convolution tile on its fp32 values (acc0 = the joined sums): bias,
@@ -239,6 +246,48 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
     stage(ybuf);
     __syncthreads();
     drain(ybuf, ep.y);
+    if (ep.pool_x) {
+      // pooled pixel (py, px) of the tile from staged pixels (2py + a, 2px + b), first maximum in
+      // the order (0,0) (0,1) (1,0) (1,1) as k_cpnet_pool_x3; one item per (pooled pixel, group of 8)
+      static_assert(TY % 2 == 0 && TX % 2 == 0, "pooled tiles");
+      constexpr int PH = TY / 2, PW2 = TX / 2, G8 = BM / 8;
+      for (int it = tid; it < PH * PW2 * G8; it += NT) {
+        const int gi = it % G8, pp = it / G8;
+        const int py = pp / PW2, px = pp - py * PW2;
+        const int gy = ty0 / 2 + py, gx = tx0 / 2 + px;
+        if (2 * gy >= H || 2 * gx >= W) continue;
+        const int q = (gi >> 1) * 4 + (gi & 1);  // hi chunk of the group in the block; lo = q + 2
+        float best[8];
+        f16x8 mh, ml;
+#pragma unroll
+        for (int sidx = 0; sidx < 4; ++sidx) {
+          const int spx = (2 * py + (sidx >> 1)) * TX + 2 * px + (sidx & 1);
+          const uint4 ch = ybuf[spx * QB + (q ^ swzq<QB>(spx))];
+          const uint4 cl = ybuf[spx * QB + ((q + 2) ^ swzq<QB>(spx))];
+          float f[8];
+          join8(ch, cl, f);
+          const f16x8 fh = __builtin_bit_cast(f16x8, ch), fl = __builtin_bit_cast(f16x8, cl);
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (sidx == 0 || f[k] > best[k]) {  // max_pool2d: first maximum
+              best[k] = f[k];
+              mh[k] = fh[k];
+              ml[k] = fl[k];
+            }
+        }
+        const long long op = ((long long)n * (H / 2) + gy) * (W / 2) + gx;
+        ep.pool_x[op * QC + nb * QB + q] = __builtin_bit_cast(uint4, mh);
+        ep.pool_x[op * QC + nb * QB + q + 2] = __builtin_bit_cast(uint4, ml);
+        const int c0 = nb * BM + gi * 8;
+        float zz[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) zz[k] = fmaxf(ep.pool_scale[c0 + k] * best[k] + ep.pool_shift[c0 + k], 0.0f);
+        uint4 zh, zl;
+        split8(zz, zh, zl, bad);
+        ep.pool_z[op * QC + nb * QB + q] = zh;
+        ep.pool_z[op * QC + nb * QB + q + 2] = zl;
+      }
+    }
     if (zbuf == ybuf) __syncthreads();  // z is staged over y's tile
   }
   if (!ep.z && !ep.head) {
@@ -1099,8 +1148,25 @@ extern "C" int cpx_cpnet_x3_conv(cpx_ctx* ctx, int ks, int variant, const void* 
               CPX_ERR_ARG, "cpx_cpnet_x3_conv: head needs a 3x3 conv with cout 32, no z_out, 1..4 outputs");
   CPX_REQUIRE(!z_up || z_out, CPX_ERR_ARG, "cpx_cpnet_x3_conv: z_up without z_out");
   X3Epi ep{bias, (const uint4*)res, style, scale, shift, (uint4*)y_out, (uint4*)z_out, res_up, relu,
-           z_up, style_stride, head_w, head_b, head_out, n_head, ovf, in_up, nullptr, nullptr};
+           z_up, style_stride, head_w, head_b, head_out, n_head, ovf, in_up, nullptr, nullptr,
+           nullptr, nullptr, nullptr, nullptr};
   return x3_launch(ctx, ks, cin, cout, variant, in, wpk, ep, N, H, W);
+}
+
+extern "C" int cpx_cpnet_x3_conv_pool(cpx_ctx* ctx, int variant, const void* in, int N, int H, int W, int cin,
+                                      int cout, const void* wpk, const float* bias, const void* res,
+                                      void* y_out, void* pool_x, void* pool_z, const float* pool_scale,
+                                      const float* pool_shift, int* ovf) {
+  CPX_REQUIRE(ctx && in && wpk && res && y_out && pool_x && pool_z && pool_scale && pool_shift, CPX_ERR_ARG,
+              "cpx_cpnet_x3_conv_pool: null argument");
+  CPX_REQUIRE(N > 0 && H > 0 && W > 0 && H % 2 == 0 && W % 2 == 0, CPX_ERR_ARG,
+              "cpx_cpnet_x3_conv_pool: bad sizes (even H, W)");
+  CPX_REQUIRE(((uintptr_t)in | (uintptr_t)wpk | (uintptr_t)res | (uintptr_t)y_out | (uintptr_t)pool_x |
+               (uintptr_t)pool_z) % 16 == 0, CPX_ERR_ARG, "cpx_cpnet_x3_conv_pool: misaligned buffers");
+  X3Epi ep{bias, (const uint4*)res, nullptr, nullptr, nullptr, (uint4*)y_out, nullptr, 0, 0, 0, 0,
+           nullptr, nullptr, nullptr, 0, ovf, 0, nullptr, nullptr,
+           (uint4*)pool_x, (uint4*)pool_z, pool_scale, pool_shift};
+  return x3_launch(ctx, 3, cin, cout, variant, in, wpk, ep, N, H, W);
 }
 
 extern "C" int cpx_cpnet_x3_conv_proj(cpx_ctx* ctx, int variant, const void* in, int N, int H, int W,
@@ -1119,7 +1185,8 @@ extern "C" int cpx_cpnet_x3_conv_proj(cpx_ctx* ctx, int variant, const void* in,
               CPX_ERR_ARG, "cpx_cpnet_x3_conv_proj: style needs a 16-byte aligned [N][stride >= cout] table");
   CPX_REQUIRE(!z_up || z_out, CPX_ERR_ARG, "cpx_cpnet_x3_conv_proj: z_up without z_out");
   X3Epi ep{bias, nullptr, style, scale, shift, (uint4*)y_out, (uint4*)z_out, 0, relu, z_up, style_stride,
-           nullptr, nullptr, nullptr, 0, ovf, 0, (const uint4*)in2, (const uint4*)wpk2};
+           nullptr, nullptr, nullptr, 0, ovf, 0, (const uint4*)in2, (const uint4*)wpk2,
+           nullptr, nullptr, nullptr, nullptr};
   return x3_launch_proj(ctx, cin, cout, cin2, variant, in, wpk, ep, N, H, W);
 }
 

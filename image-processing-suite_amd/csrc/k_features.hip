@@ -537,3 +537,26 @@ extern "C" int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float
   return cpx_features_fast(ctx, labels_dev, corr_dev, B, C, H, W, max_label, F, objects_dev, hdr_dev,
                            feats_dev, &fb, launch_fallbacks, &fa);
 }
+
+extern "C" int cpx_features_pair(cpx_ctx* ctx, const int32_t* cells_dev, const int32_t* cyto_dev,
+                                 const float* corr_dev, int B, int C, int H, int W, int max_label,
+                                 const cpx_object* cells_objects_dev, const cpx_fov_objects* cells_hdr_dev,
+                                 double* cells_feats_dev, const cpx_object* cyto_objects_dev,
+                                 const cpx_fov_objects* cyto_hdr_dev, double* cyto_feats_dev) {
+  CPX_REQUIRE(ctx && cells_dev && cyto_dev && corr_dev && cells_objects_dev && cells_hdr_dev && cells_feats_dev &&
+                  cyto_objects_dev && cyto_hdr_dev && cyto_feats_dev,
+              CPX_ERR_ARG, "cpx_features_pair: null argument");
+  CPX_REQUIRE(B > 0 && B <= 65535 && C > 0 && C <= 65535 && H > 0 && W > 0 && max_label > 0,
+              CPX_ERR_ARG, "cpx_features_pair: bad sizes");
+  const int F = CPX_N_SHAPE + C * CPX_FEATURES_PER_CHANNEL;
+  cpx_fallback_lists fb, tfb;
+  int rc = cpx_features_pair_fast(ctx, cells_dev, cyto_dev, corr_dev, B, C, H, W, max_label, F, cells_objects_dev,
+                                  cells_hdr_dev, cells_feats_dev, cyto_objects_dev, cyto_hdr_dev, cyto_feats_dev,
+                                  &fb, &tfb);
+  if (rc) return rc;
+  FallbackArgs fa{cells_dev, corr_dev, B, C, H, W, max_label, F, cells_objects_dev, cells_feats_dev};
+  FallbackArgs ta{cyto_dev, corr_dev, B, C, H, W, max_label, F, cyto_objects_dev, cyto_feats_dev};
+  if ((rc = launch_fallbacks(ctx, ctx->stream, fb, &fa))) return rc;
+  return launch_fallbacks(ctx, ctx->stream, tfb, &ta);
+}
+

@@ -789,6 +789,23 @@ __device__ __forceinline__ void int_acc(IntAcc& a, float v, bool in) {
   }
 }
 
+// The twin object set of a k_obj_stage<true> pass (Cytoplasm beside Cells: the same ObjectNumber,
+// its pixels a subset of the cell's, so a Cytoplasm object whose bbox equals its cell's is staged
+// from the same reads of the channels): its label image, tables and staging outputs, the Cells
+// object -> twin object map, and the per-object flags of the twins staged here (the twin set's
+// own k_obj_stage pass skips them).
+struct StageTwin {
+  const int* labels;
+  const cpx_object* objects;
+  const long long* crop_off;
+  unsigned char* scratch;
+  long long* raws;
+  double* feats;
+  const int* map;   // [B][max_label]: Cells object k -> twin object index, or -1
+  int* done;        // [B][max_label]: twin object staged by the Cells pass
+};
+
+template <bool TWIN>
 __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ labels,
                                                   const float* __restrict__ corr, int C, int H,
                                                   int W, int max_label, int F,
@@ -799,15 +816,17 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
                                                   long long scratch_per_fov,
                                                   long long* __restrict__ raws,
                                                   int* __restrict__ obj_next,
-                                                  double* __restrict__ feats) {
+                                                  double* __restrict__ feats,
+                                                  const int* __restrict__ skip, StageTwin tw) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned int* M = reinterpret_cast<unsigned int*>(smem);
   unsigned int* Bd = M + kShapeW;
+  unsigned int* M2 = Bd + kShapeW;  // the twin's membership mask (TWIN only)
   __shared__ long long red[6][kOT / 64];
   __shared__ int redi[3][kOT / 64];
-  __shared__ double sd_[2][2][kOT / 64];  // [channel parity]: no barrier before the next channel's
-  __shared__ long long sn_[2][kOT / 64];   // partials overwrite them
-  __shared__ float sf_[2][4][kOT / 64];
+  __shared__ double sd_[2][2][2][kOT / 64];  // [set / twin][channel parity]: no barrier before the
+  __shared__ long long sn_[2][2][kOT / 64];   // next channel's partials overwrite them
+  __shared__ float sf_[2][2][4][kOT / 64];
   __shared__ int s_code;
   const int fov = blockIdx.y, B = gridDim.y;
   const long long N = (long long)H * W;
@@ -820,13 +839,38 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
     const int code = __builtin_amdgcn_readfirstlane(s_code);  // block-uniform: scalar registers
     if (code < 0) break;
     const int fov = code >> 20, k = code & 0xfffff;
+    if (skip && skip[(long long)fov * max_label + k]) continue;  // staged by the twin pass
     const int* lab = labels + (long long)fov * N;
     const cpx_object o = objects[(long long)fov * max_label + k];
     if (!shape_fits(o)) continue;  // shape and texture both in the fallback kernels
+    const long long off = crop_off[(long long)fov * max_label + k];
+    // the twin rides along when it has the same bbox and both crops are staged (block-uniform)
+    int ky = -1;
+    long long offy = -1;
+    if constexpr (TWIN) {
+      ky = tw.map[(long long)fov * max_label + k];
+      if (ky >= 0) {
+        const cpx_object y = tw.objects[(long long)fov * max_label + ky];
+        offy = tw.crop_off[(long long)fov * max_label + ky];
+        if (off < 0 || offy < 0 || y.bbox[0] != o.bbox[0] || y.bbox[1] != o.bbox[1] ||
+            y.bbox[2] != o.bbox[2] || y.bbox[3] != o.bbox[3])
+          ky = -1;
+      }
+      ky = __builtin_amdgcn_readfirstlane(ky);
+    }
     shape_mask<kOT>(lab, H, W, o, M);
+    if (TWIN && ky >= 0) {
+      const cpx_object y = tw.objects[(long long)fov * max_label + ky];
+      shape_mask<kOT>(tw.labels + (long long)fov * N, H, W, y, M2);
+    }
     __syncthreads();
     shape_sums<kOT>(o, M, Bd, red, redi, raws + ((long long)fov * max_label + k) * kShapeRaw);
-    const long long off = crop_off[(long long)fov * max_label + k];
+    if (TWIN && ky >= 0) {
+      const cpx_object y = tw.objects[(long long)fov * max_label + ky];
+      __syncthreads();  // the first sums' reads of Bd / red are done
+      shape_sums<kOT>(y, M2, Bd, red, redi, tw.raws + ((long long)fov * max_label + ky) * kShapeRaw);
+      if (threadIdx.x == 0) tw.done[(long long)fov * max_label + ky] = 1;
+    }
     if (off < 0) continue;  // texture not staged: fallback kernel (block-uniform)
     const int r0 = o.bbox[0], c0 = o.bbox[1];
     const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
@@ -838,12 +882,21 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
     // the group's first pixel (< 2^24: shape_fits bounds bh by 4092, and only images with
     // W <= 4096 stage crops)
     // | member bits << 24 | valid pixels (1..4) << 28
-    unsigned int gd[kOG];
+    unsigned int gd[kOG], gm2[kOG];  // gm2: the twin's member bits of the same groups
 #pragma unroll
-    for (int i = 0; i < kOG; ++i) gd[i] = group_desc(M, wpr, bw, bwp, W, min(threadIdx.x + i * kOT, ng - 1));
+    for (int i = 0; i < kOG; ++i) {
+      const int g = min((int)threadIdx.x + i * kOT, ng - 1);
+      gd[i] = group_desc(M, wpr, bw, bwp, W, g);
+      gm2[i] = 0u;
+      if (TWIN && ky >= 0) {
+        const int f0 = 4 * g, r = f0 / bwp, c = f0 - r * bwp;
+        gm2[i] = member4(M2, wpr, r, c);
+      }
+    }
     for (int ch = 0; ch < C; ++ch) {
       const float* img = corr + ((long long)fov * C + ch) * N + (long long)r0 * W + c0;
       IntAcc a{0, 0.0, 0.0, INFINITY, -INFINITY, INFINITY, -INFINITY};
+      IntAcc a2{0, 0.0, 0.0, INFINITY, -INFINITY, INFINITY, -INFINITY};
       float v[kOG][4];
       // opaque per channel: keeps the compiler from hoisting every load's offset out of the
       // channel loop (4 * kOG more VGPRs live across it)
@@ -861,7 +914,10 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
         const unsigned int mb = (gd[i] >> 24) & 15u, nv = gd[i] >> 28;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if ((unsigned int)u < nv) int_acc(a, v[i][u], (mb >> u) & 1u);
+          if ((unsigned int)u < nv) {
+            int_acc(a, v[i][u], (mb >> u) & 1u);
+            if (TWIN && ky >= 0) int_acc(a2, v[i][u], (gm2[i] >> u) & 1u);
+          }
       }
       // groups past the register-held ones (large bboxes) are read twice; the block's working
       // set (one channel of one bbox) stays in L2 between the two passes.  kOR groups per
@@ -880,68 +936,91 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
         for (int r = 0; r < kOR; ++r) {
           if (g0 + r * kOT >= ng) continue;
           const unsigned int mb = (d[r] >> 24) & 15u, nv = d[r] >> 28;
+          unsigned int mb2 = 0u;
+          if (TWIN && ky >= 0) {
+            const int f0 = 4 * (g0 + r * kOT), rr = f0 / bwp, cc = f0 - rr * bwp;
+            mb2 = member4(M2, wpr, rr, cc);
+          }
 #pragma unroll
           for (int u = 0; u < 4; ++u)
-            if ((unsigned int)u < nv) int_acc(a, w4[r][u], (mb >> u) & 1u);
+            if ((unsigned int)u < nv) {
+              int_acc(a, w4[r][u], (mb >> u) & 1u);
+              if (TWIN && ky >= 0) int_acc(a2, w4[r][u], (mb2 >> u) & 1u);
+            }
         }
       }
-      a.n = wave_sum(a.n);
-      a.sm = wave_sum(a.sm);
-      a.ss = wave_sum(a.ss);
-      a.omin = wave_min(a.omin);
-      a.omax = wave_max(a.omax);
-      a.mmin = wave_min(a.mmin);
-      a.mmax = wave_max(a.mmax);
-      long long* sn = sn_[ch & 1];
-      double(*sd)[kOT / 64] = sd_[ch & 1];
-      float(*sf)[kOT / 64] = sf_[ch & 1];
-      if (lane == 0) {
-        sn[wid] = a.n;
-        sd[0][wid] = a.sm;
-        sd[1][wid] = a.ss;
-        sf[0][wid] = a.omin;
-        sf[1][wid] = a.omax;
-        sf[2][wid] = a.mmin;
-        sf[3][wid] = a.mmax;
-      }
-      __syncthreads();
-      // every thread needs only the crop range; thread 0 finishes the Intensity columns
-      float mmin = sf[2][0], mmax = sf[3][0];
+      auto reduce = [&](IntAcc& x, int t, double* fout, float& mmin, float& mmax) {
+        // t: which partial slots (0: this set, 1: the twin); channel parity double-buffers them
+        x.n = wave_sum(x.n);
+        x.sm = wave_sum(x.sm);
+        x.ss = wave_sum(x.ss);
+        x.omin = wave_min(x.omin);
+        x.omax = wave_max(x.omax);
+        x.mmin = wave_min(x.mmin);
+        x.mmax = wave_max(x.mmax);
+        long long* sn = sn_[t][ch & 1];
+        double(*sd)[kOT / 64] = sd_[t][ch & 1];
+        float(*sf)[kOT / 64] = sf_[t][ch & 1];
+        if (lane == 0) {
+          sn[wid] = x.n;
+          sd[0][wid] = x.sm;
+          sd[1][wid] = x.ss;
+          sf[0][wid] = x.omin;
+          sf[1][wid] = x.omax;
+          sf[2][wid] = x.mmin;
+          sf[3][wid] = x.mmax;
+        }
+        __syncthreads();
+        // every thread needs only the crop range; thread 0 finishes the Intensity columns
+        mmin = sf[2][0];
+        mmax = sf[3][0];
 #pragma unroll
-      for (int w = 1; w < kOT / 64; ++w) {
-        mmin = fminf(mmin, sf[2][w]);
-        mmax = fmaxf(mmax, sf[3][w]);
-      }
-      if (threadIdx.x == 0) {
-        long long n = 0;
-        double sm = 0.0, ss = 0.0;
-        float omin = INFINITY, omax = -INFINITY;
-        for (int w = 0; w < kOT / 64; ++w) {
-          n += sn[w];
-          sm += sd[0][w];
-          ss += sd[1][w];
-          omin = fminf(omin, sf[0][w]);
-          omax = fmaxf(omax, sf[1][w]);
+        for (int w = 1; w < kOT / 64; ++w) {
+          mmin = fminf(mmin, sf[2][w]);
+          mmax = fmaxf(mmax, sf[3][w]);
         }
-        int_finish(feats + ((long long)fov * max_label + k) * F + CPX_N_SHAPE +
-                       (long long)ch * CPX_FEATURES_PER_CHANNEL, n, sm, ss, omin, omax);
-      }
+        if (threadIdx.x == 0) {
+          long long n = 0;
+          double sm = 0.0, ss = 0.0;
+          float omin = INFINITY, omax = -INFINITY;
+          for (int w = 0; w < kOT / 64; ++w) {
+            n += sn[w];
+            sm += sd[0][w];
+            ss += sd[1][w];
+            omin = fminf(omin, sf[0][w]);
+            omax = fmaxf(omax, sf[1][w]);
+          }
+          int_finish(fout + CPX_N_SHAPE + (long long)ch * CPX_FEATURES_PER_CHANNEL, n, sm, ss, omin, omax);
+        }
+      };
+      float mmin, mmax, mmin2 = 0.0f, mmax2 = 0.0f;
+      reduce(a, 0, feats + ((long long)fov * max_label + k) * F, mmin, mmax);
+      if (TWIN && ky >= 0) reduce(a2, 1, tw.feats + ((long long)fov * max_label + ky) * F, mmin2, mmax2);
       const float rng = mmax - mmin;
       const bool flat = !(mmax != mmin);
+      const float rng2 = mmax2 - mmin2;
+      const bool flat2 = !(mmax2 != mmin2);
       unsigned char* dst = scratch + (long long)fov * scratch_per_fov + off + (long long)ch * cbytes;
+      unsigned char* dst2 = TWIN && ky >= 0 ? tw.scratch + (long long)fov * scratch_per_fov + offy + (long long)ch * cbytes
+                                            : nullptr;
       // the crop at the padded row stride (pad bytes 0), one 32-bit store per 4-pixel group
 #pragma unroll
       for (int i = 0; i < kOG; ++i) {
         const int g = threadIdx.x + i * kOT;
         if (g >= ng) continue;
         const unsigned int mb = (gd[i] >> 24) & 15u, nv = gd[i] >> 28;
-        unsigned int word = 0u;
+        unsigned int word = 0u, word2 = 0u;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const unsigned int q = (unsigned int)quantize(v[i][u], (mb >> u) & 1u, mmin, rng, flat);
           word |= ((unsigned int)u < nv ? q : 0u) << (8 * u);
+          if (TWIN && ky >= 0) {
+            const unsigned int q2 = (unsigned int)quantize(v[i][u], (gm2[i] >> u) & 1u, mmin2, rng2, flat2);
+            word2 |= ((unsigned int)u < nv ? q2 : 0u) << (8 * u);
+          }
         }
         *reinterpret_cast<unsigned int*>(dst + 4 * g) = word;
+        if (TWIN && ky >= 0) *reinterpret_cast<unsigned int*>(dst2 + 4 * g) = word2;
       }
       for (int g0 = threadIdx.x + kOG * kOT; g0 < ng; g0 += kOR * kOT) {
         unsigned int d[kOR];
@@ -958,13 +1037,23 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
           const int g = g0 + r * kOT;
           if (g >= ng) continue;
           const unsigned int mb = (d[r] >> 24) & 15u, nv = d[r] >> 28;
-          unsigned int word = 0u;
+          unsigned int mb2 = 0u;
+          if (TWIN && ky >= 0) {
+            const int f0 = 4 * g, rr = f0 / bwp, cc = f0 - rr * bwp;
+            mb2 = member4(M2, wpr, rr, cc);
+          }
+          unsigned int word = 0u, word2 = 0u;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const unsigned int q = (unsigned int)quantize(w4[r][u], (mb >> u) & 1u, mmin, rng, flat);
             word |= ((unsigned int)u < nv ? q : 0u) << (8 * u);
+            if (TWIN && ky >= 0) {
+              const unsigned int q2 = (unsigned int)quantize(w4[r][u], (mb2 >> u) & 1u, mmin2, rng2, flat2);
+              word2 |= ((unsigned int)u < nv ? q2 : 0u) << (8 * u);
+            }
           }
           *reinterpret_cast<unsigned int*>(dst + 4 * g) = word;
+          if (TWIN && ky >= 0) *reinterpret_cast<unsigned int*>(dst2 + 4 * g) = word2;
         }
       }
     }
@@ -975,69 +1064,192 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
 
 
 // internal launchers used by cpx_features (k_features.hip)
+namespace {
+
+// one object set's feature workspace (slot WS_MISC or WS_MISC2): crop offsets [B][max_label],
+// the GLCM / k_obj_stage queue counters, the fallback lists, the AreaShape raw sums, the GLCM
+// integer totals and the 8-bit crop scratch (2 bytes per pixel-channel per FOV)
+struct FeatWs {
+  long long* crop_off;
+  int* glcm_next;
+  cpx_fallback_lists fb;
+  long long* raws;
+  unsigned long long* glcm_raw;
+  unsigned char* scratch;
+  long long per_fov;
+  int* twin;  // [2][B][max_label]: the twin map and done flags (cpx_features_pair only)
+};
+
+int feat_ws(cpx_ctx* ctx, int slot, int B, int C, int H, int W, int max_label, bool twin, FeatWs* w) {
+  w->per_fov = ((2LL * H * W * C + 255) / 256) * 256;
+  const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + sizeof(int) * (size_t)B * 4 +
+                             sizeof(int) * 2 * (size_t)B * max_label + 255) / 256) * 256;
+  const size_t raw_bytes = ((sizeof(long long) * kShapeRaw * (size_t)B * max_label + 255) / 256) * 256;
+  const size_t glcm_bytes = ((sizeof(unsigned long long) * 4 * kRedW * (size_t)B * max_label * C + 255) / 256) * 256;
+  const size_t twin_bytes = twin ? ((sizeof(int) * 2 * (size_t)B * max_label + 255) / 256) * 256 : 0;
+  unsigned char* ws = (unsigned char*)cpx_ws(ctx, slot, off_bytes + raw_bytes + glcm_bytes + twin_bytes +
+                                             (size_t)B * w->per_fov + 256);  // +256: crop read slack
+  if (!ws) return CPX_ERR_OOM;
+  w->crop_off = (long long*)ws;
+  w->glcm_next = (int*)(w->crop_off + (size_t)B * max_label);  // + k_obj_stage's queues at B
+  w->fb.n_shape = w->glcm_next + 2 * B;
+  w->fb.n_tex = w->fb.n_shape + B;
+  w->fb.shape = w->fb.n_tex + B;
+  w->fb.tex = w->fb.shape + (size_t)B * max_label;
+  w->raws = (long long*)(ws + off_bytes);
+  w->glcm_raw = (unsigned long long*)(ws + off_bytes + raw_bytes);
+  w->twin = twin ? (int*)(ws + off_bytes + raw_bytes + glcm_bytes) : nullptr;
+  w->scratch = ws + off_bytes + raw_bytes + glcm_bytes + twin_bytes;
+  return CPX_OK;
+}
+
+size_t obj_stage_lds(bool twin) { return sizeof(unsigned int) * (twin ? 3 : 2) * kShapeW; }
+
+int obj_stage_attr() {
+  static bool attr = false;
+  if (!attr) {
+    CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_obj_stage<false>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)obj_stage_lds(false)));
+    CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_obj_stage<true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)obj_stage_lds(true)));
+    attr = true;
+  }
+  return CPX_OK;
+}
+
+// Cells object k -> Cytoplasm object with the same label (both tables ascending by label), or -1;
+// clears the done flags.  One block per FOV.
+__global__ __launch_bounds__(256) void k_twin_map(int max_label, const cpx_object* __restrict__ objects,
+                                                  const cpx_fov_objects* __restrict__ hdr,
+                                                  const cpx_object* __restrict__ tobjects,
+                                                  const cpx_fov_objects* __restrict__ thdr,
+                                                  int* __restrict__ map, int* __restrict__ done) {
+  const int fov = blockIdx.x;
+  const int n = hdr[fov].n_objects, nt = thdr[fov].n_objects;
+  const cpx_object* t = tobjects + (long long)fov * max_label;
+  for (int k = threadIdx.x; k < max_label; k += blockDim.x) {
+    int m = -1;
+    if (k < n) {
+      const int L = objects[(long long)fov * max_label + k].label;
+      int lo = 0, hi = nt;  // first index with label >= L
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (t[mid].label < L) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo < nt && t[lo].label == L) m = lo;
+    }
+    map[(long long)fov * max_label + k] = m;
+    done[(long long)fov * max_label + k] = 0;
+  }
+}
+
+struct SetArgs {
+  const int32_t* labels;
+  const cpx_object* objects;
+  const cpx_fov_objects* hdr;
+  double* feats;
+};
+
+int launch_offsets(cpx_ctx* ctx, const SetArgs& a, FeatWs& w, int B, int C, int W, int max_label) {
+  // k_obj_stage packs a staged crop's bbox offsets (bh <= 4092) x W in 24 bits: wider images
+  // measure texture in the fallback kernel (cap 0: nothing staged)
+  hipLaunchKernelGGL(k_crop_offsets, dim3(B), dim3(1024), 0, ctx->stream, C, max_label,
+                     a.objects, a.hdr, W <= 4096 ? w.per_fov : 0LL, w.crop_off, w.glcm_next, w.fb);
+  CPX_CHECK_LAUNCH("k_crop_offsets");
+  return CPX_OK;
+}
+
+int launch_stage(cpx_ctx* ctx, const SetArgs& a, FeatWs& w, const float* corr, int B, int C, int H, int W,
+                 int max_label, int F, const int* skip, const StageTwin* tw) {
+  int rc = obj_stage_attr();
+  if (rc) return rc;
+  const int per_fov_o = std::max(1, std::min(max_label, (2 * ctx->n_cu + B - 1) / B));  // resident
+  if (tw)
+    hipLaunchKernelGGL(k_obj_stage<true>, dim3(per_fov_o, B), dim3(kOT), obj_stage_lds(true), ctx->stream,
+                       (const int*)a.labels, corr, C, H, W, max_label, F, a.objects, a.hdr,
+                       (const long long*)w.crop_off, w.scratch, w.per_fov, w.raws, w.glcm_next + B, a.feats,
+                       skip, *tw);
+  else
+    hipLaunchKernelGGL(k_obj_stage<false>, dim3(per_fov_o, B), dim3(kOT), obj_stage_lds(false), ctx->stream,
+                       (const int*)a.labels, corr, C, H, W, max_label, F, a.objects, a.hdr,
+                       (const long long*)w.crop_off, w.scratch, w.per_fov, w.raws, w.glcm_next + B, a.feats,
+                       skip, StageTwin{});
+  CPX_CHECK_LAUNCH("k_obj_stage");
+  return CPX_OK;
+}
+
+int launch_texture(cpx_ctx* ctx, const SetArgs& a, FeatWs& w, int B, int C, int max_label, int F) {
+  hipLaunchKernelGGL(k_shape_props, dim3(cpx_div_up(max_label, 256), B), dim3(256), 0, ctx->stream,
+                     max_label, F, a.objects, a.hdr, (const long long*)w.raws, a.feats);
+  CPX_CHECK_LAUNCH("k_shape_props");
+  const int per_fov_t = std::max(1, std::min(max_label * C, (ctx->n_cu + B - 1) / B));
+  hipLaunchKernelGGL(k_tex_glcm, dim3(per_fov_t, B), dim3(kTT), 0, ctx->stream, C, max_label,
+                     F, a.objects, a.hdr, (const long long*)w.crop_off,
+                     (const unsigned char*)w.scratch, w.per_fov, w.glcm_next, w.glcm_raw);
+  CPX_CHECK_LAUNCH("k_tex_glcm");
+  hipLaunchKernelGGL(k_glcm_props, dim3(cpx_div_up(max_label * C * 4, 256), B), dim3(256), 0, ctx->stream,
+                     C, max_label, F, a.objects, a.hdr, (const long long*)w.crop_off,
+                     (const unsigned long long*)w.glcm_raw, a.feats);
+  CPX_CHECK_LAUNCH("k_glcm_props");
+  return CPX_OK;
+}
+
+}  // namespace
+
 int cpx_features_fast(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B, int C,
                       int H, int W, int max_label, int F, const cpx_object* objects_dev,
                       const cpx_fov_objects* hdr_dev, double* feats_dev, cpx_fallback_lists* fb,
                       cpx_fallback_fn fallback, void* fallback_arg) {
-  static bool attr = false;
   static_assert(sizeof(unsigned int) * kTabW + kSmall + kCrop == 160 * 1024, "GLCM LDS budget");
   static_assert(sizeof(unsigned long long) * 4 * kRedW == 320 && kCrop % 16 == 0, "GLCM LDS layout");
   static_assert(2 * kRedW * kTT <= kTabW, "reduction scratch inside the table");
-  const size_t lds_s = sizeof(unsigned int) * 2 * kShapeW;
-  if (!attr) {
-    CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_obj_stage,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_s));
-    attr = true;
-  }
-  // workspace: crop offsets [B][max_label] + scratch (2 bytes per pixel-channel per FOV)
-  const long long per_fov = ((2LL * H * W * C + 255) / 256) * 256;
-  // + one GLCM and one k_obj_stage work-queue counter per FOV (zeroed by k_crop_offsets) + the
-  // fallback lists
-  // + the AreaShape raw sums [B][max_label][kShapeRaw]
-  const size_t off_bytes = ((sizeof(long long) * (size_t)B * max_label + sizeof(int) * (size_t)B * 4 +
-                             sizeof(int) * 2 * (size_t)B * max_label + 255) / 256) * 256;
-  const size_t raw_bytes = ((sizeof(long long) * kShapeRaw * (size_t)B * max_label + 255) / 256) * 256;
-  // + the GLCM integer totals [B][max_label][C][4 angles][kRedW] for k_glcm_props
-  const size_t glcm_bytes = ((sizeof(unsigned long long) * 4 * kRedW * (size_t)B * max_label * C + 255) / 256) * 256;
-  unsigned char* ws = (unsigned char*)cpx_ws(ctx, WS_MISC, off_bytes + raw_bytes + glcm_bytes +
-                                             (size_t)B * per_fov + 256);  // +256: crop read slack
-  if (!ws) return CPX_ERR_OOM;
   CPX_REQUIRE(B < 2048 && (long long)max_label * C < (1 << 20), CPX_ERR_SHAPE,
               "GLCM queue codes hold fov < 2048 and items < 2^20");
-  long long* crop_off = (long long*)ws;
-  int* glcm_next = (int*)(crop_off + (size_t)B * max_label);  // + k_obj_stage's queues at B
-  fb->n_shape = glcm_next + 2 * B;
-  fb->n_tex = fb->n_shape + B;
-  fb->shape = fb->n_tex + B;
-  fb->tex = fb->shape + (size_t)B * max_label;
-  long long* raws = (long long*)(ws + off_bytes);
-  unsigned long long* glcm_raw = (unsigned long long*)(ws + off_bytes + raw_bytes);
-  unsigned char* scratch = ws + off_bytes + raw_bytes + glcm_bytes;
-  // k_obj_stage packs a staged crop's bbox offsets (bh <= 4092) x W in 24 bits: wider images
-  // measure texture in the fallback kernel (cap 0: nothing staged)
-  hipLaunchKernelGGL(k_crop_offsets, dim3(B), dim3(1024), 0, ctx->stream, C, max_label,
-                     objects_dev, hdr_dev, W <= 4096 ? per_fov : 0LL, crop_off, glcm_next, *fb);
-  CPX_CHECK_LAUNCH("k_crop_offsets");
-  const int per_fov_o = std::max(1, std::min(max_label, (2 * ctx->n_cu + B - 1) / B));  // resident
-  hipLaunchKernelGGL(k_obj_stage, dim3(per_fov_o, B), dim3(kOT), lds_s, ctx->stream,
-                     (const int*)labels_dev, corr_dev, C, H, W, max_label, F, objects_dev, hdr_dev,
-                     (const long long*)crop_off, scratch, per_fov, raws, glcm_next + B, feats_dev);
-  CPX_CHECK_LAUNCH("k_obj_stage");
-  hipLaunchKernelGGL(k_shape_props, dim3(cpx_div_up(max_label, 256), B), dim3(256), 0, ctx->stream,
-                     max_label, F, objects_dev, hdr_dev, (const long long*)raws, feats_dev);
-  CPX_CHECK_LAUNCH("k_shape_props");
-  const int per_fov_t = std::max(1, std::min(max_label * C, (ctx->n_cu + B - 1) / B));
-  hipLaunchKernelGGL(k_tex_glcm, dim3(per_fov_t, B), dim3(kTT), 0, ctx->stream, C, max_label,
-                     F, objects_dev, hdr_dev, (const long long*)crop_off,
-                     (const unsigned char*)scratch, per_fov, glcm_next, glcm_raw);
-  CPX_CHECK_LAUNCH("k_tex_glcm");
-  hipLaunchKernelGGL(k_glcm_props, dim3(cpx_div_up(max_label * C * 4, 256), B), dim3(256), 0, ctx->stream,
-                     C, max_label, F, objects_dev, hdr_dev, (const long long*)crop_off,
-                     (const unsigned long long*)glcm_raw, feats_dev);
-  CPX_CHECK_LAUNCH("k_glcm_props");
+  FeatWs w;
+  int rc = feat_ws(ctx, WS_MISC, B, C, H, W, max_label, false, &w);
+  if (rc) return rc;
+  *fb = w.fb;
+  const SetArgs a{labels_dev, objects_dev, hdr_dev, feats_dev};
+  if ((rc = launch_offsets(ctx, a, w, B, C, W, max_label))) return rc;
+  if ((rc = launch_stage(ctx, a, w, corr_dev, B, C, H, W, max_label, F, nullptr, nullptr))) return rc;
+  if ((rc = launch_texture(ctx, a, w, B, C, max_label, F))) return rc;
   // the fallback kernels (the few largest objects, one long block each) as the tail
   if (fallback) return fallback(ctx, ctx->stream, *fb, fallback_arg);
   return CPX_OK;
+}
+
+// Cells and Cytoplasm together: one pass over the channels of a Cells object also stages its
+// Cytoplasm object when the two share the bbox (the common case: the nucleus lies inside the
+// cell); the Cytoplasm pass then stages only the rest.  Same outputs as two cpx_features_fast
+// calls (every sum and crop byte identical).
+int cpx_features_pair_fast(cpx_ctx* ctx, const int32_t* labels_dev, const int32_t* tlabels_dev,
+                           const float* corr_dev, int B, int C, int H, int W, int max_label, int F,
+                           const cpx_object* objects_dev, const cpx_fov_objects* hdr_dev, double* feats_dev,
+                           const cpx_object* tobjects_dev, const cpx_fov_objects* thdr_dev, double* tfeats_dev,
+                           cpx_fallback_lists* fb, cpx_fallback_lists* tfb) {
+  CPX_REQUIRE(B < 2048 && (long long)max_label * C < (1 << 20), CPX_ERR_SHAPE,
+              "GLCM queue codes hold fov < 2048 and items < 2^20");
+  FeatWs w, tw;
+  int rc = feat_ws(ctx, WS_MISC, B, C, H, W, max_label, true, &w);
+  if (rc) return rc;
+  if ((rc = feat_ws(ctx, WS_MISC2, B, C, H, W, max_label, false, &tw))) return rc;
+  *fb = w.fb;
+  *tfb = tw.fb;
+  const SetArgs a{labels_dev, objects_dev, hdr_dev, feats_dev};
+  const SetArgs t{tlabels_dev, tobjects_dev, thdr_dev, tfeats_dev};
+  int* map = w.twin;
+  int* done = w.twin + (size_t)B * max_label;
+  if ((rc = launch_offsets(ctx, a, w, B, C, W, max_label))) return rc;
+  if ((rc = launch_offsets(ctx, t, tw, B, C, W, max_label))) return rc;
+  hipLaunchKernelGGL(k_twin_map, dim3(B), dim3(256), 0, ctx->stream, max_label, objects_dev, hdr_dev,
+                     tobjects_dev, thdr_dev, map, done);
+  CPX_CHECK_LAUNCH("k_twin_map");
+  const StageTwin st{tlabels_dev, tobjects_dev, tw.crop_off, tw.scratch, tw.raws, tfeats_dev, map, done};
+  if ((rc = launch_stage(ctx, a, w, corr_dev, B, C, H, W, max_label, F, nullptr, &st))) return rc;
+  if ((rc = launch_stage(ctx, t, tw, corr_dev, B, C, H, W, max_label, F, done, nullptr))) return rc;
+  if ((rc = launch_texture(ctx, a, w, B, C, max_label, F))) return rc;
+  return launch_texture(ctx, t, tw, B, C, max_label, F);
 }
 
 #ifdef CPX_GLCM_PROF

@@ -275,6 +275,16 @@ int cpx_crops(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, in
 int cpx_features(cpx_ctx* ctx, const int32_t* labels_dev, const float* corr_dev, int B, int C,
                  int H, int W, int max_label, const cpx_object* objects_dev,
                  const cpx_fov_objects* hdr_dev, double* feats_dev);
+/* cpx_features of the Cells and the Cytoplasm object sets in one call (same outputs as two
+ * cpx_features calls): a Cytoplasm object with the same label and bbox as its Cells object is
+ * measured from the same reads of the channel planes.  cyto_dev must be the Cytoplasm of
+ * cells_dev (every Cytoplasm pixel carries its cell's label, as cpx_watershed_cells /
+ * cpx_expand_labels produce it).                                                              */
+int cpx_features_pair(cpx_ctx* ctx, const int32_t* cells_dev, const int32_t* cyto_dev,
+                      const float* corr_dev, int B, int C, int H, int W, int max_label,
+                      const cpx_object* cells_objects_dev, const cpx_fov_objects* cells_hdr_dev,
+                      double* cells_feats_dev, const cpx_object* cyto_objects_dev,
+                      const cpx_fov_objects* cyto_hdr_dev, double* cyto_feats_dev);
 
 /* ---- secondary objects for the Cells / Cytoplasm tables (Pycyto_pertime.py:46-49) -------- *
  * cells = skimage.segmentation.expand_labels(nuclei, distance) (0.18.3: nearest label pixel by
@@ -484,6 +494,15 @@ int cpx_cpnet_x3_conv_proj(cpx_ctx* ctx, int variant, const void* in, int N, int
                            int cout, const void* wpk, const void* in2, int cin2, const void* wpk2,
                            const float* bias, const float* style, int style_stride, const float* scale,
                            const float* shift, int relu, void* y_out, void* z_out, int z_up, int* ovf);
+/* 3x3 convolution with residual whose y tile is also 2x2/2 max-pooled in the epilogue (a down
+ * block's last convolution, fused with the next block's entry): y_out = conv(in) + bias + res,
+ * pool_x [N][H/2][W/2][cout] = max_pool2d(y) (the maximum's own hi/lo pair, first maximum) and
+ * pool_z = split(relu(pool_scale pool_x + pool_shift)) — cpx_cpnet_x3_conv followed by
+ * cpx_cpnet_x3_pool, bit for bit, without reading y back.  H and W even.                      */
+int cpx_cpnet_x3_conv_pool(cpx_ctx* ctx, int variant, const void* in, int N, int H, int W, int cin,
+                           int cout, const void* wpk, const float* bias, const void* res, void* y_out,
+                           void* pool_x, void* pool_z, const float* pool_scale, const float* pool_shift,
+                           int* ovf);
 /* stem on the fp32 network input x [N][H][W][2] (CPX_TILE_F32_NHWC tiles): z0 = relu(scale0 x
  * + shift0), z_out = relu(scale1 (conv3x3(z0, w0) + bias0) + shift1), p_out = conv1x1(x, wp),
  * fp32 arithmetic, split stores (32 channels).                                               */

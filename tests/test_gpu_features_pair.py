@@ -1,0 +1,98 @@
+"""GPU: cpx_features_pair (Cells and Cytoplasm measured together) equals two cpx_features calls.
+
+A Cytoplasm object shares its cell's ObjectNumber and lies inside it; when both have the same
+bbox, k_obj_stage<true> stages the Cytoplasm object (AreaShape sums, Intensity columns, the 8-bit
+crop the GLCM reads) from the Cells pass's reads of the channel planes, and the Cytoplasm pass
+skips it.  Every output must be bit-identical to the per-set path: here on synthetic labels where
+some nuclei reach their cell's bbox edge (different bboxes: the Cytoplasm pass stages those) and
+some cells have no cytoplasm at all, and through FovPipeline on bench FOVs.
+"""
+import numpy as np
+import pytest
+import torch
+
+import cpx_oracle as orc
+import synth_golden as sg
+from cpx.device import n_features
+
+pytestmark = pytest.mark.gpu
+
+
+def _tables(dev, lab, max_label):
+    B = lab.shape[0]
+    lst = dev.empty_bytes(64 * B * (max_label + 1))
+    obj = dev.empty_bytes(56 * B * max_label)
+    hdr = dev.empty_bytes(16 * B)
+    dev.objects(lab, max_label, 200, lst, obj, hdr)
+    return obj, hdr
+
+
+def test_pair_equals_per_set_on_synthetic_labels(dev):
+    B, C, H, W = 2, 3, 520, 560
+    td = dev.torch_device
+    nuc = np.stack([sg.labels(70 + b, H, W, n=30, rmin=6, rmax=30, skip_every=0) for b in range(B)])
+    cells = np.stack([orc.expand_labels(nuc[b], 12) for b in range(B)])
+    # some cells lose their cytoplasm entirely; some nuclei grow to their cell's bbox edge
+    for b in range(B):
+        ids = np.unique(cells[b][cells[b] > 0])
+        for L in ids[::7]:
+            nuc[b][cells[b] == L] = L
+        for L in ids[3::7]:
+            ys, xs = np.nonzero(cells[b] == L)
+            top = ys.min()
+            nuc[b][(cells[b] == L) & (np.arange(H)[:, None] == top)] = L
+    cyto = np.where(nuc == 0, cells, 0).astype(np.int32)
+    planes = np.stack([np.stack([sg.plane(800 + 10 * b + c, H, W, n_blobs=20).astype(np.float32) /
+                                 sg.illum(900 + c, H, W) for c in range(C)]) for b in range(B)]).astype(np.float32)
+    ML = 256
+    F = n_features(C)
+    cl = torch.from_numpy(cells.astype(np.int32)).to(td)
+    cy = torch.from_numpy(cyto).to(td)
+    corr = torch.from_numpy(planes).to(td)
+    oc, hc = _tables(dev, cl, ML)
+    oy, hy = _tables(dev, cy, ML)
+    ref = [torch.zeros((B, ML, F), dtype=torch.float64, device=td) for _ in range(2)]
+    dev.features(cl, corr, C, ML, oc, hc, ref[0])
+    dev.features(cy, corr, C, ML, oy, hy, ref[1])
+    got = [torch.zeros((B, ML, F), dtype=torch.float64, device=td) for _ in range(2)]
+    dev.features_pair(cl, cy, corr, C, ML, (oc, hc, got[0]), (oy, hy, got[1]))
+    dev.sync()
+    for r, g in zip(ref, got):
+        assert torch.equal(r, g)
+    # both paths were exercised: shared bboxes and different ones
+    from cpx.device import as_numpy
+    oc_np = as_numpy(oc, "object").reshape(B, ML)
+    oy_np = as_numpy(oy, "object").reshape(B, ML)
+    nc, ny = as_numpy(hc, "hdr")["n_objects"], as_numpy(hy, "hdr")["n_objects"]
+    same = diff = 0
+    for b in range(B):
+        bb = {int(o["label"]): tuple(o["bbox"]) for o in oc_np[b, :nc[b]]}
+        for o in oy_np[b, :ny[b]]:
+            if bb[int(o["label"])] == tuple(o["bbox"]):
+                same += 1
+            else:
+                diff += 1
+        assert ny[b] < nc[b]  # some cells have no cytoplasm
+    assert same > 10 and diff > 2, (same, diff)
+
+
+def test_pipeline_pair_features_bit_identical(dev, monkeypatch):
+    import os
+    import cpx.pipeline as pl
+    from cpx import shard
+    from cpx.synth import synth_fovs, synth_illum
+    w = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "image-processing-suite_amd",
+                     "cpx", "weights", "cpnet_nuclei_synth.pt")
+    cfg = pl.PipelineConfig(H=2080, W=2080, C=5, batch=2, weights=w if os.path.exists(w) else None)
+    illum = synth_illum(5, 2080, 2080, seed=1)
+    raw = synth_fovs(2, 5, 2080, 2080, dev.torch_device, seed=shard.fov_seed(shard.plate_fovs(n_wells=384)[11]))
+    monkeypatch.setattr(pl, "PAIR_FEATURES", True)
+    p1 = pl.FovPipeline(dev, cfg, illum)
+    a = p1.fetch(p1.run(raw))
+    monkeypatch.setattr(pl, "PAIR_FEATURES", False)
+    p2 = pl.FovPipeline(dev, cfg, illum)
+    b = p2.fetch(p2.run(raw))
+    for s in pl.OBJECT_SETS:
+        for f in range(2):
+            np.testing.assert_array_equal(a.objects[s][f], b.objects[s][f])
+            np.testing.assert_array_equal(a.feats[s][f], b.feats[s][f])

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--forward", type=int, default=5)
     ap.add_argument("--variants", type=int, nargs="+", default=[0, 1])
+    ap.add_argument("--zvariant", type=int, default=None, help="cpx.cpnet_x3 z-only conv variant (-1: none)")
     a = ap.parse_args()
     dev = Device(0)
     td = dev.torch_device
@@ -35,7 +36,7 @@ def main():
     real = lib.cpx_cpnet_x3_conv
     ref_out = None
     for v in a.variants:
-        f = FusedCPnetX3(net, dev, variant=v)
+        f = FusedCPnetX3(net, dev, variant=v, zvariant=a.zvariant)
         rows = []
 
         def wrap(*args):
