@@ -174,7 +174,12 @@ def main():
     queue = None
     if world > 1 and a.scheduler == "queue":
         # the product's multi-GPU scheduler (cpx.launch -> cpx.plate.WorkQueue): one shared counter
-        # over the job's steps x N batches, each rank claiming the next one when it can take it
+        # over the job's steps x N batches, each rank claiming the next one when it can take it.
+        # The counter is a file in rank 0's /tmp: every rank must be on rank 0's host (one node)
+        lws = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        if lws != world:
+            raise SystemExit(f"bench.py --scheduler queue needs a single-node job (LOCAL_WORLD_SIZE {lws} != "
+                             f"WORLD_SIZE {world}); use --scheduler static across nodes")
         import tempfile
         from cpx.plate import WorkQueue
         qd = [tempfile.mkdtemp(prefix="cpx_benchq_") if rank == 0 else None]

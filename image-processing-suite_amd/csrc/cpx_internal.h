@@ -122,6 +122,11 @@ __device__ __forceinline__ T wave_max(T v) {
 // CPX_SEG_ERR_INTERNAL in every FOV's stats instead of a kernel that never ends.
 constexpr int kClaimBroken = 1 << 30;
 
+// Flow-error register classes (k_flowerr_reg.hip fe_reg_class): every such mask's bbox is within
+// kFeRegMaxLong x kFeRegMaxShort in one orientation or the other (k_seg.hip checks that the fp32
+// screening's largest LDS class holds all of them)
+constexpr int kFeRegMaxLong = 128, kFeRegMaxShort = 120;
+
 // Objects handled by the LDS fast paths in k_texture.hip; the rest go to the k_features.hip
 // fallback kernels (the two predicates must agree between the translation units).
 constexpr int kFastShapeWords = 4096;  // 32 KiB of LDS for both masks: 5 blocks per CU (watershed

@@ -94,6 +94,11 @@ __device__ __forceinline__ void split8(const float* v, uint4& hi, uint4& lo, boo
   lo = make_uint4(l0.x, l0.y, l1.x, l1.y);
 }
 
+// CPX_X3_NT (experiment): the epilogue's y / z tile stores as non-temporal stores
+#ifndef CPX_X3_NT
+#define CPX_X3_NT 0
+#endif
+
 struct X3Epi {
   const float* bias;
   const uint4* res;    // split [N][h][w][COUT] (res_up: [N][h/2][w/2][COUT])
@@ -234,7 +239,15 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
       const int i = tid + r * NT;
       const int px = i / QB, k = i - px * QB;
       const long long gp = gpix(px);
-      if (i < P * QB && gp >= 0) dst[gp * QC + nb * QB + k] = buf[px * QB + (k ^ swzq<QB>(px))];
+      if (i < P * QB && gp >= 0) {
+#if CPX_X3_NT
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, buf[px * QB + (k ^ swzq<QB>(px))]),
+                                    reinterpret_cast<u32x4*>(dst + gp * QC + nb * QB + k));
+#else
+        dst[gp * QC + nb * QB + k] = buf[px * QB + (k ^ swzq<QB>(px))];
+#endif
+      }
     }
   };
   auto flag = [&]() {
@@ -655,6 +668,7 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
 // tiles of one XCD form a contiguous range that its blocks walk in step, so vertically adjacent
 // tiles (which share halo rows) are in flight together in that XCD's L2.  Per output pixel the
 // sums are formed in k_conv_x3's slab / tap / MFMA order: bit-identical results.
+template <bool kP32Touch>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, int N, int H,
                    int W, int tiles_x, int tiles_y) {
@@ -681,6 +695,7 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
     if (j < NWW)
       __builtin_amdgcn_global_load_lds((glb_void_t*)(wpk + j * 64 + fW), (lds_void_t*)(smem + j * 64), 16, 0, 0);
   }
+  unsigned touch = 0;
   const int aS = l32 * 4 + (h ^ swz4(l32));
   const int px = wid * 32 + l32;
   const int hp0 = (px / TX) * HX + (px % TX);
@@ -707,6 +722,29 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    unsigned tv0 = 0, tv1 = 0;
+    if (kP32Touch) {
+      // L2 prefetch while the MFMAs run: one 128-byte line per thread of this tile's residual
+      // (read by the epilogue) and of the block's next halo (DMA'd at the next tile's top); the
+      // loaded words are first used at the tile's end (no wait before the MFMAs) and only feed
+      // `touch`, consumed after the loop
+      const int i = threadIdx.x;
+      if (ep.res && i < TY * TX) {
+        const int gy = ty0 + i / TX, gx = tx0 + i % TX;
+        if (gy < H && gx < W) {
+          const long long rp = ep.res_up ? ((long long)n * (H >> 1) + (gy >> 1)) * (W >> 1) + (gx >> 1)
+                                         : ((long long)n * H + gy) * W + gx;
+          tv0 = reinterpret_cast<const unsigned*>(ep.res + rp * QI)[0];
+        }
+      }
+      const int t2 = t + nbx;
+      if (t2 < hi && i < NPIX) {
+        const int n2 = t2 / tiles, tt2 = t2 - n2 * tiles;
+        const int gy = (tt2 / tiles_x) * TY + i / HX - 1, gx = (tt2 % tiles_x) * TX + i % HX - 1;
+        if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+          tv1 = reinterpret_cast<const unsigned*>(in + ((long long)n2 * H * W + gy * W + gx) * QI)[0];
+      }
+    }
     // opaque per tile: keeps the compiler from hoisting every tap's fragment addresses out of the
     // tile loop (they would stay live across the epilogue: spills)
     int hpb = hp0, aSb = aS;
@@ -752,8 +790,10 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
     x3_epilogue<32, BM, TY, TX, 1, 1>(acc0, et, sx, n, 0, ty0, tx0, H, W, 0, wid, 1, tid);
+    touch ^= tv0 ^ tv1;
     __syncthreads();  // staging reads done before the next tile's halo lands
   }
+  if (kP32Touch && N < 0 && touch == 0x9e3779b9u) ep.ovf[0] = 1;  // never true: keeps the loads
 }
 
 struct X3Cfg {
@@ -841,13 +881,15 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
   // CPX_X3_P32=0)
   if ((variant == 2 || variant == 3) && cout == 32) variant = 0;  // (224^2: variant 0's kernels)
   static const bool p32 = !getenv("CPX_X3_P32") || atoi(getenv("CPX_X3_P32")) != 0;
+  static const bool p32_touch = !getenv("CPX_X3_P32_TOUCH") || atoi(getenv("CPX_X3_P32_TOUCH")) != 0;
   if (p32 && ks == 3 && cin == 32 && cout == 32 && variant == 0 && !ep.in_up) {
     const int tx = cpx_div_up(W, 32), ty = cpx_div_up(H, 8);
     const long long tiles = (long long)N * tx * ty;
     CPX_REQUIRE(tiles < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv: too many tiles");
     const int grid = (int)std::max(1LL, std::min(tiles, 2LL * ctx->n_cu));
-    hipLaunchKernelGGL(k_conv_x3_p32, dim3(grid), dim3(512), 0, ctx->stream, (const uint4*)in,
-                       (const uint4*)wpk, ep, N, H, W, tx, ty);
+    auto kern = p32_touch ? k_conv_x3_p32<true> : k_conv_x3_p32<false>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N,
+                       H, W, tx, ty);
     CPX_CHECK_LAUNCH("k_conv_x3_p32");
     return CPX_OK;
   }

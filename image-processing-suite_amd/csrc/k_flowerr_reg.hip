@@ -63,6 +63,7 @@ __device__ __forceinline__ int fe_hist_rank(const int* h, int len, long long k) 
 }
 
 constexpr int kFeRegRows = 40;  // register rows per wave (T + Wt: 4 VGPRs per row)
+static_assert(3 * kFeRegRows == kFeRegMaxShort && 2 * 64 == kFeRegMaxLong, "cpx_internal.h class bounds");
 typedef float fe_v2 __attribute__((ext_vector_type(2)));  // v_pk_*_f32 operands
 
 // Row jc (wave-uniform, 0 <= jc < RW; jc == RW or beyond: no-op) of a register array without a

@@ -861,8 +861,8 @@ static_assert(kFeKS <= 32, "unit mask bits");
 
 // the grid's row stride: bw + 2 columns (zero border) rounded up to even, so a column pair
 // (2m, 2m + 1) is one 16-byte LDS word
-__host__ __device__ inline int fe_stride(int bw) { return (bw + 3) & ~1; }
-__host__ __device__ inline bool fe_fits(int bh, int bw, int threads, int units, int cells) {
+__host__ __device__ constexpr int fe_stride(int bw) { return (bw + 3) & ~1; }
+__host__ __device__ constexpr bool fe_fits(int bh, int bw, int threads, int units, int cells) {
   const int nsr = (bh + kFeKS - 1) / kFeKS;
   return (long long)(bh + 2) * fe_stride(bw) <= cells &&
          (long long)((bw + 1) / 2) * nsr <= (long long)threads * units;
@@ -2170,6 +2170,12 @@ constexpr int kFeMidThreads = 512, kFeMidCells = 10176;       // 80 KiB: 2 block
 constexpr int kFeLargeThreads = 1024, kFeLargeCells = 20224;  // 158 KiB: 1 block per CU
 constexpr int kFeCmpThreads = 1024, kFeCmpU = 1, kFeCmpCells = 19968;  // compact rows: 156 KiB + rows
 constexpr int kFeU = 1;                                        // 2-column x 12-row units per thread
+// every register-class mask (k_flowerr_reg.hip: bbox within 128 x 120 either way) is one the
+// largest fp32 screening class holds, so the LDS screening is what skips it (bad set by the
+// register kernel) and no register-class mask falls to k_flow_error_cmp / k_flow_error_big
+static_assert(fe_fits(kFeRegMaxLong, kFeRegMaxShort, kFeLargeThreads / 2, 2 * kFeU, kFeLargeCells) &&
+                  fe_fits(kFeRegMaxShort, kFeRegMaxLong, kFeLargeThreads / 2, 2 * kFeU, kFeLargeCells),
+              "register-class masks must fit the large screening class");
 
 extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx_seg_geom* geom,
                              int H, int W, int niter, double flow_threshold, int min_size,

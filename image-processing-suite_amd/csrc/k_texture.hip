@@ -35,6 +35,30 @@ __device__ unsigned long long g_glcm_prof[8];
   do {                   \
   } while (0)
 #endif
+// The same for k_obj_stage (-DCPX_STAGE_PROF): [0] queue, [1] membership masks, [2] AreaShape
+// sums, [3] channel reads + Intensity sums, [4] reductions, [5] crop pass, [6] objects, [7] groups
+#ifdef CPX_STAGE_PROF
+__device__ unsigned long long g_stage_prof[8];
+#define STAGE_MARK(k, pt)                                   \
+  do {                                                      \
+    if (threadIdx.x == 0) {                                 \
+      const long long t_ = clock64();                       \
+      atomicAdd(&g_stage_prof[k], (unsigned long long)(t_ - *(pt))); \
+      *(pt) = t_;                                           \
+    }                                                       \
+  } while (0)
+#define STAGE_COUNT(k, v) \
+  do {                                                      \
+    if (threadIdx.x == 0) atomicAdd(&g_stage_prof[k], (unsigned long long)(v)); \
+  } while (0)
+#else
+#define STAGE_MARK(k, pt) \
+  do {                   \
+  } while (0)
+#define STAGE_COUNT(k, v) \
+  do {                   \
+  } while (0)
+#endif
 
 constexpr int kTT = 1024;            // GLCM block (16 waves, one block per CU)
 constexpr int kNW = kTT / 64;
@@ -832,6 +856,8 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
   const long long N = (long long)H * W;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int q_fov = fov, q_visited = 0;  // thread 0's queue position (glcm_grab: own FOV first, then
+  long long tprof = clock64();      // (CPX_STAGE_PROF only)
+  (void)tprof;
   while (true) {                    // the next ones, each FOV at most once)
     __syncthreads();  // the previous object's LDS reads are done before s_code / M change
     if (threadIdx.x == 0) s_code = glcm_grab(q_fov, q_visited, B, 1, hdr, obj_next);
@@ -844,6 +870,7 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
     const cpx_object o = objects[(long long)fov * max_label + k];
     if (!shape_fits(o)) continue;  // shape and texture both in the fallback kernels
     const long long off = crop_off[(long long)fov * max_label + k];
+    STAGE_MARK(0, &tprof);
     // the twin rides along when it has the same bbox and both crops are staged (block-uniform)
     int ky = -1;
     long long offy = -1;
@@ -864,6 +891,7 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
       shape_mask<kOT>(tw.labels + (long long)fov * N, H, W, y, M2);
     }
     __syncthreads();
+    STAGE_MARK(1, &tprof);
     shape_sums<kOT>(o, M, Bd, red, redi, raws + ((long long)fov * max_label + k) * kShapeRaw);
     if (TWIN && ky >= 0) {
       const cpx_object y = tw.objects[(long long)fov * max_label + ky];
@@ -871,6 +899,7 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
       shape_sums<kOT>(y, M2, Bd, red, redi, tw.raws + ((long long)fov * max_label + ky) * kShapeRaw);
       if (threadIdx.x == 0) tw.done[(long long)fov * max_label + ky] = 1;
     }
+    STAGE_MARK(2, &tprof);
     if (off < 0) continue;  // texture not staged: fallback kernel (block-uniform)
     const int r0 = o.bbox[0], c0 = o.bbox[1];
     const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
@@ -878,6 +907,8 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
     const int bwp = crop_stride(bw);
     const int ng = bh * bwp / 4;  // 4-pixel groups (bwp % 4 == 0: a group never spans rows)
     const long long cbytes = crop_bytes(bh, bw);
+    STAGE_COUNT(6, 1);
+    STAGE_COUNT(7, ng);
     // group descriptors of the register-held groups, the same for every channel: bbox offset of
     // the group's first pixel (< 2^24: shape_fits bounds bh by 4092, and only images with
     // W <= 4096 stage crops)
@@ -949,6 +980,7 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
             }
         }
       }
+      STAGE_MARK(3, &tprof);
       auto reduce = [&](IntAcc& x, int t, double* fout, float& mmin, float& mmax) {
         // t: which partial slots (0: this set, 1: the twin); channel parity double-buffers them
         x.n = wave_sum(x.n);
@@ -996,6 +1028,7 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
       float mmin, mmax, mmin2 = 0.0f, mmax2 = 0.0f;
       reduce(a, 0, feats + ((long long)fov * max_label + k) * F, mmin, mmax);
       if (TWIN && ky >= 0) reduce(a2, 1, tw.feats + ((long long)fov * max_label + ky) * F, mmin2, mmax2);
+      STAGE_MARK(4, &tprof);
       const float rng = mmax - mmin;
       const bool flat = !(mmax != mmin);
       const float rng2 = mmax2 - mmin2;
@@ -1056,6 +1089,7 @@ __global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ la
           if (TWIN && ky >= 0) *reinterpret_cast<unsigned int*>(dst2 + 4 * g) = word2;
         }
       }
+      STAGE_MARK(5, &tprof);
     }
   }
 }
@@ -1251,6 +1285,18 @@ int cpx_features_pair_fast(cpx_ctx* ctx, const int32_t* labels_dev, const int32_
   if ((rc = launch_texture(ctx, a, w, B, C, max_label, F))) return rc;
   return launch_texture(ctx, t, tw, B, C, max_label, F);
 }
+
+#ifdef CPX_STAGE_PROF
+extern "C" int cpx_debug_stage_prof(unsigned long long* host8, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return CPX_ERR_HIP;
+  if (host8 && hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_stage_prof), 64) != hipSuccess) return CPX_ERR_HIP;
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stage_prof), z, 64) != hipSuccess) return CPX_ERR_HIP;
+  }
+  return CPX_OK;
+}
+#endif
 
 #ifdef CPX_GLCM_PROF
 extern "C" int cpx_debug_glcm_prof(unsigned long long* host8, int reset) {

@@ -2,7 +2,7 @@
 
 Runs the pipeline once on a synthetic batch, then times cpx_features per object set with HIP
 events; with a -DCPX_GLCM_PROF build (tools/build_variants.sh, CPX_LIB=...) also prints the
-k_tex_glcm phase breakdown.  --dump writes FOV 0's Cells labels + corrected planes (fp16).
+k_tex_glcm phase breakdown, with -DCPX_STAGE_PROF the k_obj_stage one.  --dump writes FOV 0's Cells labels + corrected planes (fp16).
 """
 import argparse
 import ctypes as ct
@@ -53,12 +53,20 @@ def main():
         prof.argtypes = [ct.c_void_p, ct.c_int]
     except AttributeError:
         prof = None
+    try:
+        sprof = dev.lib.cpx_debug_stage_prof
+        sprof.argtypes = [ct.c_void_p, ct.c_int]
+    except AttributeError:
+        sprof = None
     buf = (ct.c_ulonglong * 8)()
+    sbuf = (ct.c_ulonglong * 8)()
     for s in OBJECT_SETS:
         dev.objects(pipe.labels[s], cfg.max_objects, cfg.box, pipe.lstats, pipe.objects[s], pipe.hdr[s])
         torch.cuda.synchronize()
         if prof:
             prof(buf, 1)
+        if sprof:
+            sprof(sbuf, 1)
         ts = []
         for _ in range(a.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -75,6 +83,12 @@ def main():
             names = ["reduce", "zero", "count", "scan", "props"]
             line += " | cycles/item " + " ".join(f"{nm}={buf[k] / items:.0f}" for k, nm in enumerate(names))
             line += f" | items {buf[5] // a.reps} px/item {buf[6] / items:.0f} global {buf[7] / items:.2f}"
+        if sprof:
+            sprof(sbuf, 1)
+            objs = max(sbuf[6], 1)
+            names = ["queue", "masks", "shape", "reads", "reduce", "crop"]
+            line += " | k_obj_stage cycles/object " + " ".join(f"{nm}={sbuf[k] / objs:.0f}" for k, nm in enumerate(names))
+            line += f" | objects {sbuf[6] // a.reps} groups/object {sbuf[7] / objs:.0f}"
         print(line)
     if a.dump:
         lab = pipe.labels["Cells"][0].cpu().numpy()
