@@ -94,9 +94,11 @@ __device__ __forceinline__ void split8(const float* v, uint4& hi, uint4& lo, boo
   lo = make_uint4(l0.x, l0.y, l1.x, l1.y);
 }
 
-// CPX_X3_NT (experiment): the epilogue's y / z tile stores as non-temporal stores
+// The epilogue's y / z tile stores are non-temporal (streamed past L2: the next reader is another
+// launch, and the halo lines the tile loop prefetches stay cached; p32 2.22 -> 2.17 ms per call,
+// the deep levels unchanged, `gpurun_out/r05j`); -DCPX_X3_NT=0 for plain stores
 #ifndef CPX_X3_NT
-#define CPX_X3_NT 0
+#define CPX_X3_NT 1
 #endif
 
 struct X3Epi {

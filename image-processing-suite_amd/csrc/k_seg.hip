@@ -407,6 +407,11 @@ struct FollowItem {
   int pad;
 };
 
+// NI items per thread (items i0 + j kT + t, j < NI): NI independent trajectories per lane, all
+// their gathers issued before any is used, so a wave keeps NI times the gathers in flight (the
+// kernel is bound by the latency of each trajectory's dependent gather chain, not by issue).
+// Per item the arithmetic and the order of the next round's list are those of NI = 1.
+template <int NI>
 __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, int step0, int K,
                                                    int from_act, const FollowItem* __restrict__ in,
                                                    const int* __restrict__ in_cnt,
@@ -424,87 +429,118 @@ __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, in
   FollowItem* dst = out + (long long)fov * n;
   const float fLy = (float)(Dy - 1), fLx = (float)(Dx - 1);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  __shared__ int wsum[kT / 64];
+  const unsigned char* Ib = reinterpret_cast<const unsigned char*>(I);
+  __shared__ int wsum[NI][kT / 64];
   __shared__ int sbase;
-  for (int i0 = blockIdx.x * kT; i0 < n_in; i0 += gridDim.x * kT) {  // block-uniform
-    const int i = i0 + threadIdx.x;
-    bool active = i < n_in;
-    int q = 0;
-    float py = 0.0f, px = 0.0f;
-    if (active) {
-      if (from_act) {
-        q = d.act[(long long)fov * n + i];
-        py = (float)(q / Dx);
-        px = (float)(q % Dx);
-      } else {
-        const FollowItem it = src[i];
-        q = it.q;
-        py = it.py;
-        px = it.px;
+  for (int i0 = blockIdx.x * kT * NI; i0 < n_in; i0 += gridDim.x * kT * NI) {  // block-uniform
+    bool active[NI], done[NI];
+    int q[NI];
+    float py[NI], px[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int i = i0 + j * kT + threadIdx.x;
+      active[j] = i < n_in;
+      q[j] = 0;
+      py[j] = 0.0f;
+      px[j] = 0.0f;
+      if (active[j]) {
+        if (from_act) {
+          q[j] = d.act[(long long)fov * n + i];
+          py[j] = (float)(q[j] / Dx);
+          px[j] = (float)(q[j] % Dx);
+        } else {
+          const FollowItem it = src[i];
+          q[j] = it.q;
+          py[j] = it.py;
+          px[j] = it.px;
+        }
       }
+      done[j] = !active[j];
     }
-    bool done = !active;
     for (int s = 0; s < steps; ++s) {
-      if (done) continue;
-      const int yi = (int)py, xi = (int)px;
-      const int y0 = min(Dy - 1, max(0, yi)), x0 = min(Dx - 1, max(0, xi));
-      // 32-bit byte offsets from the FOV's (block-uniform) field base: SGPR-base + VGPR-offset
-      // loads, no 64-bit address arithmetic per step (the field is < 4 GiB per FOV)
-      const unsigned int b00 = 8u * (unsigned int)(y0 * Dx + x0);
-      const unsigned int bdx = x0 + 1 < Dx ? 8u : 0u, bdy = y0 + 1 < Dy ? 8u * (unsigned int)Dx : 0u;
-      const unsigned char* Ib = reinterpret_cast<const unsigned char*>(I);
-      const float2 af = *reinterpret_cast<const float2*>(Ib + b00);
-      const float2 bf = *reinterpret_cast<const float2*>(Ib + (b00 + bdx));
-      const float2 cf = *reinterpret_cast<const float2*>(Ib + (b00 + bdy));
-      const float2 ef = *reinterpret_cast<const float2*>(Ib + (b00 + bdy + bdx));
-      const double2 a = {(double)af.x, (double)af.y}, b = {(double)bf.x, (double)bf.y},
-                    c = {(double)cf.x, (double)cf.y}, e = {(double)ef.x, (double)ef.y};
-      double vy, vx;
-      if (py >= 1.0f && px >= 1.0f) {
-        // yy = frac(py) and 1 - yy are exact in fp32 (multiples of 2^-23 in [0, 1]), so
-        // I * (1 - yy) is exact in fp64 and (I * (1 - yy)) * (1 - xx) == I * w00 with
-        // w00 = (1 - yy) * (1 - xx) exact: the same single rounding, four fewer multiplies
-        const float yf = py - (float)yi, xf = px - (float)xi;
-        const double y1 = (double)yf, x1 = (double)xf, y0d = (double)(1.0f - yf), x0d = (double)(1.0f - xf);
-        const double w00 = y0d * x0d, w01 = y0d * x1, w10 = y1 * x0d, w11 = y1 * x1;
-        vy = a.x * w00 + b.x * w01 + c.x * w10 + e.x * w11;
-        vx = a.y * w00 + b.y * w01 + c.y * w10 + e.y * w11;
-      } else {  // within one pixel of the top / left edge: the literal expression
-        const double yy = (double)py - (double)yi, xx = (double)px - (double)xi;
-        vy = a.x * (1.0 - yy) * (1.0 - xx) + b.x * (1.0 - yy) * xx + c.x * yy * (1.0 - xx) + e.x * yy * xx;
-        vx = a.y * (1.0 - yy) * (1.0 - xx) + b.y * (1.0 - yy) * xx + c.y * yy * (1.0 - xx) + e.y * yy * xx;
+      bool all = true;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) all = all && done[j];
+      if (all) break;
+      // every item's four gathers first (a finished item re-reads its own cell: a valid address,
+      // its update is discarded below)
+      float2 af[NI], bf[NI], cf[NI], ef[NI];
+      int yi[NI], xi[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        yi[j] = (int)py[j];
+        xi[j] = (int)px[j];
+        const int y0 = min(Dy - 1, max(0, yi[j])), x0 = min(Dx - 1, max(0, xi[j]));
+        // 32-bit byte offsets from the FOV's (block-uniform) field base: SGPR-base + VGPR-offset
+        // loads, no 64-bit address arithmetic per step (the field is < 4 GiB per FOV)
+        const unsigned int b00 = 8u * (unsigned int)(y0 * Dx + x0);
+        const unsigned int bdx = x0 + 1 < Dx ? 8u : 0u, bdy = y0 + 1 < Dy ? 8u * (unsigned int)Dx : 0u;
+        af[j] = *reinterpret_cast<const float2*>(Ib + b00);
+        bf[j] = *reinterpret_cast<const float2*>(Ib + (b00 + bdx));
+        cf[j] = *reinterpret_cast<const float2*>(Ib + (b00 + bdy));
+        ef[j] = *reinterpret_cast<const float2*>(Ib + (b00 + bdy + bdx));
       }
-      // clamp to [0, L - 1] in one v_med3_f32 (= fminf(L, fmaxf(0, .)) for the finite values here)
-      const float ny = __builtin_amdgcn_fmed3f(py + (float)vy, 0.0f, fLy);
-      const float nx = __builtin_amdgcn_fmed3f(px + (float)vx, 0.0f, fLx);
-      if (ny == py && nx == px) done = true;  // exact fixed point
-      py = ny;
-      px = nx;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const double2 a = {(double)af[j].x, (double)af[j].y}, b = {(double)bf[j].x, (double)bf[j].y},
+                      c = {(double)cf[j].x, (double)cf[j].y}, e = {(double)ef[j].x, (double)ef[j].y};
+        double vy, vx;
+        if (py[j] >= 1.0f && px[j] >= 1.0f) {
+          // yy = frac(py) and 1 - yy are exact in fp32 (multiples of 2^-23 in [0, 1]), so
+          // I * (1 - yy) is exact in fp64 and (I * (1 - yy)) * (1 - xx) == I * w00 with
+          // w00 = (1 - yy) * (1 - xx) exact: the same single rounding, four fewer multiplies
+          const float yf = py[j] - (float)yi[j], xf = px[j] - (float)xi[j];
+          const double y1 = (double)yf, x1 = (double)xf, y0d = (double)(1.0f - yf), x0d = (double)(1.0f - xf);
+          const double w00 = y0d * x0d, w01 = y0d * x1, w10 = y1 * x0d, w11 = y1 * x1;
+          vy = a.x * w00 + b.x * w01 + c.x * w10 + e.x * w11;
+          vx = a.y * w00 + b.y * w01 + c.y * w10 + e.y * w11;
+        } else {  // within one pixel of the top / left edge: the literal expression
+          const double yy = (double)py[j] - (double)yi[j], xx = (double)px[j] - (double)xi[j];
+          vy = a.x * (1.0 - yy) * (1.0 - xx) + b.x * (1.0 - yy) * xx + c.x * yy * (1.0 - xx) + e.x * yy * xx;
+          vx = a.y * (1.0 - yy) * (1.0 - xx) + b.y * (1.0 - yy) * xx + c.y * yy * (1.0 - xx) + e.y * yy * xx;
+        }
+        // clamp to [0, L - 1] in one v_med3_f32 (= fminf(L, fmaxf(0, .)) for the finite values here)
+        const float ny = __builtin_amdgcn_fmed3f(py[j] + (float)vy, 0.0f, fLy);
+        const float nx = __builtin_amdgcn_fmed3f(px[j] + (float)vx, 0.0f, fLx);
+        if (!done[j]) {
+          if (ny == py[j] && nx == px[j]) done[j] = true;  // exact fixed point
+          py[j] = ny;
+          px[j] = nx;
+        }
+      }
     }
     const bool last = step0 + steps >= niter;
-    if (active && (done || last)) P[q] = make_float2(py, px);
-    const bool carry = active && !done && !last;
-    const unsigned long long bal = __ballot(carry);
-    if (lane == 0) wsum[wid] = __popcll(bal);
+    bool carry[NI];
+    unsigned long long bal[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      if (active[j] && (done[j] || last)) P[q[j]] = make_float2(py[j], px[j]);
+      carry[j] = active[j] && !done[j] && !last;
+      bal[j] = __ballot(carry[j]);
+      if (lane == 0) wsum[j][wid] = __popcll(bal[j]);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-      int s = 0;
-      for (int w = 0; w < kT / 64; ++w) {
-        const int c = wsum[w];
-        wsum[w] = s;
-        s += c;
-      }
-      sbase = s ? atomicAdd(&out_cnt[fov], s) : 0;
+      int t = 0;
+      for (int j = 0; j < NI; ++j)
+        for (int w = 0; w < kT / 64; ++w) {
+          const int c = wsum[j][w];
+          wsum[j][w] = t;
+          t += c;
+        }
+      sbase = t ? atomicAdd(&out_cnt[fov], t) : 0;
     }
     __syncthreads();
-    if (carry) {
-      FollowItem it;
-      it.q = q;
-      it.py = py;
-      it.px = px;
-      it.pad = 0;
-      dst[sbase + wsum[wid] + __popcll(bal & ((1ull << lane) - 1ull))] = it;
-    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+      if (carry[j]) {
+        FollowItem it;
+        it.q = q[j];
+        it.py = py[j];
+        it.px = px[j];
+        it.pad = 0;
+        dst[sbase + wsum[j][wid] + __popcll(bal[j] & ((1ull << lane) - 1ull))] = it;
+      }
     __syncthreads();
   }
 }
@@ -2263,15 +2299,26 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
     hipLaunchKernelGGL(k_dyn_prep<false>, gprep, dim3(kT), 0, ctx->stream, yf_dev, Ly, Lx, Dy, Dx,
                        tabs.uy, tabs.ux, d);
   const int fblk = std::max(1, std::min(cpx_div_up(n, kT), (16 * ctx->n_cu + B - 1) / B));
+  // trajectories per thread of k_dyn_follow (CPX_FOLLOW_NI: 1, 2 or 4)
+  static const int follow_ni = getenv("CPX_FOLLOW_NI") ? atoi(getenv("CPX_FOLLOW_NI")) : 1;
   {
     int step = 0, r = 0;
     do {  // at least one round: with niter = 0 it only records the start positions
       const int K = step < sw ? k0 : k1;
       const FollowItem* in = (const FollowItem*)(r & 1 ? d.fitems1 : d.fitems0);
       FollowItem* out = (FollowItem*)(r & 1 ? d.fitems0 : d.fitems1);
-      hipLaunchKernelGGL(k_dyn_follow, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step,
-                         K, r == 0 ? 1 : 0, in, (const int*)(d.fcnt + (size_t)B * r), out,
-                         d.fcnt + (size_t)B * (r + 1), d);
+      if (follow_ni == 4)
+        hipLaunchKernelGGL(k_dyn_follow<4>, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step,
+                           K, r == 0 ? 1 : 0, in, (const int*)(d.fcnt + (size_t)B * r), out,
+                           d.fcnt + (size_t)B * (r + 1), d);
+      else if (follow_ni == 2)
+        hipLaunchKernelGGL(k_dyn_follow<2>, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step,
+                           K, r == 0 ? 1 : 0, in, (const int*)(d.fcnt + (size_t)B * r), out,
+                           d.fcnt + (size_t)B * (r + 1), d);
+      else
+        hipLaunchKernelGGL(k_dyn_follow<1>, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step,
+                           K, r == 0 ? 1 : 0, in, (const int*)(d.fcnt + (size_t)B * r), out,
+                           d.fcnt + (size_t)B * (r + 1), d);
       step += K;
       ++r;
     } while (step < niter);

@@ -656,32 +656,63 @@ __device__ void shape_sums(const cpx_object& o, const unsigned int* M, unsigned 
     Bd[w] = x & ~(up & dn & lf & rt);
   }
   __syncthreads();
+  // per word, bit-parallel (every sum is an exact integer, so the order does not matter): the
+  // column sums from popcounts of the word against the bit-index masks (sum b = sum_k 2^k
+  // popc(x & m_k), sum b^2 from the pairwise products), and the Benkrid-Crookes codes
+  // 1 + 2 a + 10 d (a / d = border 4- / diagonal neighbours) from bit-sliced neighbour counts:
+  // n1 = codes 5, 7, 15, 17, 25, 27 (a in {2, 3}, d <= 2), n2 = 21, 33 ((a, d) = (0, 2) or
+  // (1, 3)), n3 = 13, 23 (a = 1, d in {1, 2})
+  constexpr unsigned int kBm[5] = {0xAAAAAAAAu, 0xCCCCCCCCu, 0xF0F0F0F0u, 0xFF00FF00u, 0xFFFF0000u};
   long long n = 0, sr = 0, sc = 0, srr = 0, scc = 0, src = 0;
   int n1 = 0, n2 = 0, n3 = 0;
   for (int w = threadIdx.x; w < rows * wpr; w += NT) {
     const int r = w / wpr, cw = w - r * wpr;
-    unsigned int x = M[w];
+    const unsigned int x = M[w];
+    if (x) {
+      const long long p = __popc(x);
+      int pk[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) pk[k] = __popc(x & kBm[k]);
+      long long s1 = 0, s2 = 0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        s1 += (long long)pk[k] << k;
+        s2 += (long long)pk[k] << (2 * k);
+#pragma unroll
+        for (int j = k + 1; j < 5; ++j) s2 += (long long)__popc(x & kBm[k] & kBm[j]) << (k + j + 1);
+      }
+      const long long rr = r - 2, base = (long long)cw * 32 - 2;  // bbox-local row, column of bit 0
+      const long long csum = base * p + s1;
+      n += p;
+      sr += rr * p;
+      srr += rr * rr * p;
+      sc += csum;
+      scc += base * base * p + 2 * base * s1 + s2;
+      src += rr * csum;
+    }
     const unsigned int bx = Bd[w];
-    while (x) {
-      const int b = __ffs(x) - 1;
-      x &= x - 1;
-      const int c = cw * 32 + b;
-      const long long rr = r - 2, cc = c - 2;  // bbox-local coordinates
-      n += 1;
-      sr += rr;
-      sc += cc;
-      srr += rr * rr;
-      scc += cc * cc;
-      src += rr * cc;
-      if (!((bx >> b) & 1u)) continue;
-      auto bit = [&](int rr2, int cc2) -> int {
-        return (int)((getw(Bd, wpr, rows, rr2, cc2 >> 5) >> (cc2 & 31)) & 1u);
+    if (bx) {
+      auto lf = [&](int rw, unsigned int v) { return (v << 1) | (getw(Bd, wpr, rows, rw, cw - 1) >> 31); };
+      auto rt = [&](int rw, unsigned int v) { return (v >> 1) | (getw(Bd, wpr, rows, rw, cw + 1) << 31); };
+      const unsigned int U = getw(Bd, wpr, rows, r - 1, cw), D = getw(Bd, wpr, rows, r + 1, cw);
+      // bit-sliced a = U + D + L + R and d = UL + UR + DL + DR (0..4 each: bits a2 a1 a0)
+      auto count4 = [](unsigned int A, unsigned int B, unsigned int C, unsigned int E, unsigned int& c2,
+                       unsigned int& c1, unsigned int& c0) {
+        const unsigned int s0 = A ^ B, k0 = A & B, s1_ = C ^ E, k1 = C & E;
+        const unsigned int cy = s0 & s1_;
+        c0 = s0 ^ s1_;
+        c1 = k0 ^ k1 ^ cy;
+        c2 = (k0 & k1) | (cy & (k0 ^ k1));
       };
-      const int code = 1 + 2 * (bit(r - 1, c) + bit(r + 1, c) + bit(r, c - 1) + bit(r, c + 1)) +
-                       10 * (bit(r - 1, c - 1) + bit(r - 1, c + 1) + bit(r + 1, c - 1) + bit(r + 1, c + 1));
-      if (code == 5 || code == 7 || code == 15 || code == 17 || code == 25 || code == 27) n1 += 1;
-      else if (code == 21 || code == 33) n2 += 1;
-      else if (code == 13 || code == 23) n3 += 1;
+      unsigned int a2, a1, a0, d2, d1, d0;
+      count4(U, D, lf(r, bx), rt(r, bx), a2, a1, a0);
+      count4(lf(r - 1, U), rt(r - 1, U), lf(r + 1, D), rt(r + 1, D), d2, d1, d0);
+      const unsigned int aeq0 = ~a2 & ~a1 & ~a0, aeq1 = ~a2 & ~a1 & a0, a23 = ~a2 & a1;
+      const unsigned int deq1 = ~d2 & ~d1 & d0, deq2 = ~d2 & d1 & ~d0, deq3 = ~d2 & d1 & d0;
+      const unsigned int dle2 = ~d2 & ~(d1 & d0);
+      n1 += __popc(bx & a23 & dle2);
+      n2 += __popc(bx & ((aeq0 & deq2) | (aeq1 & deq3)));
+      n3 += __popc(bx & aeq1 & (deq1 | deq2));
     }
   }
   n = wave_sum(n); sr = wave_sum(sr); sc = wave_sum(sc);
@@ -758,7 +789,20 @@ __global__ __launch_bounds__(256) void k_shape_props(int max_label, int F,
 // quantised into the object's 8-bit crop slot for k_tex_glcm.  The first kOT * kOG 4-pixel
 // groups stay in registers between the two passes; the rest of a large bbox is read twice, with
 // the block's working set (one channel of one bbox, two blocks per CU) L2-resident in between.
-constexpr int kOT = 512;
+// block size and waves per SIMD of k_obj_stage (the object-per-block staging is latency-bound:
+// objects in flight per CU = blocks per CU); development builds override them
+#ifndef CPX_STAGE_NT
+#define CPX_STAGE_NT 512
+#endif
+#ifndef CPX_STAGE_WPE0
+#define CPX_STAGE_WPE0 4
+#endif
+#ifndef CPX_STAGE_WPE1
+#define CPX_STAGE_WPE1 4
+#endif
+constexpr int kOT = CPX_STAGE_NT;
+constexpr int stage_wpe(bool twin) { return twin ? CPX_STAGE_WPE1 : CPX_STAGE_WPE0; }
+constexpr int stage_blocks_per_cu(bool twin) { return stage_wpe(twin) * 4 / (kOT / 64); }
 constexpr int kOG = 1;
 constexpr int kOR = 4;  // groups per iteration beyond the register-held ones
 
@@ -830,7 +874,7 @@ struct StageTwin {
 };
 
 template <bool TWIN>
-__global__ __launch_bounds__(kOT, 4) void k_obj_stage(const int* __restrict__ labels,
+__global__ __launch_bounds__(kOT) __attribute__((amdgpu_waves_per_eu(stage_wpe(TWIN)))) void k_obj_stage(const int* __restrict__ labels,
                                                   const float* __restrict__ corr, int C, int H,
                                                   int W, int max_label, int F,
                                                   const cpx_object* __restrict__ objects,
@@ -1198,7 +1242,8 @@ int launch_stage(cpx_ctx* ctx, const SetArgs& a, FeatWs& w, const float* corr, i
                  int max_label, int F, const int* skip, const StageTwin* tw) {
   int rc = obj_stage_attr();
   if (rc) return rc;
-  const int per_fov_o = std::max(1, std::min(max_label, (2 * ctx->n_cu + B - 1) / B));  // resident
+  const int bpc = stage_blocks_per_cu(tw != nullptr);
+  const int per_fov_o = std::max(1, std::min(max_label, (bpc * ctx->n_cu + B - 1) / B));  // resident
   if (tw)
     hipLaunchKernelGGL(k_obj_stage<true>, dim3(per_fov_o, B), dim3(kOT), obj_stage_lds(true), ctx->stream,
                        (const int*)a.labels, corr, C, H, W, max_label, F, a.objects, a.hdr,
