@@ -411,7 +411,10 @@ struct FollowItem {
 // their gathers issued before any is used, so a wave keeps NI times the gathers in flight (the
 // kernel is bound by the latency of each trajectory's dependent gather chain, not by issue).
 // Per item the arithmetic and the order of the next round's list are those of NI = 1.
-template <int NI>
+// V4: the two horizontal neighbours of a row in one 16-byte load (two gathers per step instead
+// of four; the gathers' address processing, not their bytes, bounds the kernel): (x0, x0 + 1),
+// or at the right edge (x0 - 1, x0) with the upper half taken for both.
+template <int NI, bool V4>
 __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, int step0, int K,
                                                    int from_act, const FollowItem* __restrict__ in,
                                                    const int* __restrict__ in_cnt,
@@ -430,6 +433,10 @@ __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, in
   const float fLy = (float)(Dy - 1), fLx = (float)(Dx - 1);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned char* Ib = reinterpret_cast<const unsigned char*>(I);
+  // V4: the FOV's field as a buffer resource (8 n < 2^31 bytes, checked by the host)
+  const __amdgpu_buffer_rsrc_t rsI =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(I), (short)0, (int)(8 * n), 0x00020000);
+  (void)rsI;
   __shared__ int wsum[NI][kT / 64];
   __shared__ int sbase;
   for (int i0 = blockIdx.x * kT * NI; i0 < n_in; i0 += gridDim.x * kT * NI) {  // block-uniform
@@ -475,10 +482,22 @@ __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, in
         // loads, no 64-bit address arithmetic per step (the field is < 4 GiB per FOV)
         const unsigned int b00 = 8u * (unsigned int)(y0 * Dx + x0);
         const unsigned int bdx = x0 + 1 < Dx ? 8u : 0u, bdy = y0 + 1 < Dy ? 8u * (unsigned int)Dx : 0u;
-        af[j] = *reinterpret_cast<const float2*>(Ib + b00);
-        bf[j] = *reinterpret_cast<const float2*>(Ib + (b00 + bdx));
-        cf[j] = *reinterpret_cast<const float2*>(Ib + (b00 + bdy));
-        ef[j] = *reinterpret_cast<const float2*>(Ib + (b00 + bdy + bdx));
+        if constexpr (V4) {
+          // raw buffer loads: one 16-byte access each (a plain float4 load of an 8-byte aligned
+          // address is split into two 8-byte loads by the compiler)
+          const unsigned int o = bdx ? b00 : b00 - 8u;  // x0 = Dx - 1 >= 1 when bdx == 0
+          const float4 r0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsI, o, 0, 0));
+          const float4 r1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsI, o + bdy, 0, 0));
+          af[j] = bdx ? make_float2(r0.x, r0.y) : make_float2(r0.z, r0.w);
+          bf[j] = make_float2(r0.z, r0.w);
+          cf[j] = bdx ? make_float2(r1.x, r1.y) : make_float2(r1.z, r1.w);
+          ef[j] = make_float2(r1.z, r1.w);
+        } else {
+          af[j] = *reinterpret_cast<const float2*>(Ib + b00);
+          bf[j] = *reinterpret_cast<const float2*>(Ib + (b00 + bdx));
+          cf[j] = *reinterpret_cast<const float2*>(Ib + (b00 + bdy));
+          ef[j] = *reinterpret_cast<const float2*>(Ib + (b00 + bdy + bdx));
+        }
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
@@ -2299,26 +2318,25 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
     hipLaunchKernelGGL(k_dyn_prep<false>, gprep, dim3(kT), 0, ctx->stream, yf_dev, Ly, Lx, Dy, Dx,
                        tabs.uy, tabs.ux, d);
   const int fblk = std::max(1, std::min(cpx_div_up(n, kT), (16 * ctx->n_cu + B - 1) / B));
-  // trajectories per thread of k_dyn_follow (CPX_FOLLOW_NI: 1, 2 or 4)
-  static const int follow_ni = getenv("CPX_FOLLOW_NI") ? atoi(getenv("CPX_FOLLOW_NI")) : 1;
+  // k_dyn_follow: trajectories per thread (CPX_FOLLOW_NI 1, 2 or 4) and paired 16-byte gathers
+  // (CPX_FOLLOW_V4); per 48-FOV step (`gpurun_out/r05l`, `r05m`): 1 / scalar 12.11 ms, 2 / scalar
+  // 11.83, 4 / scalar 12.54, 1 / paired 11.46, 2 / paired 11.02 (the default); every setting passes
+  // the segmentation parity tests
+  static const int follow_ni = getenv("CPX_FOLLOW_NI") ? atoi(getenv("CPX_FOLLOW_NI")) : 2;
+  static const bool follow_v4 = !getenv("CPX_FOLLOW_V4") || atoi(getenv("CPX_FOLLOW_V4")) != 0;
   {
     int step = 0, r = 0;
     do {  // at least one round: with niter = 0 it only records the start positions
       const int K = step < sw ? k0 : k1;
       const FollowItem* in = (const FollowItem*)(r & 1 ? d.fitems1 : d.fitems0);
       FollowItem* out = (FollowItem*)(r & 1 ? d.fitems0 : d.fitems1);
-      if (follow_ni == 4)
-        hipLaunchKernelGGL(k_dyn_follow<4>, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step,
-                           K, r == 0 ? 1 : 0, in, (const int*)(d.fcnt + (size_t)B * r), out,
-                           d.fcnt + (size_t)B * (r + 1), d);
-      else if (follow_ni == 2)
-        hipLaunchKernelGGL(k_dyn_follow<2>, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step,
-                           K, r == 0 ? 1 : 0, in, (const int*)(d.fcnt + (size_t)B * r), out,
-                           d.fcnt + (size_t)B * (r + 1), d);
-      else
-        hipLaunchKernelGGL(k_dyn_follow<1>, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step,
-                           K, r == 0 ? 1 : 0, in, (const int*)(d.fcnt + (size_t)B * r), out,
-                           d.fcnt + (size_t)B * (r + 1), d);
+      // (the right-edge form reads x0 - 1; the buffer resource holds 8 n < 2^31 bytes)
+      const bool v4 = follow_v4 && Dx >= 2 && 8LL * n < (1LL << 31);
+      auto kern = follow_ni == 4 ? (v4 ? k_dyn_follow<4, true> : k_dyn_follow<4, false>)
+                : follow_ni == 2 ? (v4 ? k_dyn_follow<2, true> : k_dyn_follow<2, false>)
+                                 : (v4 ? k_dyn_follow<1, true> : k_dyn_follow<1, false>);
+      hipLaunchKernelGGL(kern, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step, K, r == 0 ? 1 : 0,
+                         in, (const int*)(d.fcnt + (size_t)B * r), out, d.fcnt + (size_t)B * (r + 1), d);
       step += K;
       ++r;
     } while (step < niter);
