@@ -838,15 +838,14 @@ __device__ __forceinline__ float ldg_b(const float* base, unsigned int byte_off)
   return *reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(base) + byte_off);
 }
 
-// CPX_STAGE_V4: a 4-pixel group as one 16-byte raw buffer load (dword-aligned; the lanes past a
-// row's bbox read pixels they then ignore, past the plane the buffer returns 0) instead of four
-// 4-byte loads — a quarter of the vector-memory instructions
-#ifndef CPX_STAGE_V4
-#define CPX_STAGE_V4 0
-#endif
+// A 4-pixel group as one 16-byte raw buffer load (dword-aligned; the lanes past a row's bbox read
+// pixels they then ignore, past the plane the buffer returns 0) instead of four 4-byte loads: a
+// quarter of the vector-memory instructions (k_obj_stage 5.52 -> 5.28 ms per step,
+// `gpurun_out/r05n`).  v4 is false for planes of 2^29 or more pixels (the buffer's byte range is
+// an int): four 4-byte loads then.
 __device__ __forceinline__ void ld_group(float (&dst)[4], const float* img, __amdgpu_buffer_rsrc_t rs,
-                                         unsigned int img_off, unsigned int o0, unsigned int nv) {
-  if constexpr (CPX_STAGE_V4) {
+                                         unsigned int img_off, unsigned int o0, unsigned int nv, bool v4) {
+  if (v4) {
     const float4 t = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, 4u * (img_off + o0), 0, 0));
     dst[0] = t.x;
     dst[1] = t.y;
@@ -992,8 +991,9 @@ __global__ __launch_bounds__(kOT) __attribute__((amdgpu_waves_per_eu(stage_wpe(T
       const float* plane = corr + ((long long)fov * C + ch) * N;
       const float* img = plane + (long long)r0 * W + c0;
       const unsigned int img_off = (unsigned int)(r0 * W + c0);
+      const bool v4 = N < (1LL << 29);  // block-uniform
       const __amdgpu_buffer_rsrc_t rsp =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(plane), (short)0, (int)(4 * N), 0x00020000);
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(plane), (short)0, v4 ? (int)(4 * N) : 0, 0x00020000);
       IntAcc a{0, 0.0, 0.0, INFINITY, -INFINITY, INFINITY, -INFINITY};
       IntAcc a2{0, 0.0, 0.0, INFINITY, -INFINITY, INFINITY, -INFINITY};
       float v[kOG][4];
@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(kOT) __attribute__((amdgpu_waves_per_eu(stage_wpe(T
 #pragma unroll
       for (int i = 0; i < kOG; ++i) {
         const unsigned int o0 = gd[i] & 0xffffffu, nv = gd[i] >> 28;
-        ld_group(v[i], img, rsp, img_off, o0, nv);
+        ld_group(v[i], img, rsp, img_off, o0, nv, v4);
       }
 #pragma unroll
       for (int i = 0; i < kOG; ++i) {
@@ -1027,7 +1027,7 @@ __global__ __launch_bounds__(kOT) __attribute__((amdgpu_waves_per_eu(stage_wpe(T
         for (int r = 0; r < kOR; ++r) {
           d[r] = group_desc(M, wpr, bw, bwp, W, min(g0 + r * kOT, ng - 1));
           const unsigned int o0 = d[r] & 0xffffffu, nv = d[r] >> 28;
-          ld_group(w4[r], img, rsp, img_off, o0, nv);
+          ld_group(w4[r], img, rsp, img_off, o0, nv, v4);
         }
 #pragma unroll
         for (int r = 0; r < kOR; ++r) {
@@ -1128,7 +1128,7 @@ __global__ __launch_bounds__(kOT) __attribute__((amdgpu_waves_per_eu(stage_wpe(T
         for (int r = 0; r < kOR; ++r) {
           d[r] = group_desc(M, wpr, bw, bwp, W, min(g0 + r * kOT, ng - 1));
           const unsigned int o0 = d[r] & 0xffffffu, nv = d[r] >> 28;
-          ld_group(w4[r], img, rsp, img_off, o0, nv);
+          ld_group(w4[r], img, rsp, img_off, o0, nv, v4);
         }
 #pragma unroll
         for (int r = 0; r < kOR; ++r) {
