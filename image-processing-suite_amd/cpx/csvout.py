@@ -28,6 +28,97 @@ INTENSITY_NAMES = ["IntegratedIntensity", "MeanIntensity", "StdIntensity", "MinI
 TEXTURE_NAMES = ["Contrast", "Dissimilarity", "Homogeneity", "AngularSecondMoment", "Energy", "Correlation"]
 TEXTURE_SCALE = 3
 OBJECT_TABLES = ("Nuclei", "Cells", "Cytoplasm")
+CSV_CHUNK_ROWS = 4096   # rows per native formatting call
+CSV_THREADS = 16        # formatting threads (the GPU box's CPU share per GPU)
+
+
+def _format_rows(lib, r0, r1, k, ptrs, types, strides) -> bytes:
+    import ctypes as ct
+    cap = (r1 - r0) * 33 * k
+    buf = ct.create_string_buffer(max(cap, 1))
+    m = lib.cpx_csv_format(r0, r1, k, ptrs, types, strides, buf, cap)
+    if m < 0:
+        raise RuntimeError("cpx_csv_format failed")
+    return buf.raw[:m]
+
+
+def format_object_rows(image_number: int, labels, feats) -> bytes:
+    """The CSV rows (ImageNumber, ObjectNumber, Number_Object_Number, feature columns) of one
+    FOV's objects, rows in label order: the bytes DataFrame.to_csv writes for them."""
+    import ctypes as ct
+
+    from . import _lib
+    lib = _lib.load()
+    labels = np.asarray(labels, dtype=np.int64)
+    order = np.argsort(labels, kind="stable")
+    lab = np.ascontiguousarray(labels[order])
+    f = np.ascontiguousarray(np.asarray(feats, dtype=np.float64)[order])
+    img = np.full(len(lab), int(image_number), np.int64)
+    n, F = f.shape
+    if n == 0:
+        return b""
+    k = 3 + F
+    ptrs = (ct.c_void_p * k)(img.ctypes.data, lab.ctypes.data, lab.ctypes.data,
+                             *[f.ctypes.data + 8 * j for j in range(F)])
+    types = (ct.c_int * k)(0, 0, 0, *([1] * F))
+    strides = (ct.c_int64 * k)(1, 1, 1, *([F] * F))
+    return _format_rows(lib, 0, n, k, ptrs, types, strides)
+
+
+def write_numeric_csv(path: str, names, columns, threads: int = CSV_THREADS):
+    """Write a table whose columns are int64 / float64 arrays as the bytes
+    pandas.DataFrame(...).to_csv(path, index=False) writes (header, then per row the ints in
+    decimal and the floats as Python repr, NaN as an empty field), formatted by libcpx's
+    cpx_csv_format on `threads` threads over row chunks (the call releases the GIL) and written
+    in order.  columns: 1-D arrays or column views of a 2-D array (any element stride)."""
+    import concurrent.futures
+    import ctypes as ct
+
+    from . import _lib
+    lib = _lib.load()
+    cols = []
+    for c in columns:
+        a = np.asarray(c)
+        if a.dtype.kind in "iub":
+            a = np.ascontiguousarray(a, dtype=np.int64) if a.dtype != np.int64 else a
+        elif a.dtype != np.float64:
+            a = a.astype(np.float64)
+        if a.ndim != 1:
+            raise ValueError("write_numeric_csv: columns must be 1-D")
+        cols.append(a)
+    n = len(cols[0]) if cols else 0
+    if any(len(a) != n for a in cols) or len(names) != len(cols):
+        raise ValueError("write_numeric_csv: ragged columns")
+    k = len(cols)
+    ptrs = (ct.c_void_p * k)(*[a.ctypes.data for a in cols])
+    types = (ct.c_int * k)(*[0 if a.dtype == np.int64 else 1 for a in cols])
+    strides = (ct.c_int64 * k)(*[a.strides[0] // a.itemsize for a in cols])
+    if any(a.strides[0] % a.itemsize for a in cols):
+        raise ValueError("write_numeric_csv: unaligned column stride")
+
+    def fmt(r0):
+        return _format_rows(lib, r0, min(n, r0 + CSV_CHUNK_ROWS), k, ptrs, types, strides)
+
+    with open(path, "wb") as f:
+        f.write((",".join(names) + "\n").encode())
+        starts = range(0, n, CSV_CHUNK_ROWS)
+        if threads > 1 and n > CSV_CHUNK_ROWS:
+            with concurrent.futures.ThreadPoolExecutor(max_workers=threads) as pool:
+                for chunk in pool.map(fmt, starts):
+                    f.write(chunk)
+        else:
+            for r0 in starts:
+                f.write(fmt(r0))
+
+
+def write_frame_csv(df, path: str):
+    """DataFrame.to_csv(path, index=False), natively formatted when every column is int64 or
+    float64 (the object tables), else through pandas (Image.csv with its Metadata strings)."""
+    if len(df.columns) and all(str(t) in ("int64", "float64") for t in df.dtypes) and \
+            all(isinstance(c, str) and not any(ch in c for ch in ',"\n\r') for c in df.columns):
+        write_numeric_csv(path, list(df.columns), [df[c].to_numpy() for c in df.columns])
+    else:
+        df.to_csv(path, index=False)
 
 
 def feature_names(channels):
@@ -44,11 +135,18 @@ def feature_names(channels):
 class PlateTables:
     """Accumulates per-FOV results of one plate/time and writes the four CSVs."""
 
-    def __init__(self, channels):
+    def __init__(self, channels, eager_csv: bool = False):
         self.channels = list(channels)
         self.cols = feature_names(self.channels)
         self.images = []                       # dicts
         self.objects = {t: [] for t in OBJECT_TABLES}  # (ImageNumber, labels[n], feats[n, F])
+        # eager_csv: each FOV's object rows are formatted on a thread pool as they are added
+        # (overlapping the GPU work of the next batches); write_objects then only writes them
+        self._pool = None
+        self._rows = {t: [] for t in OBJECT_TABLES}  # (ImageNumber, future of bytes)
+        if eager_csv:
+            import concurrent.futures
+            self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=CSV_THREADS)
 
     def add_image(self, image_number: int, metadata: dict, qc_slope, qc_pct, counts: dict):
         row = {"ImageNumber": int(image_number)}
@@ -67,12 +165,21 @@ class PlateTables:
             raise ValueError(f"{table}: feature block {feats.shape} for {len(labels)} objects x "
                              f"{len(self.cols)} columns")
         self.objects[table].append((int(image_number), labels, feats))
+        if self._pool is not None:
+            self._rows[table].append((int(image_number),
+                                      self._pool.submit(format_object_rows, int(image_number), labels, feats)))
 
-    def frames(self):
+    def close(self):
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+            self._pool = None
+
+    def frames(self, objects: bool = True):
+        """DataFrames of the tables (Image; with objects=True also the three object tables)."""
         import pandas as pd
         out = {"Image": pd.DataFrame(self.images).sort_values("ImageNumber", kind="stable")
                .reset_index(drop=True) if self.images else pd.DataFrame(columns=["ImageNumber"])}
-        for t in OBJECT_TABLES:
+        for t in (OBJECT_TABLES if objects else ()):
             blocks = []
             for img, labels, feats in self.objects[t]:
                 df = pd.DataFrame(feats, columns=self.cols)
@@ -88,9 +195,39 @@ class PlateTables:
             out[t] = df
         return out
 
+    def write_objects(self, d: str, table: str):
+        """<table>.csv straight from the accumulated blocks (rows by ImageNumber, then
+        ObjectNumber; the same bytes as frames()[table].to_csv(index=False))."""
+        blocks = sorted(self.objects[table], key=lambda b: b[0])  # stable: FOVs in ImageNumber order
+        names = ["ImageNumber", "ObjectNumber", "Number_Object_Number"] + self.cols
+        if self._rows[table] and len(self._rows[table]) == len(self.objects[table]):
+            with open(os.path.join(d, f"{table}.csv"), "wb") as f:
+                f.write((",".join(names) + "\n").encode())
+                for _, fut in sorted(self._rows[table], key=lambda b: b[0]):
+                    f.write(fut.result())
+            return
+        if not blocks:
+            self.frames_empty(table).to_csv(os.path.join(d, f"{table}.csv"), index=False)
+            return
+        labels = [b[1] for b in blocks]
+        order = [np.argsort(lb, kind="stable") for lb in labels]
+        lab = np.concatenate([lb[o] for lb, o in zip(labels, order)]).astype(np.int64)
+        img = np.concatenate([np.full(len(lb), b[0], np.int64) for lb, b in zip(labels, blocks)])
+        feats = np.concatenate([b[2][o] for b, o in zip(blocks, order)]) if lab.size else \
+            np.zeros((0, len(self.cols)), np.float64)
+        write_numeric_csv(os.path.join(d, f"{table}.csv"), names,
+                          [img, lab, lab] + [feats[:, j] for j in range(feats.shape[1])])
+
+    def frames_empty(self, table: str):
+        import pandas as pd
+        return pd.DataFrame(columns=["ImageNumber", "ObjectNumber", "Number_Object_Number"] + self.cols)
+
     def write(self, base: str, plate: str, time) -> str:
         d = os.path.join(base, str(plate), str(time))
         os.makedirs(d, exist_ok=True)
-        for name, df in self.frames().items():
+        frames = self.frames(objects=False)
+        for name, df in frames.items():
             df.to_csv(os.path.join(d, f"{name}.csv"), index=False)
+        for t in OBJECT_TABLES:
+            self.write_objects(d, t)
         return d

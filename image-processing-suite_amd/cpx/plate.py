@@ -33,6 +33,7 @@ import logging
 import os
 import shutil
 import time
+import time as _time  # run() binds `time` to the job's timepoint
 
 import numpy as np
 
@@ -166,6 +167,8 @@ def merge_parts(d, world=None):
     """Concatenate the ranks' parts of job directory d into the final CSVs (rows sorted by
     ImageNumber, then ObjectNumber) and remove the parts."""
     import pandas as pd
+
+    from .csvout import write_frame_csv
     parts = sorted(glob.glob(os.path.join(d, PARTS, "r*of*")))
     if world is not None and len(parts) != world:
         raise RuntimeError(f"{d}: {len(parts)} parts, expected {world}")
@@ -178,7 +181,7 @@ def merge_parts(d, world=None):
         keys = [k for k in ("ImageNumber", "ObjectNumber") if k in df.columns]
         if keys and len(df):
             df = df.sort_values(keys, kind="stable").reset_index(drop=True)
-        df.to_csv(os.path.join(d, f"{name}.csv"), index=False)
+        write_frame_csv(df, os.path.join(d, f"{name}.csv"))
     shutil.rmtree(os.path.join(d, PARTS), ignore_errors=True)
     return d
 
@@ -237,21 +240,30 @@ def run(argv=None):
     dirs = []
     for ji, load_data in enumerate(a.load_data):
         table, plate, time = _job_meta(a, load_data)
-        out = PlateTables(chans)
+        out = PlateTables(chans, eager_csv=a.world == 1)  # one rank: rows formatted as FOVs finish
         status = []  # per site: the reference's results_dict entry (Cellpose_GPU_s3fs.py:123-125,219-223)
         nsites = _run_sites(a, table, batch_source(table, a, ji), chans, state, out, status)
         if nsites:
             LAST_TIMING.append({"job": os.path.basename(load_data), "fovs": nsites, **state["timing"]})
         d = job_dir(a.out, plate, time)
-        frames = out.frames()
-        frames["site_status"] = pd.DataFrame(status, columns=["ImageNumber", "status", "n_cells"]) \
+        site_status = pd.DataFrame(status, columns=["ImageNumber", "status", "n_cells"]) \
             .sort_values("ImageNumber", kind="stable").reset_index(drop=True)
+        t_csv = _time.perf_counter()
         if a.world > 1:
+            frames = out.frames()
+            frames["site_status"] = site_status
             write_part(d, a.rank, a.world, frames)
         else:
             os.makedirs(d, exist_ok=True)
+            frames = out.frames(objects=False)
+            frames["site_status"] = site_status
             for name, df in frames.items():
                 df.to_csv(os.path.join(d, f"{name}.csv"), index=False)
+            for t in OBJECT_SETS:  # the object tables, natively formatted (csvout.format_object_rows)
+                out.write_objects(d, t)
+        out.close()
+        if LAST_TIMING and nsites:
+            LAST_TIMING[-1]["tables_write_s"] = round(_time.perf_counter() - t_csv, 3)
         log.info("rank %d/%d: %d sites of %s/%s -> %s", a.rank, a.world, nsites, plate, time, d)
         dirs.append(d)
     if a.world > 1:

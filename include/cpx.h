@@ -570,6 +570,16 @@ int cpx_fov_features(cpx_ctx* ctx, const int32_t* labels_dev, int max_objects, d
                      int* n_out);
 int cpx_fov_wait(cpx_ctx* ctx);
 
+/* ---- host: CSV rows of the measurement tables (Pycyto_pertime.py:46-49 reads them) ------- *
+ * Rows [row0, row1) of a table of n_cols columns, column c at cols[c] with element stride
+ * strides[c] (in elements), types[c] 0 = int64 (decimal) or 1 = float64 (Python repr, the text
+ * pandas.DataFrame.to_csv writes; NaN -> empty field): comma-separated, '\n'-terminated, into
+ * out (cap bytes, at least 33 * n_cols per row).  Returns the bytes written, or -1 (bad
+ * arguments / cap too small).  Pure host code, thread-safe: cpx.csvout formats row ranges on
+ * several threads.  Replaces the to_csv text of the reference's CSV outputs.                 */
+int64_t cpx_csv_format(int64_t row0, int64_t row1, int n_cols, const void* const* cols, const int* types,
+                       const int64_t* strides, char* out, int64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,96 @@
+"""CPU: the native table writer (libcpx cpx_csv_format via cpx.csvout) writes the same bytes as
+pandas.DataFrame.to_csv(index=False) — the text the reference's CSV consumers read
+(Pycyto_pertime.py:46-49 reads <Object>.csv with pandas.read_csv).
+
+Covers Python-repr float formatting at every switch point (fixed vs exponent at 1e-4 / 1e-5 and
+1e15 / 1e16, ".0" on integral values, two / three exponent digits), signed zero, subnormals, the
+extremes, inf, NaN (empty field), shortest round-trip digits of random doubles, int64 extremes,
+and the PlateTables object tables written natively vs through pandas DataFrames.
+"""
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from cpx import csvout
+
+
+def _pandas_bytes(path, names, cols):
+    df = pd.DataFrame({n: c for n, c in zip(names, cols)})
+    df.to_csv(path, index=False)
+    return open(path, "rb").read()
+
+
+SPECIAL = [0.0, -0.0, 0.1, -0.1, 1.0, -1.0, 1e-4, 1e-5, 9.999999999999999e-05, 0.00012345, 2.5e-05,
+           1e15, 1e16, 9999999999999998.0, 1.0000000000000002e16, 1234567890123456.0, 123456789012345678.0,
+           5e-324, 2.2250738585072014e-308, 1.7976931348623157e308, -1.7976931348623157e308, 1e100, 1e-100,
+           1e-99, 1e99, 123.0, 100.0, 0.5, 1 / 3, 2 / 3, np.pi, np.e, np.inf, -np.inf, np.nan, 65535.0,
+           4.35e-7, 1e22, 1e21, 1e23, 0.3, 2.0 ** 53, 2.0 ** 53 + 2, 2.0 ** -1074, 1e-310]
+
+
+def test_special_values_match_pandas(tmp_path):
+    v = np.array(SPECIAL, np.float64)
+    ints = np.arange(len(v), dtype=np.int64) - 3
+    names = ["i", "f", "g"]
+    cols = [ints, v, -v]
+    want = _pandas_bytes(tmp_path / "a.csv", names, cols)
+    csvout.write_numeric_csv(str(tmp_path / "b.csv"), names, cols, threads=1)
+    assert open(tmp_path / "b.csv", "rb").read() == want
+
+
+def test_random_doubles_and_int_extremes_match_pandas(tmp_path):
+    rng = np.random.default_rng(7)
+    n = 20000  # several native chunks, formatted on threads
+    bits = rng.integers(0, 2 ** 63, n, dtype=np.int64).view(np.float64)  # every exponent
+    bits[~np.isfinite(bits)] = 1.5
+    scaled = rng.standard_normal(n) * 10.0 ** rng.integers(-8, 20, n)
+    ints = rng.integers(np.iinfo(np.int64).min, np.iinfo(np.int64).max, n, dtype=np.int64)
+    ints[:2] = [np.iinfo(np.int64).min, np.iinfo(np.int64).max]
+    small = rng.integers(0, 5000, n).astype(np.int64)
+    names = ["ImageNumber", "a", "b", "c", "d"]
+    cols = [small, bits, scaled, ints, np.round(scaled, 3)]
+    want = _pandas_bytes(tmp_path / "a.csv", names, cols)
+    csvout.write_numeric_csv(str(tmp_path / "b.csv"), names, cols, threads=4)
+    assert open(tmp_path / "b.csv", "rb").read() == want
+
+
+def test_strided_columns_and_empty_table(tmp_path):
+    rng = np.random.default_rng(3)
+    m = rng.standard_normal((1000, 7))
+    names = [f"c{j}" for j in range(7)]
+    cols = [m[:, j] for j in range(7)]  # column views of a row-major matrix
+    want = _pandas_bytes(tmp_path / "a.csv", names, cols)
+    csvout.write_numeric_csv(str(tmp_path / "b.csv"), names, cols)
+    assert open(tmp_path / "b.csv", "rb").read() == want
+    want0 = _pandas_bytes(tmp_path / "e.csv", ["x", "y"], [np.zeros(0, np.int64), np.zeros(0)])
+    csvout.write_numeric_csv(str(tmp_path / "f.csv"), ["x", "y"], [np.zeros(0, np.int64), np.zeros(0)])
+    assert open(tmp_path / "f.csv", "rb").read() == want0
+
+
+@pytest.mark.parametrize("eager", [False, True])
+def test_plate_tables_native_equals_pandas_frames(tmp_path, eager):
+    rng = np.random.default_rng(11)
+    chans = ["DNA", "ER", "RNA", "AGP", "Mito"]
+    t = csvout.PlateTables(chans, eager_csv=eager)
+    F = len(t.cols)
+    for img in (5, 2, 9):  # FOVs out of order; labels out of order inside a FOV
+        for s in csvout.OBJECT_TABLES:
+            n = int(rng.integers(0, 40))
+            labels = rng.permutation(np.arange(1, n + 1))
+            feats = rng.standard_normal((n, F)) * 10.0 ** rng.integers(-6, 8, (n, F))
+            feats[rng.random((n, F)) < 0.02] = np.nan
+            t.add_objects(s, img, labels, feats)
+        t.add_image(img, {"Metadata_Well": "A01"}, [0.1] * 5, [0.0] * 5, {"Nuclei": 1})
+    d = t.write(str(tmp_path), "P01", 3)
+    t.close()
+    for name, df in t.frames().items():
+        df.to_csv(tmp_path / f"{name}.ref.csv", index=False)
+        assert open(os.path.join(d, f"{name}.csv"), "rb").read() == open(tmp_path / f"{name}.ref.csv", "rb").read(), name
+
+
+def test_write_frame_csv_falls_back_for_strings(tmp_path):
+    df = pd.DataFrame({"ImageNumber": [1, 2], "Metadata_Well": ["A01", "B02"], "x": [0.5, np.nan]})
+    csvout.write_frame_csv(df, str(tmp_path / "a.csv"))
+    df.to_csv(tmp_path / "b.csv", index=False)
+    assert open(tmp_path / "a.csv", "rb").read() == open(tmp_path / "b.csv", "rb").read()
