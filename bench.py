@@ -25,6 +25,8 @@ sys.path.insert(0, os.path.join(REPO, "image-processing-suite_amd"))
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3     # f32-input MFMA = f32 vector peak (MI355X_MICROARCH.md)
+LDS_ATOMICS_PER_CU_CLK = 64 / 7.59  # no-return ds_add on random words (tools/micro/lds_atomic.hip, r05p)
+CLOCK_HZ = 2.4e9            # the clock the LDS rates are quoted at (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -84,8 +86,10 @@ def main():
 
     from cpx import shard
     from cpx.cpnet import count_flops
-    from cpx.device import Device
-    from cpx.pipeline import FovPipeline, PipelineConfig
+    import ctypes as ct
+
+    from cpx.device import Device, as_numpy
+    from cpx.pipeline import OBJECT_SETS, FovPipeline, PipelineConfig
     from cpx.synth import synth_fovs, synth_illum, synth_zstack
 
     Z = a.zstack
@@ -213,6 +217,29 @@ def main():
            "features": 0.0}
     if Z > 1:
         sub["zmax"] = 0.0
+    glcm = {"ms": 0.0, "atomics": 0, "items": 0}
+
+    def glcm_acc(p):
+        # k_tex_glcm device time of this step (HIP events around its launches) and its LDS work:
+        # per staged (object, channel) item and angle, one LDS atomic per pair slot of the crop
+        # (rows - dr) x crop_stride(bw) (masked and background slots go to a sink word: atomics
+        # too) and one 128 KiB table scan
+        ms, nl = ct.c_double(), ct.c_int()
+        dev.lib.cpx_debug_glcm_ms(dev.h, ct.byref(ms), ct.byref(nl))
+        dev.lib.cpx_debug_glcm_timing(dev.h, 0)
+        glcm["ms"] += ms.value
+        for s in OBJECT_SETS:
+            objs = as_numpy(p.objects[s], "object").reshape(B, -1)
+            nobj = as_numpy(p.hdr[s], "hdr")["n_objects"]
+            for b in range(B):
+                bb = objs[b, :nobj[b]]["bbox"].astype(np.int64)
+                bh, bw = bb[:, 2] - bb[:, 0], bb[:, 3] - bb[:, 1]
+                st = bh * bw <= 65535
+                stride = (bw + 7) & ~7
+                for dr in (0, 2, 3, 2):
+                    glcm["atomics"] += int(C * np.sum(np.maximum(bh - dr, 0) * stride * st))
+                glcm["items"] += int(C * st.sum())
+
     for i in range(a.stage_steps):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(10)]
         if Z > 1:
@@ -234,9 +261,11 @@ def main():
         ev[5].record()
         pipe.stage_cells()
         ev[6].record()
+        dev.lib.cpx_debug_glcm_timing(dev.h, 1)
         pipe.stage_features()
         ev[7].record()
         torch.cuda.synchronize()
+        glcm_acc(pipe)
         sub["illum"] += ev[0].elapsed_time(ev[1])
         sub["qc_rps"] += ev[1].elapsed_time(ev[2])
         sub["seg_prep"] += ev[2].elapsed_time(ev[3])
@@ -316,6 +345,22 @@ def main():
     copy_gbs = 2 * (1 << 31) * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9
     del src_b, dst_b
 
+    # k_tex_glcm against its LDS floor: the no-return LDS atomic rate on random
+    # addresses, 64 / 7.59 per CU-cycle (tools/micro/lds_atomic.hip, profiles/r05p_lds_atomic.log),
+    # and the 4 x 128 KiB table scans per item at 256 B per CU-cycle, at 2.4 GHz on every CU
+    n_cu = torch.cuda.get_device_properties(td).multi_processor_count
+    glcm_ms = glcm["ms"] / a.stage_steps
+    atomics = glcm["atomics"] / a.stage_steps
+    items = glcm["items"] / a.stage_steps
+    atomic_peak = n_cu * LDS_ATOMICS_PER_CU_CLK * CLOCK_HZ
+    floor_ms = (atomics / LDS_ATOMICS_PER_CU_CLK + items * 4 * 131072 / 256) / (n_cu * CLOCK_HZ) * 1e3
+    glcm_roof = {"kernel": "k_tex_glcm", "bound": "lds_atomic", "achieved": round(atomics / (glcm_ms * 1e-3) / 1e9, 1),
+                 "peak": round(atomic_peak / 1e9, 1), "unit": "Gatomic/s",
+                 "frac": round(atomics / (glcm_ms * 1e-3) / atomic_peak, 4) if glcm_ms else None,
+                 "lds_floor_ms": round(floor_ms, 4), "floor_frac": round(floor_ms / glcm_ms, 4) if glcm_ms else None,
+                 "atomics_per_step": int(atomics), "items_per_step": int(items), "avg_launch_ms": round(glcm_ms, 4),
+                 "peak_source": "tools/micro/lds_atomic.hip (random 32K-word no-return atomics), profiles/r05p_lds_atomic.log"}
+
     dominant = max(kernels, key=lambda k: kernels[k]["ms"])
     line = {
         "metric": "fields-of-view/sec, 2080x2080x5ch illum+seg+feat pipe",
@@ -349,7 +394,7 @@ def main():
                             if n_obj else None),
         "stage_ms_per_step": {k: round(v, 3) for k, v in {**per_step_ms, **sub_ms}.items()},
         "roofline": roof(dominant),
-        "roofline_all": {k: roof(k) for k in kernels},
+        "roofline_all": {**{k: roof(k) for k in kernels}, "glcm": glcm_roof},
         "hbm_copy_measured_GBs": round(copy_gbs, 1),
     }
     if cpu_ctx is not None:

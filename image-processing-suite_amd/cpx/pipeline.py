@@ -29,6 +29,7 @@ from .device import Device, as_numpy, n_features
 from .segment import CELLPOSE_MODEL, DIAMETER, Segmenter
 
 OBJECT_SETS = ("Nuclei", "Cells", "Cytoplasm")
+STAGE_EXCLUSIVE = [x for x in os.environ.get("CPX_STAGE_EXCLUSIVE", "").split(",") if x]
 # Cells + Cytoplasm features in one libcpx call (CPX_PAIR_FEATURES=0: one call per set, A/B runs)
 PAIR_FEATURES = os.environ.get("CPX_PAIR_FEATURES", "1") != "0"
 log = logging.getLogger("cpx.pipeline")
@@ -190,17 +191,42 @@ class FovPipeline:
         self.qc, self.hdr, self.objects, self.feats = sl["qc"], sl["hdr"], sl["objects"], sl["feats"]
 
     # ---- stages ---------------------------------------------------------------------------
+    # CPX_STAGE_EXCLUSIVE (comma-separated stage names: illum_qc, cpnet, seg_post, cells,
+    # features): a listed stage of one pipeline waits on the device for the same stage of the
+    # pipeline enqueued before it (one shared event per device and stage), so two batches in
+    # flight never run that stage at once and overlap only across different stages
+    _excl: dict = {}
+
+    def _stage(self, name, fn):
+        if name not in STAGE_EXCLUSIVE:
+            return fn()
+        key = (self.dev.index, name)
+        stream = torch.cuda.current_stream(self.dev.torch_device)
+        ev = FovPipeline._excl.get(key)
+        if ev is not None:
+            stream.wait_event(ev)
+        out = fn()
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        FovPipeline._excl[key] = ev
+        return out
+
     def stage_illum_qc(self):
         C = self.cfg.C
-        self.dev.illum_correct(self.raw, self.illum, C, self.corr, self.stats)
-        self.dev.qc_rps(self.raw, self.illum, C, self.stats, self.qc)
+
+        def run():
+            self.dev.illum_correct(self.raw, self.illum, C, self.corr, self.stats)
+            self.dev.qc_rps(self.raw, self.illum, C, self.stats, self.qc)
+        self._stage("illum_qc", run)
 
     def stage_segment(self):
-        self.seg.segment(self.corr, self.labels["Nuclei"])
+        self.seg.prepare(self.corr)
+        self._stage("cpnet", self.seg._run_net)
+        self._stage("seg_post", lambda: self.seg.postprocess(self.labels["Nuclei"]))
 
     def stage_objects(self):
-        self.stage_cells()
-        self.stage_features()
+        self._stage("cells", self.stage_cells)
+        self._stage("features", self.stage_features)
 
     def stage_cells(self):
         """Cells (marker watershed or expand_labels) and Cytoplasm from the Nuclei labels."""

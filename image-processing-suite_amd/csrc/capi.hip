@@ -79,7 +79,35 @@ void cpx_destroy(cpx_ctx* ctx) {
   for (int i = 0; i < kWsSlots; ++i)
     if (ctx->ws[i]) (void)hipFree(ctx->ws[i]);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+  for (int i = 0; i < cpx_ctx::kGlcmEv; ++i)
+    for (int k = 0; k < 2; ++k)
+      if (ctx->glcm_ev[i][k]) (void)hipEventDestroy(ctx->glcm_ev[i][k]);
   delete ctx;
+}
+
+int cpx_debug_glcm_timing(cpx_ctx* ctx, int enable) {
+  CPX_REQUIRE(ctx != nullptr, CPX_ERR_ARG, "cpx_debug_glcm_timing: ctx is NULL");
+  if (enable && !ctx->glcm_ev[0][0])
+    for (int i = 0; i < cpx_ctx::kGlcmEv; ++i)
+      for (int k = 0; k < 2; ++k) CPX_CHECK_HIP(hipEventCreate(&ctx->glcm_ev[i][k]));
+  ctx->glcm_timing = enable ? 1 : 0;
+  ctx->glcm_nev = 0;
+  return CPX_OK;
+}
+
+int cpx_debug_glcm_ms(cpx_ctx* ctx, double* ms_out, int* launches_out) {
+  CPX_REQUIRE(ctx && ms_out, CPX_ERR_ARG, "cpx_debug_glcm_ms: null argument");
+  double ms = 0.0;
+  for (int i = 0; i < ctx->glcm_nev; ++i) {
+    CPX_CHECK_HIP(hipEventSynchronize(ctx->glcm_ev[i][1]));
+    float t = 0.0f;
+    CPX_CHECK_HIP(hipEventElapsedTime(&t, ctx->glcm_ev[i][0], ctx->glcm_ev[i][1]));
+    ms += t;
+  }
+  *ms_out = ms;
+  if (launches_out) *launches_out = ctx->glcm_nev;
+  ctx->glcm_nev = 0;
+  return CPX_OK;
 }
 
 int cpx_set_stream(cpx_ctx* ctx, void* hip_stream) {

@@ -38,6 +38,11 @@ struct cpx_ctx {
   // embedding preprocessing coefficient table currently uploaded (WS_EMBED): S, D
   int embed_key[2] = {0, 0};
   unsigned int embed_gen = 0;
+  // k_tex_glcm launch timing (cpx_debug_glcm_timing, bench.py's GLCM roofline): event pairs
+  // recorded around each launch while enabled, summed by cpx_debug_glcm_ms
+  static constexpr int kGlcmEv = 64;
+  int glcm_timing = 0, glcm_nev = 0;
+  hipEvent_t glcm_ev[kGlcmEv][2] = {};
 };
 
 void cpx_fov_free(cpx_ctx* ctx);

@@ -1284,10 +1284,13 @@ int launch_texture(cpx_ctx* ctx, const SetArgs& a, FeatWs& w, int B, int C, int 
                      max_label, F, a.objects, a.hdr, (const long long*)w.raws, a.feats);
   CPX_CHECK_LAUNCH("k_shape_props");
   const int per_fov_t = std::max(1, std::min(max_label * C, (ctx->n_cu + B - 1) / B));
+  const int tev = ctx->glcm_timing && ctx->glcm_nev < cpx_ctx::kGlcmEv ? ctx->glcm_nev++ : -1;
+  if (tev >= 0) CPX_CHECK_HIP(hipEventRecord(ctx->glcm_ev[tev][0], ctx->stream));
   hipLaunchKernelGGL(k_tex_glcm, dim3(per_fov_t, B), dim3(kTT), 0, ctx->stream, C, max_label,
                      F, a.objects, a.hdr, (const long long*)w.crop_off,
                      (const unsigned char*)w.scratch, w.per_fov, w.glcm_next, w.glcm_raw);
   CPX_CHECK_LAUNCH("k_tex_glcm");
+  if (tev >= 0) CPX_CHECK_HIP(hipEventRecord(ctx->glcm_ev[tev][1], ctx->stream));
   hipLaunchKernelGGL(k_glcm_props, dim3(cpx_div_up(max_label * C * 4, 256), B), dim3(256), 0, ctx->stream,
                      C, max_label, F, a.objects, a.hdr, (const long long*)w.crop_off,
                      (const unsigned long long*)w.glcm_raw, a.feats);

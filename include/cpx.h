@@ -570,6 +570,13 @@ int cpx_fov_features(cpx_ctx* ctx, const int32_t* labels_dev, int max_objects, d
                      int* n_out);
 int cpx_fov_wait(cpx_ctx* ctx);
 
+/* ---- profiling: device time of the k_tex_glcm launches (bench.py's GLCM LDS roofline) ----- *
+ * While enabled, every cpx_features / cpx_features_pair call records a HIP event pair around
+ * its GLCM launch (up to 64 between reads); cpx_debug_glcm_ms waits for them and returns the
+ * summed milliseconds and the launch count, then forgets them.  Not for timed regions.       */
+int cpx_debug_glcm_timing(cpx_ctx* ctx, int enable);
+int cpx_debug_glcm_ms(cpx_ctx* ctx, double* ms_out, int* launches_out);
+
 /* ---- host: CSV rows of the measurement tables (Pycyto_pertime.py:46-49 reads them) ------- *
  * Rows [row0, row1) of a table of n_cols columns, column c at cols[c] with element stride
  * strides[c] (in elements), types[c] 0 = int64 (decimal) or 1 = float64 (Python repr, the text
