@@ -29,7 +29,11 @@ from .device import Device, as_numpy, n_features
 from .segment import CELLPOSE_MODEL, DIAMETER, Segmenter
 
 OBJECT_SETS = ("Nuclei", "Cells", "Cytoplasm")
-STAGE_EXCLUSIVE = [x for x in os.environ.get("CPX_STAGE_EXCLUSIVE", "").split(",") if x]
+# stages that never overlap themselves across the batches in flight on one GPU (FovPipeline._stage;
+# "" for none): the CPnet and the feature stage, each contending with its own copy for HBM / MFMA
+# and LDS, overlap better with the other batch's different stages — 439.5 -> 446.4 FOV/s
+# (three interleaved pairs of 60-step benches, `gpurun_out/r05t`)
+STAGE_EXCLUSIVE = [x for x in os.environ.get("CPX_STAGE_EXCLUSIVE", "cpnet,features").split(",") if x]
 # Cells + Cytoplasm features in one libcpx call (CPX_PAIR_FEATURES=0: one call per set, A/B runs)
 PAIR_FEATURES = os.environ.get("CPX_PAIR_FEATURES", "1") != "0"
 log = logging.getLogger("cpx.pipeline")
