@@ -670,7 +670,7 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
 // tiles of one XCD form a contiguous range that its blocks walk in step, so vertically adjacent
 // tiles (which share halo rows) are in flight together in that XCD's L2.  Per output pixel the
 // sums are formed in k_conv_x3's slab / tap / MFMA order: bit-identical results.
-template <bool kP32Touch>
+template <int kP32Touch>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, int N, int H,
                    int W, int tiles_x, int tiles_y) {
@@ -727,9 +727,9 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
     unsigned tv0 = 0, tv1 = 0;
     if (kP32Touch) {
       // L2 prefetch while the MFMAs run: one 128-byte line per thread of this tile's residual
-      // (read by the epilogue) and of the block's next halo (DMA'd at the next tile's top); the
-      // loaded words are first used at the tile's end (no wait before the MFMAs) and only feed
-      // `touch`, consumed after the loop
+      // (read by the epilogue) and, in mode 1, of the block's next halo (DMA'd at the next tile's
+      // top); the loaded words are first used at the tile's end (no wait before the MFMAs) and
+      // only feed `touch`, consumed after the loop
       const int i = threadIdx.x;
       if (ep.res && i < TY * TX) {
         const int gy = ty0 + i / TX, gx = tx0 + i % TX;
@@ -740,7 +740,7 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
         }
       }
       const int t2 = t + nbx;
-      if (t2 < hi && i < NPIX) {
+      if (kP32Touch == 1 && t2 < hi && i < NPIX) {  // (mode 2: the residual lines only)
         const int n2 = t2 / tiles, tt2 = t2 - n2 * tiles;
         const int gy = (tt2 / tiles_x) * TY + i / HX - 1, gx = (tt2 % tiles_x) * TX + i % HX - 1;
         if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
@@ -883,13 +883,17 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
   // CPX_X3_P32=0)
   if ((variant == 2 || variant == 3) && cout == 32) variant = 0;  // (224^2: variant 0's kernels)
   static const bool p32 = !getenv("CPX_X3_P32") || atoi(getenv("CPX_X3_P32")) != 0;
-  static const bool p32_touch = !getenv("CPX_X3_P32_TOUCH") || atoi(getenv("CPX_X3_P32_TOUCH")) != 0;
+  // L2 prefetch in k_conv_x3_p32 (CPX_X3_P32_TOUCH): 2 = this tile's residual lines (default),
+  // 1 = also the block's next halo, 0 = none.  Two-pipeline benches of 60 steps (`gpurun_out/r05w`):
+  // 444.1 / 443.1 / 440.0 FOV/s; mode 1's next-halo lines are mostly evicted before the DMA reads
+  // them (+12.7 GB of PMC traffic per step), so mode 2 keeps the time without the traffic
+  static const int p32_touch = getenv("CPX_X3_P32_TOUCH") ? atoi(getenv("CPX_X3_P32_TOUCH")) : 2;
   if (p32 && ks == 3 && cin == 32 && cout == 32 && variant == 0 && !ep.in_up) {
     const int tx = cpx_div_up(W, 32), ty = cpx_div_up(H, 8);
     const long long tiles = (long long)N * tx * ty;
     CPX_REQUIRE(tiles < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv: too many tiles");
     const int grid = (int)std::max(1LL, std::min(tiles, 2LL * ctx->n_cu));
-    auto kern = p32_touch ? k_conv_x3_p32<true> : k_conv_x3_p32<false>;
+    auto kern = p32_touch == 2 ? k_conv_x3_p32<2> : p32_touch ? k_conv_x3_p32<1> : k_conv_x3_p32<0>;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N,
                        H, W, tx, ty);
     CPX_CHECK_LAUNCH("k_conv_x3_p32");

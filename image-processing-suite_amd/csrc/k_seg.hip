@@ -2317,7 +2317,6 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   else
     hipLaunchKernelGGL(k_dyn_prep<false>, gprep, dim3(kT), 0, ctx->stream, yf_dev, Ly, Lx, Dy, Dx,
                        tabs.uy, tabs.ux, d);
-  const int fblk = std::max(1, std::min(cpx_div_up(n, kT), (16 * ctx->n_cu + B - 1) / B));
   // k_dyn_follow: trajectories per thread (CPX_FOLLOW_NI 1, 2 or 4) and paired 16-byte gathers
   // (CPX_FOLLOW_V4); per 48-FOV step (`gpurun_out/r05l`, `r05m`): 1 / scalar 12.11 ms, 2 / scalar
   // 11.83, 4 / scalar 12.54, 1 / paired 11.46, 2 / paired 11.02 (the default); every setting passes
@@ -2325,6 +2324,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   static const int follow_ni = getenv("CPX_FOLLOW_NI") ? atoi(getenv("CPX_FOLLOW_NI")) : 2;
   static const bool follow_v4 = !getenv("CPX_FOLLOW_V4") || atoi(getenv("CPX_FOLLOW_V4")) != 0;
   {
+    const int fblk = std::max(1, std::min(cpx_div_up(n, kT), (16 * ctx->n_cu + B - 1) / B));
     int step = 0, r = 0;
     do {  // at least one round: with niter = 0 it only records the start positions
       const int K = step < sw ? k0 : k1;
@@ -2335,8 +2335,9 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
       auto kern = follow_ni == 4 ? (v4 ? k_dyn_follow<4, true> : k_dyn_follow<4, false>)
                 : follow_ni == 2 ? (v4 ? k_dyn_follow<2, true> : k_dyn_follow<2, false>)
                                  : (v4 ? k_dyn_follow<1, true> : k_dyn_follow<1, false>);
-      hipLaunchKernelGGL(kern, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step, K, r == 0 ? 1 : 0,
-                         in, (const int*)(d.fcnt + (size_t)B * r), out, d.fcnt + (size_t)B * (r + 1), d);
+      hipLaunchKernelGGL(kern, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step, K,
+                         r == 0 ? 1 : 0, in, (const int*)(d.fcnt + (size_t)B * r), out,
+                         d.fcnt + (size_t)B * (r + 1), d);
       step += K;
       ++r;
     } while (step < niter);
