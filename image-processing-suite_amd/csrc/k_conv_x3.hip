@@ -400,6 +400,35 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
   flag();
 }
 
+// Instruction-scheduling hint for the single-fragment tap loop (CPX_X3_SCHED): 1 (default) =
+// iglp_opt(0), the compiler's MFMA / DS-read interleave: the 32-channel-block kernels 2.5-3 %
+// faster, bit-identical outputs (`gpurun_out/r05y`); 2 = sched_group_barrier groups that issue
+// tap t + 1's fragment reads before tap t's MFMAs (DS 4, then per tap DS 4 + MFMA 3): ~1 %; 0 =
+// none.  The 224^2 persistent kernel takes the same hint after each slab's taps (-2.3 %,
+// `gpurun_out/r05z`); in the multi-fragment loop (one tap per iteration) it measured +-1 % and
+// raised spills, so it stays out there (CPX_X3_SCHED_ALL for experiments).
+#ifndef CPX_X3_SCHED
+#define CPX_X3_SCHED 1
+#endif
+#ifndef CPX_X3_SCHED_ALL
+#define CPX_X3_SCHED_ALL 0
+#endif
+template <int T, int C>
+__device__ __forceinline__ void x3_sched() {
+  if constexpr (CPX_X3_SCHED == 1) {
+    __builtin_amdgcn_iglp_opt(0);
+  } else if constexpr (CPX_X3_SCHED == 2) {
+    constexpr int R = 2 + 2 * C, M = 3 * C;  // DS reads (A hi/lo + B hi/lo per subtile) and MFMAs per tap
+    __builtin_amdgcn_sched_group_barrier(0x0100, R, 0);
+#pragma unroll
+    for (int t = 0; t + 1 < T; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x0100, R, 0);
+      __builtin_amdgcn_sched_group_barrier(0x0008, M, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x0008, M, 0);
+  }
+}
+
 template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, int CIN2 = 0, int NBUF = 2>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Epi ep, int N, int H,
@@ -610,9 +639,13 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
         // tap's MFMAs; larger wave tiles keep one tap per iteration (register budget)
 #pragma unroll
         for (int tap = 0; tap < T; ++tap) tapbody(cnt, sb, tap, tap / KS, tap % KS);
+        x3_sched<T, decltype(cnt)::value>();
       } else {
 #pragma unroll 1
-        for (int tap = 0; tap < T; ++tap) tapbody(cnt, sb, tap, tap / KS, tap % KS);
+        for (int tap = 0; tap < T; ++tap) {
+          tapbody(cnt, sb, tap, tap / KS, tap % KS);
+          if constexpr (CPX_X3_SCHED_ALL) __builtin_amdgcn_iglp_opt(0);
+        }
       }
     });
     if (NBUF == 1) {  // every wave is done with the buffer before the next slab lands in it
@@ -773,6 +806,7 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc1, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc1, 0, 0, 0);
       }
+      if constexpr (CPX_X3_SCHED == 1) __builtin_amdgcn_iglp_opt(0);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc0[0][0][r] += acc1[r] * kLoInv;  // exact product, one rounding
