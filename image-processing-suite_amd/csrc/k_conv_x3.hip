@@ -417,6 +417,8 @@ template <int T, int C>
 __device__ __forceinline__ void x3_sched() {
   if constexpr (CPX_X3_SCHED == 1) {
     __builtin_amdgcn_iglp_opt(0);
+  } else if constexpr (CPX_X3_SCHED == 3) {
+    __builtin_amdgcn_iglp_opt(1);
   } else if constexpr (CPX_X3_SCHED == 2) {
     constexpr int R = 2 + 2 * C, M = 3 * C;  // DS reads (A hi/lo + B hi/lo per subtile) and MFMAs per tap
     __builtin_amdgcn_sched_group_barrier(0x0100, R, 0);
@@ -641,10 +643,24 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
         for (int tap = 0; tap < T; ++tap) tapbody(cnt, sb, tap, tap / KS, tap % KS);
         x3_sched<T, decltype(cnt)::value>();
       } else {
+#ifndef CPX_X3_MUNROLL
+#define CPX_X3_MUNROLL 1
+#endif
+        if constexpr (CPX_X3_MUNROLL == 1) {
 #pragma unroll 1
-        for (int tap = 0; tap < T; ++tap) {
-          tapbody(cnt, sb, tap, tap / KS, tap % KS);
-          if constexpr (CPX_X3_SCHED_ALL) __builtin_amdgcn_iglp_opt(0);
+          for (int tap = 0; tap < T; ++tap) {
+            tapbody(cnt, sb, tap, tap / KS, tap % KS);
+            if constexpr (CPX_X3_SCHED_ALL) __builtin_amdgcn_iglp_opt(0);
+          }
+        } else {  // (experiment) CPX_X3_MUNROLL taps per iteration with the interleave hint
+          static_assert(T % CPX_X3_MUNROLL == 0 || T == 1, "taps per iteration");
+          constexpr int U = T == 1 ? 1 : CPX_X3_MUNROLL;
+#pragma unroll 1
+          for (int t0 = 0; t0 < T; t0 += U) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) tapbody(cnt, sb, t0 + u, (t0 + u) / KS, (t0 + u) % KS);
+            __builtin_amdgcn_iglp_opt(0);
+          }
         }
       }
     });
@@ -807,6 +823,7 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc1, 0, 0, 0);
       }
       if constexpr (CPX_X3_SCHED == 1) __builtin_amdgcn_iglp_opt(0);
+      if constexpr (CPX_X3_SCHED == 3) __builtin_amdgcn_iglp_opt(1);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc0[0][0][r] += acc1[r] * kLoInv;  // exact product, one rounding
