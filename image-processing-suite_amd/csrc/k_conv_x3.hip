@@ -643,8 +643,13 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
         for (int tap = 0; tap < T; ++tap) tapbody(cnt, sb, tap, tap / KS, tap % KS);
         x3_sched<T, decltype(cnt)::value>();
       } else {
+        // multi-fragment waves: the two-slice BM 64 tile (WM 2, WN 1) unrolls all nine taps with
+        // the interleave hint, like the single-fragment loop, where the registers allow it (no
+        // folded projection, CIN >= 64): -6 to -7.5 % on those kernels, bit-identical
+        // (`gpurun_out/r05ab`); CIN 32, the projection-folded forms and the WN 2 tiles spill
+        // unrolled and keep one tap per iteration
 #ifndef CPX_X3_MUNROLL
-#define CPX_X3_MUNROLL 1
+#define CPX_X3_MUNROLL ((WM == 2 && WN == 1 && CIN2 == 0 && CIN >= 64) ? 9 : 1)
 #endif
         if constexpr (CPX_X3_MUNROLL == 1) {
 #pragma unroll 1

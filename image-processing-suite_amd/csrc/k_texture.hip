@@ -601,9 +601,77 @@ __device__ __forceinline__ bool shape_fits(const cpx_object& o) {
 // Membership bitmask of object o over its bbox + 2-px margin (rows x wpr words in M): each
 // 32-lane half-wave builds one 32-bit word (r, cw); eight words per half-wave are loaded before
 // the first ballot so the label loads overlap.
+// The membership words from 16-byte label loads (CPX_STAGE_MASK16, default on): a lane reads 4
+// consecutive labels (raw buffer load, dword-aligned; four 4-byte loads where the piece would
+// cross the plane's ends), 8 lanes form a 32-pixel word, their 4-bit pieces OR-reduced over the
+// 8 lanes — instead of one 4-byte load per lane and pixel and a ballot per word: features -2-3 %
+// per object set (`gpurun_out/r05ab`)
+#ifndef CPX_STAGE_MASK16
+#define CPX_STAGE_MASK16 1
+#endif
+template <int NT>
+__device__ __forceinline__ void shape_mask16(const int* __restrict__ lab, int H, int W, const cpx_object& o,
+                                             unsigned int* M) {
+  constexpr int U = 4;  // words per lane group and iteration (loads in flight per lane)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int sub = lane & 7, grp = lane >> 3;  // 4-pixel piece of the word, word slot of the wave
+  const int L = o.label;
+  const int R0 = o.bbox[0] - 2, C0 = o.bbox[1] - 2;  // region origin (2-px margin)
+  const int rows = o.bbox[2] - o.bbox[0] + 4, cols = o.bbox[3] - o.bbox[1] + 4;
+  const int wpr = (cols + 31) >> 5;
+  const int nw = rows * wpr;
+  const bool v4ok = (long long)H * W < (1LL << 29);  // the buffer's byte range is an int
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(lab), (short)0, v4ok ? H * W * 4 : 0, 0x00020000);
+  for (int w0 = wv * 8 * U; w0 < nw; w0 += (NT / 64) * 8 * U) {
+    int4 lv[U];
+    int cc[U], gcc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int w = w0 + u * 8 + grp;
+      const int r = w / wpr, cw = w - r * wpr;
+      const int c = cw * 32 + sub * 4, gr = R0 + r, gc = C0 + c;
+      cc[u] = w < nw ? c : cols;  // a slot past the mask's words: no member bits
+      gcc[u] = gc;
+      const bool row_ok = w < nw && gr >= 0 && gr < H;
+      const long long idx = (long long)gr * W + gc;
+      // columns outside [0, W) are masked below; the 16 bytes must lie inside the plane (at its
+      // first and last pixels, where the piece would cross the plane's ends, four 4-byte loads)
+      if (v4ok && row_ok && idx >= 0 && idx + 4 <= (long long)H * W) {
+        lv[u] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(idx * 4), 0, 0));
+      } else {
+        int t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = (row_ok && gc + k >= 0 && gc + k < W) ? lab[idx + k] : 0;
+        lv[u] = make_int4(t[0], t[1], t[2], t[3]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int v[4] = {lv[u].x, lv[u].y, lv[u].z, lv[u].w};
+      unsigned int bits = 0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = cc[u] + k, gc = gcc[u] + k;
+        bits |= (unsigned int)(v[k] == L && c < cols && gc >= 0 && gc < W) << k;
+      }
+      unsigned int word = bits << (4 * sub);
+      word |= __shfl_xor(word, 1, 8);
+      word |= __shfl_xor(word, 2, 8);
+      word |= __shfl_xor(word, 4, 8);
+      const int w = w0 + u * 8 + grp;
+      if (sub == 0 && w < nw) M[w] = word;
+    }
+  }
+}
+
 template <int NT>
 __device__ __forceinline__ void shape_mask(const int* __restrict__ lab, int H, int W, const cpx_object& o,
                                            unsigned int* M) {
+  if constexpr (CPX_STAGE_MASK16) {
+    shape_mask16<NT>(lab, H, W, o, M);
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31;
   const int L = o.label;
