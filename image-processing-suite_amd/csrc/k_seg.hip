@@ -2333,6 +2333,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
       // (the right-edge form reads x0 - 1; the buffer resource holds 8 n < 2^31 bytes)
       const bool v4 = follow_v4 && Dx >= 2 && 8LL * n < (1LL << 31);
       auto kern = follow_ni == 4 ? (v4 ? k_dyn_follow<4, true> : k_dyn_follow<4, false>)
+                : follow_ni == 3 ? (v4 ? k_dyn_follow<3, true> : k_dyn_follow<3, false>)
                 : follow_ni == 2 ? (v4 ? k_dyn_follow<2, true> : k_dyn_follow<2, false>)
                                  : (v4 ? k_dyn_follow<1, true> : k_dyn_follow<1, false>);
       hipLaunchKernelGGL(kern, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step, K,
