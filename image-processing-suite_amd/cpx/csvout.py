@@ -132,21 +132,77 @@ def feature_names(channels):
     return names
 
 
+class _TableStream:
+    """Appends formatted CSV blocks to one file on a writer thread, in arrival order, while their
+    ImageNumbers increase; finish() reports whether the file is complete and ordered."""
+
+    def __init__(self, path: str, names):
+        import queue
+        import threading
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        self.path = path
+        self.q = queue.Queue()
+        self.last = None
+        self.ordered = True
+        self.f = open(path, "wb")
+        self.f.write((",".join(names) + "\n").encode())
+        self.t = threading.Thread(target=self._run, daemon=True)
+        self.t.start()
+
+    def put(self, image_number: int, fut):
+        if self.last is not None and image_number <= self.last:
+            self.ordered = False  # (the writer stops appending; write_objects rewrites sorted)
+        self.last = image_number
+        self.q.put(fut if self.ordered else None)
+
+    def _run(self):
+        while True:
+            fut = self.q.get()
+            if fut is None:
+                break
+            try:
+                self.f.write(fut.result())
+            except BaseException:  # noqa: BLE001 - write_objects rewrites the file and re-raises
+                self.ordered = False
+                break
+
+    def finish(self, path: str) -> bool:
+        self.q.put(None)
+        self.t.join()
+        self.f.close()
+        return self.ordered and os.path.abspath(path) == os.path.abspath(self.path)
+
+    def abort(self):
+        self.q.put(None)
+        self.t.join()
+        if not self.f.closed:
+            self.f.close()
+
+
 class PlateTables:
     """Accumulates per-FOV results of one plate/time and writes the four CSVs."""
 
-    def __init__(self, channels, eager_csv: bool = False):
+    def __init__(self, channels, eager_csv: bool = False, stream_dir: str | None = None):
         self.channels = list(channels)
         self.cols = feature_names(self.channels)
         self.images = []                       # dicts
         self.objects = {t: [] for t in OBJECT_TABLES}  # (ImageNumber, labels[n], feats[n, F])
         # eager_csv: each FOV's object rows are formatted on a thread pool as they are added
-        # (overlapping the GPU work of the next batches); write_objects then only writes them
+        # (overlapping the GPU work of the next batches); write_objects then only writes them.
+        # stream_dir (with eager_csv): a writer thread per table appends the formatted blocks to
+        # <stream_dir>/<table>.csv while the job runs, as long as they arrive in ImageNumber order
+        # (the plate CLI's batches do); an out-of-order block makes write_objects rewrite the
+        # file sorted at the end, so the bytes never depend on the order of arrival
         self._pool = None
         self._rows = {t: [] for t in OBJECT_TABLES}  # (ImageNumber, future of bytes)
+        self._stream = {}
         if eager_csv:
             import concurrent.futures
             self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=CSV_THREADS)
+            if stream_dir is not None:
+                for t in OBJECT_TABLES:
+                    self._stream[t] = _TableStream(os.path.join(stream_dir, f"{t}.csv"),
+                                                   ["ImageNumber", "ObjectNumber", "Number_Object_Number"] + self.cols)
 
     def add_image(self, image_number: int, metadata: dict, qc_slope, qc_pct, counts: dict):
         row = {"ImageNumber": int(image_number)}
@@ -166,10 +222,15 @@ class PlateTables:
                              f"{len(self.cols)} columns")
         self.objects[table].append((int(image_number), labels, feats))
         if self._pool is not None:
-            self._rows[table].append((int(image_number),
-                                      self._pool.submit(format_object_rows, int(image_number), labels, feats)))
+            fut = self._pool.submit(format_object_rows, int(image_number), labels, feats)
+            self._rows[table].append((int(image_number), fut))
+            if table in self._stream:
+                self._stream[table].put(int(image_number), fut)
 
     def close(self):
+        for st in self._stream.values():
+            st.abort()
+        self._stream = {}
         if self._pool is not None:
             self._pool.shutdown(wait=True)
             self._pool = None
@@ -200,6 +261,9 @@ class PlateTables:
         ObjectNumber; the same bytes as frames()[table].to_csv(index=False))."""
         blocks = sorted(self.objects[table], key=lambda b: b[0])  # stable: FOVs in ImageNumber order
         names = ["ImageNumber", "ObjectNumber", "Number_Object_Number"] + self.cols
+        st = self._stream.pop(table, None)
+        if st is not None and st.finish(os.path.join(d, f"{table}.csv")):
+            return  # streamed in order, complete
         if self._rows[table] and len(self._rows[table]) == len(self.objects[table]):
             with open(os.path.join(d, f"{table}.csv"), "wb") as f:
                 f.write((",".join(names) + "\n").encode())

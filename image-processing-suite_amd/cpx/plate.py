@@ -240,7 +240,9 @@ def run(argv=None):
     dirs = []
     for ji, load_data in enumerate(a.load_data):
         table, plate, time = _job_meta(a, load_data)
-        out = PlateTables(chans, eager_csv=a.world == 1)  # one rank: rows formatted as FOVs finish
+        # one rank: each FOV's rows formatted as it finishes and streamed into the job's CSVs
+        out = PlateTables(chans, eager_csv=a.world == 1,
+                          stream_dir=job_dir(a.out, plate, time) if a.world == 1 else None)
         status = []  # per site: the reference's results_dict entry (Cellpose_GPU_s3fs.py:123-125,219-223)
         nsites = _run_sites(a, table, batch_source(table, a, ji), chans, state, out, status)
         if nsites:

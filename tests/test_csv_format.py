@@ -68,13 +68,17 @@ def test_strided_columns_and_empty_table(tmp_path):
     assert open(tmp_path / "f.csv", "rb").read() == want0
 
 
-@pytest.mark.parametrize("eager", [False, True])
-def test_plate_tables_native_equals_pandas_frames(tmp_path, eager):
+@pytest.mark.parametrize("mode", ["pandas-free", "eager", "stream"])
+def test_plate_tables_native_equals_pandas_frames(tmp_path, mode):
+    """FOVs added out of order (the streamed files then fall back to a sorted rewrite) and in
+    order (streamed as they arrive): every file equals the pandas frames' to_csv bytes."""
     rng = np.random.default_rng(11)
     chans = ["DNA", "ER", "RNA", "AGP", "Mito"]
-    t = csvout.PlateTables(chans, eager_csv=eager)
+    stream = str(tmp_path / "P01" / "3") if mode == "stream" else None
+    t = csvout.PlateTables(chans, eager_csv=mode != "pandas-free", stream_dir=stream)
     F = len(t.cols)
-    for img in (5, 2, 9):  # FOVs out of order; labels out of order inside a FOV
+    order = (5, 2, 9) if mode != "stream" else (2, 5, 9)  # (the stream test: in order)
+    for img in order:  # labels out of order inside a FOV
         for s in csvout.OBJECT_TABLES:
             n = int(rng.integers(0, 40))
             labels = rng.permutation(np.arange(1, n + 1))
@@ -94,3 +98,19 @@ def test_write_frame_csv_falls_back_for_strings(tmp_path):
     csvout.write_frame_csv(df, str(tmp_path / "a.csv"))
     df.to_csv(tmp_path / "b.csv", index=False)
     assert open(tmp_path / "a.csv", "rb").read() == open(tmp_path / "b.csv", "rb").read()
+
+
+def test_streamed_tables_fall_back_when_out_of_order(tmp_path):
+    rng = np.random.default_rng(12)
+    t = csvout.PlateTables(["DNA"], eager_csv=True, stream_dir=str(tmp_path / "P" / "1"))
+    F = len(t.cols)
+    for img in (3, 7, 5, 11):  # 5 after 7: the stream stops, write() rewrites sorted
+        for s in csvout.OBJECT_TABLES:
+            n = int(rng.integers(1, 10))
+            t.add_objects(s, img, np.arange(1, n + 1), rng.standard_normal((n, F)))
+        t.add_image(img, {"Metadata_Well": "A01"}, [0.1], [0.0], {"Nuclei": 1})
+    d = t.write(str(tmp_path), "P", 1)
+    t.close()
+    for name, df in t.frames().items():
+        df.to_csv(tmp_path / f"{name}.ref.csv", index=False)
+        assert open(os.path.join(d, f"{name}.csv"), "rb").read() == open(tmp_path / f"{name}.ref.csv", "rb").read()

@@ -1,5 +1,6 @@
 # Round 5: the multi-fragment (BM 64) tap loop unrolled 3 or 9 taps per iteration with iglp_opt(0) (tools/_var/libcpx_mu{3,9}.so): output
-# hash, one-pipeline kernel traces against the default; then the default bench.
+# hash, one-pipeline kernel traces against the default; then the 16-byte label loads of
+# k_obj_stage's membership masks.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r05ab
@@ -31,4 +32,12 @@ for L in default mu3 mu9; do
   python tools/prof_summary.py /tmp/kt_$L/run_kernel_trace.csv --steps 4 --md > $O/k_$L.md
   rm -rf /tmp/kt_$L
 done
+# k_obj_stage membership words from 16-byte label loads (tools/_var/libcpx_mask16.so): feature
+# parity with the variant, tex_bench both, kernel trace of the variant
+cd $R
+timeout -k 10 600 env CPX_LIB=$R/tools/_var/libcpx_mask16.so python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_features_pair.py tests/test_gpu_parity.py tests/test_gpu_capacity.py > $O/t_mask16.log 2>&1
+tail -1 $O/t_mask16.log
+timeout -k 10 200 python -u tools/tex_bench.py --batch 16 --reps 3 2>&1 | grep "features\[" > $O/tex_def.log
+timeout -k 10 200 env CPX_LIB=$R/tools/_var/libcpx_mask16.so python -u tools/tex_bench.py --batch 16 --reps 3 2>&1 | grep "features\[" > $O/tex_mask16.log
+cat $O/tex_def.log $O/tex_mask16.log
 echo done
