@@ -461,6 +461,16 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   static_assert(NBUF == 1 || NBUF == 2, "slab buffers");
   constexpr int SMEM = NBUF == 2 ? 2 * SB : (P * QB > SB ? P * QB : SB);
   static_assert(P * QB <= SMEM, "output tile must fit the staging LDS");
+  // projection slabs packed PK per slab buffer: a projection slab reads only the tile's centre
+  // pixels (P * 4 slots, no halo) and one tap of weights (BM * 4 slots), so two fit where a 3x3
+  // slab's nine weight taps and halo go — half the DMA waits and barriers of the projection
+  // (CPX_X3_PROJ_PACK=0 keeps one per buffer with the full halo)
+  constexpr int NPR = (P * 4 + 63) / 64;              // centre-pixel DMA rows of one projection slab
+#ifndef CPX_X3_PROJ_PACK
+#define CPX_X3_PROJ_PACK 1
+#endif
+  constexpr int PK = (CPX_X3_PROJ_PACK && CIN2 > 0 && 2 * BM * 4 + 2 * NPR * 64 <= SB) ? 2 : 1;
+  constexpr int NCHP = (NCH2 + PK - 1) / PK;          // projection slab buffers
   static_assert(SMEM * 16 <= 163840, "LDS");
   __shared__ uint4 smem[SMEM];
 
@@ -500,7 +510,7 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   const uint4* inb2 = CIN2 ? ep.in2 + (long long)n * H * W * QI2 : nullptr;
   // the residual tile, DMA'd during the last slab into the slab buffer that slab does not use, in
   // the epilogue's staging layout (chunk k of pixel px at px * QB + (k ^ swzq(px)))
-  constexpr int NCHT_ = NCH + NCH2;
+  constexpr int NCHT_ = NCH + NCHP;
   constexpr bool kResPre = NBUF == 2 && P * QB <= SB;
   uint4* const bufO = smem + (NBUF == 2 ? ((NCHT_ - 1) & 1) * SB : 0);  // the last slab's buffer
   uint4* const bufR = smem + (NBUF == 2 ? (NCHT_ & 1) * SB : 0);        // free during the last slab
@@ -544,7 +554,7 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
           __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(dst + SW + j * 64), 16, 0, 0);
         }
       }
-    } else {
+    } else if constexpr (PK == 1) {
       const int c2 = ch - NCH;
       const uint4* wsl = ep.wpk2 + (long long)(nb * NCH2 + c2) * (BM * 4);
       if (wid < NW2)
@@ -556,6 +566,32 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
           const uint4* src = inPC[jj] >= 0 ? inb2 + (long long)(inPC[jj] >> 2) * QI2 + (inPC[jj] & 3) + c2 * 4
                                            : &g_x3_zero16;
           __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(dst + SW + j * 64), 16, 0, 0);
+        }
+      }
+    } else {
+      // packed: weights of slab u at [u BM 4, ...), its centre pixels at [PK BM 4 + u NPR 64, ...)
+      // (pixel p, chunk k at slot p * 4 + (k ^ swz4(p)), as the halo layout without the halo)
+#pragma unroll
+      for (int u = 0; u < PK; ++u) {
+        const int c2 = (ch - NCH) * PK + u;
+        if (c2 < NCH2) {
+          const uint4* wsl = ep.wpk2 + (long long)(nb * NCH2 + c2) * (BM * 4);
+          if (wid < NW2)
+            __builtin_amdgcn_global_load_lds((glb_void_t*)(wsl + wid * 64 + fW),
+                                             (lds_void_t*)(dst + u * BM * 4 + wid * 64), 16, 0, 0);
+#pragma unroll
+          for (int jj = 0; jj < (NPR + NWV - 1) / NWV; ++jj) {
+            const int j = wid + NWV * jj;
+            if (j < NPR) {
+              const int si = j * 64 + lane, pp = si >> 2, cq = si & 3;
+              const int gy = ty0 + pp / TX, gx = tx0 + pp % TX;
+              const uint4* src = (pp < P && gy < H && gx < W)
+                                     ? inb2 + ((long long)gy * W + gx) * QI2 + (cq ^ swz4(pp)) + c2 * 4
+                                     : &g_x3_zero16;
+              __builtin_amdgcn_global_load_lds((glb_void_t*)src,
+                                               (lds_void_t*)(dst + PK * BM * 4 + u * NPR * 64 + j * 64), 16, 0, 0);
+            }
+          }
         }
       }
     }
@@ -589,7 +625,7 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  constexpr int NCHT = NCH + NCH2;
+  constexpr int NCHT = NCH + NCHP;
   // weights of tap `tw` against the halo at (ky, kx) of slab buffer sb, over C subtiles
   auto tapbody = [&](auto cnt, const uint4* sb, int tw, int ky, int kx) {
     constexpr int C = decltype(cnt)::value;
@@ -682,7 +718,38 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
     if (NBUF == 2 && ch + 1 < NCHT) issue(ch + 1, (ch + 1) & 1);
     if (kResPre && ch + 1 == NCHT && ep.res) issue_res();
     const uint4* sb = smem + (NBUF == 2 ? (ch & 1) * SB : 0);
-    per_nsub([&](auto cnt) { tapbody(cnt, sb, 0, HALO, HALO); });
+    if constexpr (PK == 1) {
+      per_nsub([&](auto cnt) { tapbody(cnt, sb, 0, HALO, HALO); });
+    } else {
+      // the packed slabs in channel order, each the centre tap's MFMAs of tapbody
+      per_nsub([&](auto cnt) {
+        constexpr int C = decltype(cnt)::value;
+#pragma unroll
+        for (int u = 0; u < PK; ++u) {
+          if ((ch - NCH) * PK + u < NCH2) {
+            f16x8 ah[WM], al[WM];
+#pragma unroll
+            for (int m = 0; m < WM; ++m) {
+              ah[m] = __builtin_bit_cast(f16x8, sb[aS[m] + u * BM * 4]);
+              al[m] = __builtin_bit_cast(f16x8, sb[(aS[m] ^ 2) + u * BM * 4]);
+            }
+#pragma unroll
+            for (int j = 0; j < C; ++j) {
+              const int pp = min((pg * WN + j) * 32 + l32, P - 1);
+              const int bs = PK * BM * 4 + u * NPR * 64 + pp * 4 + (h ^ swz4(pp));
+              const f16x8 bh = __builtin_bit_cast(f16x8, sb[bs]);
+              const f16x8 bl = __builtin_bit_cast(f16x8, sb[bs ^ 2]);
+#pragma unroll
+              for (int m = 0; m < WM; ++m) {
+                acc0[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh, acc0[m][j], 0, 0, 0);
+                acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bl, acc1[m][j], 0, 0, 0);
+                acc1[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bh, acc1[m][j], 0, 0, 0);
+              }
+            }
+          }
+        }
+      });
+    }
     if (NBUF == 1) {
       __syncthreads();
       if (ch + 1 < NCHT) issue(ch + 1, 0);
