@@ -41,6 +41,9 @@ log = logging.getLogger("cpx.plate")
 # per job of the last run(): {"job", "fovs", "seconds", "threads", "batch", "pipes"} — decode, upload,
 # GPU pipeline and table assembly, from the first decode to the last recorded site (pipeline
 # construction excluded); the I/O-inclusive throughput of the drop-in (tools/plate_bench.py)
+# (A/B knob) CPX_PLATE_UPLOAD=pipeline: each batch's upload in front of it on its pipeline's own
+# stream (the other pipeline computes meanwhile) instead of the device's upload stream
+UPLOAD_ON_PIPELINE_STREAM = os.environ.get("CPX_PLATE_UPLOAD", "device") == "pipeline"
 LAST_TIMING: list = []
 PARTS = ".parts"
 def parse_args(argv=None):
@@ -431,7 +434,8 @@ def _run_sites(a, table, source, chans, state, out, status):
             # stream) never wait behind it; the pipeline's stream waits for it.  pipes[p_i].raw
             # is the staging buffer of the pipeline's next result slot, whose previous batch was
             # fetched (retired) before this one was claimed
-            cs = FovPipeline.upload_stream(torch.device("cuda", a.device))
+            cs = (streams[p_i] if UPLOAD_ON_PIPELINE_STREAM
+                  else FovPipeline.upload_stream(torch.device("cuda", a.device)))
             with torch.cuda.stream(cs):
                 evs[0].record(cs)
                 pipes[p_i].raw.copy_(hosts[p_i], non_blocking=True)
