@@ -37,15 +37,22 @@ import time as _time  # run() binds `time` to the job's timepoint
 
 import numpy as np
 
+# The plate run keeps five HIP streams busy (two pipelines, the result copies, the uploads and
+# the default stream); with HIP's default of four hardware queues per process two of them share
+# a queue and the pipelines' kernels serialise: kernels of both pipelines ran together 3 % of the
+# time (`profiles/r05ai_plate_overlap_q4.txt`) against 39 % with eight queues
+# (`r05aj_plate_overlap_q8.txt`), 362.8 -> 378.5 FOV/s on 768 FOVs (`r05aj_plate_bench.jsonl`).
+# Set before the process's first HIP call (HIP reads it once); an explicit setting wins.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 log = logging.getLogger("cpx.plate")
 # per job of the last run(): {"job", "fovs", "seconds", "threads", "batch", "pipes"} — decode, upload,
 # GPU pipeline and table assembly, from the first decode to the last recorded site (pipeline
 # construction excluded); the I/O-inclusive throughput of the drop-in (tools/plate_bench.py)
-# (A/B knob) CPX_PLATE_UPLOAD=pipeline: each batch's upload in front of it on its pipeline's own
-# stream (the other pipeline computes meanwhile) instead of the device's upload stream
-UPLOAD_ON_PIPELINE_STREAM = os.environ.get("CPX_PLATE_UPLOAD", "device") == "pipeline"
 LAST_TIMING: list = []
 PARTS = ".parts"
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(prog="python -m cpx.plate", description="GPU per-object measurement of one plate/time")
     ap.add_argument("--load-data", required=True, nargs="+", help="one LoadData CSV per (plate, time) job")
@@ -434,8 +441,7 @@ def _run_sites(a, table, source, chans, state, out, status):
             # stream) never wait behind it; the pipeline's stream waits for it.  pipes[p_i].raw
             # is the staging buffer of the pipeline's next result slot, whose previous batch was
             # fetched (retired) before this one was claimed
-            cs = (streams[p_i] if UPLOAD_ON_PIPELINE_STREAM
-                  else FovPipeline.upload_stream(torch.device("cuda", a.device)))
+            cs = FovPipeline.upload_stream(torch.device("cuda", a.device))
             with torch.cuda.stream(cs):
                 evs[0].record(cs)
                 pipes[p_i].raw.copy_(hosts[p_i], non_blocking=True)
