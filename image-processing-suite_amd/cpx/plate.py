@@ -37,13 +37,17 @@ import time as _time  # run() binds `time` to the job's timepoint
 
 import numpy as np
 
-# The plate run keeps five HIP streams busy (two pipelines, the result copies, the uploads and
-# the default stream); with HIP's default of four hardware queues per process two of them share
-# a queue and the pipelines' kernels serialise: kernels of both pipelines ran together 3 % of the
-# time (`profiles/r05ai_plate_overlap_q4.txt`) against 39 % with eight queues
-# (`r05aj_plate_overlap_q8.txt`), 362.8 -> 378.5 FOV/s on 768 FOVs (`r05aj_plate_bench.jsonl`).
-# Set before the process's first HIP call (HIP reads it once); an explicit setting wins.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# Hardware queues: with HIP's default of four per process the plate run's two pipelines hardly
+# overlap on the GPU — kernels of both ran together 3-5 % of the time, also with the uploads moved
+# onto the result-copy stream (`profiles/r05ai_plate_overlap_q4.txt`, `r05ap_plate_overlap.txt`)
+# — against 39 % with eight (`r05aj_plate_overlap_q8.txt`); plate bench 362.8 -> 378.5 FOV/s on
+# 768 FOVs and 368 -> 391 on 1,536 (means of `r05aj_plate_bench.jsonl`, `r05ap_plate_bench.jsonl`).
+# HIP reads it when the process first uses the GPU, so it takes effect when this module is
+# imported first (`python -m cpx.plate`, cpx.launch's ranks).  A lower value in the environment
+# (the GPU boxes export HIP's default of 4) is raised; CPX_PLATE_HW_QUEUES overrides the 8.
+PLATE_HW_QUEUES = int(os.environ.get("CPX_PLATE_HW_QUEUES", "8"))
+if int(os.environ.get("GPU_MAX_HW_QUEUES") or 4) < PLATE_HW_QUEUES:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(PLATE_HW_QUEUES)
 
 log = logging.getLogger("cpx.plate")
 # per job of the last run(): {"job", "fovs", "seconds", "threads", "batch", "pipes"} — decode, upload,
