@@ -196,6 +196,7 @@ class PlateTables:
         self._pool = None
         self._rows = {t: [] for t in OBJECT_TABLES}  # (ImageNumber, future of bytes)
         self._stream = {}
+        self.streamed = set()  # tables whose file the stream completed (write_objects)
         if eager_csv:
             import concurrent.futures
             self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=CSV_THREADS)
@@ -263,6 +264,7 @@ class PlateTables:
         names = ["ImageNumber", "ObjectNumber", "Number_Object_Number"] + self.cols
         st = self._stream.pop(table, None)
         if st is not None and st.finish(os.path.join(d, f"{table}.csv")):
+            self.streamed.add(table)
             return  # streamed in order, complete
         if self._rows[table] and len(self._rows[table]) == len(self.objects[table]):
             with open(os.path.join(d, f"{table}.csv"), "wb") as f:

@@ -88,6 +88,7 @@ def test_plate_tables_native_equals_pandas_frames(tmp_path, mode):
         t.add_image(img, {"Metadata_Well": "A01"}, [0.1] * 5, [0.0] * 5, {"Nuclei": 1})
     d = t.write(str(tmp_path), "P01", 3)
     t.close()
+    assert t.streamed == (set(csvout.OBJECT_TABLES) if mode == "stream" else set())
     for name, df in t.frames().items():
         df.to_csv(tmp_path / f"{name}.ref.csv", index=False)
         assert open(os.path.join(d, f"{name}.csv"), "rb").read() == open(tmp_path / f"{name}.ref.csv", "rb").read(), name
@@ -111,6 +112,7 @@ def test_streamed_tables_fall_back_when_out_of_order(tmp_path):
         t.add_image(img, {"Metadata_Well": "A01"}, [0.1], [0.0], {"Nuclei": 1})
     d = t.write(str(tmp_path), "P", 1)
     t.close()
+    assert not t.streamed  # every table saw 5 after 7: rewritten sorted
     for name, df in t.frames().items():
         df.to_csv(tmp_path / f"{name}.ref.csv", index=False)
         assert open(os.path.join(d, f"{name}.csv"), "rb").read() == open(tmp_path / f"{name}.ref.csv", "rb").read()
