@@ -329,22 +329,36 @@ class FovPipeline:
         if (sovf & SEG_ERR_INTERNAL).any():
             raise RuntimeError("cpx_seg_masks: a flow-error work loop reached its claim bound "
                                "(CPX_SEG_ERR_INTERNAL): the batch's masks are invalid")
-        nmax = {s: min(ML, max(int(hdrs[s]["n_objects"].max()) if B else 0, 1)) for s in OBJECT_SETS}
+        # only each FOV's own rows cross PCIe: the rows are gathered on the device into one
+        # contiguous block per table (one D2H each) instead of copying [:, :max n] of every FOV
+        # (~30 % padding rows: each FOV has its own object count)
+        n_bs = {s: np.minimum(hdrs[s]["n_objects"].astype(np.int64), ML) for s in OBJECT_SETS}
+        keep = []  # device index tensors and their pinned sources, alive until the copies end
         with torch.cuda.stream(cs):
             for s in OBJECT_SETS:
-                n = nmax[s]
-                hb["feats"][s][:B * n * F].view(B, n, F).copy_(sl["feats"][s][:, :n], non_blocking=True)
-                hb["objects"][s][:B * n * 56].view(B, n * 56).copy_(
-                    sl["objects"][s].view(B, ML * 56)[:, :n * 56], non_blocking=True)
+                n_b = n_bs[s]
+                tot = int(n_b.sum())
+                if tot == 0:
+                    continue
+                rows = np.concatenate([b * ML + np.arange(n_b[b], dtype=np.int64) for b in range(B)])
+                src = torch.from_numpy(rows).pin_memory()
+                idx = src.to(self.dev.torch_device, non_blocking=True)
+                fg = sl["feats"][s].view(B * ML, F).index_select(0, idx)
+                og = sl["objects"][s].view(B * ML, 56).index_select(0, idx)
+                hb["feats"][s][:tot * F].view(tot, F).copy_(fg, non_blocking=True)
+                hb["objects"][s][:tot * 56].view(tot, 56).copy_(og, non_blocking=True)
+                keep.append((src, idx, fg, og))
         _sync_after(cs)
+        del keep
         objs, feats = {}, {}
         for s in OBJECT_SETS:
-            n_b = np.minimum(hdrs[s]["n_objects"].astype(int), ML)
-            n = nmax[s]
-            f = hb["feats"][s][:B * n * F].view(B, n, F).numpy()
-            o = as_numpy(hb["objects"][s][:B * n * 56], "object").reshape(B, n)
-            feats[s] = [f[b, : n_b[b]].copy() for b in range(B)]
-            objs[s] = [o[b, : n_b[b]].copy() for b in range(B)]
+            n_b = n_bs[s]
+            tot = int(n_b.sum())
+            off = np.concatenate([[0], np.cumsum(n_b)])
+            f = hb["feats"][s][:tot * F].view(tot, F).numpy()
+            o = as_numpy(hb["objects"][s][:max(tot, 1) * 56], "object")[:tot]
+            feats[s] = [f[off[b]:off[b + 1]].copy() for b in range(B)]
+            objs[s] = [o[off[b]:off[b + 1]].copy() for b in range(B)]
         nt = self.seg.geom.n_tiles
         ovf = hb["cpnet_ovf"][:B * nt].numpy().reshape(B, nt).any(axis=1)
         failed = np.zeros(B, dtype=bool)
