@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--pipes", type=int, default=2,
                     help="pipelines (own libcpx context, buffers and HIP stream) per GPU: step i "
                          "runs on pipeline i %% pipes, so that many batches are in flight")
+    ap.add_argument("--cu-split", choices=("auto", "none", "interleave", "halves"), default=None,
+                    help="each pipeline's stream restricted to its own share of the CUs "
+                         "(cpx.device.pipeline_streams; default CPX_CU_SPLIT or auto: halves for "
+                         "two pipelines)")
     ap.add_argument("--cpnet-precision", choices=("f16x3", "bf16", "fp32"), default="f16x3",
                     help="CPnet arithmetic: f16x3 = native split-fp16 MFMA kernels at the fp32 network's "
                          "accuracy (default: the reference's precision, masks and IDs identical to the fp32 "
@@ -108,7 +112,8 @@ def main():
     # P pipelines, each with its own libcpx context (workspaces), buffers and HIP stream: the
     # kernels of one batch fill the gaps of the other (many post-processing / feature kernels
     # do not fill 256 CUs on their own)
-    streams = [torch.cuda.Stream(device=td) for _ in range(max(1, a.pipes))]
+    from cpx.device import pipeline_streams
+    streams = pipeline_streams(td, max(1, a.pipes), a.cu_split)
     pipes = []
     for p_i, st in enumerate(streams):
         with torch.cuda.stream(st):

@@ -7,6 +7,7 @@ copies.  All per-FOV arithmetic runs in the hand-written HIP kernels of libcpx.
 from __future__ import annotations
 
 import ctypes as ct
+import os
 
 import torch
 
@@ -240,6 +241,45 @@ class Device:
         check(self.lib.cpx_features_pair(self.h, _ptr(cells), _ptr(cyto), _ptr(corr), B, C, H, W, max_label,
                                          *(_ptr(t) for t in cells_tab), *(_ptr(t) for t in cyto_tab)),
               "cpx_features_pair")
+
+
+# Pipeline streams with their own CUs (round 5): two pipelines whose streams each hold a CU mask
+# of one contiguous half of the GPU's CUs (hipExtStreamCreateWithCUMask) ran the bench 0.8-0.9 %
+# faster than two unrestricted streams, four of four same-box pairs (`gpurun_out/r05as`,
+# `r05at`: 457.0 -> 461.1 FOV/s): the two batches' kernels stop evicting each other from the
+# CUs' LDS and L2 while the stage exclusivity (pipeline.STAGE_EXCLUSIVE) still keeps their CPnets
+# apart; interleaved CUs measured no better than none, dropping the exclusivity 2 % worse,
+# three pipelines in thirds 18 % worse.  CPX_CU_SPLIT=none|halves|interleave overrides.
+CU_SPLIT = os.environ.get("CPX_CU_SPLIT", "auto")
+
+
+def pipeline_streams(device, n: int, split: str | None = None) -> list:
+    """HIP streams for n pipelines on `device`: with split "halves" (the default for n == 2) each
+    stream is restricted to a contiguous 1/n of the CUs, "interleave" to every n-th CU, "none"
+    plain torch streams."""
+    td = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+    split = split or CU_SPLIT
+    if split == "auto":
+        split = "halves" if n == 2 else "none"
+    if split == "none" or n < 2:
+        return [torch.cuda.Stream(device=td) for _ in range(n)]
+    if split not in ("halves", "interleave"):
+        raise ValueError(f"CPX_CU_SPLIT: {split!r}")
+    n_cu = torch.cuda.get_device_properties(td).multi_processor_count
+    hip = ct.CDLL("libamdhip64.so")
+    out = []
+    with torch.cuda.device(td):
+        for p in range(n):
+            words = (ct.c_uint32 * ((n_cu + 31) // 32))()
+            for i in range(n_cu):
+                if (i % n == p) if split == "interleave" else (i * n // n_cu == p):
+                    words[i // 32] |= 1 << (i % 32)
+            h = ct.c_void_p()
+            rc = hip.hipExtStreamCreateWithCUMask(ct.byref(h), ct.c_uint32(len(words)), words)
+            if rc != 0:
+                raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+            out.append(torch.cuda.ExternalStream(h.value, device=td))
+    return out
 
 
 def n_features(C: int) -> int:

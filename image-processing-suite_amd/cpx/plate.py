@@ -346,9 +346,9 @@ def _run_sites(a, table, source, chans, state, out, status):
         if a.ws_rounds:
             cfg.ws_rounds = tuple(a.ws_rounds)
         illum = _illum(a.illum_path, chans, H, W)
+        from .device import pipeline_streams
         streams, pipes = [], []
-        for _ in range(max(1, a.pipes)):
-            st = torch.cuda.Stream(device=torch.device("cuda", a.device))
+        for st in pipeline_streams(a.device, max(1, a.pipes)):
             with torch.cuda.stream(st):
                 pipes.append(FovPipeline(Device(a.device), cfg, illum))
             streams.append(st)
