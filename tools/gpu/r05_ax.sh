@@ -1,0 +1,11 @@
+# Round 5: closing rehearsal of the final tree: smoke() and the whole -m gpu suite.
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r05ax
+mkdir -p $O
+cd $R
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+tail -1 $O/smoke.log
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+tail -1 $O/tests.log
+echo done
