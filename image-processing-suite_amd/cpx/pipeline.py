@@ -181,9 +181,10 @@ class FovPipeline:
 
     @staticmethod
     def upload_stream(device: torch.device) -> torch.cuda.Stream:
-        """One host-to-device upload stream per device (cpx.plate's staging uploads): with the
-        two pipeline streams and the result-copy stream that is four streams, one hardware queue
-        each (GPU_MAX_HW_QUEUES = 4), and a result fetch never queues behind an upload."""
+        """One host-to-device upload stream per device (cpx.plate's staging uploads), so a result
+        fetch never queues behind an upload.  With the two pipeline streams, the result-copy
+        stream and the default stream the plate process holds five streams: cpx.plate raises
+        GPU_MAX_HW_QUEUES to 8 so that no two of them share a hardware queue."""
         key = torch.device(device).index
         if key not in FovPipeline._upload_streams:
             FovPipeline._upload_streams[key] = torch.cuda.Stream(device=device)
