@@ -23,9 +23,12 @@ def _same(a, b):
 
 
 @pytest.mark.gpu
-def test_two_streams_match_serial():
+@pytest.mark.parametrize("split", ["none", "halves"])
+def test_two_streams_match_serial(split):
+    """split "halves": the product default (cpx.device.pipeline_streams), each stream on its own
+    half of the CUs by a CU mask."""
     import torch
-    from cpx.device import Device
+    from cpx.device import Device, pipeline_streams
     from cpx.pipeline import FovPipeline, PipelineConfig
     from cpx.synth import synth_fovs, synth_illum
     H = W = 1040
@@ -33,7 +36,7 @@ def test_two_streams_match_serial():
     w = os.path.join(REPO, "image-processing-suite_amd", "cpx", "weights", "cpnet_nuclei_synth.pt")
     illum = synth_illum(C, H, W, seed=1)
     cfg = PipelineConfig(H=H, W=W, C=C, batch=B, weights=w, max_objects=512)
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    streams = pipeline_streams(0, 2, split)
     pipes = []
     for st in streams:
         with torch.cuda.stream(st):
