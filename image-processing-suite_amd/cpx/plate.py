@@ -348,7 +348,11 @@ def _run_sites(a, table, source, chans, state, out, status):
         illum = _illum(a.illum_path, chans, H, W)
         from .device import pipeline_streams
         streams, pipes = [], []
-        for st in pipeline_streams(a.device, max(1, a.pipes)):
+        # unrestricted CUs here unless CPX_CU_SPLIT says otherwise: with its uploads and result
+        # copies beside the pipelines the plate measured 372-389 FOV/s with CU-split streams
+        # against 367-403 without (`gpurun_out/r05au`, `r05az`; the bench gains from the split)
+        split = None if "CPX_CU_SPLIT" in os.environ else "none"
+        for st in pipeline_streams(a.device, max(1, a.pipes), split):
             with torch.cuda.stream(st):
                 pipes.append(FovPipeline(Device(a.device), cfg, illum))
             streams.append(st)
