@@ -85,6 +85,8 @@ SIGNATURES = {
     "cpx_last_error": (ct.c_char_p, []),
     "cpx_set_stream": (_I, [_P, _P]),
     "cpx_sync": (_I, [_P]),
+    "cpx_stream_create_cu_mask": (_I, [_I, _P, _I, _P]),
+    "cpx_stream_destroy": (_I, [_P]),
     "cpx_reserve": (_I, [_P, _I, _I, _I, _I, _I]),
     "cpx_illum_correct": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "cpx_qc_rps": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),

@@ -140,11 +140,14 @@ class _TableStream:
         import queue
         import threading
         os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        # the rows go to a hidden partial file that finish() renames onto `path`: a job that
+        # fails or is killed leaves no truncated <table>.csv for a downstream step to ingest
         self.path = path
+        self.partial = os.path.join(os.path.dirname(path), f".{os.path.basename(path)}.partial")
         self.q = queue.Queue()
         self.last = None
         self.ordered = True
-        self.f = open(path, "wb")
+        self.f = open(self.partial, "wb")
         self.f.write((",".join(names) + "\n").encode())
         self.t = threading.Thread(target=self._run, daemon=True)
         self.t.start()
@@ -167,16 +170,29 @@ class _TableStream:
                 break
 
     def finish(self, path: str) -> bool:
+        """Complete and ordered for `path`: the partial file becomes `path` (True); otherwise it
+        is removed and the caller writes the table itself (False)."""
         self.q.put(None)
         self.t.join()
         self.f.close()
-        return self.ordered and os.path.abspath(path) == os.path.abspath(self.path)
+        if self.ordered and os.path.abspath(path) == os.path.abspath(self.path):
+            os.replace(self.partial, self.path)
+            return True
+        self._remove()
+        return False
 
     def abort(self):
         self.q.put(None)
         self.t.join()
         if not self.f.closed:
             self.f.close()
+        self._remove()
+
+    def _remove(self):
+        try:
+            os.remove(self.partial)
+        except FileNotFoundError:
+            pass
 
 
 class PlateTables:

@@ -6,6 +6,7 @@ copies.  All per-FOV arithmetic runs in the hand-written HIP kernels of libcpx.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as ct
 import os
 
@@ -253,37 +254,66 @@ class Device:
 CU_SPLIT = os.environ.get("CPX_CU_SPLIT", "auto")
 
 
+class _MaskedStreams:
+    """Owner of the CU-masked pipeline streams: created once per (device, n, split) by libcpx
+    (cpx_stream_create_cu_mask — the HIP runtime libcpx and torch share, never a second copy of
+    libamdhip64), handed out as torch ExternalStreams, and destroyed at interpreter exit after
+    their work has drained (each holds a hardware queue; round 5 created a fresh pair per call
+    from ctypes and never released them)."""
+    _cache: dict = {}
+
+    @classmethod
+    def get(cls, td: torch.device, n: int, split: str) -> list:
+        key = (td.index, n, split)
+        if key not in cls._cache:
+            if not cls._cache:
+                atexit.register(cls.release_all)
+            lib = _lib.load()
+            n_cu = torch.cuda.get_device_properties(td).multi_processor_count
+            handles = []
+            try:
+                for p in range(n):
+                    words = (ct.c_uint32 * ((n_cu + 31) // 32))()
+                    for i in range(n_cu):
+                        if (i % n == p) if split == "interleave" else (i * n // n_cu == p):
+                            words[i // 32] |= 1 << (i % 32)
+                    h = ct.c_void_p()
+                    check(lib.cpx_stream_create_cu_mask(td.index, words, len(words), ct.byref(h)),
+                          "cpx_stream_create_cu_mask")
+                    handles.append(h.value)
+            except Exception:
+                for h in handles:
+                    lib.cpx_stream_destroy(ct.c_void_p(h))
+                raise
+            cls._cache[key] = (handles, [torch.cuda.ExternalStream(h, device=td) for h in handles])
+        return list(cls._cache[key][1])
+
+    @classmethod
+    def release_all(cls):
+        lib = _lib._lib
+        for handles, _ in cls._cache.values():
+            for h in handles:
+                if lib is not None:
+                    lib.cpx_stream_destroy(ct.c_void_p(h))
+        cls._cache.clear()
+
+
 def pipeline_streams(device, n: int, split: str | None = None) -> list:
     """HIP streams for n pipelines on `device`: with split "halves" (the default for n == 2) each
     stream is restricted to a contiguous 1/n of the CUs, "interleave" to every n-th CU, "none"
-    plain torch streams."""
+    plain torch streams.  The masked streams are shared per (device, n, split) for the process
+    and released at exit (_MaskedStreams)."""
     td = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+    if td.index is None:
+        td = torch.device("cuda", torch.cuda.current_device())
     split = split or CU_SPLIT
     if split == "auto":
         split = "halves" if n == 2 else "none"
-    # under the rocprofv3 tracer (its preloaded SDK) the masked streams are not used: the
-    # two-pipeline kernel trace of the bench segfaulted once they became the default (round 5
-    # profile pass); traces of the two-pipeline bench therefore show unrestricted streams
-    profiled = "rocprofiler-sdk" in os.environ.get("LD_PRELOAD", "") or "ROCPROFILER_LIBRARY_CTOR" in os.environ
-    if split == "none" or n < 2 or profiled:
+    if split == "none" or n < 2:
         return [torch.cuda.Stream(device=td) for _ in range(n)]
     if split not in ("halves", "interleave"):
         raise ValueError(f"CPX_CU_SPLIT: {split!r}")
-    n_cu = torch.cuda.get_device_properties(td).multi_processor_count
-    hip = ct.CDLL("libamdhip64.so")
-    out = []
-    with torch.cuda.device(td):
-        for p in range(n):
-            words = (ct.c_uint32 * ((n_cu + 31) // 32))()
-            for i in range(n_cu):
-                if (i % n == p) if split == "interleave" else (i * n // n_cu == p):
-                    words[i // 32] |= 1 << (i % 32)
-            h = ct.c_void_p()
-            rc = hip.hipExtStreamCreateWithCUMask(ct.byref(h), ct.c_uint32(len(words)), words)
-            if rc != 0:
-                raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
-            out.append(torch.cuda.ExternalStream(h.value, device=td))
-    return out
+    return _MaskedStreams.get(td, n, split)
 
 
 def n_features(C: int) -> int:

@@ -95,7 +95,9 @@ class FovResults:
                                          # CPnet ran in fp32; RECOVER_WS: its watershed needed more
                                          # rounds; RECOVER_CAPACITY: it has more seeds / objects
                                          # than max_objects, so it ran with larger tables; bits
-                                         # combine)
+                                         # combine; RECOVER_FILL_SEQ: not a re-run — a mask lay
+                                         # partly inside an earlier mask's holes, so libcpx ran
+                                         # Cellpose's sequential fill loop for this FOV)
     crops8: dict | None = None           # FOV -> device uint8 [1][ML'][C][box][box]: the a7 crops
                                          # of a re-run FOV (cfg.crops), replacing its batch slot
 
@@ -103,6 +105,7 @@ class FovResults:
 RECOVER_FP32 = 1
 RECOVER_WS = 2
 RECOVER_CAPACITY = 4
+RECOVER_FILL_SEQ = 8
 WS_RETRIES = 4   # at most this many re-runs of a FOV whose watershed did not converge, with 2x,
                  # 4x, 8x, 16x the configured rounds
 REC_CACHE = 4    # single-FOV recovery pipelines kept per process (shared by every pipeline)
@@ -310,7 +313,7 @@ class FovPipeline:
         """Copy one slot's results to the host (default: the last run) and return them.  Waits
         only for that slot's step (its recorded event), with the copies on the device's copy stream, so a
         step enqueued after it keeps the GPU busy meanwhile."""
-        from .segment import SEG_ERR_INTERNAL, SEG_OVF_SEEDS, SEG_STATS_DTYPE
+        from .segment import SEG_ERR_INTERNAL, SEG_OVF_FILL_PARTIAL, SEG_OVF_SEEDS, SEG_STATS_DTYPE
         k = self.cur if slot is None else slot
         sl, hb = self._slots[k], self._host
         B, ML, F = self.cfg.batch, self.cfg.max_objects, self.F
@@ -371,8 +374,11 @@ class FovPipeline:
         need = np.where(sovf & SEG_OVF_SEEDS, seg_stats["n_seeds_found"].ravel()[:B], 0)
         for s in OBJECT_SETS:
             need = np.maximum(need, np.where(hdrs[s]["overflow"] != 0, hdrs[s]["max_label"], 0))
+        # a FOV with a partly absorbed mask already took the sequential fill on the GPU
+        # (k_fill_seq, cpx.h CPX_SEG_OVF_FILL_PARTIAL): its labels are the reference loop's
+        recovered = np.where(sovf & SEG_OVF_FILL_PARTIAL, RECOVER_FILL_SEQ, 0).astype(np.int32)
         res = FovResults(qc=qc, hdr=hdrs, objects=objs, feats=feats, seg_stats=seg_stats, failed=failed,
-                         recovered=np.zeros(B, dtype=np.int32))
+                         recovered=recovered)
         if self._recovery and (ovf.any() or failed.any() or (need > ML).any()):
             self._recover(sl["raw"], res, ovf, failed, need)
         elif (need > ML).any():
@@ -436,6 +442,7 @@ class FovPipeline:
                 while True:
                     rp = self._recovery_pipe(precision, ml)
                     rp.ws_rounds = rounds
+                    rp.illum = self.illum  # the cached pipeline may have been built for another flat-field
                     rp.raw.copy_(raw[b * C:(b + 1) * C])
                     r1 = rp.fetch(rp.run())
                     if not r1.failed[0] or doublings >= WS_RETRIES:
@@ -452,7 +459,7 @@ class FovPipeline:
                     res.feats[s][b] = r1.feats[s][0]
                 res.seg_stats[b] = r1.seg_stats[0]
                 res.failed[b] = bool(r1.failed[0])
-                res.recovered[b] = flag
+                res.recovered[b] = flag | (RECOVER_FILL_SEQ if r1.recovered[0] & RECOVER_FILL_SEQ else 0)
                 if self.cfg.crops:
                     if res.crops8 is None:
                         res.crops8 = {}

@@ -258,26 +258,30 @@ def run(argv=None):
         out = PlateTables(chans, eager_csv=a.world == 1,
                           stream_dir=job_dir(a.out, plate, time) if a.world == 1 else None)
         status = []  # per site: the reference's results_dict entry (Cellpose_GPU_s3fs.py:123-125,219-223)
-        nsites = _run_sites(a, table, batch_source(table, a, ji), chans, state, out, status)
-        if nsites:
-            LAST_TIMING.append({"job": os.path.basename(load_data), "fovs": nsites, **state["timing"]})
         d = job_dir(a.out, plate, time)
-        site_status = pd.DataFrame(status, columns=["ImageNumber", "status", "n_cells"]) \
-            .sort_values("ImageNumber", kind="stable").reset_index(drop=True)
-        t_csv = _time.perf_counter()
-        if a.world > 1:
-            frames = out.frames()
-            frames["site_status"] = site_status
-            write_part(d, a.rank, a.world, frames)
-        else:
-            os.makedirs(d, exist_ok=True)
-            frames = out.frames(objects=False)
-            frames["site_status"] = site_status
-            for name, df in frames.items():
-                df.to_csv(os.path.join(d, f"{name}.csv"), index=False)
-            for t in OBJECT_SETS:  # the object tables, natively formatted (csvout.format_object_rows)
-                out.write_objects(d, t)
-        out.close()
+        try:
+            nsites = _run_sites(a, table, batch_source(table, a, ji), chans, state, out, status)
+            if nsites:
+                LAST_TIMING.append({"job": os.path.basename(load_data), "fovs": nsites, **state["timing"]})
+            site_status = pd.DataFrame(status, columns=["ImageNumber", "status", "n_cells"]) \
+                .sort_values("ImageNumber", kind="stable").reset_index(drop=True)
+            t_csv = _time.perf_counter()
+            if a.world > 1:
+                frames = out.frames()
+                frames["site_status"] = site_status
+                write_part(d, a.rank, a.world, frames)
+            else:
+                os.makedirs(d, exist_ok=True)
+                frames = out.frames(objects=False)
+                frames["site_status"] = site_status
+                for name, df in frames.items():
+                    df.to_csv(os.path.join(d, f"{name}.csv"), index=False)
+                for t in OBJECT_SETS:  # the object tables, natively formatted (csvout.format_object_rows)
+                    out.write_objects(d, t)
+        finally:
+            # on an error: the streamed partial tables are removed and the writer threads and
+            # format pool stopped, so a failed job leaves no truncated object CSV behind
+            out.close()
         if LAST_TIMING and nsites:
             LAST_TIMING[-1]["tables_write_s"] = round(_time.perf_counter() - t_csv, 3)
         log.info("rank %d/%d: %d sites of %s/%s -> %s", a.rank, a.world, nsites, plate, time, d)

@@ -61,7 +61,7 @@ SEG_STATS_DTYPE = np.dtype([("n_moving", "i4"), ("n_seeds", "i4"), ("n_masks", "
                             ("n_fill_partial", "i4"), ("_reserved", "i4", (3,))])
 SEG_STATS_BYTES = 48
 assert SEG_STATS_DTYPE.itemsize == SEG_STATS_BYTES
-SEG_OVF_FILL_PARTIAL = 2  # cpx.h CPX_SEG_OVF_FILL_PARTIAL: a partly absorbed mask (fill approximation)
+SEG_OVF_FILL_PARTIAL = 2  # cpx.h CPX_SEG_OVF_FILL_PARTIAL: a partly absorbed mask; the FOV took the sequential fill
 SEG_OVF_SEEDS = 1        # cpx.h CPX_SEG_OVF_SEEDS: more seeds than max_objects (re-run with more)
 SEG_ERR_INTERNAL = 8     # cpx.h CPX_SEG_ERR_INTERNAL: a flow-error work loop hit its claim bound
 

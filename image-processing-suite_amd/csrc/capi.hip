@@ -131,6 +131,29 @@ int cpx_sync(cpx_ctx* ctx) {
   return CPX_OK;
 }
 
+int cpx_stream_create_cu_mask(int device, const uint32_t* cu_mask, int n_words, void** out) {
+  CPX_REQUIRE(cu_mask && out && n_words > 0, CPX_ERR_ARG, "cpx_stream_create_cu_mask: bad argument");
+  int n = 0;
+  CPX_CHECK_HIP(hipGetDeviceCount(&n));
+  CPX_REQUIRE(device >= 0 && device < n, CPX_ERR_ARG, "cpx_stream_create_cu_mask: device %d of %d", device, n);
+  int prev = 0;
+  CPX_CHECK_HIP(hipGetDevice(&prev));
+  CPX_CHECK_HIP(hipSetDevice(device));
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, cu_mask);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) return cpx_hip_fail(e, "hipExtStreamCreateWithCUMask");
+  *out = (void*)s;
+  return CPX_OK;
+}
+
+int cpx_stream_destroy(void* stream) {
+  CPX_REQUIRE(stream != nullptr, CPX_ERR_ARG, "cpx_stream_destroy: stream is NULL");
+  CPX_CHECK_HIP(hipStreamSynchronize((hipStream_t)stream));
+  CPX_CHECK_HIP(hipStreamDestroy((hipStream_t)stream));
+  return CPX_OK;
+}
+
 }  // extern "C"
 
 extern "C" int cpx_reserve(cpx_ctx* ctx, int max_planes, int H, int W, int max_fovs,

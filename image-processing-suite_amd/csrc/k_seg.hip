@@ -1851,29 +1851,42 @@ __device__ __forceinline__ void fill_st(unsigned int* p, unsigned int v) {
   else *p = v;
 }
 
-template <bool G>
-__device__ __forceinline__ void fill_one(const int* __restrict__ lab, int W, int max_label, int k,
-                                         const cpx_object& o, unsigned int* own, unsigned int* reach,
-                                         const int* __restrict__ l2i, int* __restrict__ fillidx,
-                                         int* __restrict__ absorber) {
-  const int r0 = o.bbox[0], c0 = o.bbox[1];
-  const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
+// The bbox bitmasks of label `lab_k` (own) and the seeds of the border flood (reach: border pixels
+// outside the mask); returns this thread's count of mask pixels.  L: label loads at agent scope
+// (k_fill_seq re-reads pixels its own block rewrote, which a plain load could take from a stale L1 line).
+template <bool G, bool L>
+__device__ __forceinline__ int fill_bits(const int* __restrict__ lab, int W, int lab_k, int r0, int c0,
+                                         int bh, int bw, unsigned int* own, unsigned int* reach) {
   const int wpr = (bw + 31) / 32;
   const int nw = wpr * bh;
+  int cnt = 0;
   for (int w = threadIdx.x; w < nw; w += blockDim.x) {
     const int r = w / wpr, cw = w - r * wpr;
     unsigned int bits = 0, rb = 0;
     for (int b = 0; b < 32; ++b) {
       const int c = cw * 32 + b;
       if (c >= bw) break;
-      const bool in = lab[(long long)(r0 + r) * W + c0 + c] == o.label;
+      const int* p = lab + (long long)(r0 + r) * W + c0 + c;
+      const int v = L ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+      const bool in = v == lab_k;
       bits |= (unsigned int)in << b;
       const bool border = (r == 0 || r == bh - 1 || c == 0 || c == bw - 1);
       rb |= (unsigned int)(border && !in) << b;
     }
     fill_st<G>(own + w, bits);
     fill_st<G>(reach + w, rb);
+    cnt += __popc(bits);
   }
+  return cnt;
+}
+
+// Flood the bbox's non-mask pixels from the border seeds in `reach` (4-connectivity, the
+// background structure of ndi.binary_fill_holes); afterwards the holes are ~own & ~reach.
+// Block-uniform; starts and ends with a barrier.
+template <bool G>
+__device__ __forceinline__ void fill_flood(const unsigned int* own, unsigned int* reach, int bh, int bw) {
+  const int wpr = (bw + 31) / 32;
+  const int nw = wpr * bh;
   if (G) __threadfence();
   __syncthreads();
   // flood in place until stable (a stale neighbour read only delays a change to a later
@@ -1902,6 +1915,19 @@ __device__ __forceinline__ void fill_one(const int* __restrict__ lab, int W, int
     // broke out early: an incomplete flood, barriers out of step)
     if (!__syncthreads_or(ch)) break;
   }
+}
+
+template <bool G>
+__device__ __forceinline__ void fill_one(const int* __restrict__ lab, int W, int max_label, int k,
+                                         const cpx_object& o, unsigned int* own, unsigned int* reach,
+                                         const int* __restrict__ l2i, int* __restrict__ fillidx,
+                                         int* __restrict__ absorber) {
+  const int r0 = o.bbox[0], c0 = o.bbox[1];
+  const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
+  const int wpr = (bw + 31) / 32;
+  const int nw = wpr * bh;
+  fill_bits<G, false>(lab, W, o.label, r0, c0, bh, bw, own, reach);
+  fill_flood<G>(own, reach, bh, bw);
   // holes: free and unreached; mark fill owner and absorbed objects
   for (int w = threadIdx.x; w < nw; w += blockDim.x) {
     const int r = w / wpr, cw = w - r * wpr;
@@ -1961,26 +1987,56 @@ __global__ __launch_bounds__(1024) void k_fill_holes_big(
   }
 }
 
-// one block per FOV: kept flags + sequential new labels
+// One block per FOV: kept flags + sequential new labels, and the check that the parallel fill is
+// exact for this FOV.  It is when every mask is, at its turn in the reference's loop, either
+// untouched or wholly overwritten by the earlier masks' fills: then each kept mask fills the holes
+// of its original shape, as k_fill_holes computed them.  A mask of >= min_size pixels some of whose
+// pixels lie in an earlier mask's holes (absorber < k) is checked pixel by pixel: a pixel with
+// no covering fill (fillidx 0), or whose last covering fill is a later mask's (fillidx > k + 1:
+// an earlier cover is then undecided), makes the FOV take k_fill_seq instead
+// (CPX_SEG_OVF_FILL_PARTIAL; n_fill_partial = such masks).  Smaller masks need no check: the
+// reference clears their remainder and they never fill, as here.
 __global__ __launch_bounds__(1024) void k_fill_final(int max_label, int min_size,
                                                      const cpx_object* __restrict__ objects,
                                                      const cpx_fov_objects* __restrict__ hdr,
                                                      const int* __restrict__ absorber,
+                                                     const int* __restrict__ labels,
+                                                     const int* __restrict__ fillidx, int W, long long N,
                                                      int* __restrict__ newlab,
                                                      cpx_seg_stats* __restrict__ st) {
   const int fov = blockIdx.x;
   const int n = hdr[fov].n_objects;
   __shared__ int wsum[16];
-  __shared__ int base;
-  if (threadIdx.x == 0) base = 0;
+  __shared__ int base, npart;
+  if (threadIdx.x == 0) base = npart = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int* lab = labels + (long long)fov * N;
+  const int* fid = fillidx + (long long)fov * N;
   for (int k0 = 0; k0 < n; k0 += blockDim.x) {
     const int k = k0 + threadIdx.x;
-    int kept = 0;
+    int kept = 0, check = 0;
     if (k < n) {
       const cpx_object o = objects[(long long)fov * max_label + k];
-      kept = o.area >= min_size && !(absorber[(long long)fov * max_label + k] < k);
+      const bool absorbed = absorber[(long long)fov * max_label + k] < k;
+      kept = o.area >= min_size && !absorbed;
+      check = o.area >= min_size && absorbed;
+    }
+    // each wave checks its own absorbed masks (rare) over their bboxes, lanes across the columns
+    for (unsigned long long cb = __ballot(check); cb; cb &= cb - 1) {
+      const int kk = k0 + wid * 64 + __ffsll((long long)cb) - 1;
+      const cpx_object o = objects[(long long)fov * max_label + kk];
+      const int bw = o.bbox[3] - o.bbox[1];
+      int bad = 0;
+      for (int r = o.bbox[0]; r < o.bbox[2] && !bad; ++r) {
+        for (int c = lane; c < bw; c += 64) {
+          const long long q = (long long)r * W + o.bbox[1] + c;
+          const int f = fid[q];
+          bad |= lab[q] == o.label && (f == 0 || f > kk + 1);
+        }
+        bad = __any(bad);
+      }
+      if (bad && lane == 0) atomicAdd(&npart, 1);
     }
     const unsigned long long b = __ballot(kept);
     const unsigned long long lower = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -1997,29 +2053,32 @@ __global__ __launch_bounds__(1024) void k_fill_final(int max_label, int min_size
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) st[fov].n_final = base;
+  if (threadIdx.x == 0) {
+    st[fov].n_final = base;
+    if (npart) {
+      st[fov].n_fill_partial = npart;
+      st[fov].overflow |= CPX_SEG_OVF_FILL_PARTIAL;
+    }
+  }
 }
 
 // Final labels: a pixel takes the new label of the last kept mask whose holes cover it (masks
 // fill in label order, the later fill wins), else its own mask's if kept.  A filler that is not
 // kept was itself inside an earlier mask's holes (absorbed), and so is everything its holes
 // cover: the chain filler -> absorber[filler] leads to the mask whose fill the reference leaves
-// there (tests/test_gpu_capacity.py: holes inside a mask inside a ring).  A pixel of an absorbed
-// mask that no kept fill covers (the mask was only partly inside the earlier holes — disconnected
-// or diagonal-touching masks) is 0 here, where the reference's sequential loop keeps the rest of
-// that mask if it still has min_size pixels: counted in n_fill_partial (CPX_SEG_OVF_FILL_PARTIAL).
+// there (tests/test_gpu_capacity.py: holes inside a mask inside a ring).  FOVs that k_fill_final
+// flagged (a mask partly inside an earlier mask's holes) are left to k_fill_seq.
 __global__ __launch_bounds__(kT) void k_fill_apply(int* __restrict__ labels, long long n, int max_label,
                                                    const int* __restrict__ lab2idx,
                                                    const int* __restrict__ fillidx,
                                                    const int* __restrict__ newlab,
                                                    const int* __restrict__ absorber,
-                                                   const cpx_object* __restrict__ objects, int min_size,
-                                                   cpx_seg_stats* __restrict__ st) {
+                                                   const cpx_seg_stats* __restrict__ st) {
   const int fov = blockIdx.y;
+  if (st[fov].overflow & CPX_SEG_OVF_FILL_PARTIAL) return;
   const int* l2i = lab2idx + (long long)fov * (max_label + 1);
   const int* nl = newlab + (long long)fov * max_label;
   const int* ab = absorber + (long long)fov * max_label;
-  int partial = 0;
   // four independent pixels per iteration: their dependent lookups (label -> index -> new
   // label) overlap instead of one chain of loads at a time
   const long long stride = (long long)gridDim.x * kT;
@@ -2051,15 +2110,74 @@ __global__ __launch_bounds__(kT) void k_fill_apply(int* __restrict__ labels, lon
       if (q >= n) continue;
       const int best = max(cand[u], fk[u]);
       labels[(long long)fov * n + q] = best ? nl[best - 1] : 0;
-      partial += !best && k[u] >= 0 && ab[k[u]] < k[u] &&
-                 objects[(long long)fov * max_label + k[u]].area >= min_size;
     }
   }
-  partial = wave_sum(partial);
-  if ((threadIdx.x & 63) == 0 && partial) {
-    atomicAdd(&st[fov].n_fill_partial, partial);
-    atomicOr(&st[fov].overflow, CPX_SEG_OVF_FILL_PARTIAL);
+}
+
+// The reference's own loop for the FOVs k_fill_final flagged: utils.fill_holes_and_remove_small_masks
+// restated literally (oracle/seg_oracle.py:376-391, Cellpose_GPU_s3fs.py:143) — the masks in label
+// order over the find_objects boxes of the pre-fill labels, each taking the pixels that still
+// carry its label: fewer than min_size are cleared, otherwise its holes are filled and the mask
+// relabelled j + 1 (j + 1 <= its own label, so no later mask's pixels are confused with it).  One
+// block per FOV, in place; the labels are re-read at agent scope after the block's own stores.
+// Bitmasks in LDS, or in the per-FOV global scratch for bboxes beyond kFillMaxWords.
+__global__ __launch_bounds__(1024) void k_fill_seq(int* __restrict__ labels, int H, int W, int max_label,
+                                                   int min_size, const cpx_object* __restrict__ objects,
+                                                   const cpx_fov_objects* __restrict__ hdr,
+                                                   unsigned int* __restrict__ scratch,
+                                                   cpx_seg_stats* __restrict__ st) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int wcnt[16];
+  const int fov = blockIdx.x;
+  if (!(st[fov].overflow & CPX_SEG_OVF_FILL_PARTIAL)) return;
+  int* lab = labels + (long long)fov * H * W;
+  const long long per = (long long)((W + 31) / 32) * H;
+  const int nobj = hdr[fov].n_objects;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  int j = 0;
+  for (int k = 0; k < nobj; ++k) {
+    const cpx_object o = objects[(long long)fov * max_label + k];
+    const int r0 = o.bbox[0], c0 = o.bbox[1];
+    const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
+    const int wpr = (bw + 31) / 32, nw = wpr * bh;
+    const bool g = nw > kFillMaxWords;
+    unsigned int* own = g ? scratch + (long long)fov * 2 * per : reinterpret_cast<unsigned int*>(smem);
+    unsigned int* reach = g ? own + per : own + kFillMaxWords;
+    int cnt = g ? fill_bits<true, true>(lab, W, o.label, r0, c0, bh, bw, own, reach)
+                : fill_bits<false, true>(lab, W, o.label, r0, c0, bh, bw, own, reach);
+    cnt = wave_sum(cnt);
+    if (lane == 0) wcnt[wid] = cnt;
+    __syncthreads();
+    int npix = 0;
+    for (int w = 0; w < nwv; ++w) npix += wcnt[w];
+    __syncthreads();  // (wcnt is rewritten for the next mask)
+    if (npix == 0) continue;
+    const bool clear = min_size > 0 && npix < min_size;
+    if (!clear) {
+      if (g) fill_flood<true>(own, reach, bh, bw);
+      else fill_flood<false>(own, reach, bh, bw);
+    } else if (g) {
+      __threadfence();
+    }
+    __syncthreads();
+    const int v = clear ? 0 : j + 1;
+    for (int w = threadIdx.x; w < nw; w += blockDim.x) {
+      const int r = w / wpr, cw = w - r * wpr;
+      const unsigned int valid = (cw == wpr - 1 && (bw & 31)) ? ((1u << (bw & 31)) - 1u) : 0xffffffffu;
+      const unsigned int ow = g ? fill_ld<true>(own + w) : own[w];
+      const unsigned int rw = clear ? 0xffffffffu : (g ? fill_ld<true>(reach + w) : reach[w]);
+      unsigned int set = (ow | (~ow & ~rw)) & valid;
+      while (set) {
+        const int b = __ffs(set) - 1;
+        set &= set - 1;
+        lab[(long long)(r0 + r) * W + c0 + cw * 32 + b] = v;
+      }
+    }
+    j += !clear;
+    __threadfence();
+    __syncthreads();
   }
+  if (threadIdx.x == 0) st[fov].n_final = j;
 }
 
 void axis_coeffs(int n_src, int n_dst, int* i0, int* i1, float* w) {
@@ -2488,6 +2606,8 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   if (!fattr) {
     CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_fill_holes,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)flds));
+    CPX_CHECK_HIP(hipFuncSetAttribute((const void*)k_fill_seq,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)flds));
     fattr = true;
   }
   hipLaunchKernelGGL(k_fill_holes, dim3(std::max(1, std::min(ML, (2 * ctx->n_cu + B - 1) / B)), B),
@@ -2499,11 +2619,15 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
                      (const cpx_fov_objects*)hdr, (const int*)l2i, fillidx, absorber, fscr);
   hipLaunchKernelGGL(k_fill_final, dim3(B), dim3(1024), 0, ctx->stream, ML, min_size,
                      (const cpx_object*)obj, (const cpx_fov_objects*)hdr, (const int*)absorber,
-                     newlab, stats_dev);
+                     (const int*)labels_dev, (const int*)fillidx, W, N, newlab, stats_dev);
   hipLaunchKernelGGL(k_fill_apply, dim3(std::max(1, std::min(cpx_div_up(N, kT), 4 * ctx->n_cu / B + 1)), B),
                      dim3(kT), 0, ctx->stream, labels_dev, N, ML, (const int*)l2i,
                      (const int*)fillidx, (const int*)newlab, (const int*)absorber,
-                     (const cpx_object*)obj, min_size, stats_dev);
+                     (const cpx_seg_stats*)stats_dev);
+  // the flagged FOVs (none on the bench plates): the reference's sequential loop, one block each;
+  // the others' blocks exit at once
+  hipLaunchKernelGGL(k_fill_seq, dim3(B), dim3(1024), flds, ctx->stream, labels_dev, H, W, ML, min_size,
+                     (const cpx_object*)obj, (const cpx_fov_objects*)hdr, fscr, stats_dev);
   CPX_CHECK_LAUNCH("cpx_seg_masks fill holes");
   return CPX_OK;
 }

@@ -146,6 +146,14 @@ const char* cpx_last_error(void);
  * ordered.                                                                                  */
 int cpx_set_stream(cpx_ctx* ctx, void* hip_stream);
 int cpx_sync(cpx_ctx* ctx);
+/* A HIP stream on `device` restricted to the CUs set in cu_mask (n_words 32-bit words, bit i =
+ * CU i; hipExtStreamCreateWithCUMask), created by libcpx's own HIP runtime — the one the
+ * context's launches use — so the handle is valid for cpx_set_stream.  One pipeline per stream
+ * (the host's per-GPU batches in flight; no reference counterpart: the reference
+ * runs one consumer per GPU, Cellpose_GPU_s3fs.py:97).  The caller owns the stream and releases
+ * it with cpx_stream_destroy (which waits for its work first).                                */
+int cpx_stream_create_cu_mask(int device, const uint32_t* cu_mask, int n_words, void** out);
+int cpx_stream_destroy(void* stream);
 /* Pre-size internal workspaces (so a later hipGraph capture performs no allocation). */
 int cpx_reserve(cpx_ctx* ctx, int max_planes, int H, int W, int max_fovs, int max_label);
 
@@ -333,7 +341,7 @@ typedef struct cpx_seg_stats {
   int32_t overflow;   /* CPX_SEG_OVF_* bits; 0 = the labels are complete                       */
   int32_t cells_status; /* written by cpx_watershed_cells when pointed here (else untouched)     */
   int32_t n_seeds_found; /* histogram maxima found (n_seeds is min(found, max_objects))          */
-  int32_t n_fill_partial; /* pixels of CPX_SEG_OVF_FILL_PARTIAL masks (see below)                   */
+  int32_t n_fill_partial; /* masks partly inside earlier holes (CPX_SEG_OVF_FILL_PARTIAL, below)   */
   int32_t _reserved[3];
 } cpx_seg_stats;      /* 48 bytes */
 
@@ -342,10 +350,11 @@ typedef struct cpx_seg_stats {
  *   CPX_SEG_OVF_SEEDS  more seeds than max_objects were found: only the first max_objects (raster
  *                      order) were expanded, so masks are missing; re-run the FOV with
  *                      max_objects >= n_seeds_found (masks <= seeds: that run cannot overflow).
- *   CPX_SEG_OVF_FILL_PARTIAL a mask lay partly (not wholly) inside an earlier mask's filled holes:
- *                      the reference's sequential fill keeps the rest of it if it still has
- *                      min_size pixels, libcpx's parallel fill removes it (n_fill_partial pixels;
- *                      disconnected / diagonal-touching masks only).
+ *   CPX_SEG_OVF_FILL_PARTIAL informational, the labels are complete: a mask lay partly (not
+ *                      wholly) inside an earlier mask's filled holes (disconnected or diagonal-
+ *                      touching masks), where the parallel fill is not the reference's
+ *                      order-dependent loop, so this FOV's fill ran as that sequential loop on
+ *                      the GPU (n_fill_partial = such masks).
  *   CPX_SEG_ERR_INTERNAL a flow-error work loop reached its claim bound (cannot happen in a correct
  *                      build; the labels are invalid and the host must raise).
  * Fill-holes has no size limit (masks whose bbox exceeds the LDS bitmasks use global memory). */

@@ -116,3 +116,19 @@ def test_streamed_tables_fall_back_when_out_of_order(tmp_path):
     for name, df in t.frames().items():
         df.to_csv(tmp_path / f"{name}.ref.csv", index=False)
         assert open(os.path.join(d, f"{name}.csv"), "rb").read() == open(tmp_path / f"{name}.ref.csv", "rb").read()
+
+
+def test_aborted_stream_leaves_no_object_tables(tmp_path):
+    """A job that fails after some FOVs were streamed (PlateTables.close() without write()): no
+    <table>.csv and no partial file remain in the job directory, and while the job
+    runs the rows go to hidden partial files, never to the final names."""
+    rng = np.random.default_rng(13)
+    d = tmp_path / "P" / "1"
+    t = csvout.PlateTables(["DNA"], eager_csv=True, stream_dir=str(d))
+    F = len(t.cols)
+    for img in (1, 2):
+        for s in csvout.OBJECT_TABLES:
+            t.add_objects(s, img, np.arange(1, 4), rng.standard_normal((3, F)))
+    assert not any((d / f"{s}.csv").exists() for s in csvout.OBJECT_TABLES)
+    t.close()  # (plate.run's finally on an exception)
+    assert sorted(os.listdir(d)) == []

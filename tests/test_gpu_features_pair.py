@@ -13,7 +13,7 @@ import torch
 
 import cpx_oracle as orc
 import synth_golden as sg
-from cpx.device import n_features
+from cpx.device import as_numpy as as_np, n_features
 
 pytestmark = pytest.mark.gpu
 
@@ -59,6 +59,13 @@ def test_pair_equals_per_set_on_synthetic_labels(dev):
     dev.sync()
     for r, g in zip(ref, got):
         assert torch.equal(r, g)
+    # and the pair path directly against the oracle (skimage 0.18.3 definitions, rtol 1e-5), both
+    # sets of every FOV: the Cytoplasm rows staged from the Cells pass included
+    from test_gpu_parity import _feat_close
+    hc_np, hy_np = (as_np(h, "hdr")["n_objects"] for h in (hc, hy))
+    for b in range(B):
+        _feat_close(got[0][b, :hc_np[b]].cpu().numpy(), orc.features(cells[b].astype(np.int32), planes[b]))
+        _feat_close(got[1][b, :hy_np[b]].cpu().numpy(), orc.features(cyto[b], planes[b]))
     # both paths were exercised: shared bboxes and different ones
     from cpx.device import as_numpy
     oc_np = as_numpy(oc, "object").reshape(B, ML)

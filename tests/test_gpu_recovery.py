@@ -112,6 +112,27 @@ def test_watershed_nonconvergence_rerun_with_more_rounds(dev, batch):
         _same_tables(res, base, b, b)
 
 
+def test_recovery_uses_each_pipelines_own_flat_field(dev, batch):
+    """The single-FOV recovery pipelines are shared per process (keyed by the config, which does
+    not hold the flat-field): two pipelines with different flat-fields both forcing a re-run each
+    get tables equal to their own default run (the cached pipeline kept the first
+    caller's flat-field)."""
+    from cpx.pipeline import RECOVER_WS, FovPipeline
+    illum, raw = batch
+    r = raw[:5]
+    feats = []
+    for il in (illum, (illum * np.float32(1.25)).astype(illum.dtype)):
+        full = FovPipeline(dev, dataclasses.replace(_cfg(), batch=1), il)
+        base = full.fetch(full.run(r))
+        short = FovPipeline(dev, dataclasses.replace(_cfg(ws_rounds=(1, 1)), batch=1), il)
+        res = short.fetch(short.run(r))
+        assert res.recovered.tolist() == [RECOVER_WS]
+        _same_tables(res, base, 0, 0)
+        feats.append(res.feats["Nuclei"][0])
+        del full, short
+    assert not np.array_equal(feats[0], feats[1])  # the two flat-fields did differ
+
+
 def test_plate_with_too_few_watershed_rounds_matches_default(tmp_path, dev, caplog):
     from cpx import plate, tiffio
     from cpx.csvout import OBJECT_TABLES
