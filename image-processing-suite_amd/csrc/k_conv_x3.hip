@@ -96,10 +96,7 @@ __device__ __forceinline__ void split8(const float* v, uint4& hi, uint4& lo, boo
 
 // The epilogue's y / z tile stores are non-temporal (streamed past L2: the next reader is another
 // launch, and the halo lines the tile loop prefetches stay cached; p32 2.22 -> 2.17 ms per call,
-// the deep levels unchanged, `gpurun_out/r05j`); -DCPX_X3_NT=0 for plain stores
-#ifndef CPX_X3_NT
-#define CPX_X3_NT 1
-#endif
+// the deep levels unchanged, `gpurun_out/r05j`)
 
 struct X3Epi {
   const float* bias;
@@ -242,13 +239,9 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
       const int px = i / QB, k = i - px * QB;
       const long long gp = gpix(px);
       if (i < P * QB && gp >= 0) {
-#if CPX_X3_NT
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         __builtin_nontemporal_store(__builtin_bit_cast(u32x4, buf[px * QB + (k ^ swzq<QB>(px))]),
                                     reinterpret_cast<u32x4*>(dst + gp * QC + nb * QB + k));
-#else
-        dst[gp * QC + nb * QB + k] = buf[px * QB + (k ^ swzq<QB>(px))];
-#endif
       }
     }
   };
@@ -400,36 +393,13 @@ __device__ __forceinline__ void x3_epilogue(f32x16 (&acc0)[WM][WN], const X3Epi&
   flag();
 }
 
-// Instruction-scheduling hint for the single-fragment tap loop (CPX_X3_SCHED): 1 (default) =
-// iglp_opt(0), the compiler's MFMA / DS-read interleave: the 32-channel-block kernels 2.5-3 %
-// faster, bit-identical outputs (`gpurun_out/r05y`); 2 = sched_group_barrier groups that issue
-// tap t + 1's fragment reads before tap t's MFMAs (DS 4, then per tap DS 4 + MFMA 3): ~1 %; 0 =
-// none.  The 224^2 persistent kernel takes the same hint after each slab's taps (-2.3 %,
-// `gpurun_out/r05z`); in the multi-fragment loop (one tap per iteration) it measured +-1 % and
-// raised spills, so it stays out there (CPX_X3_SCHED_ALL for experiments).
-#ifndef CPX_X3_SCHED
-#define CPX_X3_SCHED 1
-#endif
-#ifndef CPX_X3_SCHED_ALL
-#define CPX_X3_SCHED_ALL 0
-#endif
-template <int T, int C>
-__device__ __forceinline__ void x3_sched() {
-  if constexpr (CPX_X3_SCHED == 1) {
-    __builtin_amdgcn_iglp_opt(0);
-  } else if constexpr (CPX_X3_SCHED == 3) {
-    __builtin_amdgcn_iglp_opt(1);
-  } else if constexpr (CPX_X3_SCHED == 2) {
-    constexpr int R = 2 + 2 * C, M = 3 * C;  // DS reads (A hi/lo + B hi/lo per subtile) and MFMAs per tap
-    __builtin_amdgcn_sched_group_barrier(0x0100, R, 0);
-#pragma unroll
-    for (int t = 0; t + 1 < T; ++t) {
-      __builtin_amdgcn_sched_group_barrier(0x0100, R, 0);
-      __builtin_amdgcn_sched_group_barrier(0x0008, M, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x0008, M, 0);
-  }
-}
+// Instruction-scheduling hint after an unrolled tap loop: iglp_opt(0), the compiler's MFMA /
+// DS-read interleave — the 32-channel-block kernels 2.5-3 % faster, bit-identical outputs
+// (`gpurun_out/r05y`; sched_group_barrier groups that issue tap t + 1's fragment reads before tap
+// t's MFMAs measured ~1 %).  The 224^2 persistent kernel takes the same hint after each slab's
+// taps (-2.3 %, `gpurun_out/r05z`); the multi-fragment loop with one tap per iteration does not
+// (+-1 % and more spills).
+__device__ __forceinline__ void x3_sched() { __builtin_amdgcn_iglp_opt(0); }
 
 template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, int CIN2 = 0, int NBUF = 2>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE)))
@@ -464,12 +434,8 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
   // projection slabs packed PK per slab buffer: a projection slab reads only the tile's centre
   // pixels (P * 4 slots, no halo) and one tap of weights (BM * 4 slots), so two fit where a 3x3
   // slab's nine weight taps and halo go — half the DMA waits and barriers of the projection
-  // (CPX_X3_PROJ_PACK=0 keeps one per buffer with the full halo)
   constexpr int NPR = (P * 4 + 63) / 64;              // centre-pixel DMA rows of one projection slab
-#ifndef CPX_X3_PROJ_PACK
-#define CPX_X3_PROJ_PACK 1
-#endif
-  constexpr int PK = (CPX_X3_PROJ_PACK && CIN2 > 0 && 2 * BM * 4 + 2 * NPR * 64 <= SB) ? 2 : 1;
+  constexpr int PK = (CIN2 > 0 && 2 * BM * 4 + 2 * NPR * 64 <= SB) ? 2 : 1;
   constexpr int NCHP = (NCH2 + PK - 1) / PK;          // projection slab buffers
   static_assert(SMEM * 16 <= 163840, "LDS");
   __shared__ uint4 smem[SMEM];
@@ -660,15 +626,8 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
       static_assert(WN <= 2, "WN");
     }
   };
-  // CPX_X3_DIAG (development timing builds, tools/build_variants.sh; wrong results by
-  // construction): 1 = no slab DMA after the first (compute + barriers only), 2 = that and no
-  // per-slab barrier, 3 = no epilogue, 4 = 2 and 3 (the MFMA + fragment-read loop alone)
-#ifndef CPX_X3_DIAG
-#define CPX_X3_DIAG 0
-#endif
   for (int ch = 0; ch < NCH; ++ch) {
-    if (NBUF == 2 && CPX_X3_DIAG != 1 && CPX_X3_DIAG != 2 && CPX_X3_DIAG != 4 && ch + 1 < NCHT)
-      issue(ch + 1, (ch + 1) & 1);
+    if (NBUF == 2 && ch + 1 < NCHT) issue(ch + 1, (ch + 1) & 1);
     if (kResPre && ch + 1 == NCHT && ep.res) issue_res();
     const uint4* sb = smem + (NBUF == 2 ? (ch & 1) * SB : 0);
     per_nsub([&](auto cnt) {
@@ -677,31 +636,20 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
         // tap's MFMAs; larger wave tiles keep one tap per iteration (register budget)
 #pragma unroll
         for (int tap = 0; tap < T; ++tap) tapbody(cnt, sb, tap, tap / KS, tap % KS);
-        x3_sched<T, decltype(cnt)::value>();
+        x3_sched();
       } else {
         // multi-fragment waves: the two-slice BM 64 tile (WM 2, WN 1) unrolls all nine taps with
         // the interleave hint, like the single-fragment loop, where the registers allow it (no
         // folded projection, CIN >= 64): -6 to -7.5 % on those kernels, bit-identical
         // (`gpurun_out/r05ab`); CIN 32, the projection-folded forms and the WN 2 tiles spill
         // unrolled and keep one tap per iteration
-#ifndef CPX_X3_MUNROLL
-#define CPX_X3_MUNROLL ((WM == 2 && WN == 1 && CIN2 == 0 && CIN >= 64) ? 9 : 1)
-#endif
-        if constexpr (CPX_X3_MUNROLL == 1) {
-#pragma unroll 1
-          for (int tap = 0; tap < T; ++tap) {
-            tapbody(cnt, sb, tap, tap / KS, tap % KS);
-            if constexpr (CPX_X3_SCHED_ALL) __builtin_amdgcn_iglp_opt(0);
-          }
-        } else {  // (experiment) CPX_X3_MUNROLL taps per iteration with the interleave hint
-          static_assert(T % CPX_X3_MUNROLL == 0 || T == 1, "taps per iteration");
-          constexpr int U = T == 1 ? 1 : CPX_X3_MUNROLL;
-#pragma unroll 1
-          for (int t0 = 0; t0 < T; t0 += U) {
+        if constexpr (WM == 2 && WN == 1 && CIN2 == 0 && CIN >= 64) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) tapbody(cnt, sb, t0 + u, (t0 + u) / KS, (t0 + u) % KS);
-            __builtin_amdgcn_iglp_opt(0);
-          }
+          for (int tap = 0; tap < T; ++tap) tapbody(cnt, sb, tap, tap / KS, tap % KS);
+          x3_sched();
+        } else {
+#pragma unroll 1
+          for (int tap = 0; tap < T; ++tap) tapbody(cnt, sb, tap, tap / KS, tap % KS);
         }
       }
     });
@@ -710,7 +658,7 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
       if (ch + 1 < NCHT) issue(ch + 1, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (CPX_X3_DIAG != 2 && CPX_X3_DIAG != 4) __syncthreads();
+    __syncthreads();
   }
   // folded projection: one centre tap per slab of in2 (weight slot 0)
 #pragma unroll 1
@@ -766,17 +714,6 @@ void k_conv_x3(const uint4* __restrict__ in, const uint4* __restrict__ wpk, X3Ep
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc0[m][j][r] += acc1[m][j][r] * kLoInv;  // exact product, one rounding
 
-  if (CPX_X3_DIAG == 3 || CPX_X3_DIAG == 4) {  // keep the sums alive without the epilogue
-    float t = 0.0f;
-#pragma unroll
-    for (int m = 0; m < WM; ++m)
-#pragma unroll
-      for (int j = 0; j < WN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += acc0[m][j][r];
-    if (t == 1.2345e-30f && ep.ovf) atomicOr(ep.ovf, 2);
-    return;
-  }
   if constexpr (kResPre)
     x3_epilogue<COUT, BM, TY, TX, WM, WN>(acc0, ep, bufO, n, nb, ty0, tx0, H, W, mw, pg, nsub, -1,
                                           ep.res ? bufR : nullptr);
@@ -894,8 +831,7 @@ void k_conv_x3_p32(const uint4* __restrict__ in, const uint4* __restrict__ wpk, 
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc1, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc1, 0, 0, 0);
       }
-      if constexpr (CPX_X3_SCHED == 1) __builtin_amdgcn_iglp_opt(0);
-      if constexpr (CPX_X3_SCHED == 3) __builtin_amdgcn_iglp_opt(1);
+      x3_sched();
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc0[0][0][r] += acc1[r] * kLoInv;  // exact product, one rounding
@@ -946,20 +882,13 @@ bool x3_cfg(int ks, int cin, int cout, int variant, X3Cfg* c) {
   return true;
 }
 
-// development knob (A/B runs): CPX_X3_LDS_PAD bytes of unused dynamic LDS per convolution block,
-// which lowers the convolutions' residency per CU and leaves room for the other pipeline's kernels
-static size_t x3_lds_pad() {
-  static const size_t pad = getenv("CPX_X3_LDS_PAD") ? (size_t)atol(getenv("CPX_X3_LDS_PAD")) : 0;
-  return pad;
-}
-
 template <int KS, int CIN, int COUT, int BM, int TY, int TX, int WM, int WN, int WPE, int CIN2 = 0, int NBUF = 2>
 int x3_run(cpx_ctx* ctx, const void* in, const void* wpk, const X3Epi& ep, int N, int H, int W) {
   const int tx = cpx_div_up(W, TX), ty = cpx_div_up(H, TY);
   const long long blocks = (long long)N * tx * ty * (COUT / BM);  // (tile, output-channel block) items
   CPX_REQUIRE(blocks < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv: too many tiles");
   hipLaunchKernelGGL((k_conv_x3<KS, CIN, COUT, BM, TY, TX, WM, WN, WPE, CIN2, NBUF>), dim3((unsigned)blocks),
-                     dim3(512), x3_lds_pad(), ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N, H, W, tx, ty);
+                     dim3(512), 0, ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N, H, W, tx, ty);
   CPX_CHECK_LAUNCH("k_conv_x3");
   return CPX_OK;
 }
@@ -1002,22 +931,17 @@ int x3_launch(cpx_ctx* ctx, int ks, int cin, int cout, int variant, const void* 
 #define X3_1(CI, CO)                                                                     \
   if (ks == 1 && cin == CI && cout == CO)                                                \
     return x3_run<1, CI, CO, 32, 16, 16, 1, 1, 4>(ctx, in, wpk, ep, N, H, W);
-  // 224^2 level (32 -> 32 without in_up: the persistent weights-resident kernel unless
-  // CPX_X3_P32=0)
+  // 224^2 level (32 -> 32 without in_up): the persistent weights-resident kernel, with the L2
+  // prefetch of each tile's residual lines (mode 2; also touching the block's next halo, mode 1,
+  // measured 443.1 against 444.1 FOV/s and +12.7 GB of PMC traffic per step, none 440.0 —
+  // two-pipeline benches of 60 steps, `gpurun_out/r05w`)
   if ((variant == 2 || variant == 3) && cout == 32) variant = 0;  // (224^2: variant 0's kernels)
-  static const bool p32 = !getenv("CPX_X3_P32") || atoi(getenv("CPX_X3_P32")) != 0;
-  // L2 prefetch in k_conv_x3_p32 (CPX_X3_P32_TOUCH): 2 = this tile's residual lines (default),
-  // 1 = also the block's next halo, 0 = none.  Two-pipeline benches of 60 steps (`gpurun_out/r05w`):
-  // 444.1 / 443.1 / 440.0 FOV/s; mode 1's next-halo lines are mostly evicted before the DMA reads
-  // them (+12.7 GB of PMC traffic per step), so mode 2 keeps the time without the traffic
-  static const int p32_touch = getenv("CPX_X3_P32_TOUCH") ? atoi(getenv("CPX_X3_P32_TOUCH")) : 2;
-  if (p32 && ks == 3 && cin == 32 && cout == 32 && variant == 0 && !ep.in_up) {
+  if (ks == 3 && cin == 32 && cout == 32 && variant == 0 && !ep.in_up) {
     const int tx = cpx_div_up(W, 32), ty = cpx_div_up(H, 8);
     const long long tiles = (long long)N * tx * ty;
     CPX_REQUIRE(tiles < (1LL << 31), CPX_ERR_ARG, "cpx_cpnet_x3_conv: too many tiles");
     const int grid = (int)std::max(1LL, std::min(tiles, 2LL * ctx->n_cu));
-    auto kern = p32_touch == 2 ? k_conv_x3_p32<2> : p32_touch ? k_conv_x3_p32<1> : k_conv_x3_p32<0>;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N,
+    hipLaunchKernelGGL(k_conv_x3_p32<2>, dim3(grid), dim3(512), 0, ctx->stream, (const uint4*)in, (const uint4*)wpk, ep, N,
                        H, W, tx, ty);
     CPX_CHECK_LAUNCH("k_conv_x3_p32");
     return CPX_OK;

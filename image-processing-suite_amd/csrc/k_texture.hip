@@ -282,13 +282,21 @@ __device__ __forceinline__ unsigned long long half_wave_sum_u64(unsigned long lo
   return v;
 }
 
+// pair slots the dense count visits for angle a: the angle's rows x the padded row width
+__device__ __forceinline__ unsigned long long glcm_slots(int a, int bh, int bw) {
+  const int dr = a == 0 ? 0 : a == 2 ? 3 : 2;
+  const int dc = a == 0 ? 3 : a == 1 ? 2 : a == 2 ? 0 : -2;
+  const int rend = bh - dr, cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
+  return rend > 0 && cend > cbeg ? (unsigned long long)rend * crop_stride(bw) : 0ull;
+}
+
 // Finish: the four angles' per-thread sums are reduced through LDS in two rounds of two angles
 // (`red` = 2 * kRedW * kTT words of the all-zero table, zeroed again before returning; `tot` =
 // 4 * kRedW u64 of static LDS), then 4 * kRedW lanes store the item's totals to `raw` for
 // k_glcm_props (greycoprops in fp64 on four lanes here held the block's other 1020 threads at
 // the next barrier).
 __device__ void glcm_finish(const GlcmSums (&S)[4], unsigned int* red, unsigned long long* tot,
-                            unsigned long long* __restrict__ raw, long long* pt) {
+                            unsigned long long* __restrict__ raw, long long* pt, int bh, int bw) {
   const int t = threadIdx.x, lane = t & 63;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -319,7 +327,18 @@ __device__ void glcm_finish(const GlcmSums (&S)[4], unsigned int* red, unsigned 
 #pragma unroll
   for (int k = 0; k < 2 * kRedW; ++k) red[k * kTT + t] = 0u;
   GLCM_MARK(1, pt);
-  if (t < 4 * kRedW) raw[t] = tot[t];
+  if (t < 4 * kRedW) {
+    // homogeneity as k_tex_band reports it: over the non-background pairs (the count visited
+    // every pair slot of the padded rows, each masked or background slot adding hom(0))
+    const int a = t / kRedW, k = t - a * kRedW;
+    unsigned long long v = tot[t];
+    if (k >= 8) {
+      const unsigned long long h = tot[a * kRedW + 8] + (tot[a * kRedW + 9] << 32);
+      const unsigned long long hn = h - (glcm_slots(a, bh, bw) - tot[a * kRedW + 7]) * kHom.m[0];
+      v = k == 8 ? (hn & 0xffffffffull) : (hn >> 32);
+    }
+    raw[t] = v;
+  }
 }
 
 // greycoprops from k_tex_glcm's integer totals, one thread per (object, channel, angle) of the
@@ -348,9 +367,8 @@ __global__ __launch_bounds__(256) void k_glcm_props(int C, int max_label, int F,
                   tsjj = (long long)v[3], tsij = (long long)v[4];
   const unsigned long long dt = v[5], tas = v[6], ncnt = v[7];
   const unsigned long long nbg = (unsigned long long)T - ncnt;  // background pairs (0, 0)
-  // the count visited rend * crop_stride(bw) pair slots; the masked ones added hom(0) each
-  const unsigned long long slots = rend > 0 ? (unsigned long long)rend * crop_stride(bw) : 0ull;
-  const unsigned long long hs = v[8] + (v[9] << 32) - (slots - (unsigned long long)T) * kHom.m[0];
+  // v[8], v[9]: homogeneity over the non-background pairs; each background pair adds hom(0)
+  const unsigned long long hs = v[8] + (v[9] << 32) + nbg * kHom.m[0];
   double con = 0.0, dis = 0.0, hom = 0.0, asmv = 0.0, ene = 0.0, cor = 1.0;
   if (T > 0) {
     const double Td = (double)T;
@@ -388,7 +406,11 @@ struct GlcmItem {
 // visits each FOV at most once, so every block reaches the exit).
 __device__ __forceinline__ int glcm_grab(int& f, int& visited, int B, int C,
                                          const cpx_fov_objects* __restrict__ hdr,
-                                         int* __restrict__ next) {
+                                         int* __restrict__ next, int* __restrict__ redo = nullptr) {
+  if (redo) {  // k_tex_glcm over the items k_tex_band handed back: one list, one claim counter
+    const int v = atomicAdd(&redo[1], 1);
+    return v < redo[0] ? redo[2 + v] : -1;
+  }
   while (visited < B) {
     const int n_items = hdr[f].n_objects * C;
     const int v = atomicAdd(&next[f], 1);
@@ -453,7 +475,8 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
                                                  const unsigned char* __restrict__ scratch,
                                                  long long scratch_per_fov,
                                                  int* __restrict__ glcm_next,
-                                                 unsigned long long* __restrict__ glcm_raw) {
+                                                 unsigned long long* __restrict__ glcm_raw,
+                                                 int* __restrict__ redo) {
   // LDS: table at offset 0 (static, so the atomics' addresses need no base), then the
   // 64 sink words, the reduction totals, the queue codes and the crop
   __shared__ __attribute__((aligned(16))) unsigned int lds[40 * 1024];  // all 160 KiB, static
@@ -468,8 +491,8 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
   for (int x = threadIdx.x; x < kTabW; x += kTT) tab[x] = 0u;
   if (threadIdx.x < 256) s_hom[threadIdx.x] = kHom.m[threadIdx.x];
   if (threadIdx.x == 0) {
-    s_code[0] = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next);
-    s_code[1] = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next);
+    s_code[0] = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next, redo);
+    s_code[1] = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next, redo);
   }
   __syncthreads();
   // software pipeline: the next item's metadata is loaded and its crop's lines are touched into
@@ -498,7 +521,7 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
     const GlcmItem it = cur;
     cur = glcm_item(s_code[par], C, max_label, objects, crop_off, scratch, scratch_per_fov);
     touched = glcm_touch(cur);
-    if (threadIdx.x == 0) ahead = s_code[par] >= 0 ? glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next) : -1;
+    if (threadIdx.x == 0) ahead = s_code[par] >= 0 ? glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next, redo) : -1;
     if (it.nb <= 0) continue;
     unsigned long long* f = glcm_raw + (((long long)it.fov * max_label + it.k) * C + it.ch) * (4 * kRedW);
     long long pt = 0;
@@ -515,11 +538,448 @@ __global__ __launch_bounds__(kTT) void k_tex_glcm(int C, int max_label, int F,
     glcm_angle<1>(it, crop, tab, s_hom, S[1], &pt);
     glcm_angle<2>(it, crop, tab, s_hom, S[2], &pt);
     glcm_angle<3>(it, crop, tab, s_hom, S[3], &pt);
-    glcm_finish(S, tab, s_tot, f, &pt);
+    glcm_finish(S, tab, s_tot, f, &pt, it.bh, it.bw);
     GLCM_MARK(4, &pt);
   }
   // keeps the touch loads alive: never true (C > 0), but the compiler cannot know that
   if (C < 0 && sink_word + touched == 0x9e3779b9u) glcm_raw[0] = 0ull;
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_tex_band: the GLCM of one (object, channel) item per block, three blocks per CU.
+//
+// On the bench plates (tools/glcm_stats.py, one FOV, 5010 items x 4 angles) half the pair slots
+// are background (0, 0), an item-angle has ~1,000 distinct keys, and of the pairs with both
+// values non-zero 99.76 % have |j - i| < 32.  So instead of the 128 KiB dense table (k_tex_glcm:
+// one item per CU, eight block-wide barrier phases of 1024 threads per item) the counts live in
+// a 33 KiB band table of u16 counters, 256 per row:
+//   rows 0..62: pairs (i, i + d), d = row - 31, by i (zeros included: (0, j <= 31) is row j + 31,
+//   entry 0); row 63: (0, j) and row 64: (i, 0) for the larger values; row 65: per-lane sink
+//   counters (never read) that take the background pairs and the outliers, so every pair is one
+//   unconditional no-return atomic;
+//   a pair with both values non-zero and |j - i| > 31 is also appended to an outlier list (<=
+//   kOutCap keys per angle); an item whose list overflows in any angle is handed to k_tex_glcm
+//   (the dense table) through the redo list.
+// The keys of four pairs come from byte-SIMD arithmetic on the packed 8-bit pixels (zero-byte
+// flags, per-byte (j - i + 31) mod 256, byte selects and two byte permutes), and the count pass
+// does nothing else: every sum greycoprops needs comes from the table in the scan — per group of
+// 8 counters with known (d, i0): s0 = sum c, s1 = sum c i, s2 = sum c i^2, q = sum c^2, and
+// sum j = s1 + d s0, sum j^2 = s2 + 2 d s1 + d^2 s0, sum ij = s2 + d s1, dissimilarity |d| s0,
+// homogeneity H(|d|) s0 — the same integers as the dense kernel's.  Each sum fits 32 bits for an
+// item (T <= 65535 pairs of 8-bit values: sum i^2 <= 65535 * 255^2 < 2^32), so per-thread
+// partials add modulo 2^32 and the total is exact; homogeneity is a u64 fixed-point sum (kHom).
+// The next item's metadata and crop (into registers) load while the current item runs.
+// 256 threads per block: 512 measured 1.5 % faster with spills at the register budget three
+// blocks per CU need, and no faster without them (`gpurun_out/r06h`, `r06k`)
+constexpr int kBT = 256;
+constexpr int kBandD = 31;                     // band half-width
+constexpr int kBandScan = 2 * kBandD + 1 + 2;  // scanned rows: band + (0, j) + (i, 0)
+constexpr int kSinkRow = kBandScan;            // + one row of sink counters
+constexpr int kBandW = (kBandScan + 1) * 128;  // u32 words (two u16 counters each)
+constexpr int kOutCap = 512;                   // outlier keys per angle
+constexpr int kBandCrop = 16 * 1024;           // crops up to this many bytes staged in LDS
+constexpr int kBandLds = 4 * kBandW + 2 * kOutCap + 8 * 256 + 8 * 4 * kRedW + 16 + kBandCrop;
+static_assert(3 * kBandLds <= 160 * 1024, "three k_tex_band blocks per CU");
+constexpr int kScanG = (kBandScan * 32 + kBT - 1) / kBT;  // 16-byte groups per thread in the scan
+constexpr int kCropG = kBandCrop / 16 / kBT;              // uint4 of a staged crop per thread
+static_assert(kBandCrop == kCropG * 16 * kBT, "a staged crop is whole uint4 per thread");
+
+struct BandAcc {
+  unsigned int si, sj, sii, sjj, sij, dis, asq, cnt;  // modulo 2^32 (exact totals < 2^32)
+  unsigned long long hom;                             // sum c * kHom(|i - j|)
+};
+
+// per-byte 0x80 flags of the zero bytes of x (exact: no carry crosses a byte)
+__device__ __forceinline__ unsigned int zero_bytes(unsigned int x) {
+  return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+}
+
+// Counter keys (row << 8 | entry) of four pairs (a, b) given as packed bytes: klo holds pairs
+// 0, 1, khi pairs 2, 3 (16 bits each); outf flags (0x80 per byte) the outliers.
+__device__ __forceinline__ void band_keys(unsigned int a, unsigned int b, unsigned int sink4, unsigned int& klo,
+                                          unsigned int& khi, unsigned int& outf) {
+  const unsigned int za = zero_bytes(a), zb = zero_bytes(b);
+  // per-byte (j - i) mod 256 (bytes_sub) and its borrow (j < i): t's bit 7 is set iff the low
+  // seven bits did not borrow
+  const unsigned int t = (b | 0x80808080u) - (a & 0x7f7f7f7fu);
+  const unsigned int dd = t ^ ((b ^ ~a) & 0x80808080u);
+  const unsigned int bor = ((~b & a) | (~(b ^ a) & ~t)) & 0x80808080u;
+  const unsigned int r = ((dd & 0x7f7f7f7fu) + 0x1f1f1f1fu) ^ (dd & 0x80808080u);  // + 31
+  // in the band: r <= 62 and (r >= 31, i.e. dd <= 31) exactly when j >= i — otherwise the pair
+  // aliases a band key modulo 256 (|j - i| >= 225) and is out of band
+  const unsigned int up = ((r & 0x7f7f7f7fu) + 0x61616161u) & 0x80808080u;  // r >= 31 (r < 128)
+  const unsigned int oob = ((r | ((r | 0x80808080u) - 0x3f3f3f3fu)) | ~(up ^ bor)) & 0x80808080u;
+  const unsigned int z1 = oob & za;                 // (0, j > 31)
+  const unsigned int z2 = oob & zb & ~za;           // (i > 31, 0)
+  outf = oob & ~za & ~zb;                           // both non-zero, |j - i| > 31
+  // 0x80 flags -> 0xff byte masks (0x80 - 0x01 = 0x7f: no borrow leaves a byte)
+  const unsigned int m1 = z1 | (z1 - (z1 >> 7)), m2 = z2 | (z2 - (z2 >> 7));
+  const unsigned int fs = (za & zb) | outf;  // background or outlier: the sink row
+  const unsigned int ms = fs | (fs - (fs >> 7));
+  unsigned int row = (m1 & 0x3f3f3f3fu) | (~m1 & r);
+  row = (m2 & 0x40404040u) | (~m2 & row);
+  row = (ms & (0x01010101u * kSinkRow)) | (~ms & row);
+  unsigned int ent = (m1 & b) | (~m1 & a);
+  ent = (ms & sink4) | (~ms & ent);
+  klo = __builtin_amdgcn_perm(row, ent, 0x05010400u);
+  khi = __builtin_amdgcn_perm(row, ent, 0x07030602u);
+}
+
+// k: key in bits 0-15.  (Adding a wave's lanes on its first active lane's word at once — a
+// flat crop's dominant key serialises its lanes on one address — measured 15 % slower: the
+// ballots cost more than the conflicts, `gpurun_out/r06i`.)
+__device__ __forceinline__ void band_add(unsigned int* tab, unsigned int k) {
+  atomicAdd(&tab[(k & 0xffffu) >> 1], (k & 1u) * 0xffffu + 1u);
+}
+
+// One chunk of eight reference pixels: a (A) and the b bytes at the angle's offset.
+template <int SH, bool SINGLE>
+__device__ __forceinline__ void band_load(const unsigned char* pa, int boff, uint2& A, uint2& L, uint2& R) {
+  A = *reinterpret_cast<const uint2*>(pa);
+  L = *reinterpret_cast<const uint2*>(pa + boff);
+  if constexpr (!SINGLE) R = *reinterpret_cast<const uint2*>(pa + boff + 8);
+}
+
+template <int ANG, bool LDS_CROP>
+__device__ __forceinline__ void band_count(const unsigned char* __restrict__ crop, unsigned int* tab,
+                                           unsigned short* outl, int* n_out, int bh, int bw) {
+  constexpr int dr = ANG == 0 ? 0 : ANG == 2 ? 3 : 2;
+  constexpr int dc = ANG == 0 ? 3 : ANG == 1 ? 2 : ANG == 2 ? 0 : -2;
+  constexpr int sh = dc >= 0 ? dc : dc + 8;  // byte offset of b in its aligned 16-byte window
+  const int bwp = crop_stride(bw), nch = bwp >> 3;
+  const int rend = bh - dr;
+  const int cbeg = dc >= 0 ? 0 : -dc, cend = dc >= 0 ? bw - dc : bw;
+  if (rend <= 0 || cend <= cbeg) return;
+  const int nc = rend * nch;
+  // scattered visiting order (as k_tex_glcm's count): neighbouring chunks of a smooth crop share
+  // keys, and same-address lanes of one atomic instruction serialise
+  const int mul = nc % 7919 ? 7919 : 7907;
+  unsigned p = (threadIdx.x * (unsigned)mul) % (unsigned)nc;
+  const unsigned step = ((unsigned)kBT * (unsigned)mul) % (unsigned)nc;
+  const int sc = step % nch;
+  int ci = p % nch;
+  const int boff = dr * bwp + (dc < 0 ? -8 : 0);
+  const unsigned int sink4 = 0x01010101u * (2u * (threadIdx.x & 63));  // one sink word per lane
+  // software pipeline: the next chunk's bytes are loaded before this chunk's atomics are issued
+  uint2 A, L, R = {0u, 0u};
+  if ((int)threadIdx.x < nc) band_load<sh, sh == 0>(crop + 8 * (int)p, boff, A, L, R);
+  // eight no-op atomics after the first load too, so that the loop is entered with the same LDS
+  // wait state as its back edge (otherwise the merge makes every iteration wait for all)
+  unsigned int* sinkw = tab + kSinkRow * 128 + (threadIdx.x & 63);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) atomicAdd(sinkw, 0u);
+  for (int q = threadIdx.x; q < nc; q += kBT) {
+    // every loaded dword stays live to here (also the ones this angle does not read): otherwise
+    // their registers are reused right after the load, and the write-after-write forces a wait
+    // for the load before this chunk's atomics — the pipeline is gone
+    asm volatile("" ::"v"(A.x), "v"(A.y), "v"(L.x), "v"(L.y), "v"(R.x), "v"(R.y));
+    unsigned int b0, b1;
+    if constexpr (sh == 0) {
+      b0 = L.x;
+      b1 = L.y;
+    } else if constexpr (sh < 4) {
+      b0 = __builtin_amdgcn_alignbyte(L.y, L.x, sh);
+      b1 = __builtin_amdgcn_alignbyte(R.x, L.y, sh);
+    } else {
+      b0 = __builtin_amdgcn_alignbyte(R.x, L.y, sh - 4);
+      b1 = __builtin_amdgcn_alignbyte(R.y, R.x, sh - 4);
+    }
+    const int c0 = 8 * ci;
+    const int hi = min(cend - c0, 8), lo = max(cbeg - c0, 0);
+    unsigned long long m = hi >= 8 ? ~0ull : (hi <= 0 ? 0ull : (1ull << (8 * hi)) - 1ull);
+    m &= ~0ull << (8 * lo);
+    const unsigned int m0 = (unsigned int)m, m1 = (unsigned int)(m >> 32);
+    const unsigned int a0 = A.x & m0, a1 = A.y & m1;
+    b0 &= m0;
+    b1 &= m1;
+    unsigned int k0, k1, k2, k3, o0, o1;
+    band_keys(a0, b0, sink4, k0, k1, o0);
+    band_keys(a1, b1, sink4, k2, k3, o1);
+    // Order matters for the LDS wait counts (LDS operations complete in order): the rare
+    // outlier appends (a returning atomic) first, then the next chunk's loads, then this chunk's
+    // eight atomics — every path then has the loads followed by exactly eight LDS operations, so
+    // the next iteration waits for the loads only (lgkmcnt(8)), not for the atomics.  For the
+    // same reason every pair is added (background and outliers to the lane's sink counter): a
+    // skipped chunk would leave the wait count path-dependent, i.e. a full drain.
+    if ((o0 | o1) != 0u) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int sft = 8 * (u & 3);
+        if (((u < 4 ? o0 : o1) >> sft) & 0x80u) {
+          const unsigned int a = ((u < 4 ? a0 : a1) >> sft) & 255u, b = ((u < 4 ? b0 : b1) >> sft) & 255u;
+          const int pos = atomicAdd(n_out, 1);
+          if (pos < kOutCap) outl[pos] = (unsigned short)((a << 8) | b);
+        }
+      }
+    }
+    p += step;
+    ci += sc;
+    if (ci >= nch) ci -= nch;
+    if (p >= (unsigned)nc) p -= nc;
+    band_load<sh, sh == 0>(crop + 8 * (int)p, boff, A, L, R);  // (p < nc: past the last chunk a spare valid load)
+    band_add(tab, k0);
+    band_add(tab, k0 >> 16);
+    band_add(tab, k1);
+    band_add(tab, k1 >> 16);
+    band_add(tab, k2);
+    band_add(tab, k2 >> 16);
+    band_add(tab, k3);
+    band_add(tab, k3 >> 16);
+  }
+}
+
+// Scan + clear of the band table (nine 16-byte groups per thread, all loaded before the first
+// use), then the outlier keys (sum c^2 from equal-key counts).
+__device__ __forceinline__ void band_scan(unsigned int* tab, const unsigned short* outl, int n_out,
+                                          const unsigned long long* hom, BandAcc& S) {
+  uint4* t4 = reinterpret_cast<uint4*>(tab);
+  constexpr int n4 = kBandScan * 32;
+  uint4 w[kScanG];
+#pragma unroll
+  for (int k = 0; k < kScanG; ++k) {
+    const int u = threadIdx.x + k * kBT;
+    w[k] = u < n4 ? t4[u] : uint4{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int k = 0; k < kScanG; ++k) {
+    const int u = threadIdx.x + k * kBT;
+    if ((w[k].x | w[k].y | w[k].z | w[k].w) == 0u) continue;
+    t4[u] = uint4{0u, 0u, 0u, 0u};
+    const int row = u >> 5;
+    const unsigned int e0 = (unsigned int)(u & 31) << 3;
+    unsigned int s0 = dot2_u16(w[k].x, 0x10001u, 0u);
+    s0 = dot2_u16(w[k].y, 0x10001u, s0);
+    s0 = dot2_u16(w[k].z, 0x10001u, s0);
+    s0 = dot2_u16(w[k].w, 0x10001u, s0);
+    unsigned int q = dot2_u16(w[k].x, w[k].x, 0u);
+    q = dot2_u16(w[k].y, w[k].y, q);
+    q = dot2_u16(w[k].z, w[k].z, q);
+    q = dot2_u16(w[k].w, w[k].w, q);
+    // sum h c_h and sum h^2 c_h over the group's counters h = 0..7 (low half first)
+    unsigned int sk = dot2_u16(w[k].x, 0x00010000u, 0u);
+    sk = dot2_u16(w[k].y, 0x00030002u, sk);
+    sk = dot2_u16(w[k].z, 0x00050004u, sk);
+    sk = dot2_u16(w[k].w, 0x00070006u, sk);
+    unsigned int skk = dot2_u16(w[k].x, 0x00010000u, 0u);
+    skk = dot2_u16(w[k].y, 0x00090004u, skk);
+    skk = dot2_u16(w[k].z, 0x00190010u, skk);
+    skk = dot2_u16(w[k].w, 0x00310024u, skk);
+    const unsigned int s1 = e0 * s0 + sk, s2 = e0 * e0 * s0 + 2u * e0 * sk + skk;
+    S.cnt += s0;
+    S.asq += q;
+    if (row < 2 * kBandD + 1) {
+      const int d = row - kBandD;
+      const unsigned int ud = (unsigned int)d, ad = (unsigned int)(d < 0 ? -d : d);
+      S.si += s1;
+      S.sj += s1 + ud * s0;
+      S.sii += s2;
+      S.sjj += s2 + 2u * ud * s1 + ud * ud * s0;
+      S.sij += s2 + ud * s1;
+      S.dis += ad * s0;
+      S.hom += hom[ad] * s0;
+    } else {
+      // (0, j = e) or (i = e, 0): |i - j| = e
+      if (row == 2 * kBandD + 1) {
+        S.sj += s1;
+        S.sjj += s2;
+      } else {
+        S.si += s1;
+        S.sii += s2;
+      }
+      S.dis += s1;
+      const unsigned int v[4] = {w[k].x, w[k].y, w[k].z, w[k].w};
+#pragma unroll
+      for (int h = 0; h < 8; ++h) S.hom += hom[e0 + h] * ((v[h >> 1] >> (16 * (h & 1))) & 0xffffu);
+    }
+  }
+  for (int e = threadIdx.x; e < n_out; e += kBT) {
+    const unsigned int key = outl[e];
+    unsigned int c = 0;
+    for (int f = 0; f < n_out; ++f) c += outl[f] == key;
+    const unsigned int i = key >> 8, j = key & 255u, ad = i > j ? i - j : j - i;
+    S.asq += c;
+    S.cnt += 1u;
+    S.si += i;
+    S.sj += j;
+    S.sii += i * i;
+    S.sjj += j * j;
+    S.sij += i * j;
+    S.dis += ad;
+    S.hom += hom[ad];
+  }
+}
+
+// Wave totals on the DPP path (row shifts within 16 lanes, then the row broadcasts): lane 63
+// holds the sum.
+__device__ __forceinline__ unsigned int wave_total_u32(unsigned int v) {
+  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_total_u64(unsigned long long v) {
+#define CPX_U64_DPP_STEP(CTRL, ROWMASK)                                                         \
+  {                                                                                            \
+    const unsigned int lo_ = (unsigned int)__builtin_amdgcn_update_dpp(0, (int)(unsigned int)v, \
+                                                                       CTRL, ROWMASK, 0xf, false); \
+    const unsigned int hi_ = (unsigned int)__builtin_amdgcn_update_dpp(                        \
+        0, (int)(unsigned int)(v >> 32), CTRL, ROWMASK, 0xf, false);                           \
+    v += ((unsigned long long)hi_ << 32) | lo_;                                                \
+  }
+  CPX_U64_DPP_STEP(0x111, 0xf)
+  CPX_U64_DPP_STEP(0x112, 0xf)
+  CPX_U64_DPP_STEP(0x114, 0xf)
+  CPX_U64_DPP_STEP(0x118, 0xf)
+  CPX_U64_DPP_STEP(0x142, 0xa)
+  CPX_U64_DPP_STEP(0x143, 0xc)
+#undef CPX_U64_DPP_STEP
+  return v;
+}
+
+// greycoprops totals of one angle (raw layout of k_glcm_props: si, sj, sii, sjj, sij, dis, asq,
+// cnt, homogeneity split into low / high 32 bits at write-back): lane 63 of each wave adds its
+// wave's totals to the block's
+__device__ __forceinline__ void band_reduce(const BandAcc& S, unsigned long long* tot) {
+  const unsigned int v[8] = {S.si, S.sj, S.sii, S.sjj, S.sij, S.dis, S.asq, S.cnt};
+  unsigned int x[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = wave_total_u32(v[k]);
+  const unsigned long long h = wave_total_u64(S.hom);
+  if ((threadIdx.x & 63) == 63) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) atomicAdd(&tot[k], (unsigned long long)x[k]);
+    atomicAdd(&tot[8], h);
+  }
+}
+
+template <int A>
+__device__ __forceinline__ void band_angle(const GlcmItem& it, const unsigned char* crop, unsigned int* tab,
+                                           unsigned short* outl, int* n_out, const unsigned long long* hom,
+                                           unsigned long long* tot, bool& overflow) {
+  // the outlier counters alternate by angle: this angle's is read by every thread after the
+  // barrier below, the other one (read by the previous angle before it) is reset meanwhile
+  int* cnt = n_out + (A & 1);
+  long long pt = 0;
+#ifdef CPX_GLCM_PROF
+  if (threadIdx.x == 0) pt = clock64();
+#endif
+  if (it.bytes <= kBandCrop) band_count<A, true>(crop, tab, outl, cnt, it.bh, it.bw);
+  else band_count<A, false>(it.src, tab, outl, cnt, it.bh, it.bw);
+  __syncthreads();
+  GLCM_MARK(1, &pt);
+  const int n = *cnt;
+  if (threadIdx.x == 0) n_out[(A + 1) & 1] = 0;
+  overflow |= n > kOutCap;
+  BandAcc S{};
+  band_scan(tab, outl, min(n, kOutCap), hom, S);
+  GLCM_MARK(2, &pt);
+  band_reduce(S, tot + A * kRedW);
+  __syncthreads();  // the table is clear and the outlier list read before the next angle
+  GLCM_MARK(3, &pt);
+}
+
+// the LDS-sized crop of an item into registers (kCropG uint4 per thread; zeros past its end)
+__device__ __forceinline__ void band_crop_regs(const GlcmItem& g, uint4 (&r)[kCropG]) {
+  const int n16 = (g.nb > 0 && g.bytes <= kBandCrop) ? g.bytes / 16 : 0;
+  const uint4* s16 = reinterpret_cast<const uint4*>(g.src);
+#pragma unroll
+  for (int k = 0; k < kCropG; ++k) {
+    const int x = threadIdx.x + k * kBT;
+    r[k] = x < n16 ? s16[x] : uint4{0u, 0u, 0u, 0u};
+  }
+}
+
+// Per-item GLCM (see above).  Items come from the per-FOV queues as in k_tex_glcm, one item
+// ahead: the next item's code is claimed, its metadata loaded and its crop read into registers
+// while the current item runs.  An item whose outlier list overflowed is appended to `redo`
+// ([0] count, [1] claim counter, [2..] codes) for k_tex_glcm, which writes its raw sums.
+__global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(3 * kBT / 256))) void k_tex_band(int C, int max_label,
+                                                 const cpx_object* __restrict__ objects,
+                                                 const cpx_fov_objects* __restrict__ hdr,
+                                                 const long long* __restrict__ crop_off,
+                                                 const unsigned char* __restrict__ scratch,
+                                                 long long scratch_per_fov, int* __restrict__ glcm_next,
+                                                 unsigned long long* __restrict__ glcm_raw,
+                                                 int* __restrict__ redo) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[kBandLds];
+  unsigned int* tab = reinterpret_cast<unsigned int*>(lds);
+  unsigned short* outl = reinterpret_cast<unsigned short*>(lds + 4 * kBandW);
+  unsigned long long* s_hom = reinterpret_cast<unsigned long long*>(lds + 4 * kBandW + 2 * kOutCap);
+  unsigned long long* s_tot = s_hom + 256;
+  int* s_cnt = reinterpret_cast<int*>(s_tot + 4 * kRedW);  // [0], [1] outlier counters
+  int* s_code = s_cnt + 2;                                  // [0], [1] queue codes by parity
+  unsigned char* crop = lds + kBandLds - kBandCrop;
+  const int B = gridDim.y;
+  int q_fov = blockIdx.y, q_visited = 0;  // thread 0's queue position
+  for (int x = threadIdx.x; x < kBandW; x += kBT) tab[x] = 0u;
+  for (int x = threadIdx.x; x < 256; x += kBT) s_hom[x] = kHom.m[x];
+  for (int x = threadIdx.x; x < 4 * kRedW; x += kBT) s_tot[x] = 0ull;
+  if (threadIdx.x == 0) {
+    s_cnt[0] = s_cnt[1] = 0;
+    s_code[0] = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next);
+    s_code[1] = s_code[0] >= 0 ? glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next) : -1;
+  }
+  __syncthreads();
+  GlcmItem cur = glcm_item(s_code[0], C, max_label, objects, crop_off, scratch, scratch_per_fov);
+  uint4 pre[kCropG];
+  band_crop_regs(cur, pre);
+  long long pt0 = 0;
+#ifdef CPX_GLCM_PROF
+  if (threadIdx.x == 0) pt0 = clock64();
+#endif
+  for (int par = 0; s_code[par] >= 0; par ^= 1) {
+    // s_code[par]: the current item (cur), s_code[par ^ 1]: the next one; s_code[par] receives
+    // the item after that before the closing barrier
+    const GlcmItem it = cur;
+    const int code = s_code[par];
+#pragma unroll
+    for (int k = 0; k < kCropG; ++k)
+      if (threadIdx.x + k * kBT < it.bytes / 16 && it.bytes <= kBandCrop)
+        reinterpret_cast<uint4*>(crop)[threadIdx.x + k * kBT] = pre[k];
+    __syncthreads();  // crop staged
+    GLCM_MARK(0, &pt0);
+    const int ncode = s_code[par ^ 1];
+    int ahead = -1;
+    if (threadIdx.x == 0 && ncode >= 0) ahead = glcm_grab(q_fov, q_visited, B, C, hdr, glcm_next);
+    cur = glcm_item(ncode, C, max_label, objects, crop_off, scratch, scratch_per_fov);
+    bool overflow = false;
+    if (it.nb > 0) {
+#ifdef CPX_GLCM_PROF
+      if (threadIdx.x == 0) {
+        atomicAdd(&g_glcm_prof[5], 1ull);
+        atomicAdd(&g_glcm_prof[6], (unsigned long long)it.nb);
+      }
+#endif
+      band_angle<0>(it, crop, tab, outl, s_cnt, s_hom, s_tot, overflow);
+      band_crop_regs(cur, pre);  // (the next item's metadata has arrived by now)
+      band_angle<1>(it, crop, tab, outl, s_cnt, s_hom, s_tot, overflow);
+      band_angle<2>(it, crop, tab, outl, s_cnt, s_hom, s_tot, overflow);
+      band_angle<3>(it, crop, tab, outl, s_cnt, s_hom, s_tot, overflow);
+      unsigned long long* f = glcm_raw + (((long long)it.fov * max_label + it.k) * C + it.ch) * (4 * kRedW);
+      if (overflow) {
+        if (threadIdx.x == 0) redo[2 + atomicAdd(&redo[0], 1)] = code;
+      } else if (threadIdx.x < 4 * kRedW) {
+        const int a = threadIdx.x / kRedW, k = threadIdx.x - a * kRedW;
+        const unsigned long long h = s_tot[a * kRedW + 8];
+        f[threadIdx.x] = k < 8 ? s_tot[threadIdx.x] : k == 8 ? (h & 0xffffffffull) : (h >> 32);
+      }
+    } else {
+      band_crop_regs(cur, pre);
+    }
+    if (threadIdx.x == 0) s_code[par] = ahead;
+    __syncthreads();  // totals read, the crop buffer free, the codes visible
+    for (int x = threadIdx.x; x < 4 * kRedW; x += kBT) s_tot[x] = 0ull;
+#ifdef CPX_GLCM_PROF
+    if (threadIdx.x == 0) {
+      const long long t_ = clock64();
+      atomicAdd(&g_glcm_prof[4], (unsigned long long)(t_ - pt0));
+      pt0 = t_;
+    }
+#endif
+  }
 }
 
 // crop slots: per FOV exclusive scan of C * bbox area; objects beyond the scratch capacity or
@@ -528,12 +988,14 @@ __global__ __launch_bounds__(1024) void k_crop_offsets(int C, int max_label,
                                                       const cpx_object* __restrict__ objects,
                                                       const cpx_fov_objects* __restrict__ hdr,
                                                       long long cap, long long* __restrict__ crop_off,
-                                                      int* __restrict__ glcm_next, cpx_fallback_lists fb) {
+                                                      int* __restrict__ glcm_next, cpx_fallback_lists fb,
+                                                      int* __restrict__ redo) {
   const int fov = blockIdx.x;
   const int n = hdr[fov].n_objects;
-  if (threadIdx.x == 0) {  // this FOV's work queues: k_tex_glcm [0, B), k_obj_stage [B, 2B)
+  if (threadIdx.x == 0) {  // this FOV's work queues: k_tex_band [0, B), k_obj_stage [B, 2B)
     glcm_next[fov] = 0;
     glcm_next[gridDim.x + fov] = 0;
+    if (fov == 0) redo[0] = redo[1] = 0;
   }
   __shared__ long long wsum[16];
   __shared__ long long base;
@@ -601,14 +1063,11 @@ __device__ __forceinline__ bool shape_fits(const cpx_object& o) {
 // Membership bitmask of object o over its bbox + 2-px margin (rows x wpr words in M): each
 // 32-lane half-wave builds one 32-bit word (r, cw); eight words per half-wave are loaded before
 // the first ballot so the label loads overlap.
-// The membership words from 16-byte label loads (CPX_STAGE_MASK16, default on): a lane reads 4
+// The membership words from 16-byte label loads: a lane reads 4
 // consecutive labels (raw buffer load, dword-aligned; four 4-byte loads where the piece would
 // cross the plane's ends), 8 lanes form a 32-pixel word, their 4-bit pieces OR-reduced over the
 // 8 lanes — instead of one 4-byte load per lane and pixel and a ballot per word: features -2-3 %
 // per object set (`gpurun_out/r05ab`)
-#ifndef CPX_STAGE_MASK16
-#define CPX_STAGE_MASK16 1
-#endif
 template <int NT>
 __device__ __forceinline__ void shape_mask16(const int* __restrict__ lab, int H, int W, const cpx_object& o,
                                              unsigned int* M) {
@@ -668,38 +1127,7 @@ __device__ __forceinline__ void shape_mask16(const int* __restrict__ lab, int H,
 template <int NT>
 __device__ __forceinline__ void shape_mask(const int* __restrict__ lab, int H, int W, const cpx_object& o,
                                            unsigned int* M) {
-  if constexpr (CPX_STAGE_MASK16) {
-    shape_mask16<NT>(lab, H, W, o, M);
-    return;
-  }
-  const int lane = threadIdx.x & 63;
-  const int ty = threadIdx.x >> 5, tx = threadIdx.x & 31;
-  const int L = o.label;
-  const int R0 = o.bbox[0] - 2, C0 = o.bbox[1] - 2;  // region origin (2-px margin)
-  const int rows = o.bbox[2] - o.bbox[0] + 4, cols = o.bbox[3] - o.bbox[1] + 4;
-  const int wpr = (cols + 31) >> 5;
-  const int nw = rows * wpr;
-  for (int w0 = 0; w0 < nw; w0 += 8 * (NT / 32)) {
-    int lv[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int w = w0 + u * (NT / 32) + ty;
-      const int r = w / wpr, cw = w - r * wpr;
-      const int c = cw * 32 + tx;
-      const int gr = R0 + r, gc = C0 + c;
-      const bool ok = w < nw && c < cols && gr >= 0 && gr < H && gc >= 0 && gc < W;
-      lv[u] = ok ? lab[(long long)gr * W + gc] : -1;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int w = w0 + u * (NT / 32) + ty;
-      const unsigned long long b = __ballot(lv[u] == L);
-      if (w < nw) {
-        if (lane == 0) M[w] = (unsigned int)b;
-        if (lane == 32) M[w] = (unsigned int)(b >> 32);
-      }
-    }
-  }
+  shape_mask16<NT>(lab, H, W, o, M);
 }
 
 // AreaShape sums of object o from its membership mask M (shape_mask; all threads, M complete and
@@ -858,18 +1286,10 @@ __global__ __launch_bounds__(256) void k_shape_props(int max_label, int F,
 // groups stay in registers between the two passes; the rest of a large bbox is read twice, with
 // the block's working set (one channel of one bbox, two blocks per CU) L2-resident in between.
 // block size and waves per SIMD of k_obj_stage (the object-per-block staging is latency-bound:
-// objects in flight per CU = blocks per CU); development builds override them
-#ifndef CPX_STAGE_NT
-#define CPX_STAGE_NT 512
-#endif
-#ifndef CPX_STAGE_WPE0
-#define CPX_STAGE_WPE0 4
-#endif
-#ifndef CPX_STAGE_WPE1
-#define CPX_STAGE_WPE1 4
-#endif
-constexpr int kOT = CPX_STAGE_NT;
-constexpr int stage_wpe(bool twin) { return twin ? CPX_STAGE_WPE1 : CPX_STAGE_WPE0; }
+// objects in flight per CU = blocks per CU; 3 blocks per CU at 80 VGPRs and 256-thread blocks at
+// 6 / 4 and 8 / 5 measured equal or slower, `gpurun_out/r05k`)
+constexpr int kOT = 512;
+constexpr int stage_wpe(bool) { return 4; }
 constexpr int stage_blocks_per_cu(bool twin) { return stage_wpe(twin) * 4 / (kOT / 64); }
 constexpr int kOG = 1;
 constexpr int kOR = 4;  // groups per iteration beyond the register-held ones
@@ -1242,6 +1662,7 @@ struct FeatWs {
   cpx_fallback_lists fb;
   long long* raws;
   unsigned long long* glcm_raw;
+  int* redo;  // k_tex_band -> k_tex_glcm: [0] count, [1] claim counter, [2..] item codes
   unsigned char* scratch;
   long long per_fov;
   int* twin;  // [2][B][max_label]: the twin map and done flags (cpx_features_pair only)
@@ -1254,8 +1675,9 @@ int feat_ws(cpx_ctx* ctx, int slot, int B, int C, int H, int W, int max_label, b
   const size_t raw_bytes = ((sizeof(long long) * kShapeRaw * (size_t)B * max_label + 255) / 256) * 256;
   const size_t glcm_bytes = ((sizeof(unsigned long long) * 4 * kRedW * (size_t)B * max_label * C + 255) / 256) * 256;
   const size_t twin_bytes = twin ? ((sizeof(int) * 2 * (size_t)B * max_label + 255) / 256) * 256 : 0;
+  const size_t redo_bytes = ((sizeof(int) * (2 + (size_t)B * max_label * C) + 255) / 256) * 256;
   unsigned char* ws = (unsigned char*)cpx_ws(ctx, slot, off_bytes + raw_bytes + glcm_bytes + twin_bytes +
-                                             (size_t)B * w->per_fov + 256);  // +256: crop read slack
+                                             redo_bytes + (size_t)B * w->per_fov + 256);  // +256: crop read slack
   if (!ws) return CPX_ERR_OOM;
   w->crop_off = (long long*)ws;
   w->glcm_next = (int*)(w->crop_off + (size_t)B * max_label);  // + k_obj_stage's queues at B
@@ -1266,7 +1688,8 @@ int feat_ws(cpx_ctx* ctx, int slot, int B, int C, int H, int W, int max_label, b
   w->raws = (long long*)(ws + off_bytes);
   w->glcm_raw = (unsigned long long*)(ws + off_bytes + raw_bytes);
   w->twin = twin ? (int*)(ws + off_bytes + raw_bytes + glcm_bytes) : nullptr;
-  w->scratch = ws + off_bytes + raw_bytes + glcm_bytes + twin_bytes;
+  w->redo = (int*)(ws + off_bytes + raw_bytes + glcm_bytes + twin_bytes);
+  w->scratch = ws + off_bytes + raw_bytes + glcm_bytes + twin_bytes + redo_bytes;
   return CPX_OK;
 }
 
@@ -1322,7 +1745,7 @@ int launch_offsets(cpx_ctx* ctx, const SetArgs& a, FeatWs& w, int B, int C, int 
   // k_obj_stage packs a staged crop's bbox offsets (bh <= 4092) x W in 24 bits: wider images
   // measure texture in the fallback kernel (cap 0: nothing staged)
   hipLaunchKernelGGL(k_crop_offsets, dim3(B), dim3(1024), 0, ctx->stream, C, max_label,
-                     a.objects, a.hdr, W <= 4096 ? w.per_fov : 0LL, w.crop_off, w.glcm_next, w.fb);
+                     a.objects, a.hdr, W <= 4096 ? w.per_fov : 0LL, w.crop_off, w.glcm_next, w.fb, w.redo);
   CPX_CHECK_LAUNCH("k_crop_offsets");
   return CPX_OK;
 }
@@ -1351,12 +1774,19 @@ int launch_texture(cpx_ctx* ctx, const SetArgs& a, FeatWs& w, int B, int C, int 
   hipLaunchKernelGGL(k_shape_props, dim3(cpx_div_up(max_label, 256), B), dim3(256), 0, ctx->stream,
                      max_label, F, a.objects, a.hdr, (const long long*)w.raws, a.feats);
   CPX_CHECK_LAUNCH("k_shape_props");
-  const int per_fov_t = std::max(1, std::min(max_label * C, (ctx->n_cu + B - 1) / B));
+  // three 256-thread band blocks per CU over the per-FOV queues, then the dense kernel (one block
+  // per CU) over the items whose outliers overflowed the band kernel's list (none on the bench
+  // plates; its blocks exit at once when the list is empty)
+  const int per_fov_b = std::max(1, std::min(max_label * C, (3 * ctx->n_cu + B - 1) / B));
   const int tev = ctx->glcm_timing && ctx->glcm_nev < cpx_ctx::kGlcmEv ? ctx->glcm_nev++ : -1;
   if (tev >= 0) CPX_CHECK_HIP(hipEventRecord(ctx->glcm_ev[tev][0], ctx->stream));
-  hipLaunchKernelGGL(k_tex_glcm, dim3(per_fov_t, B), dim3(kTT), 0, ctx->stream, C, max_label,
+  hipLaunchKernelGGL(k_tex_band, dim3(per_fov_b, B), dim3(kBT), 0, ctx->stream, C, max_label,
+                     a.objects, a.hdr, (const long long*)w.crop_off, (const unsigned char*)w.scratch,
+                     w.per_fov, w.glcm_next, w.glcm_raw, w.redo);
+  CPX_CHECK_LAUNCH("k_tex_band");
+  hipLaunchKernelGGL(k_tex_glcm, dim3(ctx->n_cu, 1), dim3(kTT), 0, ctx->stream, C, max_label,
                      F, a.objects, a.hdr, (const long long*)w.crop_off,
-                     (const unsigned char*)w.scratch, w.per_fov, w.glcm_next, w.glcm_raw);
+                     (const unsigned char*)w.scratch, w.per_fov, w.glcm_next, w.glcm_raw, w.redo);
   CPX_CHECK_LAUNCH("k_tex_glcm");
   if (tev >= 0) CPX_CHECK_HIP(hipEventRecord(ctx->glcm_ev[tev][1], ctx->stream));
   hipLaunchKernelGGL(k_glcm_props, dim3(cpx_div_up(max_label * C * 4, 256), B), dim3(256), 0, ctx->stream,
