@@ -47,7 +47,7 @@ def parse():
                          "runs on pipeline i %% pipes, so that many batches are in flight")
     ap.add_argument("--cu-split", choices=("auto", "none", "interleave", "halves"), default=None,
                     help="each pipeline's stream restricted to its own share of the CUs "
-                         "(cpx.device.pipeline_streams; default CPX_CU_SPLIT or auto: halves for "
+                         "(cpx.device.pipeline_streams; default auto: halves for "
                          "two pipelines)")
     ap.add_argument("--cpnet-precision", choices=("f16x3", "bf16", "fp32"), default="f16x3",
                     help="CPnet arithmetic: f16x3 = native split-fp16 MFMA kernels at the fp32 network's "

@@ -250,8 +250,7 @@ class Device:
 # `r05at`: 457.0 -> 461.1 FOV/s): the two batches' kernels stop evicting each other from the
 # CUs' LDS and L2 while the stage exclusivity (pipeline.STAGE_EXCLUSIVE) still keeps their CPnets
 # apart; interleaved CUs measured no better than none, dropping the exclusivity 2 % worse,
-# three pipelines in thirds 18 % worse.  CPX_CU_SPLIT=none|halves|interleave overrides.
-CU_SPLIT = os.environ.get("CPX_CU_SPLIT", "auto")
+# three pipelines in thirds 18 % worse.  Callers choose with `split` (bench.py --cu-split).
 
 
 class _MaskedStreams:
@@ -306,13 +305,13 @@ def pipeline_streams(device, n: int, split: str | None = None) -> list:
     td = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
     if td.index is None:
         td = torch.device("cuda", torch.cuda.current_device())
-    split = split or CU_SPLIT
+    split = split or "auto"
     if split == "auto":
         split = "halves" if n == 2 else "none"
     if split == "none" or n < 2:
         return [torch.cuda.Stream(device=td) for _ in range(n)]
     if split not in ("halves", "interleave"):
-        raise ValueError(f"CPX_CU_SPLIT: {split!r}")
+        raise ValueError(f"pipeline_streams: split {split!r}")
     return _MaskedStreams.get(td, n, split)
 
 

@@ -29,13 +29,14 @@ from .device import Device, as_numpy, n_features
 from .segment import CELLPOSE_MODEL, DIAMETER, Segmenter
 
 OBJECT_SETS = ("Nuclei", "Cells", "Cytoplasm")
-# stages that never overlap themselves across the batches in flight on one GPU (FovPipeline._stage;
-# "" for none): the CPnet and the feature stage, each contending with its own copy for HBM / MFMA
-# and LDS, overlap better with the other batch's different stages — 439.5 -> 446.4 FOV/s
-# (three interleaved pairs of 60-step benches, `gpurun_out/r05t`)
-STAGE_EXCLUSIVE = [x for x in os.environ.get("CPX_STAGE_EXCLUSIVE", "cpnet,features").split(",") if x]
-# Cells + Cytoplasm features in one libcpx call (CPX_PAIR_FEATURES=0: one call per set, A/B runs)
-PAIR_FEATURES = os.environ.get("CPX_PAIR_FEATURES", "1") != "0"
+# stages that never overlap themselves across the batches in flight on one GPU (FovPipeline._stage):
+# the CPnet and the feature stage, each contending with its own copy for HBM / MFMA and LDS,
+# overlap better with the other batch's different stages — 439.5 -> 446.4 FOV/s (three interleaved
+# pairs of 60-step benches, `gpurun_out/r05t`); tests/test_gpu_streams.py runs both settings
+STAGE_EXCLUSIVE = ("cpnet", "features")
+# Cells + Cytoplasm features in one libcpx call (tests/test_gpu_features_pair.py checks it against
+# one call per set, bit for bit)
+PAIR_FEATURES = True
 log = logging.getLogger("cpx.pipeline")
 
 
@@ -199,10 +200,10 @@ class FovPipeline:
         self.qc, self.hdr, self.objects, self.feats = sl["qc"], sl["hdr"], sl["objects"], sl["feats"]
 
     # ---- stages ---------------------------------------------------------------------------
-    # CPX_STAGE_EXCLUSIVE (comma-separated stage names: illum_qc, cpnet, seg_post, cells,
-    # features): a listed stage of one pipeline waits on the device for the same stage of the
-    # pipeline enqueued before it (one shared event per device and stage), so two batches in
-    # flight never run that stage at once and overlap only across different stages
+    # A stage in STAGE_EXCLUSIVE (of illum_qc, cpnet, seg_post, cells, features) of one pipeline
+    # waits on the device for the same stage of the pipeline enqueued before it (one shared event
+    # per device and stage), so two batches in flight never run that stage at once and overlap
+    # only across different stages
     _excl: dict = {}
 
     def _stage(self, name, fn):

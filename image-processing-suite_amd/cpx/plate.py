@@ -32,6 +32,7 @@ import json
 import logging
 import os
 import shutil
+import sys
 import time
 import time as _time  # run() binds `time` to the job's timepoint
 
@@ -46,7 +47,10 @@ import numpy as np
 # imported first (`python -m cpx.plate`, cpx.launch's ranks).  A lower value in the environment
 # (the GPU boxes export HIP's default of 4) is raised; CPX_PLATE_HW_QUEUES overrides the 8.
 PLATE_HW_QUEUES = int(os.environ.get("CPX_PLATE_HW_QUEUES", "8"))
+_HW_QUEUES_LATE = False  # the raise came after HIP was initialised in this process (no effect)
 if int(os.environ.get("GPU_MAX_HW_QUEUES") or 4) < PLATE_HW_QUEUES:
+    _torch = sys.modules.get("torch")
+    _HW_QUEUES_LATE = bool(_torch is not None and _torch.cuda.is_initialized())
     os.environ["GPU_MAX_HW_QUEUES"] = str(PLATE_HW_QUEUES)
 
 log = logging.getLogger("cpx.plate")
@@ -247,6 +251,10 @@ def run(argv=None):
 
     a = parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s: %(message)s")
+    if _HW_QUEUES_LATE:
+        log.warning("GPU_MAX_HW_QUEUES was raised to %d after HIP was initialised in this process, so "
+                    "the pipelines keep HIP's default hardware queues and overlap less; import "
+                    "cpx.plate before any GPU call (python -m cpx.plate / cpx.launch do)", PLATE_HW_QUEUES)
     chans = list(a.channels)
     C = len(chans)
     LAST_TIMING.clear()
@@ -300,7 +308,7 @@ def _torchrun_merge(a, dirs):
     if not dist.is_available() or "MASTER_ADDR" not in os.environ:
         return
     if not dist.is_initialized():
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", rank=a.rank, world_size=a.world)
     dist.barrier()
     if a.rank == 0:
         for d in dirs:
@@ -352,10 +360,10 @@ def _run_sites(a, table, source, chans, state, out, status):
         illum = _illum(a.illum_path, chans, H, W)
         from .device import pipeline_streams
         streams, pipes = [], []
-        # unrestricted CUs here unless CPX_CU_SPLIT says otherwise: with its uploads and result
-        # copies beside the pipelines the plate measured 372-389 FOV/s with CU-split streams
-        # against 367-403 without (`gpurun_out/r05au`, `r05az`; the bench gains from the split)
-        split = None if "CPX_CU_SPLIT" in os.environ else "none"
+        # unrestricted CUs here: with its uploads and result copies beside the pipelines the plate
+        # measured 372-389 FOV/s with CU-split streams against 367-403 without (`gpurun_out/r05au`,
+        # `r05az`; the HBM-resident bench gains from the split)
+        split = "none"
         for st in pipeline_streams(a.device, max(1, a.pipes), split):
             with torch.cuda.stream(st):
                 pipes.append(FovPipeline(Device(a.device), cfg, illum))

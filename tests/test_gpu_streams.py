@@ -23,11 +23,15 @@ def _same(a, b):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("split", ["none", "halves"])
-def test_two_streams_match_serial(split):
+@pytest.mark.parametrize("split,exclusive", [("none", ("cpnet", "features")), ("halves", ("cpnet", "features")),
+                                             ("halves", ())])
+def test_two_streams_match_serial(split, exclusive, monkeypatch):
     """split "halves": the product default (cpx.device.pipeline_streams), each stream on its own
-    half of the CUs by a CU mask."""
+    half of the CUs by a CU mask; exclusive: the stages that wait for the other pipeline's same
+    stage (the product's pipeline.STAGE_EXCLUSIVE, and none)."""
     import torch
+    import cpx.pipeline as pl
+    monkeypatch.setattr(pl, "STAGE_EXCLUSIVE", exclusive)
     from cpx.device import Device, pipeline_streams
     from cpx.pipeline import FovPipeline, PipelineConfig
     from cpx.synth import synth_fovs, synth_illum

@@ -7,6 +7,8 @@ import filecmp
 import json
 import os
 import socket
+import time
+import zlib
 
 import numpy as np
 import pandas as pd
@@ -178,3 +180,102 @@ def test_work_queue_reused_directory(tmp_path, caplog):
     with caplog.at_level("ERROR", logger="cpx.plate"):
         assert list(plate.batch_source(table, bare, 0)) == []
     assert "already exhausted" in caplog.text
+
+
+# ---- configs[3]'s job shape at world size 8 (multi-GPU readiness without hardware)
+# 8 plates x 4 times = 32 (plate, time) jobs, one LoadData CSV each (Feature_extraction_opt.py:
+# 63-76 fans them out), drained by eight ranks from the shared WorkQueue of cpx.plate exactly as
+# on an 8-GPU node; the per-site GPU measurement is replaced by a deterministic CPU stub of what
+# FovPipeline.fetch hands plate.run (the same add_image / add_objects / status calls).
+
+W8_CHANS = ("DNA", "AGP")
+
+
+def _w8_jobs(tmp, n_plates=8, times=(6, 12, 24, 48), wells=3, sites=2):
+    paths = []
+    for p in range(n_plates):
+        for t in times:
+            rows = [{"Metadata_Plate": f"P{p + 1:02d}", "Metadata_Well": f"B{w + 1:02d}", "Metadata_Site": s + 1,
+                     "Metadata_Timepoint": t, **{f"FileName_{c}": f"p{p}t{t}w{w}s{s}{c}.tiff" for c in W8_CHANS}}
+                    for w in range(wells) for s in range(sites)]
+            path = os.path.join(tmp, f"ld_P{p + 1:02d}_{t}.csv")
+            pd.DataFrame(rows).to_csv(path, index=False)
+            paths.append(path)
+    return paths
+
+
+def _w8_stub_run_sites(claims_path):
+    """A _run_sites that measures each claimed batch with a seeded stub (no GPU) and logs the
+    claimed rows per job to claims_path."""
+    def run_sites(a, table, source, chans, state, out, status):
+        n = 0
+        job = f"{table['Metadata_Plate'].iloc[0]}/{table['Metadata_Timepoint'].iloc[0]}"
+        for rows in source:
+            with open(claims_path, "a") as f:
+                f.write(json.dumps({"job": job, "rows": rows}) + "\n")
+            time.sleep(0.02)  # (so that every rank gets to claim, as slower GPU batches would)
+            for r in rows:
+                img = int(table.index[r]) + 1
+                meta = table.iloc[r].to_dict()
+                rng = np.random.default_rng([zlib.crc32(job.encode()), img])
+                k = int(rng.integers(0, 5))
+                out.add_image(img, meta, rng.standard_normal(len(chans)), rng.random(len(chans)),
+                              {t: k for t in OBJECT_TABLES})
+                for t in OBJECT_TABLES:
+                    out.add_objects(t, img, rng.permutation(np.arange(1, k + 1)),
+                                    rng.standard_normal((k, len(out.cols))))
+                status.append({"ImageNumber": img, "status": "success" if k else "empty", "n_cells": k})
+                n += 1
+        state["timing"] = {}
+        return n
+    return run_sites
+
+
+def _w8_rank(rank, world, port, argv, claims_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    plate._run_sites = _w8_stub_run_sites(claims_path)
+    plate.run(argv + ["--rank", str(rank), "--world", str(world)])
+    dist.destroy_process_group()
+
+
+def test_gloo_world8_work_queue_configs3_jobs(tmp_path):
+    """Eight gloo ranks drain 32 jobs (8 plates x 4 times, 2 FOVs per batch) from one WorkQueue:
+    every batch of every job is claimed exactly once, the merged <plate>/<time>/ CSVs equal a
+    one-process run byte for byte, and the per-rank claim counts are reported."""
+    jobs = _w8_jobs(str(tmp_path))
+    common = ["--load-data", *jobs, "--data-path", str(tmp_path), "--channels", *W8_CHANS, "--batch", "2"]
+    # one process
+    plate._run_sites, keep = _w8_stub_run_sites(str(tmp_path / "claims_w1.jsonl")), plate._run_sites
+    try:
+        plate.run(common + ["--out", str(tmp_path / "one"), "--world", "1", "--rank", "0"])
+    finally:
+        plate._run_sites = keep
+    # eight ranks, one shared queue
+    world, port = 8, _port()
+    argv = common + ["--out", str(tmp_path / "eight"), "--queue", str(tmp_path / "queue"), "--queue-token", "w8"]
+    claims = [str(tmp_path / f"claims_r{r}.jsonl") for r in range(world)]
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_w8_rank, args=(r, world, port, argv, claims[r])) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    got = {}
+    per_rank = []
+    for r, c in enumerate(claims):
+        lines = [json.loads(x) for x in open(c)] if os.path.exists(c) else []
+        per_rank.append(len(lines))
+        for x in lines:
+            got.setdefault(x["job"], []).append(x["rows"])
+    print("[world8] batches claimed per rank:", per_rank, flush=True)
+    assert len(got) == len(jobs)
+    for job, batches in got.items():  # 6 rows per job -> batches [0,1], [2,3], [4,5], once each
+        assert sorted(batches) == [[0, 1], [2, 3], [4, 5]], (job, batches)
+    assert sum(per_rank) == 3 * len(jobs)
+    for p in range(8):
+        for t in (6, 12, 24, 48):
+            d1, d8 = tmp_path / "one" / f"P{p + 1:02d}" / str(t), tmp_path / "eight" / f"P{p + 1:02d}" / str(t)
+            assert not (d8 / plate.PARTS).exists()
+            for name in ("Image", *OBJECT_TABLES, "site_status"):
+                assert filecmp.cmp(d1 / f"{name}.csv", d8 / f"{name}.csv", shallow=False), (p, t, name)
