@@ -223,12 +223,13 @@ def main():
     if Z > 1:
         sub["zmax"] = 0.0
     glcm = {"ms": 0.0, "atomics": 0, "items": 0}
+    segt = {"follow_ms": 0.0, "item_steps": 0.0, "fe_reg_ms": 0.0}
 
     def glcm_acc(p):
-        # k_tex_glcm device time of this step (HIP events around its launches) and its LDS work:
-        # per staged (object, channel) item and angle, one LDS atomic per pair slot of the crop
-        # (rows - dr) x crop_stride(bw) (masked and background slots go to a sink word: atomics
-        # too) and one 128 KiB table scan
+        # GLCM device time of this step (HIP events around k_tex_band and the k_tex_glcm redo
+        # pass) and its LDS work: per staged (object, channel) item and angle, one LDS atomic per
+        # pair slot of the crop (rows - dr) x crop_stride(bw) (masked and background slots go to a
+        # sink counter: atomics too) and one scan of the 65 x 512-byte band table
         ms, nl = ct.c_double(), ct.c_int()
         dev.lib.cpx_debug_glcm_ms(dev.h, ct.byref(ms), ct.byref(nl))
         dev.lib.cpx_debug_glcm_timing(dev.h, 0)
@@ -262,6 +263,7 @@ def main():
         ev[3].record()
         pipe.seg._run_net()
         ev[4].record()
+        dev.lib.cpx_debug_seg_timing(dev.h, 1)
         pipe.seg.postprocess(pipe.labels["Nuclei"])
         ev[5].record()
         pipe.stage_cells()
@@ -271,6 +273,12 @@ def main():
         ev[7].record()
         torch.cuda.synchronize()
         glcm_acc(pipe)
+        fm, isteps, fe = ct.c_double(), ct.c_double(), ct.c_double()
+        dev.lib.cpx_debug_seg_stats(dev.h, ct.byref(fm), ct.byref(isteps), ct.byref(fe), None)
+        dev.lib.cpx_debug_seg_timing(dev.h, 0)
+        segt["follow_ms"] += fm.value
+        segt["item_steps"] += isteps.value
+        segt["fe_reg_ms"] += fe.value
         sub["illum"] += ev[0].elapsed_time(ev[1])
         sub["qc_rps"] += ev[1].elapsed_time(ev[2])
         sub["seg_prep"] += ev[2].elapsed_time(ev[3])
@@ -350,16 +358,41 @@ def main():
     copy_gbs = 2 * (1 << 31) * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9
     del src_b, dst_b
 
-    # k_tex_glcm against its LDS floor: the no-return LDS atomic rate on random
+    # the GLCM against its LDS floor: the no-return LDS atomic rate on random
     # addresses, 64 / 7.59 per CU-cycle (tools/micro/lds_atomic.hip, profiles/r05p_lds_atomic.log),
-    # and the 4 x 128 KiB table scans per item at 256 B per CU-cycle, at 2.4 GHz on every CU
+    # and the 4 band-table scans (65 x 512 B) per item at 256 B per CU-cycle, at 2.4 GHz on every CU
     n_cu = torch.cuda.get_device_properties(td).multi_processor_count
     glcm_ms = glcm["ms"] / a.stage_steps
     atomics = glcm["atomics"] / a.stage_steps
     items = glcm["items"] / a.stage_steps
     atomic_peak = n_cu * LDS_ATOMICS_PER_CU_CLK * CLOCK_HZ
-    floor_ms = (atomics / LDS_ATOMICS_PER_CU_CLK + items * 4 * 131072 / 256) / (n_cu * CLOCK_HZ) * 1e3
-    glcm_roof = {"kernel": "k_tex_glcm", "bound": "lds_atomic", "achieved": round(atomics / (glcm_ms * 1e-3) / 1e9, 1),
+    floor_ms = (atomics / LDS_ATOMICS_PER_CU_CLK + items * 4 * 65 * 512 / 256) / (n_cu * CLOCK_HZ) * 1e3
+    # flow following (k_dyn_follow): each step of a trajectory is two 16-byte gathers
+    # of the float2 field returned through the CU's L1 at 64 B per clock, i.e. 2 item-steps per
+    # CU-clock; item-steps = items per round x steps per round (an upper bound: a trajectory at an
+    # exact fixed point stops early) over the follow rounds' device time
+    follow_ms = segt["follow_ms"] / a.stage_steps
+    isteps = segt["item_steps"] / a.stage_steps
+    follow_peak = n_cu * 2.0 * CLOCK_HZ
+    follow_roof = {"kernel": "k_dyn_follow", "bound": "l1_return", "unit": "G item-steps/s",
+                   "achieved": round(isteps / (follow_ms * 1e-3) / 1e9, 1) if follow_ms else None,
+                   "peak": round(follow_peak / 1e9, 1),
+                   "frac": round(isteps / (follow_ms * 1e-3) / follow_peak, 4) if follow_ms else None,
+                   "item_steps_per_step": int(isteps), "avg_launch_ms": round(follow_ms, 4),
+                   "note": "item-steps are an upper bound (items per round x steps per round)"}
+    # the register flow-error screening kernels (k_flow_error_reg*): VALU-issue bound —
+    # instructions from the committed SQ_INSTS_VALU pass (profiles/r*_sq_flow_error.json, scaled
+    # to the batch), 2 cycles per wave64 VALU instruction on 4 SIMDs per CU, over their live time
+    fe_ms = segt["fe_reg_ms"] / a.stage_steps
+    fe_valu, fe_src = sq_flow_error(B) if (Z <= 1 and H == 2080) else (None, None)
+    fe_peak = n_cu * 4 * CLOCK_HZ / 2.0  # wave-instructions per second
+    fe_roof = {"kernel": "k_flow_error_reg*", "bound": "valu_issue", "unit": "G wave-instr/s",
+               "achieved": round(fe_valu / (fe_ms * 1e-3) / 1e9, 1) if fe_valu and fe_ms else None,
+               "peak": round(fe_peak / 1e9, 1),
+               "frac": round(fe_valu / (fe_ms * 1e-3) / fe_peak, 4) if fe_valu and fe_ms else None,
+               "valu_wave_instr_per_step": int(fe_valu) if fe_valu else None, "valu_source": fe_src,
+               "avg_launch_ms": round(fe_ms, 4)}
+    glcm_roof = {"kernel": "k_tex_band", "bound": "lds_atomic", "achieved": round(atomics / (glcm_ms * 1e-3) / 1e9, 1),
                  "peak": round(atomic_peak / 1e9, 1), "unit": "Gatomic/s",
                  "frac": round(atomics / (glcm_ms * 1e-3) / atomic_peak, 4) if glcm_ms else None,
                  "lds_floor_ms": round(floor_ms, 4), "floor_frac": round(floor_ms / glcm_ms, 4) if glcm_ms else None,
@@ -399,7 +432,8 @@ def main():
                             if n_obj else None),
         "stage_ms_per_step": {k: round(v, 3) for k, v in {**per_step_ms, **sub_ms}.items()},
         "roofline": roof(dominant),
-        "roofline_all": {**{k: roof(k) for k in kernels}, "glcm": glcm_roof},
+        "roofline_all": {**{k: roof(k) for k in kernels}, "glcm": glcm_roof, "follow": follow_roof,
+                         "flow_error_reg": fe_roof},
         "hbm_copy_measured_GBs": round(copy_gbs, 1),
     }
     if cpu_ctx is not None:
@@ -435,6 +469,18 @@ def pmc_traffic(batch, precision):
     if "cpnet" in fam:
         out.setdefault("cpnet", int(fam["cpnet"]["total"] * scale))
     return out, os.path.relpath(files[-1], REPO)
+
+
+def sq_flow_error(batch):
+    """SQ_INSTS_VALU (wave-instructions) of the register flow-error kernels per step of `batch`
+    FOVs, from the newest profiles/r*_sq_flow_error.json (tools/pmc_sq.py --json over a
+    rocprofv3 --pmc pass of this bench); (None, None) if none is present."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_sq_flow_error.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d["valu_per_step"] * batch / float(d["fovs_per_step"]), os.path.relpath(files[-1], REPO)
 
 
 CPU_BASELINE_MAX_CORES = 16  # the GPU box's CPU share per GPU (os.cpu_count() shows the host)

@@ -107,6 +107,9 @@ SIGNATURES = {
     "cpx_csv_format": (_I64, [_I64, _I64, _I, _P, _P, _P, _P, _I64]),
     "cpx_debug_glcm_timing": (_I, [_P, _I]),
     "cpx_debug_glcm_ms": (_I, [_P, ct.POINTER(ct.c_double), ct.POINTER(_I)]),
+    "cpx_debug_seg_timing": (_I, [_P, _I]),
+    "cpx_debug_seg_stats": (_I, [_P, ct.POINTER(ct.c_double), ct.POINTER(ct.c_double), ct.POINTER(ct.c_double),
+                                 ct.POINTER(_I)]),
     "cpx_expand_labels": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     "cpx_watershed_cells": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I]),
     "cpx_seg_percentiles": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),

@@ -82,6 +82,11 @@ void cpx_destroy(cpx_ctx* ctx) {
   for (int i = 0; i < cpx_ctx::kGlcmEv; ++i)
     for (int k = 0; k < 2; ++k)
       if (ctx->glcm_ev[i][k]) (void)hipEventDestroy(ctx->glcm_ev[i][k]);
+  for (int i = 0; i < cpx_ctx::kSegEv; ++i) {
+    for (int k = 0; k < 4; ++k)
+      if (ctx->seg_ev[i][k]) (void)hipEventDestroy(ctx->seg_ev[i][k]);
+    if (ctx->seg_cnt[i]) (void)hipHostFree(ctx->seg_cnt[i]);
+  }
   delete ctx;
 }
 
@@ -107,6 +112,39 @@ int cpx_debug_glcm_ms(cpx_ctx* ctx, double* ms_out, int* launches_out) {
   *ms_out = ms;
   if (launches_out) *launches_out = ctx->glcm_nev;
   ctx->glcm_nev = 0;
+  return CPX_OK;
+}
+
+int cpx_debug_seg_timing(cpx_ctx* ctx, int enable) {
+  CPX_REQUIRE(ctx != nullptr, CPX_ERR_ARG, "cpx_debug_seg_timing: ctx is NULL");
+  if (enable && !ctx->seg_ev[0][0])
+    for (int i = 0; i < cpx_ctx::kSegEv; ++i)
+      for (int k = 0; k < 4; ++k) CPX_CHECK_HIP(hipEventCreate(&ctx->seg_ev[i][k]));
+  ctx->seg_timing = enable ? 1 : 0;
+  ctx->seg_nev = 0;
+  return CPX_OK;
+}
+
+int cpx_debug_seg_stats(cpx_ctx* ctx, double* follow_ms, double* item_steps, double* fe_reg_ms, int* calls) {
+  CPX_REQUIRE(ctx && follow_ms && item_steps && fe_reg_ms, CPX_ERR_ARG, "cpx_debug_seg_stats: null argument");
+  double fm = 0.0, st = 0.0, fe = 0.0;
+  for (int i = 0; i < ctx->seg_nev; ++i) {
+    CPX_CHECK_HIP(hipEventSynchronize(ctx->seg_ev[i][3]));
+    float t = 0.0f;
+    CPX_CHECK_HIP(hipEventElapsedTime(&t, ctx->seg_ev[i][0], ctx->seg_ev[i][1]));
+    fm += t;
+    CPX_CHECK_HIP(hipEventElapsedTime(&t, ctx->seg_ev[i][2], ctx->seg_ev[i][3]));
+    fe += t;
+    const int B = ctx->seg_B[i];
+    const int* c = ctx->seg_cnt[i];
+    for (int r = 0; r < ctx->seg_rounds[i]; ++r)
+      for (int b = 0; b < B; ++b) st += (double)c[r * B + b] * ctx->seg_K[i][r];
+  }
+  *follow_ms = fm;
+  *item_steps = st;
+  *fe_reg_ms = fe;
+  if (calls) *calls = ctx->seg_nev;
+  ctx->seg_nev = 0;
   return CPX_OK;
 }
 

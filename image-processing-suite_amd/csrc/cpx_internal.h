@@ -43,6 +43,16 @@ struct cpx_ctx {
   static constexpr int kGlcmEv = 64;
   int glcm_timing = 0, glcm_nev = 0;
   hipEvent_t glcm_ev[kGlcmEv][2] = {};
+  // segmentation post-processing timing (cpx_debug_seg_timing, bench.py's flow-following and
+  // flow-error rooflines): per cpx_seg_masks call, events around the follow rounds and around
+  // the register flow-error kernels, the per-round item counts (pinned host copy) and steps
+  static constexpr int kSegEv = 16;
+  int seg_timing = 0, seg_nev = 0;
+  hipEvent_t seg_ev[kSegEv][4] = {};
+  int* seg_cnt[kSegEv] = {};          // pinned: [B] n_moving, then [rounds][B] items of rounds >= 1
+  int seg_cnt_cap[kSegEv] = {};
+  int seg_B[kSegEv] = {}, seg_rounds[kSegEv] = {};
+  int seg_K[kSegEv][64] = {};         // steps per round
 };
 
 void cpx_fov_free(cpx_ctx* ctx);

@@ -2441,6 +2441,10 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   // the segmentation parity tests
   static const int follow_ni = getenv("CPX_FOLLOW_NI") ? atoi(getenv("CPX_FOLLOW_NI")) : 2;
   static const bool follow_v4 = !getenv("CPX_FOLLOW_V4") || atoi(getenv("CPX_FOLLOW_V4")) != 0;
+  // (development / bench instrumentation: cpx_debug_seg_timing)
+  const int sev = ctx->seg_timing && ctx->seg_nev < cpx_ctx::kSegEv ? ctx->seg_nev++ : -1;
+  bool fe_timed = false;  // the register flow-error kernels were bracketed (else a zero interval)
+  if (sev >= 0) CPX_CHECK_HIP(hipEventRecord(ctx->seg_ev[sev][0], ctx->stream));
   {
     const int fblk = std::max(1, std::min(cpx_div_up(n, kT), (16 * ctx->n_cu + B - 1) / B));
     int step = 0, r = 0;
@@ -2457,9 +2461,29 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
       hipLaunchKernelGGL(kern, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step, K,
                          r == 0 ? 1 : 0, in, (const int*)(d.fcnt + (size_t)B * r), out,
                          d.fcnt + (size_t)B * (r + 1), d);
+      if (sev >= 0 && r < 64) ctx->seg_K[sev][r] = std::min(K, std::max(niter - step, 0));
       step += K;
       ++r;
     } while (step < niter);
+    if (sev >= 0) {
+      // items of round 0 = the moving pixels (cpx_seg_stats.n_moving, int 0 of each 48-byte
+      // record), of round r >= 1 = fcnt[B r + b]
+      CPX_CHECK_HIP(hipEventRecord(ctx->seg_ev[sev][1], ctx->stream));
+      const int rr = std::min(r, 64);
+      const int need = B * rr;
+      if (ctx->seg_cnt_cap[sev] < need) {
+        if (ctx->seg_cnt[sev]) CPX_CHECK_HIP(hipHostFree(ctx->seg_cnt[sev]));
+        CPX_CHECK_HIP(hipHostMalloc((void**)&ctx->seg_cnt[sev], sizeof(int) * need));
+        ctx->seg_cnt_cap[sev] = need;
+      }
+      CPX_CHECK_HIP(hipMemcpy2DAsync(ctx->seg_cnt[sev], sizeof(int), stats_dev, sizeof(cpx_seg_stats),
+                                     sizeof(int), B, hipMemcpyDeviceToHost, ctx->stream));
+      if (rr > 1)
+        CPX_CHECK_HIP(hipMemcpyAsync(ctx->seg_cnt[sev] + B, d.fcnt + B, sizeof(int) * B * (rr - 1),
+                                     hipMemcpyDeviceToHost, ctx->stream));
+      ctx->seg_B[sev] = B;
+      ctx->seg_rounds[sev] = rr;
+    }
   }
   hipLaunchKernelGGL(k_hist_init, gh, dim3(kT), 0, ctx->stream, Dy, Dx, d);
   hipLaunchKernelGGL(k_hist_moving, gp, dim3(kT), 0, ctx->stream, Dy, Dx, d);
@@ -2527,10 +2551,15 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
       // 128 x 120 in column pairs over two / three waves)
       // first, in VGPRs (k_flow_error_reg); the LDS kernels skip the masks those flagged
       static const bool reg = !getenv("CPX_FE_NOREG");
+      if (sev >= 0) CPX_CHECK_HIP(hipEventRecord(ctx->seg_ev[sev][2], ctx->stream));
       if (reg) {
         rc = cpx_flow_error_reg_launch(ctx->n_cu, ctx->stream, d.m0, (const float2*)d.dpf, Dy, Dx, B, ML,
                                        obj, off, off + B + 9, flow_threshold, bad, und);
         if (rc) return rc;
+      }
+      if (sev >= 0) {
+        CPX_CHECK_HIP(hipEventRecord(ctx->seg_ev[sev][3], ctx->stream));
+        fe_timed = true;
       }
       // six waves per SIMD for the small and mid classes; the large class as 512 threads with two
       // units each (the same masks as the fp64 1024 x 1 kernel), two 79 KiB blocks per CU
@@ -2617,6 +2646,10 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   hipLaunchKernelGGL(k_fill_holes_big, dim3(B), dim3(1024), 0, ctx->stream,
                      (const int*)labels_dev, H, W, ML, min_size, (const cpx_object*)obj,
                      (const cpx_fov_objects*)hdr, (const int*)l2i, fillidx, absorber, fscr);
+  if (sev >= 0 && !fe_timed) {
+    CPX_CHECK_HIP(hipEventRecord(ctx->seg_ev[sev][2], ctx->stream));
+    CPX_CHECK_HIP(hipEventRecord(ctx->seg_ev[sev][3], ctx->stream));
+  }
   hipLaunchKernelGGL(k_fill_final, dim3(B), dim3(1024), 0, ctx->stream, ML, min_size,
                      (const cpx_object*)obj, (const cpx_fov_objects*)hdr, (const int*)absorber,
                      (const int*)labels_dev, (const int*)fillidx, W, N, newlab, stats_dev);

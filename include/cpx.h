@@ -585,6 +585,15 @@ int cpx_fov_wait(cpx_ctx* ctx);
  * summed milliseconds and the launch count, then forgets them.  Not for timed regions.       */
 int cpx_debug_glcm_timing(cpx_ctx* ctx, int enable);
 int cpx_debug_glcm_ms(cpx_ctx* ctx, double* ms_out, int* launches_out);
+/* Segmentation post-processing instrumentation (bench.py's flow-following and flow-error
+ * rooflines): while enabled, each cpx_seg_masks call (up to 16 between reads) records events
+ * around its flow-following rounds and around its register flow-error kernels, and copies the
+ * per-round item counts to pinned host memory (a synchronous copy on the context's stream: not
+ * for captured or production runs).  cpx_debug_seg_stats waits for them and returns the summed
+ * milliseconds and the item-steps of the rounds (items per round x steps per round: an upper
+ * bound, an item at an exact fixed point stops early), then resets.                           */
+int cpx_debug_seg_timing(cpx_ctx* ctx, int enable);
+int cpx_debug_seg_stats(cpx_ctx* ctx, double* follow_ms, double* item_steps, double* fe_reg_ms, int* calls);
 
 /* ---- host: CSV rows of the measurement tables (Pycyto_pertime.py:46-49 reads them) ------- *
  * Rows [row0, row1) of a table of n_cols columns, column c at cols[c] with element stride
