@@ -621,11 +621,6 @@ __device__ __forceinline__ void band_keys(unsigned int a, unsigned int b, unsign
   row = (ms & (0x01010101u * kSinkRow)) | (~ms & row);
   unsigned int ent = (m1 & b) | (~m1 & a);
   ent = (ms & sink4) | (~ms & ent);
-  // table layout (band_add): entry e of row r is half (e >> 7) of word r * 128 + ((e + 8 r) mod
-  // 128) — counters i and i + 1 in different words, and the same i of neighbouring rows eight
-  // banks apart (a flat crop's hot keys (i, i + d), |d| <= 1, otherwise share one bank or word);
-  // per byte: bit 7 the half, bits 0-6 the rotated word offset
-  ent = (((ent & 0x7f7f7f7fu) + ((row & 0x0f0f0f0fu) << 3)) & 0x7f7f7f7fu) | (ent & 0x80808080u);
   klo = __builtin_amdgcn_perm(row, ent, 0x05010400u);
   khi = __builtin_amdgcn_perm(row, ent, 0x07030602u);
 }
@@ -634,7 +629,7 @@ __device__ __forceinline__ void band_keys(unsigned int a, unsigned int b, unsign
 // flat crop's dominant key serialises its lanes on one address — measured 15 % slower: the
 // ballots cost more than the conflicts, `gpurun_out/r06i`.)
 __device__ __forceinline__ void band_add(unsigned int* tab, unsigned int k) {
-  atomicAdd(&tab[((k >> 1) & 0x7f80u) | (k & 0x7fu)], ((k >> 7) & 1u) * 0xffffu + 1u);
+  atomicAdd(&tab[(k & 0xffffu) >> 1], (k & 1u) * 0xffffu + 1u);
 }
 
 // One chunk of eight reference pixels: a (A) and the b bytes at the angle's offset.
@@ -751,9 +746,7 @@ __device__ __forceinline__ void band_scan(unsigned int* tab, const unsigned shor
     if ((w[k].x | w[k].y | w[k].z | w[k].w) == 0u) continue;
     t4[u] = uint4{0u, 0u, 0u, 0u};
     const int row = u >> 5;
-    // the group's four words hold entries w0 + h (low halves) and w0 + 128 + h (high halves),
-    // h = 0..3, w0 the word offset before the row's rotation (band_keys)
-    const unsigned int w0 = (4u * (unsigned int)(u & 31) - 8u * (unsigned int)(row & 15)) & 127u;
+    const unsigned int e0 = (unsigned int)(u & 31) << 3;
     unsigned int s0 = dot2_u16(w[k].x, 0x10001u, 0u);
     s0 = dot2_u16(w[k].y, 0x10001u, s0);
     s0 = dot2_u16(w[k].z, 0x10001u, s0);
@@ -762,24 +755,16 @@ __device__ __forceinline__ void band_scan(unsigned int* tab, const unsigned shor
     q = dot2_u16(w[k].y, w[k].y, q);
     q = dot2_u16(w[k].z, w[k].z, q);
     q = dot2_u16(w[k].w, w[k].w, q);
-    // s1 = sum e c = w0 s0 + 128 s0hi + sh, s2 = sum e^2 c = w0^2 s0 + 2 w0 sh + shh +
-    // 256 w0 s0hi + 256 shi + 16384 s0hi, with sh = sum h (lo + hi), shh = sum h^2 (lo + hi),
-    // shi = sum h hi, s0hi = sum hi over the four words h
-    unsigned int s0hi = dot2_u16(w[k].x, 0x10000u, 0u);
-    s0hi = dot2_u16(w[k].y, 0x10000u, s0hi);
-    s0hi = dot2_u16(w[k].z, 0x10000u, s0hi);
-    s0hi = dot2_u16(w[k].w, 0x10000u, s0hi);
-    unsigned int sh = dot2_u16(w[k].y, 0x10001u, 0u);
-    sh = dot2_u16(w[k].z, 0x20002u, sh);
-    sh = dot2_u16(w[k].w, 0x30003u, sh);
-    unsigned int shh = dot2_u16(w[k].y, 0x10001u, 0u);
-    shh = dot2_u16(w[k].z, 0x40004u, shh);
-    shh = dot2_u16(w[k].w, 0x90009u, shh);
-    unsigned int shi = dot2_u16(w[k].y, 0x10000u, 0u);
-    shi = dot2_u16(w[k].z, 0x20000u, shi);
-    shi = dot2_u16(w[k].w, 0x30000u, shi);
-    const unsigned int s1 = w0 * s0 + 128u * s0hi + sh;
-    const unsigned int s2 = w0 * w0 * s0 + 2u * w0 * sh + shh + 256u * w0 * s0hi + 256u * shi + 16384u * s0hi;
+    // sum h c_h and sum h^2 c_h over the group's counters h = 0..7 (low half first)
+    unsigned int sk = dot2_u16(w[k].x, 0x00010000u, 0u);
+    sk = dot2_u16(w[k].y, 0x00030002u, sk);
+    sk = dot2_u16(w[k].z, 0x00050004u, sk);
+    sk = dot2_u16(w[k].w, 0x00070006u, sk);
+    unsigned int skk = dot2_u16(w[k].x, 0x00010000u, 0u);
+    skk = dot2_u16(w[k].y, 0x00090004u, skk);
+    skk = dot2_u16(w[k].z, 0x00190010u, skk);
+    skk = dot2_u16(w[k].w, 0x00310024u, skk);
+    const unsigned int s1 = e0 * s0 + sk, s2 = e0 * e0 * s0 + 2u * e0 * sk + skk;
     S.cnt += s0;
     S.asq += q;
     if (row < 2 * kBandD + 1) {
@@ -804,8 +789,7 @@ __device__ __forceinline__ void band_scan(unsigned int* tab, const unsigned shor
       S.dis += s1;
       const unsigned int v[4] = {w[k].x, w[k].y, w[k].z, w[k].w};
 #pragma unroll
-      for (int h = 0; h < 4; ++h)
-        S.hom += hom[w0 + h] * (v[h] & 0xffffu) + hom[w0 + 128 + h] * (v[h] >> 16);
+      for (int h = 0; h < 8; ++h) S.hom += hom[e0 + h] * ((v[h >> 1] >> (16 * (h & 1))) & 0xffffu);
     }
   }
   for (int e = threadIdx.x; e < n_out; e += kBT) {
