@@ -19,6 +19,7 @@
 //   * ring sums are fixed-order (one lane per ring per column, then a fixed-order column sum),
 //     the slope is computed on device exactly as scipy.stats.linregress (np.cov, bias=1).
 #include "cpx_internal.h"
+#include <type_traits>
 #include <math.h>
 #include <vector>
 
@@ -505,22 +506,23 @@ __device__ __forceinline__ void fill_t260(cplx* t260, const cplx* __restrict__ t
     t260[i] = i < 260 ? tw[8 * i] : cplx{kW8[i - 260][0], kW8[i - 260][1]};
 }
 
-// The three passes on one 2080-point sequence: load(n) gives point n (P1 threads call it for
-// their 13 points); on return A[j] = X[j] and A[260 + j] = X[1820 + j] (j < 260) and the block
+// The three passes on one 2080-point sequence: load(r, n) gives point n = tid + 160 r (P1
+// threads call it for their 13 points, r = 0 .. 12); on return A[j] = X[j] and A[260 + j] = X[1820 + j] (j < 260) and the block
 // is synchronised.  t260 must hold fill_t260's table (filled before, and synchronised by, P1's
 // barrier: P1 does not read it).
-template <typename Load>
-__device__ __forceinline__ void fft2080_pruned(cplx* A, const cplx* t260, Load load) {
-  const int tid = threadIdx.x;
+template <typename Load, typename AfterP1>
+__device__ __forceinline__ void fft2080_pruned(cplx* A, const cplx* t260, Load load, AfterP1 after_p1,
+                                               int tid = threadIdx.x) {
   // ---- P1
   if (tid < 160) {
     cplx v[13];
 #pragma unroll
-    for (int r = 0; r < 13; ++r) v[r] = load(tid + 160 * r);
+    for (int r = 0; r < 13; ++r) v[r] = load(r, tid + 160 * r);
     dft<13>(v, nullptr);
 #pragma unroll
     for (int r = 0; r < 13; ++r) A[13 * tid + r] = v[r];
   }
+  after_p1();
   __syncthreads();
   // ---- P2
   {
@@ -586,6 +588,52 @@ __device__ __forceinline__ void fft2080_pruned(cplx* A, const cplx* t260, Load l
   __syncthreads();
 }
 
+// A P1 thread's 13 points of both rows of a pair, as loaded (raw counts and the illumination
+// function's values): the next pair's are fetched into registers while the current pair is
+// transformed
+template <int ILLUM>
+struct QcRowPts {
+  using IT = typename std::conditional<ILLUM == 1, float, double>::type;
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  us2 r[13];     // raw counts of row 0 (x) and row 1 (y)
+  IT l[2][13];
+  // (o1 = o0 when the pair has no second row: its values are not used)
+  __device__ __forceinline__ void fetch(const unsigned short* rp, const void* il, long long o0, long long o1,
+                                        int tid) {
+    if (tid >= 160) return;
+    // uniform row bases and 32-bit lane offsets (scalar-base addressing: no 64-bit address per point)
+    const unsigned short* ra = rp + o0;
+    const unsigned short* rb = rp + o1;
+    const IT* la = static_cast<const IT*>(il) + o0;
+    const IT* lb = static_cast<const IT*>(il) + o1;
+#pragma unroll
+    for (int k = 0; k < 13; ++k) {
+      const int n = tid + 160 * k;
+      if (ILLUM != 3) {
+        r[k].x = ra[n];
+        r[k].y = rb[n];
+      }
+      if (ILLUM != 0) {
+        l[0][k] = la[n];
+        l[1][k] = lb[n];
+      }
+    }
+  }
+  // qval<ILLUM> of the loaded point
+  __device__ __forceinline__ double q(int row, int k) const {
+    const double rv = (double)(row ? r[k].y : r[k].x);
+    if (ILLUM == 1 || ILLUM == 2) return rv / (double)l[row][k];
+    if (ILLUM == 3) return (double)l[row][k];
+    return rv;
+  }
+};
+
+// kQcPairs row pairs per block, the next pair's loads in flight during the current pair's
+// transform: one pair per block left every load's latency exposed (104 VGPRs, four blocks per CU
+// by LDS: 3.61 ms per 48 FOVs); four pairs with the prefetch (158 VGPRs, three blocks per CU)
+// 2.70 ms, eight or sixteen 3.05 ms (gpurun_out/r06x)
+constexpr int kQcPairs = 4;
+
 template <int ILLUM>
 __global__ __launch_bounds__(kR2T) void k_qc_rows_2080(
     const unsigned short* __restrict__ raw, const void* __restrict__ illum, int C, int H,
@@ -596,7 +644,6 @@ __global__ __launch_bounds__(kR2T) void k_qc_rows_2080(
   __shared__ cplx t260[kT260];
   const int plane = blockIdx.y;
   const int ch = plane % C;
-  const int r0 = 2 * blockIdx.x, r1 = r0 + 1;
   const long long N = (long long)H * W;
   const unsigned short* rp = raw + (long long)plane * N;
   const void* il = nullptr;
@@ -605,28 +652,48 @@ __global__ __launch_bounds__(kR2T) void k_qc_rows_2080(
   const cpx_plane_stats st = stats[plane];
   const double mean = st.sum_q / (double)st.n;
   const int tid = threadIdx.x;
+  const int npair = (H + 1) / 2, p0 = blockIdx.x * kQcPairs, p1 = min(p0 + kQcPairs, npair);
   fill_t260(t260, tw);
   unsigned long long eq = 0;
-  // the two rows as one complex sequence (real-input pair trick), mean removed
-  fft2080_pruned(A, t260, [&](int n) {
-    const double qa = qval<ILLUM>(rp, il, (long long)r0 * W + n);
-    const double qb = r1 < H ? qval<ILLUM>(rp, il, (long long)r1 * W + n) : mean;
-    eq += (qa == mean) + (r1 < H && qb == mean);
-    return cplx{qa - mean, qb - mean};
-  });
+  QcRowPts<ILLUM> pts;
+  auto fetch = [&](int p, int lane_tid) {
+    const long long o0 = (long long)(2 * p) * W;
+    pts.fetch(rp, il, o0, 2 * p + 1 < H ? o0 + W : o0, lane_tid);
+  };
+  fetch(p0, tid);
+  for (int p = p0; p < p1; ++p) {
+    const int r0 = 2 * p, r1 = r0 + 1;
+    // the twiddles are re-read from LDS and the index arithmetic redone for each pair (an opaque
+    // copy of the thread index): hoisted out of the loop they held ~70-100 VGPRs
+    asm volatile("" ::: "memory");
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    // the two rows as one complex sequence (real-input pair trick), mean removed; the next
+    // pair's loads are issued once P1 has consumed this pair's
+    fft2080_pruned(A, t260, [&](int k, int) {
+      const bool has1 = r1 < H;  // (branch-free: row 1 was loaded as row 0 when it is missing)
+      const double qa = pts.q(0, k), q1 = pts.q(1, k);
+      const double qb = has1 ? q1 : mean;
+      eq += (qa == mean) + (has1 && qb == mean);
+      return cplx{qa - mean, qb - mean};
+    }, [&] {
+      if (p + 1 < p1) fetch(p + 1, t);
+    }, t);
+    // unpack the two real rows for k < KC: Z[N - k] = X[1820 + (260 - k)]
+    cplx* outa = rowspec + ((long long)plane * H + r0) * kR2KC;
+    for (int k = t; k < kR2KC; k += kR2T) {
+      const cplx zk = A[k];
+      const cplx zn = k == 0 ? A[0] : A[260 + 260 - k];
+      const cplx xa = {0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)};
+      const cplx dlt = {zk.x - zn.x, zk.y + zn.y};
+      const cplx xb = {0.5 * dlt.y, -0.5 * dlt.x};
+      outa[k] = xa;
+      if (r1 < H) outa[kR2KC + k] = xb;
+    }
+    __syncthreads();  // A is the next pair's P1 output
+  }
   eq = wave_sum(eq);
   if ((tid & 63) == 0 && eq) atomicAdd(&aux[plane].eq_count, eq);
-  // unpack the two real rows for k < KC: Z[N - k] = X[1820 + (260 - k)]
-  cplx* outa = rowspec + ((long long)plane * H + r0) * kR2KC;
-  for (int k = tid; k < kR2KC; k += kR2T) {
-    const cplx zk = A[k];
-    const cplx zn = k == 0 ? A[0] : A[260 + 260 - k];
-    const cplx xa = {0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)};
-    const cplx dlt = {zk.x - zn.x, zk.y + zn.y};
-    const cplx xb = {0.5 * dlt.y, -0.5 * dlt.x};
-    outa[k] = xa;
-    if (r1 < H) outa[kR2KC + k] = xb;
-  }
 }
 
 // Column pass for H = 2080: the same pruned transform of column j (the rows the rings use are
@@ -650,7 +717,7 @@ __global__ __launch_bounds__(kR2T) void k_qc_cols_2080(const cplx* __restrict__ 
   const int tid = threadIdx.x;
   fill_t260(t260, tw);
   const cplx* src = rowspec + (long long)plane * H * KC + j;
-  fft2080_pruned(A, t260, [&](int n) { return src[(long long)n * KC]; });
+  fft2080_pruned(A, t260, [&](int, int n) { return src[(long long)n * KC]; }, [] {});
   constexpr int NP = (520 + kR2T - 1) / kR2T;
   double pv[NP];
 #pragma unroll
@@ -771,10 +838,11 @@ extern "C" int cpx_qc_rps(cpx_ctx* ctx, const uint16_t* raw_dev, const void* ill
     }
     const size_t sh_rows = sizeof(cplx) * (size_t)W;
     dim3 grow((H + 1) / 2, n_planes);
+    const dim3 grow2080(cpx_div_up((H + 1) / 2, kQcPairs), n_planes);
     const void* il = illum_dtype == CPX_DTYPE_NONE ? nullptr : illum_dev;
     if (W == kR2N && KC == kR2KC && !getenv("CPX_QC_GENERIC")) {
       const cplx* t = (const cplx*)twW;
-#define CPX_R2(I) hipLaunchKernelGGL(k_qc_rows_2080<I>, grow, dim3(kR2T), 0, ctx->stream, raw_dev, il, C, H, \
+#define CPX_R2(I) hipLaunchKernelGGL(k_qc_rows_2080<I>, grow2080, dim3(kR2T), 0, ctx->stream, raw_dev, il, C, H, \
                                      stats_dev, t, rowspec, aux)
       if (illum_dtype == CPX_DTYPE_F32) CPX_R2(1);
       else if (illum_dtype == CPX_DTYPE_F64) CPX_R2(2);

@@ -125,42 +125,34 @@ __device__ __forceinline__ int border_pixel(int k) {
 }
 
 
-// Tiles of this block for this round: XCD x (the blocks b with b % 8 == x) owns the contiguous
-// tile range [total x / 8, total (x + 1) / 8) and block b takes the tiles lo + b / 8 + k * (blocks
-// on its XCD), so horizontally and vertically adjacent tiles run on one XCD at about the same
-// time and the 4-byte column halos they read from each other's lines hit that XCD's L2 (dealt
-// round-robin, every tile's halo columns pulled three lines per row from HBM).  Every thread
-// evaluates one tile's activity at once (flags of the previous round), writes the flags of
-// inactive tiles and appends active ones to the LDS list — an idle round costs one pass over the
-// flags, not a serial walk.  Active: every tile in round 0, later a tile with free pixels whose facing
-// neighbour's border changed (or whose own queue overflowed: kSelf).
-__device__ int schedule_tiles(const WsArgs& a, int round, const unsigned char* Fp,
-                              unsigned char* Fn, int* list, int* s_n) {
-  if (threadIdx.x == 0) *s_n = 0;
-  __syncthreads();
+// Tiles of a round: XCD x (the blocks b with b % 8 == x) owns the contiguous tile range
+// [total x / 8, total (x + 1) / 8) and block b takes the tiles lo + b / 8 + k * (blocks on its
+// XCD), so horizontally and vertically adjacent tiles run on one XCD at about the same time and
+// the 4-byte column halos they read from each other's lines hit that XCD's L2.  Blocks get few
+// tiles (kShare0 in round 0, kShare later) and the hardware dispatcher balances the rest: a free
+// tile costs ~10x an empty one, and with shares of 50-100 tiles per block the average wave sat
+// idle for 40 % of round 0 (SQ_WAVE_CYCLES against the kernel's duration, gpurun_out/r06o);
+// shares of 4 / 16 took the relax rounds from 5.47 to 4.61 ms per 48 FOVs (gpurun_out/r06s;
+// claiming chunks from per-XCD counters instead measured the same, 4.58 ms).  A block
+// evaluates its tiles at once, one per lane, from the flags of the previous round: inactive ones
+// get their flags written, active ones are relaxed in order.  Active: every tile in round 0,
+// later a tile with free pixels whose facing neighbour's border changed (or whose own queue
+// overflowed: kSelf).
+constexpr int kShare0 = 4, kShare = 16;
+static_assert(kShare0 <= kThreads && kShare <= kThreads, "one tile per lane");
+
+__device__ __forceinline__ bool tile_active(const WsArgs& a, int round, const unsigned char* Fp, int t) {
+  if (round == 0) return true;
   const int per = a.nty * a.ntx;
-  const int G = gridDim.x, xb = blockIdx.x & 7, xi = blockIdx.x >> 3;
-  const int ng = G < 8 ? G : 8, gx = (G - xb + 7) >> 3;
-  const int lo = (int)((long long)a.total * xb / ng), hi = (int)((long long)a.total * (xb + 1) / ng);
-  for (int k = threadIdx.x;; k += blockDim.x) {
-    const int t = lo + xi + k * gx;
-    if (t >= hi) break;
-    const int fov = t / per, tt = t - fov * per, ty = tt / a.ntx, tx = tt - ty * a.ntx;
-    // all flags loaded before use (clamped neighbour indices; edges masked after)
-    const int base = fov * per;
-    const unsigned char fs = Fp[t], fr = a.tfree[t];
-    const unsigned char fu = Fp[ty > 0 ? t - a.ntx : t], fd = Fp[ty + 1 < a.nty ? t + a.ntx : t];
-    const unsigned char fl = Fp[tx > 0 ? t - 1 : t], fg = Fp[tx + 1 < a.ntx ? t + 1 : t];
-    const bool nb = (ty > 0 && (fu & kDown)) || (ty + 1 < a.nty && (fd & kUp)) ||
-                    (tx > 0 && (fl & kRight)) || (tx + 1 < a.ntx && (fg & kLeft));
-    (void)base;
-    const bool act = round == 0 || (fr && (nb || (fs & kSelf)));
-    const unsigned char keep = 0;
-    if (act) list[atomicAdd(s_n, 1)] = t;
-    else Fn[t] = keep;
-  }
-  __syncthreads();
-  return *s_n;
+  const int fov = t / per, tt = t - fov * per, ty = tt / a.ntx, tx = tt - ty * a.ntx;
+  (void)fov;
+  // all flags loaded before use (clamped neighbour indices; edges masked after)
+  const unsigned char fs = Fp[t], fr = a.tfree[t];
+  const unsigned char fu = Fp[ty > 0 ? t - a.ntx : t], fd = Fp[ty + 1 < a.nty ? t + a.ntx : t];
+  const unsigned char fl = Fp[tx > 0 ? t - 1 : t], fg = Fp[tx + 1 < a.ntx ? t + 1 : t];
+  const bool nb = (ty > 0 && (fu & kDown)) || (ty + 1 < a.nty && (fd & kUp)) ||
+                  (tx > 0 && (fl & kRight)) || (tx + 1 < a.ntx && (fg & kLeft));
+  return fr && (nb || (fs & kSelf));
 }
 
 // border bits of a padded LDS offset (tile rows / columns 1..kT)
@@ -183,211 +175,222 @@ __global__ __launch_bounds__(kThreads, 2) void k_ws_relax(WsArgs a, int round,
   __shared__ unsigned short sQ[kQCap];
   unsigned short* sS = sQ;  // seed candidates
   __shared__ unsigned s_bits;
-  __shared__ int s_list[kThreads], s_n;
   const int lane = threadIdx.x;
   const long long hw = (long long)a.H * a.W;
-  const int nact = schedule_tiles(a, round, Fp, Fn, s_list, &s_n);
   const long long hwc = hw * a.C;
-  for (int j = 0; j < nact; ++j) {
-    const int t = s_list[j];
-    const int per = a.nty * a.ntx;
-    const int fov = t / per, tt = t - fov * per, ty = tt / a.ntx, tx = tt - ty * a.ntx;
-    const bool full = R0 || (Fp[t] & kSelf) != 0;
-    const int y0 = ty * kT, x0 = tx * kT;
-    // key of the pixel at padded LDS offset o (kBlocked for markers, blocked pixels, the halo)
-    auto key_at = [&](int o) -> unsigned long long {
-      const unsigned v = sK[o];
-      if (v == kNoKey) return kBlocked;
-      const int oy = o / kLS - 1, ox = o - (o / kLS) * kLS - 1;
-      return ((unsigned long long)v << kKeyShift) | (unsigned long long)((long long)(y0 + oy) * a.W + x0 + ox);
-    };
-    if (lane == 0) s_bits = 0;
-    const int* nucf = a.nuc + fov * hw;
-    const int* footf = a.foot + fov * hw;
-    const float* cf = a.corr + fov * hwc + (long long)a.ch * hw;
-    const unsigned long long* Bf = a.Bg + fov * hw;
-    // every load of the tile and of this lane's halo pixels in flight before any is used
-    // (round 0: nuclei, footprint, cell channel; later rounds: stored level, inverted key)
-    unsigned long long w0_[kPerThread];
-    int w1_[kPerThread];
-#pragma unroll
-    for (int k = 0; k < kPerThread; ++k) {
-      const int i = lane + k * kThreads, y = y0 + i / kT, x = x0 + i % kT;
-      const long long pix = (y < a.H && x < a.W) ? (long long)y * a.W + x : 0;
-      if (R0) {
-        w0_[k] = ((unsigned long long)(unsigned)nucf[pix] << 32) | (unsigned)footf[pix];
-        w1_[k] = __float_as_int(cf[pix]);
-      } else {
-        w0_[k] = Bf[pix];
-        w1_[k] = a.inv[fov * hw + pix];
-      }
+  const int G = gridDim.x, xb = blockIdx.x & 7, xi = blockIdx.x >> 3, ng = G < 8 ? G : 8;
+  const int gx = (G - xb + 7) >> 3;
+  const int lo = (int)((long long)a.total * xb / ng), hi = (int)((long long)a.total * (xb + 1) / ng);
+  // (shares <= 64 tiles: one pass)
+  for (int k = 0; lo + xi + k * gx < hi; k += kThreads) {
+    const int tl = lo + xi + (k + lane) * gx;  // this lane's tile
+    const bool ok = tl < hi;
+    bool act = false;
+    if (ok) {
+      act = tile_active(a, round, Fp, tl);
+      if (!act) Fn[tl] = 0;
     }
-    // halo: the facing border vectors of the four neighbour tiles' rings (contiguous; the initial
-    // rings come from k_edt_rows, later ones from the neighbours' previous visits — any of them is
-    // an upper bound of the final level, and a changed border flags this tile for the next round)
-    constexpr int kHalo = kRing / kThreads;
-    static_assert(kRing % kThreads == 0, "whole halo per lane");
-    unsigned long long hv[kHalo];
-    int ho[kHalo];
-#pragma unroll
-    for (int k = 0; k < kHalo; ++k) {
-      const int h = lane + k * kThreads, side = h / kT, j = h % kT;
-      int hy, hx;
-      halo_pos(h, hy, hx);
-      ho[k] = (1 + hy) * kLS + 1 + hx;
-      long long src = -1;
-      if (side == 0) { if (ty > 0 && x0 + j < a.W) src = (long long)(t - a.ntx) * kRing + kT + j; }
-      else if (side == 1) { if (ty + 1 < a.nty && x0 + j < a.W) src = (long long)(t + a.ntx) * kRing + j; }
-      else if (side == 2) { if (tx > 0 && y0 + j < a.H) src = (long long)(t - 1) * kRing + 3 * kT + j; }
-      else if (tx + 1 < a.ntx && y0 + j < a.H) src = (long long)(t + 1) * kRing + 2 * kT + j;
-      hv[k] = src >= 0 ? a.ring[src] : kBlocked;
-    }
-    int any_free = 0;
-#pragma unroll
-    for (int k = 0; k < kPerThread; ++k) {
-      const int i = lane + k * kThreads, y = y0 + i / kT, x = x0 + i % kT;
-      unsigned long long b = kBlocked, key = kBlocked;
-      if (y < a.H && x < a.W) {
-        const long long pix = (long long)y * a.W + x;
+    for (unsigned long long am = __ballot(act); am; am &= am - 1) {
+      const int t = __shfl(tl, __ffsll((long long)am) - 1, 64);
+      const int per = a.nty * a.ntx;
+      const int fov = t / per, tt = t - fov * per, ty = tt / a.ntx, tx = tt - ty * a.ntx;
+      const bool full = R0 || (Fp[t] & kSelf) != 0;
+      const int y0 = ty * kT, x0 = tx * kT;
+      // key of the pixel at padded LDS offset o (kBlocked for markers, blocked pixels, the halo)
+      auto key_at = [&](int o) -> unsigned long long {
+        const unsigned v = sK[o];
+        if (v == kNoKey) return kBlocked;
+        const int oy = o / kLS - 1, ox = o - (o / kLS) * kLS - 1;
+        return ((unsigned long long)v << kKeyShift) | (unsigned long long)((long long)(y0 + oy) * a.W + x0 + ox);
+      };
+      if (lane == 0) s_bits = 0;
+      const int* nucf = a.nuc + fov * hw;
+      const int* footf = a.foot + fov * hw;
+      const float* cf = a.corr + fov * hwc + (long long)a.ch * hw;
+      const unsigned long long* Bf = a.Bg + fov * hw;
+      // every load of the tile and of this lane's halo pixels in flight before any is used
+      // (round 0: nuclei, footprint, cell channel; later rounds: stored level, inverted key)
+      unsigned long long w0_[kPerThread];
+      int w1_[kPerThread];
+  #pragma unroll
+      for (int k = 0; k < kPerThread; ++k) {
+        const int i = lane + k * kThreads, y = y0 + i / kT, x = x0 + i % kT;
+        const long long pix = (y < a.H && x < a.W) ? (long long)y * a.W + x : 0;
         if (R0) {
-          const unsigned inf = info_of((int)(w0_[k] >> 32), (int)(unsigned)w0_[k], __int_as_float(w1_[k]));
-          b = init_level(inf, pix);
-          if (!(inf & (kMark | kBlk))) key = key_of(inf, pix);
+          w0_[k] = ((unsigned long long)(unsigned)nucf[pix] << 32) | (unsigned)footf[pix];
+          w1_[k] = __float_as_int(cf[pix]);
         } else {
-          const unsigned long long v = w0_[k];
-          b = level_of(v);
-          if (v != kBlocked && !stored_marker(v)) key = key_of((unsigned)w1_[k], pix);
+          w0_[k] = Bf[pix];
+          w1_[k] = a.inv[fov * hw + pix];
         }
       }
-      any_free |= key != kBlocked;
-      sB[lds_off(i)] = b;
-      sK[lds_off(i)] = key != kBlocked ? (unsigned)(key >> kKeyShift) : kNoKey;
-    }
-#pragma unroll
-    for (int k = 0; k < kHalo; ++k) {
-      sB[ho[k]] = hv[k];
-      sK[ho[k]] = kNoKey;
-    }
-    any_free = __syncthreads_or(any_free);
-    if (R0) {
-      if (lane == 0) a.tfree[t] = (unsigned char)(any_free != 0);
-      if (!any_free) {  // no free pixel: only the border ring is ever read (as a neighbour's halo)
-        for (int k = lane; k < 4 * kT; k += kThreads) {
-          const int i = border_pixel(k), y = y0 + i / kT, x = x0 + i % kT;
-          if (y < a.H && x < a.W) {
-            const unsigned long long b = sB[lds_off(i)];
-            a.Bg[fov * hw + (long long)y * a.W + x] = b == kBlocked ? b : (b | kMarkBit);
+      // halo: the facing border vectors of the four neighbour tiles' rings (contiguous; the initial
+      // rings come from k_edt_rows, later ones from the neighbours' previous visits — any of them is
+      // an upper bound of the final level, and a changed border flags this tile for the next round)
+      constexpr int kHalo = kRing / kThreads;
+      static_assert(kRing % kThreads == 0, "whole halo per lane");
+      unsigned long long hv[kHalo];
+      int ho[kHalo];
+  #pragma unroll
+      for (int k = 0; k < kHalo; ++k) {
+        const int h = lane + k * kThreads, side = h / kT, j = h % kT;
+        int hy, hx;
+        halo_pos(h, hy, hx);
+        ho[k] = (1 + hy) * kLS + 1 + hx;
+        long long src = -1;
+        if (side == 0) { if (ty > 0 && x0 + j < a.W) src = (long long)(t - a.ntx) * kRing + kT + j; }
+        else if (side == 1) { if (ty + 1 < a.nty && x0 + j < a.W) src = (long long)(t + a.ntx) * kRing + j; }
+        else if (side == 2) { if (tx > 0 && y0 + j < a.H) src = (long long)(t - 1) * kRing + 3 * kT + j; }
+        else if (tx + 1 < a.ntx && y0 + j < a.H) src = (long long)(t + 1) * kRing + 2 * kT + j;
+        hv[k] = src >= 0 ? a.ring[src] : kBlocked;
+      }
+      int any_free = 0;
+  #pragma unroll
+      for (int k = 0; k < kPerThread; ++k) {
+        const int i = lane + k * kThreads, y = y0 + i / kT, x = x0 + i % kT;
+        unsigned long long b = kBlocked, key = kBlocked;
+        if (y < a.H && x < a.W) {
+          const long long pix = (long long)y * a.W + x;
+          if (R0) {
+            const unsigned inf = info_of((int)(w0_[k] >> 32), (int)(unsigned)w0_[k], __int_as_float(w1_[k]));
+            b = init_level(inf, pix);
+            if (!(inf & (kMark | kBlk))) key = key_of(inf, pix);
+          } else {
+            const unsigned long long v = w0_[k];
+            b = level_of(v);
+            if (v != kBlocked && !stored_marker(v)) key = key_of((unsigned)w1_[k], pix);
           }
         }
-        if (lane == 0) Fn[t] = 0;
-        __syncthreads();
-        continue;
+        any_free |= key != kBlocked;
+        sB[lds_off(i)] = b;
+        sK[lds_off(i)] = key != kBlocked ? (unsigned)(key >> kKeyShift) : kNoKey;
       }
-    }
-    WaveQueue wq{sQ, 0, 0};
-    unsigned bits = 0;
-    // seeds: every free pixel (full) or the border pixels (new halo), pulled from its neighbours;
-    // the candidates are compacted first (a fifth of a tile's pixels are free)
-    int nseed = 0;
-    if (full) {
-#pragma unroll
-      for (int k = 0; k < kPerThread; ++k) {
-        const int o = lds_off(lane + k * kThreads);
-        const bool c = sK[o] != kNoKey;
-        const unsigned long long m = __ballot(c);
-        if (c) sS[nseed + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)o;
-        nseed += __popcll(m);
+  #pragma unroll
+      for (int k = 0; k < kHalo; ++k) {
+        sB[ho[k]] = hv[k];
+        sK[ho[k]] = kNoKey;
       }
-    } else {
-      for (int k = lane; k < 4 * kT; k += kThreads) sS[k] = (unsigned short)lds_off(border_pixel(k));
-      nseed = 4 * kT;
-    }
-    __syncthreads();
-    for (int base = 0; base < nseed; base += kThreads) {
-      const int o = base + lane < nseed ? (int)sS[base + lane] : kLS + 1;
-      const unsigned long long key = base + lane < nseed ? key_at(o) : kBlocked;
-      bool imp = false;
-      if (key != kBlocked) {
-        const unsigned long long u = sB[o - kLS], l = sB[o - 1], r = sB[o + 1], d = sB[o + kLS];
-        unsigned long long m = u < l ? u : l;
-        m = r < m ? r : m;
-        m = d < m ? d : m;
-        const unsigned long long nv = m > key ? m : key;
-        if (nv < sB[o]) imp = nv < atomicMin(&sB[o], nv);
+      any_free = __syncthreads_or(any_free);
+      if (R0) {
+        if (lane == 0) a.tfree[t] = (unsigned char)(any_free != 0);
+        if (!any_free) {  // no free pixel: only the border ring is ever read (as a neighbour's halo)
+          for (int k = lane; k < 4 * kT; k += kThreads) {
+            const int i = border_pixel(k), y = y0 + i / kT, x = x0 + i % kT;
+            if (y < a.H && x < a.W) {
+              const unsigned long long b = sB[lds_off(i)];
+              a.Bg[fov * hw + (long long)y * a.W + x] = b == kBlocked ? b : (b | kMarkBit);
+            }
+          }
+          if (lane == 0) Fn[t] = 0;
+          __syncthreads();
+          continue;
+        }
       }
-      if (imp) bits |= border_bits_off(o);
-      wq.push(imp, o, lane);
-    }
-    // drain: push the improved level to the four neighbours (all reads of a step issued together)
-    bool ovf = false;
-    int dsteps = 0, ditems = 0;
-    while (wq.tail != wq.head) {
-      const int cnt = min(64, wq.tail - wq.head);
-      ++dsteps;
-      ditems += cnt;
-      if (wq.tail - wq.head + 3 * cnt > kQCap) {
-        ovf = true;
-        break;
+      WaveQueue wq{sQ, 0, 0};
+      unsigned bits = 0;
+      // seeds: every free pixel (full) or the border pixels (new halo), pulled from its neighbours;
+      // the candidates are compacted first (a fifth of a tile's pixels are free)
+      int nseed = 0;
+      if (full) {
+  #pragma unroll
+        for (int k = 0; k < kPerThread; ++k) {
+          const int o = lds_off(lane + k * kThreads);
+          const bool c = sK[o] != kNoKey;
+          const unsigned long long m = __ballot(c);
+          if (c) sS[nseed + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)o;
+          nseed += __popcll(m);
+        }
+      } else {
+        for (int k = lane; k < 4 * kT; k += kThreads) sS[k] = (unsigned short)lds_off(border_pixel(k));
+        nseed = 4 * kT;
       }
-      const bool act = lane < cnt;
-      const int o = act ? (int)wq.q[(wq.head + lane) & (kQCap - 1)] : kLS + 1;
-      wq.head += cnt;
-      const int nb[4] = {o - kLS, o - 1, o + 1, o + kLS};
-      const unsigned long long b = sB[o];
-      unsigned long long kk[4], bb[4];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        kk[d] = key_at(nb[d]);
-        bb[d] = sB[nb[d]];
+      __syncthreads();
+      for (int base = 0; base < nseed; base += kThreads) {
+        const int o = base + lane < nseed ? (int)sS[base + lane] : kLS + 1;
+        const unsigned long long key = base + lane < nseed ? key_at(o) : kBlocked;
+        bool imp = false;
+        if (key != kBlocked) {
+          const unsigned long long u = sB[o - kLS], l = sB[o - 1], r = sB[o + 1], d = sB[o + kLS];
+          unsigned long long m = u < l ? u : l;
+          m = r < m ? r : m;
+          m = d < m ? d : m;
+          const unsigned long long nv = m > key ? m : key;
+          if (nv < sB[o]) imp = nv < atomicMin(&sB[o], nv);
+        }
+        if (imp) bits |= border_bits_off(o);
+        wq.push(imp, o, lane);
       }
-      bool imp[4];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const unsigned long long nv = b > kk[d] ? b : kk[d];
-        imp[d] = act && nv < bb[d];
-        if (imp[d]) imp[d] = nv < atomicMin(&sB[nb[d]], nv);
+      // drain: push the improved level to the four neighbours (all reads of a step issued together)
+      bool ovf = false;
+      int dsteps = 0, ditems = 0;
+      while (wq.tail != wq.head) {
+        const int cnt = min(64, wq.tail - wq.head);
+        ++dsteps;
+        ditems += cnt;
+        if (wq.tail - wq.head + 3 * cnt > kQCap) {
+          ovf = true;
+          break;
+        }
+        const bool act = lane < cnt;
+        const int o = act ? (int)wq.q[(wq.head + lane) & (kQCap - 1)] : kLS + 1;
+        wq.head += cnt;
+        const int nb[4] = {o - kLS, o - 1, o + 1, o + kLS};
+        const unsigned long long b = sB[o];
+        unsigned long long kk[4], bb[4];
+  #pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          kk[d] = key_at(nb[d]);
+          bb[d] = sB[nb[d]];
+        }
+        bool imp[4];
+  #pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const unsigned long long nv = b > kk[d] ? b : kk[d];
+          imp[d] = act && nv < bb[d];
+          if (imp[d]) imp[d] = nv < atomicMin(&sB[nb[d]], nv);
+        }
+  #pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          if (imp[d]) bits |= border_bits_off(nb[d]);
+          wq.push(imp[d], nb[d], lane);
+        }
       }
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        if (imp[d]) bits |= border_bits_off(nb[d]);
-        wq.push(imp[d], nb[d], lane);
+      if (ovf) bits |= kSelf;
+      if (bits) atomicOr(&s_bits, bits);
+      if (a.dbg && lane == 0) {
+        unsigned long long* c = a.dbg + (0 * 64 + round) * 4;
+        atomicAdd(c, 1ull);
+        atomicAdd(c + 1, (unsigned long long)dsteps);
+        atomicAdd(c + 2, (unsigned long long)ditems);
+        atomicAdd(c + 3, (unsigned long long)ovf);
       }
-    }
-    if (ovf) bits |= kSelf;
-    if (bits) atomicOr(&s_bits, bits);
-    if (a.dbg && lane == 0) {
-      unsigned long long* c = a.dbg + (0 * 64 + round) * 4;
-      atomicAdd(c, 1ull);
-      atomicAdd(c + 1, (unsigned long long)dsteps);
-      atomicAdd(c + 2, (unsigned long long)ditems);
-      atomicAdd(c + 3, (unsigned long long)ovf);
-    }
-    __syncthreads();
-    for (int i = lane; i < kT * kT; i += kThreads) {
-      const int y = y0 + i / kT, x = x0 + i % kT;
-      if (y >= a.H || x >= a.W) continue;
-      const long long pix = fov * hw + (long long)y * a.W + x;
-      const int o = lds_off(i);
-      const unsigned long long b = sB[o];
-      const unsigned kv = sK[o];
-      if (kv != kNoKey) {
-        a.Bg[pix] = b;
-        if (R0) a.inv[pix] = (unsigned short)kv;
-      } else if (R0) {
-        a.Bg[pix] = b == kBlocked ? b : (b | kMarkBit);
+      __syncthreads();
+      for (int i = lane; i < kT * kT; i += kThreads) {
+        const int y = y0 + i / kT, x = x0 + i % kT;
+        if (y >= a.H || x >= a.W) continue;
+        const long long pix = fov * hw + (long long)y * a.W + x;
+        const int o = lds_off(i);
+        const unsigned long long b = sB[o];
+        const unsigned kv = sK[o];
+        if (kv != kNoKey) {
+          a.Bg[pix] = b;
+          if (R0) a.inv[pix] = (unsigned short)kv;
+        } else if (R0) {
+          a.Bg[pix] = b == kBlocked ? b : (b | kMarkBit);
+        }
       }
+      // this tile's border levels for its neighbours' halos
+      for (int h = lane; h < kRing; h += kThreads) {
+        const int side = h / kT, j = h % kT;
+        const int ly = side == 0 ? 0 : side == 1 ? kT - 1 : j, lx = side == 2 ? 0 : side == 3 ? kT - 1 : j;
+        if (y0 + ly < a.H && x0 + lx < a.W) a.ring[(long long)t * kRing + h] = sB[(1 + ly) * kLS + 1 + lx];
+      }
+      if (lane == 0) {
+        Fn[t] = (unsigned char)s_bits;
+        a.last[fov * 2] = round;
+      }
+      __syncthreads();
     }
-    // this tile's border levels for its neighbours' halos
-    for (int h = lane; h < kRing; h += kThreads) {
-      const int side = h / kT, j = h % kT;
-      const int ly = side == 0 ? 0 : side == 1 ? kT - 1 : j, lx = side == 2 ? 0 : side == 3 ? kT - 1 : j;
-      if (y0 + ly < a.H && x0 + lx < a.W) a.ring[(long long)t * kRing + h] = sB[(1 + ly) * kLS + 1 + lx];
-    }
-    if (lane == 0) {
-      Fn[t] = (unsigned char)s_bits;
-      a.last[fov * 2] = round;
-    }
-    __syncthreads();
   }
 }
 
@@ -655,13 +658,13 @@ extern "C" int cpx_watershed_cells(cpx_ctx* ctx, const int32_t* nuclei_dev, cons
   }
   CPX_CHECK_HIP(hipMemsetAsync(a.last, 0xff, sizeof(int) * 2 * B, ctx->stream));
   CPX_CHECK_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (label_rounds + 1), ctx->stream));
-  // eight one-wave blocks per CU fit the LDS; each block schedules its tiles t = block + k * grid
-  // (at most kThreads of them: the LDS list)
-  const int grid = std::max(std::min(total, ctx->n_cu * 8), cpx_div_up(total, kThreads));
+  // eight one-wave blocks per CU fit the LDS; each block takes a share of kShare0 (round 0) or
+  // kShare tiles of its XCD's range
+  const int grid0 = cpx_div_up(total, kShare0), grid = cpx_div_up(total, kShare);
   // The expand footprint is read in every relax round; the label rounds then overwrite the
   // free pixels of cells / cyto (the footprint is no longer needed: blocked <=> B == kBlocked).
   for (int r = 0; r < relax_rounds; ++r)
-    hipLaunchKernelGGL(r == 0 ? k_ws_relax<true> : k_ws_relax<false>, dim3(grid), dim3(kThreads), 0,
+    hipLaunchKernelGGL(r == 0 ? k_ws_relax<true> : k_ws_relax<false>, dim3(r == 0 ? grid0 : grid), dim3(kThreads), 0,
                        ctx->stream, a, r, (const unsigned char*)Fr[(r + 1) & 1], Fr[r & 1]);
   const int jgrid = ctx->n_cu * 8;
   hipLaunchKernelGGL(k_ws_ptr_init, dim3(total), dim3(kJumpThreads), 0, ctx->stream, a, cells_dev, cyto_dev,
