@@ -464,19 +464,32 @@ __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, in
       }
       done[j] = !active[j];
     }
+    // the cell (integer position) of each item's last gathers and their values: a step that
+    // stays in the same cell — most of them once a trajectory slows near its sink — reuses them
+    // instead of gathering again (the field is read-only here: the same values, bit-identical)
+    float2 af[NI], bf[NI], cf[NI], ef[NI];
+    int cy[NI], cx[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      cy[j] = -1;
+      cx[j] = -1;
+      af[j] = bf[j] = cf[j] = ef[j] = make_float2(0.0f, 0.0f);
+    }
     for (int s = 0; s < steps; ++s) {
       bool all = true;
 #pragma unroll
       for (int j = 0; j < NI; ++j) all = all && done[j];
       if (all) break;
-      // every item's four gathers first (a finished item re-reads its own cell: a valid address,
-      // its update is discarded below)
-      float2 af[NI], bf[NI], cf[NI], ef[NI];
+      // every item's gathers first (a finished item keeps its cell: no gather, its update is
+      // discarded below)
       int yi[NI], xi[NI];
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         yi[j] = (int)py[j];
         xi[j] = (int)px[j];
+        if (yi[j] == cy[j] && xi[j] == cx[j]) continue;
+        cy[j] = yi[j];
+        cx[j] = xi[j];
         const int y0 = min(Dy - 1, max(0, yi[j])), x0 = min(Dx - 1, max(0, xi[j]));
         // 32-bit byte offsets from the FOV's (block-uniform) field base: SGPR-base + VGPR-offset
         // loads, no 64-bit address arithmetic per step (the field is < 4 GiB per FOV)
