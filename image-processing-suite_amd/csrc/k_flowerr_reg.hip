@@ -90,9 +90,15 @@ __device__ __forceinline__ void fe_row_op(V* T, int jc, V& v) {
 // columns).  Class 1 (k_flow_error_reg1): one column per lane, the mask's columns <= 64 lanes and
 // its rows <= kFeReg1Rows registers, rows = the shorter side when both fit.  Class 2
 // (k_flow_error_reg, two columns per lane over two waves): columns <= 128, rows <= 2 x kFeRegRows
-// (80); class 3 the same over three waves, rows <= 3 x kFeRegRows (120); rows = the shorter side.
+// (80); class 3 the same over four waves of kFeReg3Rows, rows <= 3 x kFeRegRows (120); rows = the
+// shorter side.
 // Class 0: the LDS kernels.
 constexpr int kFeReg1Rows = 80;
+// class 3 runs as four waves of 32 rows: two 256-thread blocks per CU at the kernel's two waves
+// per SIMD fill all eight wave slots, where three waves of 40 rows left two idle (3.27 -> 2.82 ms
+// per 32 FOVs, `gpurun_out/r06ag`; five waves of 24 rows or eight of 16 fit fewer waves per CU)
+constexpr int kFeReg3Rows = 32;
+static_assert(4 * kFeReg3Rows >= kFeRegMaxShort, "class 3 rows fit four waves");
 __device__ __forceinline__ int fe_reg_class(int bh, int bw, bool& tr) {
   const int mn = min(bh, bw), mx = max(bh, bw);
   if (mn < 1) return 0;
@@ -103,7 +109,7 @@ __device__ __forceinline__ int fe_reg_class(int bh, int bw, bool& tr) {
   return 0;
 }
 
-template <int RW, int NW>
+template <int RW, int NW, int CLS>
 __global__ __launch_bounds__(64 * NW, 2) void k_flow_error_reg(
     const int* __restrict__ m0, const float2* __restrict__ dpf, int Dy, int Dx, int B, int max_label,
     const cpx_object* __restrict__ objects, const int* __restrict__ off, int* __restrict__ ctr, int lo_rows,
@@ -136,7 +142,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_flow_error_reg(
     const int r0 = o.bbox[0], c0 = o.bbox[1];
     const int bh = o.bbox[2] - r0, bw = o.bbox[3] - c0;
     bool tr = false;
-    if (fe_reg_class(bh, bw, tr) != NW) continue;  // block-uniform (class c: NW = c waves)
+    if (fe_reg_class(bh, bw, tr) != CLS) continue;  // block-uniform
     const int SR = tr ? bw : bh, SC = tr ? bh : bw;  // storage rows / columns
     // rows per wave (the slabs split the mask evenly); this wave's rows 1 + wv RS .. wv RS + nrow
     const int RS = (SR + NW - 1) / NW;
@@ -541,10 +547,10 @@ int cpx_flow_error_reg_launch(int n_cu, hipStream_t stream, const int* m0, const
     hipLaunchKernelGGL((k_flow_error_reg1<kFeReg1Rows>), dim3(8 * n_cu), dim3(64), 0, stream, m0, dpf, Dy, Dx, B,
                        ML, obj, off, ctr, thr, bad, und);
   if (which & 2)
-    hipLaunchKernelGGL((k_flow_error_reg<kFeRegRows, 2>), dim3(4 * n_cu), dim3(128), 0, stream, m0, dpf, Dy, Dx,
+    hipLaunchKernelGGL((k_flow_error_reg<kFeRegRows, 2, 2>), dim3(4 * n_cu), dim3(128), 0, stream, m0, dpf, Dy, Dx,
                        B, ML, obj, off, ctr + 1, 0, thr, bad, und);
   if (which & 4)
-    hipLaunchKernelGGL((k_flow_error_reg<kFeRegRows, 3>), dim3(2 * n_cu), dim3(192), 0, stream, m0, dpf, Dy, Dx,
+    hipLaunchKernelGGL((k_flow_error_reg<kFeReg3Rows, 4, 3>), dim3(2 * n_cu), dim3(256), 0, stream, m0, dpf, Dy, Dx,
                        B, ML, obj, off, ctr + 2, 0, thr, bad, und);
   CPX_CHECK_LAUNCH("k_flow_error_reg");
   return CPX_OK;

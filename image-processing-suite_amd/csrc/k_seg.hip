@@ -2561,7 +2561,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
                      (const cpx_object*)obj, (const int*)off, off + B + (CTR), LT, LU, LC, flow_threshold, \
                      bad, (const int*)nullptr, und)
       // masks of fe_reg_class 1-3 (k_flowerr_reg.hip: up to 64 x 80 one column per lane, 128 x 80 /
-      // 128 x 120 in column pairs over two / three waves)
+      // 128 x 120 in column pairs over two / four waves)
       // first, in VGPRs (k_flow_error_reg); the LDS kernels skip the masks those flagged
       static const bool reg = !getenv("CPX_FE_NOREG");
       if (sev >= 0) CPX_CHECK_HIP(hipEventRecord(ctx->seg_ev[sev][2], ctx->stream));
