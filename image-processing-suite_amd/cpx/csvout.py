@@ -240,9 +240,12 @@ class PlateTables:
         self.objects[table].append((int(image_number), labels, feats))
         if self._pool is not None:
             fut = self._pool.submit(format_object_rows, int(image_number), labels, feats)
-            self._rows[table].append((int(image_number), fut))
             if table in self._stream:
+                # only the writer holds a streamed block: its bytes are freed once written (an
+                # out-of-order job re-formats the table from self.objects in write_objects)
                 self._stream[table].put(int(image_number), fut)
+            else:
+                self._rows[table].append((int(image_number), fut))
 
     def close(self):
         for st in self._stream.values():

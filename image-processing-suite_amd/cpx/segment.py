@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes as ct
 import math
+import warnings
 
 import numpy as np
 import torch
@@ -243,11 +244,20 @@ class Segmenter:
                                 int(self.resample), _ptr(labels), _ptr(self.stats)), "cpx_seg_masks")
 
     def segment(self, corr: torch.Tensor, labels: torch.Tensor | None = None) -> torch.Tensor:
+        """The whole segmentation of a batch (the direct API; FovPipeline runs the stages itself and
+        re-runs a FOV whose seeds overflowed).  Waits for the batch and warns when a FOV found more
+        seeds than max_objects: its labels are then truncated (SEG_OVF_SEEDS)."""
         if labels is None:
             labels = torch.empty((self.B, self.H, self.W), dtype=torch.int32, device=self.dev.torch_device)
         self.prepare(corr)
         self._run_net()
         self.postprocess(labels)
+        ovf = self.seg_stats()["overflow"].ravel()[: self.B]
+        bad = np.flatnonzero(ovf & SEG_OVF_SEEDS)
+        if bad.size:
+            warnings.warn(f"Segmenter.segment: FOV(s) {bad.tolist()} found more seeds than max_objects="
+                          f"{self.max_objects}; their labels are truncated (raise max_objects, or run "
+                          f"them through FovPipeline, which re-runs such FOVs)", RuntimeWarning, stacklevel=2)
         return labels
 
     def seg_stats(self) -> np.ndarray:

@@ -6,6 +6,7 @@ bit-exact on identical inputs; the CPnet forward (PyTorch-ROCm) is checked again
 network on the CPU in fp32.
 """
 import ctypes as ct
+import warnings
 
 import numpy as np
 import pytest
@@ -481,3 +482,15 @@ def test_cpnet_conv3x3_head(dev, cin, H, W):
     dev.sync()
     err = (out.float() - ref).abs()
     assert (err <= 2e-2 * ref.abs() + 5e-2).all(), err.max().item()
+
+
+def test_segmenter_warns_when_seeds_overflow(dev):
+    """The direct Segmenter API truncates a FOV with more seeds than max_objects (the pipeline
+    re-runs such FOVs instead): segment() must say so."""
+    B, C, H, W = 1, 3, 700, 760
+    corr = torch.from_numpy(_planes(B, C, H, W, seed=11)).to(dev.torch_device)
+    with pytest.warns(RuntimeWarning, match="more seeds than max_objects"):
+        Segmenter(dev, H, W, B, use_graph=False, max_objects=2).segment(corr)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        Segmenter(dev, H, W, B, use_graph=False).segment(corr)
