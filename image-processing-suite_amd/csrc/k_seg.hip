@@ -819,34 +819,63 @@ __global__ __launch_bounds__(kT) void k_seed_expand(int Dyh, int Dxh, DynBufs d)
 }
 
 // M0 = M[pflows]: every pixel's label at its final position; per label its pixel count and
-// first pixel, aggregated per wave (lanes are consecutive pixels, mostly of one label)
+// first pixel, aggregated per wave (lanes are consecutive pixels, mostly of one label).  kAsg
+// pixels per thread (q = block base + k kT + thread), each step's loads for all of them issued
+// before any is used: one pixel per thread left the three dependent loads (moving flag, final
+// position, label map) exposed per pixel
+constexpr int kAsg = 4;
 __global__ __launch_bounds__(kT) void k_assign(int Dy, int Dx, DynBufs d) {
   const int fov = blockIdx.y;
   const long long n = (long long)Dy * Dx;
-  const int q = blockIdx.x * kT + threadIdx.x;
+  const int q0 = blockIdx.x * kT * kAsg + threadIdx.x;
   const int Dxh = Dx + 2 * kRpad;
-  int l = 0;
-  if (q < n) {
-    int iy = q / Dx, ix = q - iy * Dx;
-    if (d.mov[(long long)fov * n + q] && d.st[fov].n_moving >= 5) {
-      const float2 pp = d.p[(long long)fov * n + q];
-      iy = (int)pp.x;
-      ix = (int)pp.y;
+  const bool follow = d.st[fov].n_moving >= 5;
+  const unsigned char* mov = d.mov + (long long)fov * n;
+  const float2* P = d.p + (long long)fov * n;
+  const unsigned int* M = d.M + (long long)fov * (Dy + 2 * kRpad) * Dxh;
+  unsigned char mv[kAsg];
+#pragma unroll
+  for (int k = 0; k < kAsg; ++k) {
+    const int q = q0 + k * kT;
+    mv[k] = q < n ? mov[q] : 0;
+  }
+  float2 pp[kAsg];
+#pragma unroll
+  for (int k = 0; k < kAsg; ++k) {
+    const int q = q0 + k * kT;
+    pp[k] = make_float2(0.0f, 0.0f);
+    if (follow && mv[k]) pp[k] = P[q];
+  }
+  int l[kAsg];
+#pragma unroll
+  for (int k = 0; k < kAsg; ++k) {
+    const int q = q0 + k * kT;
+    l[k] = 0;
+    if (q < n) {
+      int iy = q / Dx, ix = q - iy * Dx;
+      if (follow && mv[k]) {
+        iy = (int)pp[k].x;
+        ix = (int)pp[k].y;
+      }
+      l[k] = (int)M[(long long)(iy + kRpad) * Dxh + ix + kRpad];
     }
-    l = (int)d.M[(long long)fov * (Dy + 2 * kRpad) * Dxh + (long long)(iy + kRpad) * Dxh + ix + kRpad];
-    d.m0[(long long)fov * n + q] = l;
   }
   const int lane = threadIdx.x & 63;
-  unsigned long long pend = __ballot(l != 0);
-  while (pend) {
-    const int leader = __ffsll((long long)pend) - 1;
-    const int l0 = __shfl(l, leader);
-    const unsigned long long m = __ballot(l == l0);
-    if (lane == leader) {
-      atomicAdd(&d.cnt[(long long)fov * (d.ms + 1) + l0], __popcll(m));
-      atomicMin(&d.first[(long long)fov * (d.ms + 1) + l0], q);  // lowest lane = first pixel
+#pragma unroll
+  for (int k = 0; k < kAsg; ++k) {
+    const int q = q0 + k * kT;
+    if (q < n) d.m0[(long long)fov * n + q] = l[k];
+    unsigned long long pend = __ballot(l[k] != 0);
+    while (pend) {
+      const int leader = __ffsll((long long)pend) - 1;
+      const int l0 = __shfl(l[k], leader);
+      const unsigned long long m = __ballot(l[k] == l0);
+      if (lane == leader) {
+        atomicAdd(&d.cnt[(long long)fov * (d.ms + 1) + l0], __popcll(m));
+        atomicMin(&d.first[(long long)fov * (d.ms + 1) + l0], q);  // lowest lane = first pixel
+      }
+      pend &= ~m;
     }
-    pend &= ~m;
   }
 }
 
@@ -2508,7 +2537,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
                      (const int*)d.totals, stats_dev);
   hipLaunchKernelGGL(k_seed_expand, dim3(std::max(1, (4 * ctx->n_cu + B - 1) / B), B), dim3(kT), 0,
                      ctx->stream, Dyh, Dxh, d);
-  hipLaunchKernelGGL(k_assign, gp, dim3(kT), 0, ctx->stream, Dy, Dx, d);
+  hipLaunchKernelGGL(k_assign, dim3(cpx_div_up(n, (long long)kT * kAsg), B), dim3(kT), 0, ctx->stream, Dy, Dx, d);
   hipLaunchKernelGGL(k_relabel_mark, dim3(cpx_div_up(ms, kT), B), dim3(kT), 0, ctx->stream, Dy, Dx, d);
   CPX_CHECK_LAUNCH("cpx_seg_masks seeds");
   rc = ordered_compact(ctx, d.mark, n, B, d.tiles, d.totals, ms, d.marklist, ms);
