@@ -581,17 +581,37 @@ __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, in
 // Pixels that did not move sit at their own coordinate: one plain store per padded cell covers
 // them (and clears the rest); the moving pixels then add with wave-aggregated atomics (the
 // pixels of one cell mostly end in the same bin).
+// Four cells per thread (kPx4): one 16-byte store when the FOV's grid allows (nh % 4 == 0), the
+// per-pixel kernels below likewise — one element per thread held these full-image passes at
+// ~2 TB/s
+constexpr int kPx4 = 4;
+
 __global__ __launch_bounds__(kT) void k_hist_init(int Dy, int Dx, DynBufs d) {
   const int fov = blockIdx.y;
   const int Dxh = Dx + 2 * kRpad, Dyh = Dy + 2 * kRpad;
   const long long nh = (long long)Dyh * Dxh;
-  const long long b = (long long)blockIdx.x * kT + threadIdx.x;
-  if (b >= nh) return;
-  const int bi = (int)b;  // nh < 2^31 (cpx_seg_masks): 32-bit division
-  const int y = bi / Dxh - kRpad, x = bi - (bi / Dxh) * Dxh - kRpad;
-  int v = 0;
-  if (y >= 0 && y < Dy && x >= 0 && x < Dx) v = d.mov[(long long)fov * Dy * Dx + (long long)y * Dx + x] ? 0 : 1;
-  d.h[(long long)fov * nh + b] = v;
+  const long long b0 = ((long long)blockIdx.x * kT + threadIdx.x) * kPx4;
+  if (b0 >= nh) return;
+  const unsigned char* mov = d.mov + (long long)fov * Dy * Dx;
+  int v[kPx4];
+#pragma unroll
+  for (int u = 0; u < kPx4; ++u) {
+    const long long b = b0 + u;
+    v[u] = 0;
+    if (b < nh) {
+      const int bi = (int)b;  // nh < 2^31 (cpx_seg_masks): 32-bit division
+      const int y = bi / Dxh - kRpad, x = bi - (bi / Dxh) * Dxh - kRpad;
+      if (y >= 0 && y < Dy && x >= 0 && x < Dx) v[u] = mov[(long long)y * Dx + x] ? 0 : 1;
+    }
+  }
+  int* h = d.h + (long long)fov * nh;
+  if ((nh & 3) == 0) {
+    *reinterpret_cast<int4*>(h + b0) = make_int4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (int u = 0; u < kPx4; ++u)
+      if (b0 + u < nh) h[b0 + u] = v[u];
+  }
 }
 
 __device__ __forceinline__ void agg_add(int* base, int key, bool valid) {
@@ -624,18 +644,32 @@ __global__ __launch_bounds__(kT) void k_hist_moving(int Dy, int Dx, DynBufs d) {
   agg_add(d.h + (long long)fov * (Dy + 2 * kRpad) * Dxh, key, valid);
 }
 
-// seeds: h > 10 and h == 5x5 max (maximum_filter1d size 5 on both axes)
+// seeds: h > 10 and h == 5x5 max (maximum_filter1d size 5 on both axes); kPx4 cells per thread
 __global__ __launch_bounds__(kT) void k_seed_flags(int Dyh, int Dxh, DynBufs d) {
   const int fov = blockIdx.y;
   const long long nh = (long long)Dyh * Dxh;
-  const long long q = (long long)blockIdx.x * kT + threadIdx.x;
-  if (q >= nh) return;
+  const long long q0 = ((long long)blockIdx.x * kT + threadIdx.x) * kPx4;
+  if (q0 >= nh) return;
   const int* h = d.h + (long long)fov * nh;
-  const int v = h[q];
-  unsigned char f = 0;
-  if (v > 10) {
+  const bool vec = (nh & 3) == 0;
+  int v[kPx4];
+  if (vec) {
+    const int4 t = *reinterpret_cast<const int4*>(h + q0);
+    v[0] = t.x;
+    v[1] = t.y;
+    v[2] = t.z;
+    v[3] = t.w;
+  } else {
+#pragma unroll
+    for (int u = 0; u < kPx4; ++u) v[u] = q0 + u < nh ? h[q0 + u] : 0;
+  }
+  unsigned int fw = 0;
+#pragma unroll
+  for (int u = 0; u < kPx4; ++u) {
+    if (v[u] <= 10) continue;
+    const long long q = q0 + u;
     const int y = (int)(q / Dxh), x = (int)(q % Dxh);
-    int mx = v;
+    int mx = v[u];
     for (int dy = -2; dy <= 2; ++dy)
       for (int dx = -2; dx <= 2; ++dx) {
         int yy = y + dy, xx = x + dx;  // scipy 'reflect' boundary (never reached by seeds)
@@ -643,9 +677,16 @@ __global__ __launch_bounds__(kT) void k_seed_flags(int Dyh, int Dxh, DynBufs d) 
         xx = xx < 0 ? -xx - 1 : (xx >= Dxh ? 2 * Dxh - xx - 1 : xx);
         mx = max(mx, h[(long long)yy * Dxh + xx]);
       }
-    f = (v >= mx);
+    fw |= (unsigned int)(v[u] >= mx) << (8 * u);
   }
-  d.sflag[(long long)fov * nh + q] = f;
+  unsigned char* f = d.sflag + (long long)fov * nh;
+  if (vec && ((((uintptr_t)(f + q0)) & 3u) == 0)) {
+    *reinterpret_cast<unsigned int*>(f + q0) = fw;
+  } else {
+#pragma unroll
+    for (int u = 0; u < kPx4; ++u)
+      if (q0 + u < nh) f[q0 + u] = (unsigned char)((fw >> (8 * u)) & 1u);
+  }
 }
 
 // ---- ordered compaction of byte flags: indices of the set flags in increasing order ---------
@@ -906,11 +947,26 @@ __global__ __launch_bounds__(kT) void k_relabel_apply(int Dy, int Dx, DynBufs d)
 __global__ __launch_bounds__(kT) void k_apply_newlab(int Dy, int Dx, DynBufs d) {
   const int fov = blockIdx.y;
   const long long n = (long long)Dy * Dx;
-  const long long q = (long long)blockIdx.x * kT + threadIdx.x;
-  if (q >= n) return;
-  int* m = d.m0 + (long long)fov * n + q;
-  const int l = *m;
-  *m = l ? d.newlab[(long long)fov * (d.ms + 1) + l] : 0;  // big masks map to 0
+  const long long q0 = ((long long)blockIdx.x * kT + threadIdx.x) * kPx4;
+  if (q0 >= n) return;
+  int* m = d.m0 + (long long)fov * n;
+  const int* nl = d.newlab + (long long)fov * (d.ms + 1);
+  if ((n & 3) == 0 && (((uintptr_t)d.m0) & 15u) == 0) {  // (m0 may be the caller's buffer)
+    const int4 t = *reinterpret_cast<const int4*>(m + q0);
+    int4 o;
+    o.x = t.x ? nl[t.x] : 0;  // big masks map to 0
+    o.y = t.y ? nl[t.y] : 0;
+    o.z = t.z ? nl[t.z] : 0;
+    o.w = t.w ? nl[t.w] : 0;
+    *reinterpret_cast<int4*>(m + q0) = o;
+  } else {
+#pragma unroll
+    for (int u = 0; u < kPx4; ++u)
+      if (q0 + u < n) {
+        const int l = m[q0 + u];
+        m[q0 + u] = l ? nl[l] : 0;
+      }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1819,11 +1875,23 @@ __global__ __launch_bounds__(kT) void k_apply_bad(long long n, int max_label,
                                                   const unsigned char* __restrict__ bad,
                                                   int* __restrict__ m0) {
   const int fov = blockIdx.y;
-  const long long q = (long long)blockIdx.x * kT + threadIdx.x;
-  if (q >= n) return;
-  int* m = m0 + (long long)fov * n + q;
-  const int l = *m;
-  if (l > 0 && l <= max_label && bad[(long long)fov * (max_label + 1) + l] == 1) *m = 0;
+  const long long q0 = ((long long)blockIdx.x * kT + threadIdx.x) * kPx4;
+  if (q0 >= n) return;
+  int* m = m0 + (long long)fov * n;
+  const unsigned char* bd = bad + (long long)fov * (max_label + 1);
+  auto keep = [&](int l) { return (l > 0 && l <= max_label && bd[l] == 1) ? 0 : l; };
+  if ((n & 3) == 0 && (((uintptr_t)m0) & 15u) == 0) {
+    const int4 t = *reinterpret_cast<const int4*>(m + q0);
+    const int4 o = make_int4(keep(t.x), keep(t.y), keep(t.z), keep(t.w));
+    if (o.x != t.x || o.y != t.y || o.z != t.z || o.w != t.w) *reinterpret_cast<int4*>(m + q0) = o;
+  } else {
+#pragma unroll
+    for (int u = 0; u < kPx4; ++u)
+      if (q0 + u < n) {
+        const int l = m[q0 + u], k = keep(l);
+        if (k != l) m[q0 + u] = k;
+      }
+  }
 }
 
 __global__ void k_count_bad(int max_label, const unsigned char* __restrict__ bad,
@@ -2527,9 +2595,10 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
       ctx->seg_rounds[sev] = rr;
     }
   }
-  hipLaunchKernelGGL(k_hist_init, gh, dim3(kT), 0, ctx->stream, Dy, Dx, d);
+  const dim3 gh4(cpx_div_up(nh, (long long)kT * kPx4), B), gp4(cpx_div_up(n, (long long)kT * kPx4), B);
+  hipLaunchKernelGGL(k_hist_init, gh4, dim3(kT), 0, ctx->stream, Dy, Dx, d);
   hipLaunchKernelGGL(k_hist_moving, gp, dim3(kT), 0, ctx->stream, Dy, Dx, d);
-  hipLaunchKernelGGL(k_seed_flags, gh, dim3(kT), 0, ctx->stream, Dyh, Dxh, d);
+  hipLaunchKernelGGL(k_seed_flags, gh4, dim3(kT), 0, ctx->stream, Dyh, Dxh, d);
   CPX_CHECK_LAUNCH("cpx_seg_masks follow");
   rc = ordered_compact(ctx, d.sflag, nh, B, d.tiles, d.totals, ms, d.seeds, ms);
   if (rc) return rc;
@@ -2543,7 +2612,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   rc = ordered_compact(ctx, d.mark, n, B, d.tiles, d.totals, ms, d.marklist, ms);
   if (rc) return rc;
   hipLaunchKernelGGL(k_relabel_apply, dim3(4, B), dim3(kT), 0, ctx->stream, Dy, Dx, d);
-  hipLaunchKernelGGL(k_apply_newlab, gp, dim3(kT), 0, ctx->stream, Dy, Dx, d);
+  hipLaunchKernelGGL(k_apply_newlab, gp4, dim3(kT), 0, ctx->stream, Dy, Dx, d);
   CPX_CHECK_LAUNCH("cpx_seg_masks relabel");
   // ---- object workspaces (WS_SEG_OBJ): the flow-error and fill-holes object tables share it
   const int ML = max_objects;
@@ -2646,7 +2715,7 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
                        (const int*)d.m0, (const float2*)d.dpf, Dy, Dx, ML, (const cpx_object*)obj,
                        (const cpx_fov_objects*)hdr, kFeLargeThreads, kFeU, kFeLargeCells,
                        flow_threshold, gscr, (long long)gscr_per, bad);
-    hipLaunchKernelGGL(k_apply_bad, gp, dim3(kT), 0, ctx->stream, n, ML,
+    hipLaunchKernelGGL(k_apply_bad, gp4, dim3(kT), 0, ctx->stream, n, ML,
                        (const unsigned char*)bad, d.m0);
     hipLaunchKernelGGL(k_count_bad, dim3(B), dim3(256), 0, ctx->stream, ML,
                        (const unsigned char*)bad, (const int*)(off + B + 1), 11, stats_dev);

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--md", action="store_true")
+    ap.add_argument("--top", type=int, default=40, help="kernels listed (by time per step)")
     ap.add_argument("--series", default=None,
                     help="also list the per-dispatch durations (us) of this kernel in the last step")
     a = ap.parse_args()
@@ -43,7 +44,7 @@ def main():
     if a.md:
         print("| kernel | calls/step | avg us | us/step | % |")
         print("|---|---:|---:|---:|---:|")
-    for k, (c, t) in items[:40]:
+    for k, (c, t) in items[:a.top]:
         if a.md:
             print(f"| `{k}` | {c / n_steps:.1f} | {t / c:.1f} | {t / n_steps:.1f} | {100 * t / tot:.1f} |")
         else:
