@@ -103,6 +103,7 @@ __global__ __launch_bounds__(kT) void k_edt_cols(const int* __restrict__ labels,
 // kRowsPB rows of a kT-column segment (fewer, fuller blocks: one block per row was
 // dispatch-bound); all its rows' candidate segments are staged in LDS at once.
 constexpr int kRowsPB = 8;
+constexpr int kStageMax = (kRowsPB * (kT + 2 * 127) + kT - 1) / kT;  // staged values per thread (D <= 127)
 
 // With `ring` (the Cells watershed, k_watershed.hip): every pixel on the border ring of its
 // 32 x 32 watershed tile also stores its initial flood level (from the Nuclei label, this
@@ -118,15 +119,34 @@ __global__ __launch_bounds__(kT) void k_edt_rows(const int* __restrict__ nuc, in
   const int nr = min(kRowsPB, H - r0);
   const int c0 = blockIdx.x * kT;
   const int sw = kT + 2 * D;
-  for (int i = threadIdx.x; i < nr * sw; i += kT) {
-    const int rr = i / sw, k = i - rr * sw;
-    const int c = c0 - D + k;
-    seg[i] = (c >= 0 && c < W) ? off[((long long)fov * H + r0 + rr) * W + c] : pack_ft(kNone, 0);
+  const int c = c0 + threadIdx.x;
+  // every load of the block issued before any is used: the staged candidates (up to
+  // kStageMax per thread) and this thread's Nuclei labels of its rows — one load, one LDS store
+  // per loop trip and a label load per row had left a memory round trip per step exposed
+  int sv[kStageMax], nv_[kRowsPB];
+#pragma unroll
+  for (int u = 0; u < kStageMax; ++u) {
+    const int i = threadIdx.x + u * kT;
+    sv[u] = pack_ft(kNone, 0);
+    if (i < nr * sw) {
+      const int rr = i / sw, k = i - rr * sw;
+      const int cc = c0 - D + k;
+      if (cc >= 0 && cc < W) sv[u] = off[((long long)fov * H + r0 + rr) * W + cc];
+    }
+  }
+#pragma unroll
+  for (int rr = 0; rr < kRowsPB; ++rr)
+    nv_[rr] = (rr < nr && c < W) ? nuc[((long long)fov * H + r0 + rr) * W + c] : 0;
+#pragma unroll
+  for (int u = 0; u < kStageMax; ++u) {
+    const int i = threadIdx.x + u * kT;
+    if (i < nr * sw) seg[i] = sv[u];
   }
   __syncthreads();
-  const int c = c0 + threadIdx.x;
   if (c >= W) return;
-  for (int rr = 0; rr < nr; ++rr) {
+#pragma unroll
+  for (int rr = 0; rr < kRowsPB; ++rr) {
+    if (rr >= nr) break;
     const int* sr = seg + rr * sw + threadIdx.x;
     // branch-free lexicographic min of (d^2, k) as one key (d^2 << 8) | k: a column without a
     // feature has dr = kNone = -128, so its d^2 >= 16384 > D^2 (D <= 127) and it can only win
@@ -138,7 +158,7 @@ __global__ __launch_bounds__(kT) void k_edt_rows(const int* __restrict__ nuc, in
     }
     const int lab = (int)(best >> 8) <= D * D ? sr[best & 0xffu] >> 8 : 0;
     const long long px = ((long long)fov * H + r0 + rr) * W + c;
-    const int nv = nuc[px];
+    const int nv = nv_[rr];
     if (cells) cells[px] = lab;
     if (cyto) cyto[px] = (nv == 0) ? lab : 0;
     if (ring) {
