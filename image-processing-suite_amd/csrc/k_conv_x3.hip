@@ -1165,13 +1165,27 @@ __global__ __launch_bounds__(256) void k_cpnet_style_x3(const uint4* __restrict_
   float mean = 0.0f;
   if (c < C) {
     const int q = (c / 16) * 4 + ((c % 16) >> 3), e = c & 7;
-    double acc = 0.0;
-    for (long long p = 0; p < P; ++p) {
+    // four interleaved fp64 partial sums (fixed order: deterministic), their loads in flight
+    // together: one dependent add chain over the map's 784 pixels made this one-block-per-image
+    // kernel latency-bound
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    long long p = 0;
+    for (; p + 4 <= P; p += 4) {
+      f16x8 hi[4], lo[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        hi[u] = __builtin_bit_cast(f16x8, xb[(p + u) * Q + q]);
+        lo[u] = __builtin_bit_cast(f16x8, xb[(p + u) * Q + q + 2]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += (double)((float)hi[u][e] + (float)lo[u][e] * kLoInv);
+    }
+    for (; p < P; ++p) {
       const f16x8 hi = __builtin_bit_cast(f16x8, xb[p * Q + q]);
       const f16x8 lo = __builtin_bit_cast(f16x8, xb[p * Q + q + 2]);
-      acc += (double)((float)hi[e] + (float)lo[e] * kLoInv);
+      acc[0] += (double)((float)hi[e] + (float)lo[e] * kLoInv);
     }
-    mean = (float)(acc / (double)P);
+    mean = (float)(((acc[0] + acc[1]) + (acc[2] + acc[3])) / (double)P);
   }
   red[c] = c < C ? (double)mean * (double)mean : 0.0;
   __syncthreads();
@@ -1183,9 +1197,15 @@ __global__ __launch_bounds__(256) void k_cpnet_style_x3(const uint4* __restrict_
   if (c < C) s[c] = mean / nrm;
   __syncthreads();
   for (int j = c; j < J; j += 256) {
-    double acc = 0.0;
-    for (int k = 0; k < C; ++k) acc += (double)lin_w[(long long)j * C + k] * (double)s[k];
-    out[(long long)n * J + j] = (float)(acc + (double)lin_b[j]);
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    const float* wj = lin_w + (long long)j * C;
+    int k = 0;
+    for (; k + 4 <= C; k += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += (double)wj[k + u] * (double)s[k + u];
+    }
+    for (; k < C; ++k) acc[0] += (double)wj[k] * (double)s[k];
+    out[(long long)n * J + j] = (float)(((acc[0] + acc[1]) + (acc[2] + acc[3])) + (double)lin_b[j]);
   }
 }
 
