@@ -630,8 +630,8 @@ struct QcRowPts {
 
 // kQcPairs row pairs per block, the next pair's loads in flight during the current pair's
 // transform: one pair per block left every load's latency exposed (104 VGPRs, four blocks per CU
-// by LDS: 3.61 ms per 48 FOVs); four pairs with the prefetch (158 VGPRs, three blocks per CU)
-// 2.70 ms, eight or sixteen 3.05 ms (gpurun_out/r06x)
+// by LDS: 3.36 ms per 48 FOVs); four pairs with the prefetch (158 VGPRs, three blocks per CU)
+// 2.73 ms (gpurun_out/r06aq), eight or sixteen pairs slower (r06x)
 constexpr int kQcPairs = 4;
 
 template <int ILLUM>
