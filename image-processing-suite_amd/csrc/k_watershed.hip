@@ -365,6 +365,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_ws_relax(WsArgs a, int round,
         atomicAdd(c + 3, (unsigned long long)ovf);
       }
       __syncthreads();
+      // a later-round visit that improved no seed changed nothing: its levels and ring stay as
+      // stored (round 2 of 48 FOVs visits ~106 K tiles for 0.6 M worklist items)
+      if (!R0 && wq.tail == 0) {
+        if (lane == 0) Fn[t] = (unsigned char)s_bits;
+        __syncthreads();
+        continue;
+      }
       for (int i = lane; i < kT * kT; i += kThreads) {
         const int y = y0 + i / kT, x = x0 + i % kT;
         if (y >= a.H || x >= a.W) continue;
