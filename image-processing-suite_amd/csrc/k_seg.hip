@@ -401,6 +401,19 @@ __global__ __launch_bounds__(kT) void k_dyn_prep(const float* __restrict__ yf, i
 // the pixels still moving after r rounds (positions carried in a compact item list), runs K
 // steps, writes the finished ones and appends the rest to the next round's list in block order
 // — so the 64 lanes of a wave stay spatial neighbours and their bilinear gathers share lines.
+// wave-aggregated histogram add (lanes with equal keys: one atomic)
+__device__ __forceinline__ void agg_add(int* base, int key, bool valid) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long pend = __ballot(valid);
+  while (pend) {
+    const int leader = __ffsll((long long)pend) - 1;
+    const int k0 = __shfl(key, leader);
+    const unsigned long long m = __ballot(valid && key == k0);
+    if (lane == leader) atomicAdd(&base[k0], __popcll(m));
+    pend &= ~m;
+  }
+}
+
 struct FollowItem {
   int q;
   float py, px;
@@ -432,6 +445,8 @@ __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, in
   FollowItem* dst = out + (long long)fov * n;
   const float fLy = (float)(Dy - 1), fLx = (float)(Dx - 1);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int Dxh = Dx + 2 * kRpad;
+  int* Hh = d.h + (long long)fov * (Dy + 2 * kRpad) * Dxh;
   const unsigned char* Ib = reinterpret_cast<const unsigned char*>(I);
   // V4: the FOV's field as a buffer resource (8 n < 2^31 bytes, checked by the host)
   const __amdgpu_buffer_rsrc_t rsI =
@@ -544,6 +559,13 @@ __global__ __launch_bounds__(kT) void k_dyn_follow(int Dy, int Dx, int niter, in
     const bool last = step0 + steps >= niter;
     bool carry[NI];
     unsigned long long bal[NI];
+    // a finished item's final position goes straight into get_masks' histogram (initialised by
+    // k_hist_init before the rounds) instead of a second pass over the moving pixels
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const bool fin = active[j] && (done[j] || last);
+      agg_add(Hh, ((int)py[j] + kRpad) * Dxh + (int)px[j] + kRpad, fin);
+    }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       if (active[j] && (done[j] || last)) P[q[j]] = make_float2(py[j], px[j]);
@@ -614,24 +636,13 @@ __global__ __launch_bounds__(kT) void k_hist_init(int Dy, int Dx, DynBufs d) {
   }
 }
 
-__device__ __forceinline__ void agg_add(int* base, int key, bool valid) {
-  const int lane = threadIdx.x & 63;
-  unsigned long long pend = __ballot(valid);
-  while (pend) {
-    const int leader = __ffsll((long long)pend) - 1;
-    const int k0 = __shfl(key, leader);
-    const unsigned long long m = __ballot(valid && key == k0);
-    if (lane == leader) atomicAdd(&base[k0], __popcll(m));
-    pend &= ~m;
-  }
-}
-
 __global__ __launch_bounds__(kT) void k_hist_moving(int Dy, int Dx, DynBufs d) {
   const int fov = blockIdx.y;
   const long long n = (long long)Dy * Dx;
   const int i = blockIdx.x * kT + threadIdx.x;
   const int n_moving = d.st[fov].n_moving;
-  if ((long long)blockIdx.x * kT >= n_moving) return;  // block-uniform
+  // (FOVs with >= 5 moving pixels: k_dyn_follow added their final positions)
+  if (n_moving >= 5 || (long long)blockIdx.x * kT >= n_moving) return;  // block-uniform
   const int Dxh = Dx + 2 * kRpad;
   const bool valid = i < n_moving;
   int key = 0;
@@ -2545,6 +2556,10 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   else
     hipLaunchKernelGGL(k_dyn_prep<false>, gprep, dim3(kT), 0, ctx->stream, yf_dev, Ly, Lx, Dy, Dx,
                        tabs.uy, tabs.ux, d);
+  // get_masks' histogram: the cells of the pixels that do not move (the moving pixels' final
+  // positions are added by the follow rounds as they finish)
+  const dim3 gh4(cpx_div_up(nh, (long long)kT * kPx4), B), gp4(cpx_div_up(n, (long long)kT * kPx4), B);
+  hipLaunchKernelGGL(k_hist_init, gh4, dim3(kT), 0, ctx->stream, Dy, Dx, d);
   // k_dyn_follow: trajectories per thread (CPX_FOLLOW_NI 1, 2 or 4) and paired 16-byte gathers
   // (CPX_FOLLOW_V4); per 48-FOV step (`gpurun_out/r05l`, `r05m`): 1 / scalar 12.11 ms, 2 / scalar
   // 11.83, 4 / scalar 12.54, 1 / paired 11.46, 2 / paired 11.02 (the default); every setting passes
@@ -2595,9 +2610,8 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
       ctx->seg_rounds[sev] = rr;
     }
   }
-  const dim3 gh4(cpx_div_up(nh, (long long)kT * kPx4), B), gp4(cpx_div_up(n, (long long)kT * kPx4), B);
-  hipLaunchKernelGGL(k_hist_init, gh4, dim3(kT), 0, ctx->stream, Dy, Dx, d);
-  hipLaunchKernelGGL(k_hist_moving, gp, dim3(kT), 0, ctx->stream, Dy, Dx, d);
+  // (only FOVs with fewer than 5 moving pixels are left to it: one block per FOV)
+  hipLaunchKernelGGL(k_hist_moving, dim3(1, B), dim3(kT), 0, ctx->stream, Dy, Dx, d);
   hipLaunchKernelGGL(k_seed_flags, gh4, dim3(kT), 0, ctx->stream, Dyh, Dxh, d);
   CPX_CHECK_LAUNCH("cpx_seg_masks follow");
   rc = ordered_compact(ctx, d.sflag, nh, B, d.tiles, d.totals, ms, d.seeds, ms);
