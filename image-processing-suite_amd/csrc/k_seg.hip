@@ -2778,7 +2778,9 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   hipLaunchKernelGGL(k_fill_final, dim3(B), dim3(1024), 0, ctx->stream, ML, min_size,
                      (const cpx_object*)obj, (const cpx_fov_objects*)hdr, (const int*)absorber,
                      (const int*)labels_dev, (const int*)fillidx, W, N, newlab, stats_dev);
-  hipLaunchKernelGGL(k_fill_apply, dim3(std::max(1, std::min(cpx_div_up(N, kT), 4 * ctx->n_cu / B + 1)), B),
+  // eight 256-thread blocks per CU over the batch (the kernel's full occupancy; four left its
+  // loads short of the HBM rate)
+  hipLaunchKernelGGL(k_fill_apply, dim3(std::max(1, std::min(cpx_div_up(N, kT), 8 * ctx->n_cu / B + 1)), B),
                      dim3(kT), 0, ctx->stream, labels_dev, N, ML, (const int*)l2i,
                      (const int*)fillidx, (const int*)newlab, (const int*)absorber,
                      (const cpx_seg_stats*)stats_dev);
