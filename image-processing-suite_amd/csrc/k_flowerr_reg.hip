@@ -542,16 +542,12 @@ __global__ __launch_bounds__(64, 2) void k_flow_error_reg1(
 int cpx_flow_error_reg_launch(int n_cu, hipStream_t stream, const int* m0, const float2* dpf, int Dy, int Dx,
                               int B, int ML, const cpx_object* obj, const int* off, int* ctr, double thr,
                               unsigned char* bad, int* und) {
-  static const int which = getenv("CPX_FE_REG") ? atoi(getenv("CPX_FE_REG")) : 7;  // development A/B
-  if (which & 1)
-    hipLaunchKernelGGL((k_flow_error_reg1<kFeReg1Rows>), dim3(8 * n_cu), dim3(64), 0, stream, m0, dpf, Dy, Dx, B,
-                       ML, obj, off, ctr, thr, bad, und);
-  if (which & 2)
-    hipLaunchKernelGGL((k_flow_error_reg<kFeRegRows, 2, 2>), dim3(4 * n_cu), dim3(128), 0, stream, m0, dpf, Dy, Dx,
-                       B, ML, obj, off, ctr + 1, 0, thr, bad, und);
-  if (which & 4)
-    hipLaunchKernelGGL((k_flow_error_reg<kFeReg3Rows, 4, 3>), dim3(2 * n_cu), dim3(256), 0, stream, m0, dpf, Dy, Dx,
-                       B, ML, obj, off, ctr + 2, 0, thr, bad, und);
+  hipLaunchKernelGGL((k_flow_error_reg1<kFeReg1Rows>), dim3(8 * n_cu), dim3(64), 0, stream, m0, dpf, Dy, Dx, B,
+                     ML, obj, off, ctr, thr, bad, und);
+  hipLaunchKernelGGL((k_flow_error_reg<kFeRegRows, 2, 2>), dim3(4 * n_cu), dim3(128), 0, stream, m0, dpf, Dy, Dx,
+                     B, ML, obj, off, ctr + 1, 0, thr, bad, und);
+  hipLaunchKernelGGL((k_flow_error_reg<kFeReg3Rows, 4, 3>), dim3(2 * n_cu), dim3(256), 0, stream, m0, dpf, Dy, Dx,
+                     B, ML, obj, off, ctr + 2, 0, thr, bad, und);
   CPX_CHECK_LAUNCH("k_flow_error_reg");
   return CPX_OK;
 }

@@ -26,10 +26,7 @@
 namespace {
 
 constexpr int kThreads = 256;
-#ifndef CPX_QC_FT
-#define CPX_QC_FT 512
-#endif
-constexpr int kFT = CPX_QC_FT;  // FFT kernels: more threads -> fewer butterflies per thread in registers
+constexpr int kFT = 512;  // generic FFT kernels: more threads -> fewer butterflies per thread in registers
 constexpr int kMaxN = 4096;
 constexpr int kMaxStages = 12;
 

@@ -2506,10 +2506,8 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   const size_t sz_act = al(sizeof(int) * B * n);
   const size_t sz_small = al(sizeof(int) * (size_t)B);
   // follow rounds: K = k0 steps while most pixels still move (until step sw), then k1 for the
-  // long tail; CPX_FOLLOW_K0 / _SWITCH / _K1 override the defaults 16 / 384 / 128 (A/B runs)
-  static const int k0 = std::max(1, getenv("CPX_FOLLOW_K0") ? atoi(getenv("CPX_FOLLOW_K0")) : 16);
-  static const int sw = std::max(0, getenv("CPX_FOLLOW_SWITCH") ? atoi(getenv("CPX_FOLLOW_SWITCH")) : 384);
-  static const int k1 = std::max(1, getenv("CPX_FOLLOW_K1") ? atoi(getenv("CPX_FOLLOW_K1")) : 128);
+  // long tail (k0 = 24 / 32 / 48 measured equal to 16, `gpurun_out/r06af`)
+  constexpr int k0 = 16, sw = 384, k1 = 128;
   const int rounds = cpx_div_up(sw, k0) + cpx_div_up(std::max(0, niter - sw), k1) + 2;
   const size_t sz_fcnt = al(sizeof(int) * (size_t)B * (rounds + 1));
   const size_t sz_items = al((size_t)16 * B * n);
@@ -2560,12 +2558,10 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
   // positions are added by the follow rounds as they finish)
   const dim3 gh4(cpx_div_up(nh, (long long)kT * kPx4), B), gp4(cpx_div_up(n, (long long)kT * kPx4), B);
   hipLaunchKernelGGL(k_hist_init, gh4, dim3(kT), 0, ctx->stream, Dy, Dx, d);
-  // k_dyn_follow: trajectories per thread (CPX_FOLLOW_NI 1, 2 or 4) and paired 16-byte gathers
-  // (CPX_FOLLOW_V4); per 48-FOV step (`gpurun_out/r05l`, `r05m`): 1 / scalar 12.11 ms, 2 / scalar
-  // 11.83, 4 / scalar 12.54, 1 / paired 11.46, 2 / paired 11.02 (the default); every setting passes
-  // the segmentation parity tests
-  static const int follow_ni = getenv("CPX_FOLLOW_NI") ? atoi(getenv("CPX_FOLLOW_NI")) : 2;
-  static const bool follow_v4 = !getenv("CPX_FOLLOW_V4") || atoi(getenv("CPX_FOLLOW_V4")) != 0;
+  // k_dyn_follow: two trajectories per thread and paired 16-byte gathers; per 48-FOV step
+  // (`gpurun_out/r05l`, `r05m`, trajectories / gathers): 1 / scalar 12.11 ms, 2 / scalar 11.83,
+  // 4 / scalar 12.54, 1 / paired 11.46, 2 / paired 11.02 (kept); every setting passed the
+  // segmentation parity tests
   // (development / bench instrumentation: cpx_debug_seg_timing)
   const int sev = ctx->seg_timing && ctx->seg_nev < cpx_ctx::kSegEv ? ctx->seg_nev++ : -1;
   bool fe_timed = false;  // the register flow-error kernels were bracketed (else a zero interval)
@@ -2578,11 +2574,8 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
       const FollowItem* in = (const FollowItem*)(r & 1 ? d.fitems1 : d.fitems0);
       FollowItem* out = (FollowItem*)(r & 1 ? d.fitems0 : d.fitems1);
       // (the right-edge form reads x0 - 1; the buffer resource holds 8 n < 2^31 bytes)
-      const bool v4 = follow_v4 && Dx >= 2 && 8LL * n < (1LL << 31);
-      auto kern = follow_ni == 4 ? (v4 ? k_dyn_follow<4, true> : k_dyn_follow<4, false>)
-                : follow_ni == 3 ? (v4 ? k_dyn_follow<3, true> : k_dyn_follow<3, false>)
-                : follow_ni == 2 ? (v4 ? k_dyn_follow<2, true> : k_dyn_follow<2, false>)
-                                 : (v4 ? k_dyn_follow<1, true> : k_dyn_follow<1, false>);
+      const bool v4 = Dx >= 2 && 8LL * n < (1LL << 31);
+      auto kern = v4 ? k_dyn_follow<2, true> : k_dyn_follow<2, false>;
       hipLaunchKernelGGL(kern, dim3(fblk, B), dim3(kT), 0, ctx->stream, Dy, Dx, niter, step, K,
                          r == 0 ? 1 : 0, in, (const int*)(d.fcnt + (size_t)B * r), out,
                          d.fcnt + (size_t)B * (r + 1), d);
@@ -2664,9 +2657,8 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
                        (const cpx_fov_objects*)hdr, off);
     // fp32 screening of every mask the LDS kernels hold (half the LDS: twice the masks per CU),
     // then the fp64 sweeps for the masks it could not decide
-    static const bool screen = !getenv("CPX_FE_NOSCREEN");
     const int* lst_in = nullptr;
-    if (screen && B < 2048 && ML <= (1 << 20)) {  // list codes: fov << 20 | object
+    if (B < 2048 && ML <= (1 << 20)) {  // list codes: fov << 20 | object
 #define FE_SCREEN(TH, CE, U_, WPE, G, CTR, LT, LU, LC)                                                  \
   hipLaunchKernelGGL((k_flow_error_lds<TH, CE, U_, float, WPE>), dim3((G) * ctx->n_cu), dim3(TH), 0,    \
                      ctx->stream, (const int*)d.m0, (const float2*)d.dpf, Dy, Dx, B, ML,             \
@@ -2675,13 +2667,10 @@ extern "C" int cpx_seg_masks(cpx_ctx* ctx, const float* yf_dev, int B, const cpx
       // masks of fe_reg_class 1-3 (k_flowerr_reg.hip: up to 64 x 80 one column per lane, 128 x 80 /
       // 128 x 120 in column pairs over two / four waves)
       // first, in VGPRs (k_flow_error_reg); the LDS kernels skip the masks those flagged
-      static const bool reg = !getenv("CPX_FE_NOREG");
       if (sev >= 0) CPX_CHECK_HIP(hipEventRecord(ctx->seg_ev[sev][2], ctx->stream));
-      if (reg) {
-        rc = cpx_flow_error_reg_launch(ctx->n_cu, ctx->stream, d.m0, (const float2*)d.dpf, Dy, Dx, B, ML,
-                                       obj, off, off + B + 9, flow_threshold, bad, und);
-        if (rc) return rc;
-      }
+      rc = cpx_flow_error_reg_launch(ctx->n_cu, ctx->stream, d.m0, (const float2*)d.dpf, Dy, Dx, B, ML,
+                                     obj, off, off + B + 9, flow_threshold, bad, und);
+      if (rc) return rc;
       if (sev >= 0) {
         CPX_CHECK_HIP(hipEventRecord(ctx->seg_ev[sev][3], ctx->stream));
         fe_timed = true;
