@@ -15,7 +15,6 @@ layers, and the fp32 output head; no PyTorch compute.
 from __future__ import annotations
 
 import ctypes as ct
-import os
 
 import numpy as np
 import torch
@@ -23,19 +22,21 @@ import torch
 from ._lib import check
 from .cpnet import CPnet
 
-X3_VARIANT = int(os.environ.get("CPX_X3_VARIANT", "0"))
+# The network's build choices (module constants: the constructor's `variant` / `zvariant`
+# arguments and the tests select the others):
+X3_VARIANT = 0
 # the convolutions that write only the next input z (no residual stream y) run as variant 3 at the
 # 112^2 and deeper levels (BM 64: two channel slices per wave, one slab buffer): 5-12 % faster
 # there, slower where the epilogue also stores y (tools/conv_bench_x3.py, gpurun_out/r05c);
-# bit-identical outputs.  CPX_X3_ZVARIANT=-1 keeps every convolution at X3_VARIANT
-X3_ZVARIANT = int(os.environ.get("CPX_X3_ZVARIANT", "3"))
+# bit-identical outputs.  -1 keeps every convolution at X3_VARIANT
+X3_ZVARIANT = 3
 # each down block's last convolution also max-pools its output for the next block (the pooled
-# tensor and its BatchNorm+ReLU from the staged tile: no read of y back); CPX_X3_POOL_FUSE=0 keeps
-# the separate pool kernel
-X3_POOL_FUSE = os.environ.get("CPX_X3_POOL_FUSE", "1") != "0"
+# tensor and its BatchNorm+ReLU from the staged tile: no read of y back); False keeps the
+# separate pool kernel
+X3_POOL_FUSE = True
 # fold each down block's (and the deepest up block's) 1x1 residual projection into the block's
-# second 3x3 convolution (cpx_cpnet_x3_conv_proj); CPX_X3_FOLD=0 keeps the separate 1x1 pass
-X3_FOLD = os.environ.get("CPX_X3_FOLD", "1") != "0"
+# second 3x3 convolution (cpx_cpnet_x3_conv_proj); False keeps the separate 1x1 pass
+X3_FOLD = True
 
 
 def split_f16(w: np.ndarray):
